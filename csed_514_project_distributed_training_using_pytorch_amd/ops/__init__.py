@@ -1,0 +1,23 @@
+"""Operator library: gfx950 HIP kernels exposed as differentiable PyTorch ops."""
+from . import _native, rng
+from .functional import (
+    accuracy_count,
+    compute_dtype,
+    conv2d,
+    conv2d_pool_relu,
+    cross_entropy,
+    dropout,
+    dropout2d,
+    dropout2d_scale,
+    linear,
+    log_softmax,
+    max_pool2d_relu,
+    nll_loss,
+    set_compute_dtype,
+)
+
+__all__ = [
+    "accuracy_count", "compute_dtype", "conv2d", "conv2d_pool_relu", "cross_entropy", "dropout",
+    "dropout2d", "dropout2d_scale", "linear", "log_softmax", "max_pool2d_relu", "nll_loss",
+    "set_compute_dtype", "rng", "_native",
+]

@@ -1,0 +1,65 @@
+"""Loader for the in-tree native extension (``_C.so``, built by ``_build.py``).
+
+The extension registers the ``torch.ops.csed.*`` operators (hand-written
+gfx950 HIP kernels).  On a machine with a GPU every GPU op goes through these
+kernels; if the shared object is missing or fails to load there, the ops
+raise instead of silently running stock PyTorch kernels.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_SO = Path(__file__).resolve().parent.parent / "_C.so"
+_lock = threading.Lock()
+_loaded = False
+_error: Exception | None = None
+
+BF16, F16, F32 = 1, 2, 0
+MFMA_CODE = {torch.bfloat16: BF16, torch.float16: F16}
+
+
+def so_path() -> Path:
+    return _SO
+
+
+def load(build_if_missing: bool | None = None) -> bool:
+    """Load ``_C.so`` (optionally building it first).  Returns True on success."""
+    global _loaded, _error
+    with _lock:
+        if _loaded:
+            return True
+        if build_if_missing is None:
+            build_if_missing = os.environ.get("CSED_AUTOBUILD", "1") == "1"
+        try:
+            if not _SO.exists() and build_if_missing:
+                from .. import _build
+
+                _build.build(verbose=False)
+            torch.ops.load_library(str(_SO))
+            _loaded = True
+            _error = None
+        except Exception as e:  # pragma: no cover - exercised on broken installs
+            _error = e
+        return _loaded
+
+
+def available() -> bool:
+    return load()
+
+
+def require() -> None:
+    """Raise loudly when the HIP kernels are needed but not loadable."""
+    if not load():
+        raise RuntimeError(
+            f"csed native extension could not be loaded from {_SO}: {_error!r}. "
+            "Build it with `python -m csed_514_project_distributed_training_using_pytorch_amd._build`."
+        )
+
+
+def ops():
+    require()
+    return torch.ops.csed

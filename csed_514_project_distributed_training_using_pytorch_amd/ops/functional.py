@@ -1,0 +1,334 @@
+"""Differentiable ops backed by the gfx950 HIP kernels (``torch.ops.csed``).
+
+Device dispatch is by tensor device only: GPU tensors always go through the
+hand-written kernels (and raise if the extension is missing); CPU tensors use
+the stock PyTorch ops, which serve as the fp32 numerical oracle for the tests
+(SURVEY.md section 4, item 1).
+
+Compute precision on the GPU: activations are stored in the compute dtype
+(bf16 by default, fp16 optional), matrix-shaped work runs on
+``v_mfma_f32_16x16x32_{bf16,f16}`` with fp32 accumulation, weights stay fp32
+masters (the kernels convert while staging them into LDS), and weight
+gradients are produced in fp32.
+
+Reference parity map (ref = /root/reference):
+  conv2d / conv2d_pool_relu   <- nn.Conv2d, F.max_pool2d, F.relu      src/model.py:9-10,16-17
+  dropout / dropout2d         <- F.dropout, nn.Dropout2d              src/model.py:11,17,20
+  linear                      <- nn.Linear (+relu, +dropout fused)    src/model.py:12-13,19-21
+  log_softmax, nll_loss       <- F.log_softmax, F.nll_loss             src/model.py:22, src/train.py:74
+  cross_entropy               <- nn.CrossEntropyLoss on log-probs      src/train_dist.py:67,82
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+from .rng import default_state
+
+_compute_dtype = torch.bfloat16
+
+
+def set_compute_dtype(dtype: torch.dtype) -> None:
+    global _compute_dtype
+    if dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError("compute dtype must be torch.bfloat16 or torch.float16")
+    _compute_dtype = dtype
+
+
+def compute_dtype() -> torch.dtype:
+    return _compute_dtype
+
+
+def _mfma() -> int:
+    return _native.MFMA_CODE[_compute_dtype]
+
+
+def _ops():
+    return _native.ops()
+
+
+def _act_dtype(x: torch.Tensor) -> torch.dtype:
+    return x.dtype if x.dtype in (torch.bfloat16, torch.float16) else _compute_dtype
+
+
+def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
+    return max(1, min(N, 256)) * OC * (IC * KH * KW + 1)
+
+
+# ----------------------------------------------------------------- conv ----
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, pad, pool, chscale):
+        x = x.contiguous()
+        N, IC, H, W = x.shape
+        OC, _, KH, KW = w.shape
+        OH, OW = H + 2 * pad - KH + 1, W + 2 * pad - KW + 1
+        adt = _act_dtype(x)
+        mf = _mfma()
+        if pool:
+            y = torch.empty((N, OC, OH // 2, OW // 2), device=x.device, dtype=adt)
+            idx = torch.empty(y.shape, device=x.device, dtype=torch.uint8)
+            _ops().conv2d_fwd(x, w, b, y, pad, idx, chscale, 2, mf)
+            ctx.save_for_backward(x, w, y, idx, chscale)
+        else:
+            y = torch.empty((N, OC, OH, OW), device=x.device, dtype=adt)
+            _ops().conv2d_fwd(x, w, b, y, pad, None, None, 0, mf)
+            ctx.save_for_backward(x, w)
+        ctx.pad, ctx.pool, ctx.mf, ctx.has_bias = pad, pool, mf, b is not None
+        ctx.conv_shape = (N, OC, OH, OW)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        if ctx.pool:
+            x, w, y, idx, chscale = ctx.saved_tensors
+            dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)
+            _ops().maxpool_relu_bwd(dy.to(y.dtype), y, idx, chscale, dconv, 2)
+        else:
+            x, w = ctx.saved_tensors
+            dconv = dy
+        dx = dw = db = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            N, IC = x.shape[:2]
+            OC, _, KH, KW = w.shape
+            dw = torch.empty_like(w, dtype=torch.float32)
+            db = torch.empty((OC,), device=w.device, dtype=torch.float32) if ctx.has_bias else None
+            ws = torch.empty(wgrad_workspace_elems(N, IC, KH, KW, OC), device=w.device, dtype=torch.float32)
+            _ops().conv2d_wgrad(x, dconv, dw, db, ws, ctx.pad, ctx.mf, 0.0)
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+            _ops().conv2d_dgrad(dconv, w, dx, ctx.pad, ctx.mf)
+        return dx, dw, db, None, None, None
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0):
+    """nn.functional.conv2d (stride 1, symmetric padding) on MFMA implicit GEMM."""
+    if not x.is_cuda:
+        return F.conv2d(x, weight, bias, padding=padding)
+    return _Conv2d.apply(x, weight, bias, int(padding), False, None)
+
+
+def conv2d_pool_relu(x, weight, bias=None, chscale: torch.Tensor | None = None, padding: int = 0):
+    """relu(max_pool2d(conv2d(x) [* chscale], 2)) in one kernel (ref src/model.py:16-17).
+
+    ``chscale`` is an optional fp32 [N*C] per-channel scale (the Dropout2d mask,
+    already divided by 1-p).
+    """
+    if not x.is_cuda:
+        y = F.conv2d(x, weight, bias, padding=padding)
+        if chscale is not None:
+            y = y * chscale.view(y.shape[0], y.shape[1], 1, 1).to(y.dtype)
+        return F.relu(F.max_pool2d(y, 2))
+    return _Conv2d.apply(x, weight, bias, int(padding), True, chscale)
+
+
+# ----------------------------------------------------------------- pool ----
+class _MaxPoolRelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, chscale):
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty((N, C, H // k, W // k), device=x.device, dtype=x.dtype)
+        idx = torch.empty(y.shape, device=x.device, dtype=torch.uint8)
+        _ops().maxpool_relu_fwd(x, y, idx, chscale, k)
+        ctx.save_for_backward(y, idx, chscale)
+        ctx.k, ctx.xshape = k, x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, idx, chscale = ctx.saved_tensors
+        dx = torch.empty(ctx.xshape, device=dy.device, dtype=y.dtype)
+        _ops().maxpool_relu_bwd(dy.contiguous().to(y.dtype), y, idx, chscale, dx, ctx.k)
+        return dx, None, None
+
+
+def max_pool2d_relu(x, k: int = 2, chscale: torch.Tensor | None = None):
+    """relu(max_pool2d(x * chscale, k)) with kernel == stride == k."""
+    if not x.is_cuda:
+        if chscale is not None:
+            x = x * chscale.view(x.shape[0], x.shape[1], 1, 1).to(x.dtype)
+        return F.relu(F.max_pool2d(x, k))
+    return _MaxPoolRelu.apply(x, int(k), chscale)
+
+
+# -------------------------------------------------------------- dropout ----
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, inner, seed, offset, offset_dev):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _ops().dropout_fwd(x, y, inner, p, seed, offset, offset_dev)
+        ctx.args = (p, inner, seed, offset)
+        ctx.save_for_backward(offset_dev) if offset_dev is not None else None
+        ctx.has_dev = offset_dev is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, inner, seed, offset = ctx.args
+        offset_dev = ctx.saved_tensors[0] if ctx.has_dev else None
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        # the mask is a pure function of (seed, offset, element): regenerate it
+        _ops().dropout_fwd(dy, dx, inner, p, seed, offset, offset_dev)
+        return dx, None, None, None, None, None
+
+
+def dropout(x, p: float = 0.5, training: bool = True):
+    if not training or p == 0.0:
+        return x
+    if not x.is_cuda:
+        return F.dropout(x, p, training)
+    seed, off, dev = default_state.next()
+    return _Dropout.apply(x, float(p), 0, seed, off, dev)
+
+
+def dropout2d(x, p: float = 0.5, training: bool = True):
+    if not training or p == 0.0:
+        return x
+    if not x.is_cuda:
+        return F.dropout2d(x, p, training)
+    seed, off, dev = default_state.next()
+    inner = x.shape[2] * x.shape[3]
+    return _Dropout.apply(x, float(p), int(inner), seed, off, dev)
+
+
+def dropout2d_scale(n: int, c: int, p: float, device) -> torch.Tensor:
+    """Per-(sample, channel) Dropout2d scale vector (0 or 1/(1-p)), fp32 [n*c]."""
+    s = torch.empty(n * c, device=device, dtype=torch.float32)
+    if torch.device(device).type != "cuda":
+        return (torch.rand(n * c) >= p).float().div_(1.0 - p) if p < 1 else torch.zeros(n * c)
+    seed, off, dev = default_state.next()
+    _ops().channel_mask(s, float(p), seed, off, dev)
+    return s
+
+
+# --------------------------------------------------------------- linear ----
+_ACT = {"none": 0, "relu": 1, "relu_dropout": 2}
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act, p, seed, offset, offset_dev, out_dtype):
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        if x2.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            x2 = x2.float()
+        y = torch.empty((x2.shape[0], w.shape[0]), device=x.device, dtype=out_dtype)
+        _ops().gemm(x2, w.t(), y, b, 1.0, 0.0, act, p, seed, offset, offset_dev, None, 1.0, _mfma())
+        ctx.save_for_backward(x2, w, y if act else None)
+        ctx.act, ctx.p, ctx.has_bias, ctx.lead = act, p, b is not None, lead
+        return y.view(*lead, w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0]).contiguous()
+        gate = y if ctx.act else None
+        if gate is not None and dy2.dtype != gate.dtype:
+            dy2 = dy2.to(gate.dtype)
+        gs = 1.0 / (1.0 - ctx.p) if ctx.act == 2 else 1.0
+        mf = _mfma()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
+            _ops().gemm(dy2, w, dx, None, 1.0, 0.0, 0, 0.0, 0, 0, None, gate, gs, mf)
+            dx = dx.view(*ctx.lead, x2.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(w.shape, device=w.device, dtype=torch.float32)
+            _ops().gemm(dy2.t(), x2, dw, None, 1.0, 0.0, 0, 0.0, 0, 0, None,
+                        gate.t() if gate is not None else None, gs, mf)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.empty((w.shape[0],), device=w.device, dtype=torch.float32)
+            _ops().colsum(dy2, gate, gs, db, 0.0)
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def linear(x, weight, bias=None, act: str = "none", p: float = 0.0, out_dtype: torch.dtype | None = None):
+    """y = act(x @ W^T + b); act in {'none', 'relu', 'relu_dropout'} (dropout prob p)."""
+    if act not in _ACT:
+        raise ValueError(f"unknown activation {act!r}")
+    if not x.is_cuda:
+        y = F.linear(x, weight, bias)
+        if act != "none":
+            y = F.relu(y)
+        if act == "relu_dropout":
+            y = F.dropout(y, p, True)
+        return y
+    a = _ACT[act]
+    if a == 2 and p == 0.0:
+        a = 1
+    seed, off, dev = default_state.next() if a == 2 else (0, 0, None)
+    od = out_dtype or _act_dtype(x)
+    return _Linear.apply(x, weight, bias, a, float(p), seed, off, dev, od)
+
+
+# ----------------------------------------------------------- softmax/loss ----
+class _LogSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        y = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+        _ops().log_softmax_fwd(x, y)
+        ctx.save_for_backward(y)
+        ctx.xdtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dx = torch.empty(y.shape, device=y.device, dtype=ctx.xdtype)
+        _ops().log_softmax_bwd(dy.contiguous().float(), y, dx)
+        return dx
+
+
+def log_softmax(x, dim: int = 1):
+    if not x.is_cuda:
+        return F.log_softmax(x, dim=dim)
+    if dim not in (1, -1) or x.dim() != 2:
+        raise ValueError("log_softmax kernel supports 2-D inputs over dim 1")
+    return _LogSoftmax.apply(x)
+
+
+_RED = {"none": 0, "mean": 1, "sum": 2}
+
+
+class _NLL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logp, target, reduction):
+        logp = logp.contiguous().float()
+        target = target.contiguous().long()
+        out = torch.empty((logp.shape[0],) if reduction == 0 else (), device=logp.device, dtype=torch.float32)
+        _ops().nll_fwd(logp, target, out, reduction, None)
+        ctx.save_for_backward(target)
+        ctx.reduction, ctx.shape = reduction, logp.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (target,) = ctx.saved_tensors
+        d = torch.empty(ctx.shape, device=target.device, dtype=torch.float32)
+        _ops().nll_bwd(gout.contiguous().float(), target, d, ctx.reduction)
+        return d, None, None
+
+
+def nll_loss(logp, target, reduction: str = "mean", size_average: bool | None = None):
+    """F.nll_loss; ``size_average=False`` maps to reduction='sum' (ref src/train.py:94)."""
+    if size_average is not None:
+        reduction = "mean" if size_average else "sum"
+    if not logp.is_cuda:
+        return F.nll_loss(logp, target, reduction=reduction)
+    return _NLL.apply(logp, target, _RED[reduction])
+
+
+def cross_entropy(x, target, reduction: str = "mean"):
+    """nn.CrossEntropyLoss: log_softmax then NLL (idempotent on log-probs, ref src/train_dist.py:67)."""
+    return nll_loss(log_softmax(x), target, reduction)
+
+
+def accuracy_count(logp: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Number of argmax hits, kept on device (no host sync)."""
+    return (logp.argmax(dim=1) == target).sum()

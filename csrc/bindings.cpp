@@ -1,0 +1,315 @@
+// ATen-facing registration of the csed::* ops.
+//
+// Every op is an "out" op: the caller (Python, see ops/_native.py) allocates
+// the outputs, the op checks shapes/dtypes on the host and enqueues the HIP
+// kernel(s) on the current PyTorch HIP stream.  No op allocates, copies to
+// host or synchronises, so every op is safe inside torch.cuda.graph capture
+// (= hipStreamBeginCapture).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include "launchers.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+#define CHECK_HIP(expr)                                                              \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    TORCH_CHECK(_e == hipSuccess, "csed: HIP error '", hipGetErrorString(_e), "' in ", \
+                #expr);                                                              \
+  } while (0)
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+int dcode(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return csed::kF32;
+    case at::kBFloat16: return csed::kBF16;
+    case at::kHalf: return csed::kF16;
+    case at::kByte: return csed::kU8;
+    default: TORCH_CHECK(false, "csed: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+int mcode(int64_t mfma_dtype) {
+  TORCH_CHECK(mfma_dtype == csed::kBF16 || mfma_dtype == csed::kF16,
+              "csed: MFMA dtype must be bf16 (1) or fp16 (2)");
+  return (int)mfma_dtype;
+}
+
+void dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "csed: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "csed: ", name, " must be contiguous");
+}
+
+const void* optp(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+template <typename T> T* optpt(const optional<Tensor>& t) {
+  return t.has_value() ? t->data_ptr<T>() : nullptr;
+}
+
+// ------------------------------------------------------------------ data
+void gather_normalize(const Tensor& src, const Tensor& idx, const optional<Tensor>& cursor, int64_t B,
+                      double mean, double std_, Tensor& out, const optional<Tensor>& labels_out,
+                      const optional<Tensor>& labels_src) {
+  dev(src, "src"); dev(idx, "idx"); dev(out, "out");
+  TORCH_CHECK(src.scalar_type() == at::kByte && idx.scalar_type() == at::kLong);
+  TORCH_CHECK(out.numel() == B * (src.numel() / src.size(0)), "gather_normalize: out size mismatch");
+  TORCH_CHECK(labels_out.has_value() == labels_src.has_value());
+  const c10::DeviceGuard g(src.device());
+  const int elems = (int)(src.numel() / src.size(0));
+  CHECK_HIP(csed::launch_gather_normalize(src.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(),
+                                          optpt<int64_t>(cursor), src.size(0), (int)B, elems,
+                                          (float)mean, (float)std_, out.data_ptr(), dcode(out),
+                                          optpt<int64_t>(labels_out), optpt<int64_t>(labels_src),
+                                          cur_stream(src)));
+}
+
+// ------------------------------------------------------------- optimizer
+void sgd_flat(Tensor& p, const Tensor& g, Tensor& buf, double lr, double momentum, double dampening,
+              double weight_decay, bool nesterov, double grad_scale, Tensor& step, Tensor& ticket) {
+  dev(p, "p"); dev(g, "g"); dev(buf, "buf");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && buf.scalar_type() == at::kFloat);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == buf.numel());
+  TORCH_CHECK(step.scalar_type() == at::kLong && ticket.scalar_type() == at::kInt);
+  const c10::DeviceGuard gd(p.device());
+  CHECK_HIP(csed::launch_sgd_flat(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), p.numel(),
+                                  (float)lr, (float)momentum, (float)dampening, (float)weight_decay,
+                                  nesterov ? 1 : 0, (float)grad_scale, step.data_ptr<int64_t>(),
+                                  ticket.data_ptr<int>(), cur_stream(p)));
+}
+
+// ---------------------------------------------------------------- softmax
+void log_softmax_fwd(const Tensor& x, Tensor& y) {
+  dev(x, "x"); dev(y, "y");
+  TORCH_CHECK(y.scalar_type() == at::kFloat && x.sizes() == y.sizes() && x.dim() == 2);
+  const c10::DeviceGuard gd(x.device());
+  CHECK_HIP(csed::launch_log_softmax_fwd(x.data_ptr(), dcode(x), y.data_ptr<float>(), (int)x.size(0),
+                                         (int)x.size(1), cur_stream(x)));
+}
+
+void log_softmax_bwd(const Tensor& dy, const Tensor& y, Tensor& dx) {
+  dev(dy, "dy"); dev(y, "y"); dev(dx, "dx");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat && y.dim() == 2);
+  const c10::DeviceGuard gd(y.device());
+  CHECK_HIP(csed::launch_log_softmax_bwd(dy.data_ptr<float>(), y.data_ptr<float>(), dx.data_ptr(), dcode(dx),
+                                         (int)y.size(0), (int)y.size(1), cur_stream(y)));
+}
+
+void nll_fwd(const Tensor& logp, const Tensor& target, Tensor& out, int64_t reduction,
+             const optional<Tensor>& correct) {
+  dev(logp, "logp"); dev(target, "target"); dev(out, "out");
+  TORCH_CHECK(logp.scalar_type() == at::kFloat && target.scalar_type() == at::kLong && logp.dim() == 2);
+  TORCH_CHECK(target.numel() == logp.size(0));
+  const c10::DeviceGuard gd(logp.device());
+  CHECK_HIP(csed::launch_nll_fwd(logp.data_ptr<float>(), target.data_ptr<int64_t>(), out.data_ptr<float>(),
+                                 (int)logp.size(0), (int)logp.size(1), (int)reduction, optpt<int64_t>(correct),
+                                 cur_stream(logp)));
+}
+
+void nll_bwd(const Tensor& gout, const Tensor& target, Tensor& dlogp, int64_t reduction) {
+  dev(gout, "gout"); dev(target, "target"); dev(dlogp, "dlogp");
+  const c10::DeviceGuard gd(dlogp.device());
+  CHECK_HIP(csed::launch_nll_bwd(gout.data_ptr<float>(), target.data_ptr<int64_t>(), dlogp.data_ptr<float>(),
+                                 (int)dlogp.size(0), (int)dlogp.size(1), (int)reduction, cur_stream(dlogp)));
+}
+
+// ------------------------------------------------------------------- pool
+void maxpool_relu_fwd(const Tensor& x, Tensor& out, Tensor& idx, const optional<Tensor>& chscale, int64_t k) {
+  dev(x, "x"); dev(out, "out"); dev(idx, "idx");
+  TORCH_CHECK(x.dim() == 4 && idx.scalar_type() == at::kByte && out.scalar_type() == x.scalar_type());
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(out.numel() == (int64_t)N * C * (H / k) * (W / k) && idx.numel() == out.numel());
+  const c10::DeviceGuard gd(x.device());
+  CHECK_HIP(csed::launch_maxpool_relu_fwd(x.data_ptr(), dcode(x), out.data_ptr(), idx.data_ptr<uint8_t>(),
+                                          optpt<float>(chscale), N, C, H, W, (int)k, cur_stream(x)));
+}
+
+void maxpool_relu_bwd(const Tensor& dout, const Tensor& out, const Tensor& idx, const optional<Tensor>& chscale,
+                      Tensor& dx, int64_t k) {
+  dev(dout, "dout"); dev(out, "out"); dev(idx, "idx"); dev(dx, "dx");
+  TORCH_CHECK(dx.dim() == 4);
+  const int N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  const c10::DeviceGuard gd(dx.device());
+  CHECK_HIP(csed::launch_maxpool_relu_bwd(dout.data_ptr(), dcode(dout), out.data_ptr(), dcode(out),
+                                          idx.data_ptr<uint8_t>(), optpt<float>(chscale), dx.data_ptr(), dcode(dx),
+                                          N, C, H, W, (int)k, cur_stream(dx)));
+}
+
+// ---------------------------------------------------------------- dropout
+void dropout_fwd(const Tensor& x, Tensor& y, int64_t channel_inner, double p, int64_t seed, int64_t offset,
+                 const optional<Tensor>& offset_dev) {
+  dev(x, "x"); dev(y, "y");
+  TORCH_CHECK(x.scalar_type() == y.scalar_type() && x.numel() == y.numel());
+  const c10::DeviceGuard gd(x.device());
+  const int64_t inner = channel_inner > 0 ? channel_inner : 1;
+  CHECK_HIP(csed::launch_dropout_fwd(x.data_ptr(), dcode(x), y.data_ptr(), 1, x.numel() / inner, inner,
+                                     channel_inner > 0 ? 1 : 0, (float)p, (uint64_t)seed, (uint64_t)offset,
+                                     optpt<int64_t>(offset_dev), cur_stream(x)));
+}
+
+void channel_mask(Tensor& scale, double p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev) {
+  dev(scale, "scale");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat);
+  const c10::DeviceGuard gd(scale.device());
+  CHECK_HIP(csed::launch_channel_mask(scale.data_ptr<float>(), scale.numel(), (float)p, (uint64_t)seed,
+                                      (uint64_t)offset, optpt<int64_t>(offset_dev), cur_stream(scale)));
+}
+
+void gate_bwd(const Tensor& dout, const Tensor& y, Tensor& dx, double s) {
+  dev(dout, "dout"); dev(y, "y"); dev(dx, "dx");
+  TORCH_CHECK(dout.numel() == y.numel() && dx.numel() == y.numel());
+  const c10::DeviceGuard gd(y.device());
+  CHECK_HIP(csed::launch_gate_bwd(dout.data_ptr(), dcode(dout), y.data_ptr(), dcode(y), dx.data_ptr(), dcode(dx),
+                                  y.numel(), (float)s, cur_stream(y)));
+}
+
+// ------------------------------------------------------------------- gemm
+// C = alpha * A(MxK) @ B(KxN) + beta*C (+bias, act).  A/B/C are 2-D views with
+// arbitrary strides (e.g. .t() views); strides are read from the tensors.
+void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, double alpha, double beta,
+          int64_t act, double drop_p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev,
+          const optional<Tensor>& gate, double gate_scale, int64_t mfma_dtype) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2);
+  TORCH_CHECK(A.size(1) == B.size(0) && C.size(0) == A.size(0) && C.size(1) == B.size(1), "gemm: shape mismatch");
+  if (gate.has_value()) {
+    TORCH_CHECK(gate->sizes() == A.sizes() && gate->strides() == A.strides(), "gemm: gate must match A's layout");
+  }
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == C.size(1) && bias->is_contiguous());
+  }
+  const c10::DeviceGuard gd(A.device());
+  csed::GemmArgs a{};
+  a.A = A.data_ptr(); a.a_dtype = dcode(A); a.sam = A.stride(0); a.sak = A.stride(1);
+  a.B = B.data_ptr(); a.b_dtype = dcode(B); a.sbk = B.stride(0); a.sbn = B.stride(1);
+  a.C = C.data_ptr(); a.c_dtype = dcode(C); a.scm = C.stride(0); a.scn = C.stride(1);
+  a.G = gate.has_value() ? gate->data_ptr() : nullptr;
+  a.g_dtype = gate.has_value() ? dcode(*gate) : 0;
+  a.gate_scale = (float)gate_scale;
+  a.bias = optpt<float>(bias);
+  a.M = A.size(0); a.N = B.size(1); a.K = A.size(1);
+  a.alpha = (float)alpha; a.beta = (float)beta;
+  a.act = (int)act; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset;
+  a.offset_dev = optpt<int64_t>(offset_dev);
+  a.mfma_dtype = mcode(mfma_dtype);
+  CHECK_HIP(csed::launch_gemm(a, cur_stream(A)));
+}
+
+void colsum(const Tensor& x, const optional<Tensor>& gate, double gate_scale, Tensor& out, double beta) {
+  dev(x, "x"); dev(out, "out");
+  TORCH_CHECK(x.dim() == 2 && out.scalar_type() == at::kFloat && out.numel() == x.size(1));
+  if (gate.has_value()) dev(*gate, "gate");
+  const c10::DeviceGuard gd(x.device());
+  CHECK_HIP(csed::launch_colsum(x.data_ptr(), dcode(x), optp(gate), gate.has_value() ? dcode(*gate) : 0,
+                                (float)gate_scale, out.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
+                                (float)beta, cur_stream(x)));
+}
+
+// ------------------------------------------------------------------- conv
+void conv2d_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, Tensor& y, int64_t pad,
+                const optional<Tensor>& idx, const optional<Tensor>& chscale, int64_t pool_k, int64_t mfma_dtype) {
+  dev(x, "x"); dev(w, "w"); dev(y, "y");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.scalar_type() == at::kFloat && x.size(1) == w.size(1));
+  const int N = x.size(0), IC = x.size(1), H = x.size(2), W = x.size(3);
+  const int OC = w.size(0), KH = w.size(2), KW = w.size(3);
+  const int OH = H + 2 * pad - KH + 1, OW = W + 2 * pad - KW + 1;
+  if (pool_k) {
+    TORCH_CHECK(idx.has_value() && idx->scalar_type() == at::kByte);
+    TORCH_CHECK(y.numel() == (int64_t)N * OC * (OH / pool_k) * (OW / pool_k) && idx->numel() == y.numel());
+  } else {
+    TORCH_CHECK(y.numel() == (int64_t)N * OC * OH * OW, "conv2d_fwd: y size mismatch");
+  }
+  const c10::DeviceGuard gd(x.device());
+  csed::ConvArgs a{};
+  a.x = x.data_ptr(); a.x_dtype = dcode(x); a.w = w.data_ptr<float>(); a.bias = optpt<float>(bias);
+  a.y = y.data_ptr(); a.y_dtype = dcode(y);
+  a.idx = idx.has_value() ? idx->data_ptr<uint8_t>() : nullptr;
+  a.chscale = optpt<float>(chscale); a.pool_k = (int)pool_k;
+  a.N = N; a.IC = IC; a.H = H; a.W = W; a.OC = OC; a.KH = KH; a.KW = KW; a.pad = (int)pad;
+  a.mode = 0; a.mfma_dtype = mcode(mfma_dtype);
+  CHECK_HIP(csed::launch_conv2d(a, cur_stream(x)));
+}
+
+// dX of y = conv(x, w, pad): dy [N, OC, OH, OW] -> dx [N, IC, H, W]
+void conv2d_dgrad(const Tensor& dy, const Tensor& w, Tensor& dx, int64_t pad, int64_t mfma_dtype) {
+  dev(dy, "dy"); dev(w, "w"); dev(dx, "dx");
+  TORCH_CHECK(dy.dim() == 4 && w.dim() == 4 && dx.dim() == 4 && dy.size(1) == w.size(0) && dx.size(1) == w.size(1));
+  const c10::DeviceGuard gd(dy.device());
+  csed::ConvArgs a{};
+  a.x = dy.data_ptr(); a.x_dtype = dcode(dy); a.w = w.data_ptr<float>(); a.bias = nullptr;
+  a.y = dx.data_ptr(); a.y_dtype = dcode(dx);
+  a.N = dy.size(0); a.IC = dy.size(1); a.H = dy.size(2); a.W = dy.size(3);
+  a.OC = w.size(1); a.KH = w.size(2); a.KW = w.size(3); a.pad = (int)pad;
+  TORCH_CHECK(dx.size(2) == a.H + a.KH - 1 - 2 * pad && dx.size(3) == a.W + a.KW - 1 - 2 * pad,
+              "conv2d_dgrad: dx spatial mismatch");
+  a.mode = 1; a.mfma_dtype = mcode(mfma_dtype);
+  CHECK_HIP(csed::launch_conv2d(a, cur_stream(dy)));
+}
+
+void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<Tensor>& db, Tensor& ws,
+                  int64_t pad, int64_t mfma_dtype, double beta) {
+  dev(x, "x"); dev(dy, "dy"); dev(dw, "dw"); dev(ws, "ws");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 4 && ws.scalar_type() == at::kFloat);
+  const int N = x.size(0), IC = x.size(1), H = x.size(2), W = x.size(3);
+  const int OC = dw.size(0), KH = dw.size(2), KW = dw.size(3);
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == OC);
+  TORCH_CHECK(ws.numel() >= csed::conv2d_wgrad_workspace(N, IC, KH, KW, OC), "conv2d_wgrad: workspace too small");
+  const c10::DeviceGuard gd(x.device());
+  CHECK_HIP(csed::launch_conv2d_wgrad(x.data_ptr(), dcode(x), dy.data_ptr(), dcode(dy), dw.data_ptr<float>(),
+                                      optpt<float>(db), ws.data_ptr<float>(), N, IC, H, W, OC, KH, KW, (int)pad,
+                                      mcode(mfma_dtype), (float)beta, cur_stream(x)));
+}
+
+}  // namespace
+
+TORCH_LIBRARY(csed, m) {
+  m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "
+        "Tensor(b!)? labels_out, Tensor? labels_src) -> ()");
+  m.def("sgd_flat(Tensor(a!) p, Tensor g, Tensor(b!) buf, float lr, float momentum, float dampening, "
+        "float weight_decay, bool nesterov, float grad_scale, Tensor(c!) step, Tensor(d!) ticket) -> ()");
+  m.def("log_softmax_fwd(Tensor x, Tensor(a!) y) -> ()");
+  m.def("log_softmax_bwd(Tensor dy, Tensor y, Tensor(a!) dx) -> ()");
+  m.def("nll_fwd(Tensor logp, Tensor target, Tensor(a!) out, int reduction, Tensor(b!)? correct) -> ()");
+  m.def("nll_bwd(Tensor gout, Tensor target, Tensor(a!) dlogp, int reduction) -> ()");
+  m.def("maxpool_relu_fwd(Tensor x, Tensor(a!) out, Tensor(b!) idx, Tensor? chscale, int k) -> ()");
+  m.def("maxpool_relu_bwd(Tensor dout, Tensor out, Tensor idx, Tensor? chscale, Tensor(a!) dx, int k) -> ()");
+  m.def("dropout_fwd(Tensor x, Tensor(a!) y, int channel_inner, float p, int seed, int offset, "
+        "Tensor? offset_dev) -> ()");
+  m.def("channel_mask(Tensor(a!) scale, float p, int seed, int offset, Tensor? offset_dev) -> ()");
+  m.def("gate_bwd(Tensor dout, Tensor y, Tensor(a!) dx, float s) -> ()");
+  m.def("gemm(Tensor A, Tensor B, Tensor(a!) C, Tensor? bias, float alpha, float beta, int act, float drop_p, "
+        "int seed, int offset, Tensor? offset_dev, Tensor? gate, float gate_scale, int mfma_dtype) -> ()");
+  m.def("colsum(Tensor x, Tensor? gate, float gate_scale, Tensor(a!) out, float beta) -> ()");
+  m.def("conv2d_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, int pad, Tensor(b!)? idx, Tensor? chscale, "
+        "int pool_k, int mfma_dtype) -> ()");
+  m.def("conv2d_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int pad, int mfma_dtype) -> ()");
+  m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, int pad, int mfma_dtype, "
+        "float beta) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(csed, CUDA, m) {
+  m.impl("gather_normalize", &gather_normalize);
+  m.impl("sgd_flat", &sgd_flat);
+  m.impl("log_softmax_fwd", &log_softmax_fwd);
+  m.impl("log_softmax_bwd", &log_softmax_bwd);
+  m.impl("nll_fwd", &nll_fwd);
+  m.impl("nll_bwd", &nll_bwd);
+  m.impl("maxpool_relu_fwd", &maxpool_relu_fwd);
+  m.impl("maxpool_relu_bwd", &maxpool_relu_bwd);
+  m.impl("dropout_fwd", &dropout_fwd);
+  m.impl("channel_mask", &channel_mask);
+  m.impl("gate_bwd", &gate_bwd);
+  m.impl("gemm", &gemm);
+  m.impl("colsum", &colsum);
+  m.impl("conv2d_fwd", &conv2d_fwd);
+  m.impl("conv2d_dgrad", &conv2d_dgrad);
+  m.impl("conv2d_wgrad", &conv2d_wgrad);
+}

@@ -1,0 +1,110 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels of this framework.
+//
+// Everything here is written for a 64-lane wavefront and the gfx950 MFMA
+// instruction set; there is no other target.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace csed {
+
+constexpr int kWave = 64;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+// Compute dtype tags.  The operands of every matrix-shaped op are staged as
+// 16-bit values and multiplied on `v_mfma_f32_16x16x32_{bf16,f16}` with fp32
+// accumulation.
+enum class DType : int { F32 = 0, BF16 = 1, F16 = 2, U8 = 3 };
+
+template <typename T> struct Mfma;
+template <> struct Mfma<__bf16> {
+  typedef bf16x8 frag;
+  __device__ static inline f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<_Float16> {
+  typedef f16x8 frag;
+  __device__ static inline f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <typename T> __device__ __forceinline__ float to_f32(T x) { return (float)x; }
+template <> __device__ __forceinline__ float to_f32<uint8_t>(uint8_t x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
+
+// Raw 16-bit storage <-> typed value (LDS images are kept as raw u16 so one
+// buffer can serve bf16 and fp16 instantiations).
+template <typename T> __device__ __forceinline__ unsigned short bits_of(T v) {
+  return __builtin_bit_cast(unsigned short, v);
+}
+template <typename T> __device__ __forceinline__ T of_bits(unsigned short b) {
+  return __builtin_bit_cast(T, b);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based RNG (Philox4x32-10).  Dropout masks are a pure function of
+// (seed, offset, element), so forward and backward regenerate the identical
+// mask, and a replayed HIP graph draws fresh masks by bumping `offset` on the
+// device.
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    u32x4 n;
+    n.x = hi1 ^ ctr.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ ctr.w ^ k1;
+    n.w = lo0;
+    ctr = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return ctr;
+}
+
+// Uniform in [0,1) for element `idx` of stream (seed, offset).
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t offset, uint64_t idx) {
+  u32x4 c;
+  c.x = (uint32_t)idx;
+  c.y = (uint32_t)(idx >> 32);
+  c.z = (uint32_t)offset;
+  c.w = (uint32_t)(offset >> 32);
+  u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (float)(r.x >> 8) * (1.0f / 16777216.0f);
+}
+
+// Effective Philox offset: a host offset (fixed once captured into a graph)
+// plus a device step counter in the high bits (bumped on every replay).
+__device__ __forceinline__ uint64_t rng_offset(uint64_t offset, const int64_t* offset_dev) {
+  return offset + (offset_dev ? ((uint64_t)offset_dev[0] << 20) : 0ull);
+}
+
+// Keep-decision for dropout with drop probability p.
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t offset, uint64_t idx, float p) {
+  return philox_uniform(seed, offset, idx) >= p;
+}
+
+}  // namespace csed

@@ -1,0 +1,433 @@
+// Implicit-GEMM 2-D convolution on gfx950 MFMA: forward (with an optional
+// fused 2x2 max-pool + ReLU + Dropout2d-scale epilogue), data gradient and
+// weight+bias gradient.  Parity target: nn.Conv2d(kernel_size=5) as used by
+// ref src/model.py:9-10,16-17 (stride 1, no padding), generalised to any
+// kernel size and symmetric padding.
+//
+// GEMM views (per image, NCHW):
+//   forward : Y[pix, oc]  = sum_k  X_col[pix, k] * W[oc, k]         k = (ic, kh, kw)
+//   dgrad   : dX[pix, ic] = sum_k' dY_col[pix, k'] * W'[ic, k']      k' = (oc, kh, kw), W' = flip(W)^T
+//   wgrad   : dW[oc, k]   = sum_pix dY[oc, pix] * X_col[pix, k]      (+ db as the extra column k = K)
+//
+// The input patch of a block (all channels, the rows its output band needs,
+// zero padded) and the 16-bit weight image are staged in LDS once; A/B
+// fragments are then gathered from LDS through a k -> offset table, i.e. the
+// im2col matrix is never materialised in memory.
+//
+// Pool-fused pixel order: m = 4*window + (dy*2 + dx).  With the 16x16x32
+// MFMA C layout (row = 4*(lane>>4) + reg) every lane then holds one complete
+// 2x2 window of one channel in its 4 accumulators, so the max-pool, argmax,
+// ReLU and channel scale happen in registers with no shuffles.
+#include "common.h"
+#include "dispatch.h"
+
+namespace csed {
+
+namespace {
+
+struct ConvGeo {
+  int Ci, Co;            // conv input / output channels (after dgrad re-labelling)
+  int H, W, OH, OW;      // input / output spatial
+  int KH, KW, pad;       // effective padding
+  int K, Kp;             // K = Ci*KH*KW, Kp = roundup(K, 32)
+  int Cop;               // roundup(Co, 16)
+  int TR;                // output rows per block
+  int PR, PW;            // patch rows / cols in LDS
+  int bands;             // blocks per image
+};
+
+__device__ __forceinline__ float ldf(const void* p, int dt, int64_t i) {
+  switch (dt) {
+    case kF32: return ((const float*)p)[i];
+    case kBF16: return (float)((const __bf16*)p)[i];
+    default: return (float)((const _Float16*)p)[i];
+  }
+}
+__device__ __forceinline__ void stf(void* p, int dt, int64_t i, float v) {
+  switch (dt) {
+    case kF32: ((float*)p)[i] = v; break;
+    case kBF16: ((__bf16*)p)[i] = (__bf16)v; break;
+    default: ((_Float16*)p)[i] = (_Float16)v; break;
+  }
+}
+
+// weight element of the *effective* convolution (oc, ic, kh, kw)
+__device__ __forceinline__ float weff(const float* w, int mode, int Ci, int Co, int KH, int KW, int oc,
+                                      int ic, int kh, int kw) {
+  if (mode == 0) return w[(((int64_t)oc * Ci + ic) * KH + kh) * KW + kw];
+  // dgrad: forward weight is [Ci(eff) = fwd OC][Co(eff) = fwd IC][KH][KW], flipped
+  return w[(((int64_t)ic * Co + oc) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  typedef typename Mfma<T>::frag frag;
+  const int LDW = g.Kp + 8;                         // 16-B aligned row pad
+  unsigned short* Ws = (unsigned short*)smem;       // [Cop][LDW]
+  int* koff = (int*)(Ws + g.Cop * LDW);             // [Kp]
+  unsigned short* patch = (unsigned short*)(koff + g.Kp);  // [Ci][PR][PW]
+
+  const int n = blockIdx.x / g.bands, band = blockIdx.x % g.bands;
+  const int oh0 = band * g.TR;
+  const int rows = min(g.TR, g.OH - oh0);
+  const int npix = rows * g.OW;
+  const int tid = threadIdx.x;
+
+  // ---- stage weights (fp32 -> 16 bit) and the k -> patch offset table
+  for (int i = tid; i < g.Cop * g.Kp; i += 256) {
+    const int oc = i / g.Kp, k = i % g.Kp;
+    float v = 0.f;
+    if (oc < g.Co && k < g.K) {
+      const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
+      v = weff(a.w, a.mode, g.Ci, g.Co, g.KH, g.KW, oc, ic, r / g.KW, r % g.KW);
+    }
+    Ws[oc * LDW + k] = bits_of<T>((T)v);
+  }
+  for (int k = tid; k < g.Kp; k += 256) {
+    int o = 0;
+    if (k < g.K) {
+      const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
+      o = (ic * g.PR + r / g.KW) * g.PW + r % g.KW;
+    }
+    koff[k] = o;
+  }
+  // ---- stage the zero-padded input patch
+  const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
+  const int pe = g.Ci * g.PR * g.PW;
+  for (int i = tid; i < pe; i += 256) {
+    const int pc = i % g.PW, pr = (i / g.PW) % g.PR, ic = i / (g.PW * g.PR);
+    const int ih = oh0 - g.pad + pr, iw = pc - g.pad;
+    float v = 0.f;
+    if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) v = ldf(a.x, a.x_dtype, xbase + ((int64_t)ic * g.H + ih) * g.W + iw);
+    patch[i] = bits_of<T>((T)v);
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int mtiles = (npix + 15) >> 4;
+  const int pooled = a.pool_k == 2;
+  const int PWb = g.OW >> 1;
+  const int NT = g.Cop >> 4;
+  for (int mt = wave; mt < mtiles; mt += 4) {
+    // pixel owned by this lane as an A row
+    const int m = mt * 16 + (lane & 15);
+    int oh, ow;
+    if (pooled) {
+      const int p = m >> 2, q = m & 3;
+      oh = 2 * (p / PWb) + (q >> 1);
+      ow = 2 * (p % PWb) + (q & 1);
+    } else {
+      oh = m / g.OW;
+      ow = m % g.OW;
+    }
+    const bool valid = m < npix;
+    const int pb = valid ? oh * g.PW + ow : 0;     // oh is band-relative
+    for (int nc = 0; nc < NT; nc += 4) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+        const int kb = k0 + 8 * (lane >> 4);
+        const int4 o0 = *reinterpret_cast<const int4*>(koff + kb);
+        const int4 o1 = *reinterpret_cast<const int4*>(koff + kb + 4);
+        const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+        frag fa;
+        u16x8 raw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[j] = valid ? patch[pb + oo[j]] : (unsigned short)0;
+        fa = __builtin_bit_cast(frag, raw);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (nc + j < NT) {
+            const int oc = (nc + j) * 16 + (lane & 15);
+            const frag fb = *reinterpret_cast<const frag*>(Ws + oc * LDW + kb);
+            acc[j] = Mfma<T>::mma(fa, fb, acc[j]);
+          }
+        }
+      }
+      // ---- epilogue
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (nc + j >= NT) continue;
+        const int oc = (nc + j) * 16 + (lane & 15);
+        if (oc >= g.Co) continue;
+        const float b = a.bias ? a.bias[oc] : 0.f;
+        if (pooled) {
+          const int wbase = mt * 16 + 4 * (lane >> 4);  // first pixel of this lane's window
+          if (wbase >= npix) continue;
+          float best = acc[j][0];
+          int bi = 0;
+#pragma unroll
+          for (int r = 1; r < 4; ++r)
+            if (acc[j][r] > best) { best = acc[j][r]; bi = r; }
+          const int p = wbase >> 2;
+          const int ph = (oh0 >> 1) + p / PWb, pw = p % PWb;
+          const int PH = g.OH >> 1;
+          const float sc = a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
+          const float v = fmaxf(best + b, 0.f) * sc;
+          const int64_t o = (((int64_t)n * g.Co + oc) * PH + ph) * PWb + pw;
+          stf(a.y, a.y_dtype, o, v);
+          a.idx[o] = (uint8_t)bi;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int mm = mt * 16 + 4 * (lane >> 4) + r;
+            if (mm >= npix) continue;
+            const int ohh = oh0 + mm / g.OW, oww = mm % g.OW;
+            stf(a.y, a.y_dtype, (((int64_t)n * g.Co + oc) * g.OH + ohh) * g.OW + oww, acc[j][r] + b);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- wgrad ----
+struct WgradGeo {
+  int Ci, Co, H, W, OH, OW, KH, KW, pad;
+  int K, Kc;       // K = Ci*KH*KW ; Kc = roundup(K+1, 16) columns (last real = db)
+  int Cop;         // roundup(Co, 16)
+  int PR, PW;      // patch dims (H+2p, W+2p)
+  int npix, npp;   // OH*OW, roundup(npix, 32)
+  int per_block;   // images per block
+  int nblocks;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict__ x, int xdt,
+                                                         const void* __restrict__ dy, int dydt, int N,
+                                                         float* __restrict__ slab, WgradGeo g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  typedef typename Mfma<T>::frag frag;
+  const int LDY = g.npp + 8;
+  unsigned short* dys = (unsigned short*)smem;              // [Cop][LDY]
+  int* koff = (int*)(dys + g.Cop * LDY);                    // [Kc]
+  int* pbase = koff + g.Kc;                                 // [npp]
+  unsigned short* patch = (unsigned short*)(pbase + g.npp); // [Ci][PR][PW] (+1 slot holding 1.0)
+  const int pe = g.Ci * g.PR * g.PW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  for (int k = tid; k < g.Kc; k += 256) {
+    int o = pe;  // the constant-one slot (db column) / zero-weight padding
+    if (k < g.K) {
+      const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
+      o = (ic * g.PR + r / g.KW) * g.PW + r % g.KW;
+    }
+    koff[k] = o;
+  }
+  for (int p = tid; p < g.npp; p += 256) pbase[p] = p < g.npix ? (p / g.OW) * g.PW + p % g.OW : 0;
+
+  const int MT = g.Cop >> 4, NT = g.Kc >> 4;
+  const int psplit = NT >= 4 ? 1 : 4 / NT;
+  const int my_nt0 = NT >= 4 ? wave : wave / psplit;
+  const int my_s = NT >= 4 ? 0 : wave % psplit;
+  const int nt_step = NT >= 4 ? 4 : 1 << 30;
+  constexpr int MAXMT = 4, MAXNTW = 8;
+  f32x4 acc[MAXMT][MAXNTW];
+#pragma unroll
+  for (int i = 0; i < MAXMT; ++i)
+#pragma unroll
+    for (int j = 0; j < MAXNTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int n_begin = blockIdx.x * g.per_block;
+  const int n_end = min(N, n_begin + g.per_block);
+  for (int n = n_begin; n < n_end; ++n) {
+    __syncthreads();  // previous image's LDS reads are done
+    const int64_t xb = (int64_t)n * g.Ci * g.H * g.W;
+    for (int i = tid; i < pe + 1; i += 256) {
+      float v = 1.f;  // slot pe holds 1.0 -> db column
+      if (i < pe) {
+        const int pc = i % g.PW, pr = (i / g.PW) % g.PR, ic = i / (g.PW * g.PR);
+        const int ih = pr - g.pad, iw = pc - g.pad;
+        v = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? ldf(x, xdt, xb + ((int64_t)ic * g.H + ih) * g.W + iw) : 0.f;
+      }
+      patch[i] = bits_of<T>((T)v);
+    }
+    const int64_t yb = (int64_t)n * g.Co * g.npix;
+    for (int i = tid; i < g.Cop * g.npp; i += 256) {
+      const int oc = i / g.npp, p = i % g.npp;
+      const float v = (oc < g.Co && p < g.npix) ? ldf(dy, dydt, yb + (int64_t)oc * g.npix + p) : 0.f;
+      dys[oc * LDY + p] = bits_of<T>((T)v);
+    }
+    __syncthreads();
+    if (my_nt0 >= NT) continue;
+    for (int ps = my_s; ps * 32 < g.npp; ps += psplit) {
+      const int p0 = ps * 32 + 8 * (lane >> 4);
+      const int4 b0 = *reinterpret_cast<const int4*>(pbase + p0);
+      const int4 b1 = *reinterpret_cast<const int4*>(pbase + p0 + 4);
+      const int bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      frag fa[MAXMT];
+#pragma unroll
+      for (int mt = 0; mt < MAXMT; ++mt)
+        if (mt < MT) fa[mt] = *reinterpret_cast<const frag*>(dys + (mt * 16 + (lane & 15)) * LDY + p0);
+#pragma unroll
+      for (int jj = 0; jj < MAXNTW; ++jj) {
+        const int nt = my_nt0 + jj * nt_step;
+        if (jj > 0 && NT < 4) break;
+        if (nt >= NT) break;
+        const int ko = koff[nt * 16 + (lane & 15)];
+        u16x8 raw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[j] = patch[bb[j] * (ko != pe) + ko];
+        const frag fb = __builtin_bit_cast(frag, raw);
+#pragma unroll
+        for (int mt = 0; mt < MAXMT; ++mt)
+          if (mt < MT) acc[mt][jj] = Mfma<T>::mma(fa[mt], fb, acc[mt][jj]);
+      }
+    }
+  }
+
+  // ---- write this block's partial [Co][K+1] slab (fixed-order combine of split waves)
+  float* out = slab + (int64_t)blockIdx.x * g.Co * (g.K + 1);
+  if (psplit == 1) {
+#pragma unroll
+    for (int jj = 0; jj < MAXNTW; ++jj) {
+      const int nt = my_nt0 + jj * 4;
+      if (nt >= NT) break;
+      const int col = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int mt = 0; mt < MAXMT; ++mt) {
+        if (mt >= MT) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int oc = mt * 16 + 4 * (lane >> 4) + r;
+          if (oc < g.Co && col <= g.K) out[(int64_t)oc * (g.K + 1) + col] = acc[mt][jj][r];
+        }
+      }
+    }
+  } else {
+    __syncthreads();
+    float* red = (float*)smem;  // [4 waves][MAXMT*16][16]
+    if (my_nt0 < NT) {
+#pragma unroll
+      for (int mt = 0; mt < MAXMT; ++mt) {
+        if (mt >= MT) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(wave * MAXMT * 16 + mt * 16 + 4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[mt][0][r];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < g.Co * NT * 16; i += 256) {
+      const int oc = i / (NT * 16), col = i % (NT * 16);
+      if (col > g.K) continue;
+      const int nt = col >> 4;
+      float s = 0.f;
+      for (int q = 0; q < psplit; ++q) s += red[((nt * psplit + q) * MAXMT * 16 + oc) * 16 + (col & 15)];
+      out[(int64_t)oc * (g.K + 1) + col] = s;
+    }
+  }
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int nblocks, int Co, int K,
+                                    float* __restrict__ dw, float* __restrict__ db, float beta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int L = Co * (K + 1);
+  if (i >= L) return;
+  float s = 0.f;
+  for (int b = 0; b < nblocks; ++b) s += slab[(int64_t)b * L + i];
+  const int oc = i / (K + 1), col = i % (K + 1);
+  if (col < K) {
+    float* d = dw + (int64_t)oc * K + col;
+    *d = beta != 0.f ? fmaf(beta, *d, s) : s;
+  } else if (db) {
+    db[oc] = beta != 0.f ? fmaf(beta, db[oc], s) : s;
+  }
+}
+
+inline int rup(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace
+
+hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
+  ConvGeo g;
+  g.KH = a.KH; g.KW = a.KW;
+  g.H = a.H; g.W = a.W;
+  if (a.mode == 0) {
+    g.Ci = a.IC; g.Co = a.OC; g.pad = a.pad;
+  } else {
+    g.Ci = a.IC; g.Co = a.OC; g.pad = a.KH - 1 - a.pad;
+    if (a.KH != a.KW || g.pad < 0) return hipErrorInvalidValue;
+  }
+  g.OH = g.H + 2 * g.pad - g.KH + 1;
+  g.OW = g.W + 2 * g.pad - g.KW + 1;
+  if (g.OH <= 0 || g.OW <= 0 || a.N <= 0) return hipSuccess;
+  if (a.pool_k != 0 && (a.pool_k != 2 || a.mode != 0 || (g.OH & 1) || (g.OW & 1))) return hipErrorInvalidValue;
+  g.K = g.Ci * g.KH * g.KW;
+  g.Kp = rup(g.K, 32);
+  g.Cop = rup(g.Co, 16);
+  g.PW = g.W + 2 * g.pad;
+  // ~128 output pixels per block, LDS-limited
+  int tr = std::max(1, std::min(g.OH, (128 + g.OW - 1) / g.OW));
+  int bands = (g.OH + tr - 1) / tr;
+  tr = (g.OH + bands - 1) / bands;
+  if (a.pool_k == 2 && (tr & 1)) tr += 1;
+  auto lds_bytes = [&](int trr) {
+    const int pr = trr + g.KH - 1;
+    return (size_t)g.Cop * (g.Kp + 8) * 2 + (size_t)g.Kp * 4 + (size_t)g.Ci * pr * g.PW * 2 + 16;
+  };
+  while (tr > (a.pool_k == 2 ? 2 : 1) && lds_bytes(tr) > 96 * 1024) tr -= (a.pool_k == 2 ? 2 : 1);
+  if (lds_bytes(tr) > 160 * 1024) return hipErrorInvalidConfiguration;
+  g.TR = tr;
+  g.PR = tr + g.KH - 1;
+  g.bands = (g.OH + tr - 1) / tr;
+  const size_t lds = lds_bytes(tr);
+  dim3 grid(a.N * g.bands);
+  CSED_DISPATCH_MFMA(a.mfma_dtype, {
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_fwd_kernel<scalar_t>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(conv_fwd_kernel<scalar_t>, grid, dim3(256), lds, s, a, g);
+  });
+  return hipGetLastError();
+}
+
+static WgradGeo wgrad_geo(int N, int IC, int H, int W, int OC, int KH, int KW, int pad) {
+  WgradGeo g;
+  g.Ci = IC; g.Co = OC; g.H = H; g.W = W; g.KH = KH; g.KW = KW; g.pad = pad;
+  g.OH = H + 2 * pad - KH + 1;
+  g.OW = W + 2 * pad - KW + 1;
+  g.K = IC * KH * KW;
+  g.Kc = rup(g.K + 1, 16);
+  g.Cop = rup(OC, 16);
+  g.PR = H + 2 * pad;
+  g.PW = W + 2 * pad;
+  g.npix = g.OH * g.OW;
+  g.npp = rup(std::max(g.npix, 1), 32);
+  g.nblocks = std::max(1, std::min(N, 256));
+  g.per_block = (N + g.nblocks - 1) / g.nblocks;
+  g.nblocks = (N + g.per_block - 1) / g.per_block;
+  return g;
+}
+
+int64_t conv2d_wgrad_workspace(int N, int IC, int KH, int KW, int OC) {
+  const int nb = std::max(1, std::min(N, 256));
+  return (int64_t)nb * OC * (IC * KH * KW + 1);
+}
+
+hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw,
+                               float* db, float* ws, int N, int IC, int H, int W, int OC, int KH,
+                               int KW, int pad, int mfma_dtype, float beta, hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  WgradGeo g = wgrad_geo(N, IC, H, W, OC, KH, KW, pad);
+  if (g.OH <= 0 || g.OW <= 0) return hipErrorInvalidValue;
+  if (g.Cop > 64 || (g.Kc / 16) > 32) return hipErrorInvalidConfiguration;  // accumulator budget
+  const size_t lds_main = (size_t)g.Cop * (g.npp + 8) * 2 + (size_t)g.Kc * 4 + (size_t)g.npp * 4 +
+                          ((size_t)g.Ci * g.PR * g.PW + 1) * 2 + 16;
+  const size_t lds_red = (size_t)4 * 4 * 16 * 16 * 4;
+  const size_t lds = std::max(lds_main, lds_red);
+  if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+  CSED_DISPATCH_MFMA(mfma_dtype, {
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_wgrad_kernel<scalar_t>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(conv_wgrad_kernel<scalar_t>, dim3(g.nblocks), dim3(256), lds, s, x, x_dtype, dy,
+                       dy_dtype, N, ws, g);
+  });
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int L = OC * (g.K + 1);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 256)), dim3(256), 0, s, ws, g.nblocks, OC, g.K, dw,
+                     db, beta);
+  return hipGetLastError();
+}
+
+}  // namespace csed

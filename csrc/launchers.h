@@ -1,0 +1,171 @@
+// Plain-pointer launchers for every kernel in csrc/kernels/*.hip.
+//
+// The kernel translation units include no torch header (fast builds); the
+// ATen-facing checks and op registration live in bindings.cpp.  Every
+// launcher enqueues on the given stream, never synchronises and never
+// allocates, so all of them are legal inside HIP-graph capture.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace csed {
+
+// dtype codes shared with Python (see ops/_dtypes.py)
+enum : int { kF32 = 0, kBF16 = 1, kF16 = 2, kU8 = 3 };
+
+// ---------------------------------------------------------------- data ----
+// out[b, :] = (src[idx[b], :] / 255 - mean) / std, converted to out_dtype.
+// When `cursor` is non-null the batch indices are idx[cursor[0]*B + b]
+// (device-side cursor for graph replay); `advance` bumps the cursor once
+// the last block is done.
+hipError_t launch_gather_normalize(const uint8_t* src, const int64_t* idx, const int64_t* cursor,
+                                   int64_t n_src, int B, int elems, float mean, float std_,
+                                   void* out, int out_dtype, int64_t* labels_out,
+                                   const int64_t* labels_src, hipStream_t s);
+
+// ----------------------------------------------------------- optimizer ----
+// SGD with momentum over a flat fp32 buffer (torch.optim.SGD semantics).
+// step[0] == 0 means "momentum buffer not yet initialised" (buf = g).
+// Step counter is bumped by the last block to finish.
+hipError_t launch_sgd_flat(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
+                           float dampening, float weight_decay, int nesterov, float grad_scale,
+                           int64_t* step, int* ticket, hipStream_t s);
+
+// ------------------------------------------------------------- softmax ----
+// log_softmax over the last dim of x[rows, C] (any float dtype in, fp32 out).
+hipError_t launch_log_softmax_fwd(const void* x, int x_dtype, float* y, int rows, int C, hipStream_t s);
+// dx = dy - exp(y) * sum(dy)
+hipError_t launch_log_softmax_bwd(const float* dy, const float* y, void* dx, int dx_dtype, int rows,
+                                  int C, hipStream_t s);
+// NLL on log-probs.  reduction: 0 none, 1 mean, 2 sum.  out: [rows] or [1].
+// Also writes `correct` (argmax == target count) if non-null.
+hipError_t launch_nll_fwd(const float* logp, const int64_t* target, float* out, int rows, int C,
+                          int reduction, int64_t* correct, hipStream_t s);
+hipError_t launch_nll_bwd(const float* gout, const int64_t* target, float* dlogp, int rows, int C,
+                          int reduction, hipStream_t s);
+
+// ----------------------------------------------------------------- pool ----
+// 2-D max pool (kernel == stride == k) fused with ReLU and an optional
+// per-(n,c) scale (Dropout2d mask).  out = relu(max(window)) * scale[n,c].
+// idx (uint8) = argmax position inside the window.
+hipError_t launch_maxpool_relu_fwd(const void* x, int dtype, void* out, uint8_t* idx,
+                                   const float* chscale, int N, int C, int H, int W, int k,
+                                   hipStream_t s);
+// dx[window pos idx] = dout * (out > 0) * scale[n,c]; other positions 0.
+hipError_t launch_maxpool_relu_bwd(const void* dout, int dout_dtype, const void* out, int out_dtype,
+                                   const uint8_t* idx, const float* chscale, void* dx, int dx_dtype,
+                                   int N, int C, int H, int W, int k, hipStream_t s);
+
+// -------------------------------------------------------------- dropout ----
+// Elementwise: y = x * keep / (1-p); channel mode: one draw per (n,c) of an
+// [N, C, S] tensor.  `offset_dev` (optional) is a device counter added to
+// `offset` so graph replays draw new masks.
+hipError_t launch_dropout_fwd(const void* x, int dtype, void* y, int64_t rows, int64_t C,
+                              int64_t inner, int channel_mode, float p, uint64_t seed,
+                              uint64_t offset, const int64_t* offset_dev, hipStream_t s);
+// Per-(n,c) Dropout2d scale vector: scale[i] = keep ? 1/(1-p) : 0.
+hipError_t launch_channel_mask(float* scale, int64_t n, float p, uint64_t seed, uint64_t offset,
+                               const int64_t* offset_dev, hipStream_t s);
+// dx = dout * (y > 0) * s   (backward of relu∘dropout recovered from the output)
+hipError_t launch_gate_bwd(const void* dout, int dout_dtype, const void* y, int y_dtype, void* dx,
+                           int dx_dtype, int64_t n, float s, hipStream_t st);
+
+// ----------------------------------------------------------------- gemm ----
+// C[m,n] = alpha * sum_k A(m,k) B(k,n) + beta*C + bias[n]  (then relu /
+// relu+dropout).  A(m,k) = A[m*sam + k*sak] (optionally gated: A *= (G>0)*gs
+// with G sharing A's strides).  Operands are staged to bf16/f16 for MFMA.
+struct GemmArgs {
+  const void* A; int a_dtype; int64_t sam, sak;
+  const void* B; int b_dtype; int64_t sbk, sbn;
+  void* C; int c_dtype; int64_t scm, scn;
+  const void* G; int g_dtype; float gate_scale;  // optional A gate
+  const float* bias;                              // [N] or null
+  int M, N, K;
+  float alpha, beta;
+  int act;            // 0 none, 1 relu, 2 relu + dropout
+  float drop_p; uint64_t seed, offset; const int64_t* offset_dev;
+  int mfma_dtype;     // kBF16 or kF16
+};
+hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
+
+// Column sums of a (gated) [rows, cols] matrix -> fp32 out[cols] (fixed order).
+hipError_t launch_colsum(const void* x, int x_dtype, const void* gate, int g_dtype, float gate_scale,
+                         float* out, int rows, int cols, float beta, hipStream_t s);
+
+// ----------------------------------------------------------------- conv ----
+// Implicit-GEMM 2-D convolution, stride 1, symmetric zero padding, NCHW.
+// mode 0: y = conv(x, w) + b             (w: [OC, IC, KH, KW])
+// mode 1: dgrad: x is dY [N, OCw, ...], w is the forward weight [OCw, ICw, KH, KW]
+//         and the output is dX [N, ICw, ...] (flipped/transposed weights,
+//         padding KH-1-p), no bias.
+// pool_k > 0 fuses maxpool(k)+relu(+chscale) into the epilogue (mode 0 only):
+//   y becomes the pooled output and idx the argmax within each window.
+struct ConvArgs {
+  const void* x; int x_dtype;
+  const float* w; const float* bias;
+  void* y; int y_dtype;
+  uint8_t* idx; const float* chscale; int pool_k;
+  int N, IC, H, W, OC, KH, KW, pad;
+  int mode;
+  int mfma_dtype;
+};
+hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s);
+// Weight gradient: dW[OC, IC*KH*KW] (fp32) and db[OC] (fp32, optional) of a
+// stride-1 conv; dY may be given gated (dY *= (G > 0) * gs is NOT applied
+// here -- pass the already-unpooled gradient).  `ws` is a workspace of at
+// least conv2d_wgrad_workspace() floats.
+int64_t conv2d_wgrad_workspace(int N, int IC, int KH, int KW, int OC);
+hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw,
+                               float* db, float* ws, int N, int IC, int H, int W, int OC, int KH,
+                               int KW, int pad, int mfma_dtype, float beta, hipStream_t s);
+
+// --------------------------------------------------------------- lenet ----
+// Fused LeNet (src/model.py Net) training / evaluation kernels.  See
+// kernels/lenet_fused.hip for the layout contract.
+struct LenetTrainArgs {
+  const uint8_t* images;     // [n_src, 784] raw MNIST pixels
+  const int64_t* labels;     // [n_src]
+  const int64_t* perm;       // sample order for the epoch (global indices)
+  const int64_t* cursor;     // device step counter (batch index into perm)
+  int64_t perm_len;          // valid entries in perm
+  int B;                     // per-rank batch for this step
+  int rank_stride;           // unused (sharding is folded into perm)
+  const uint16_t* wimg;      // packed 16-bit weight images (see layout)
+  const float* params;       // flat fp32 master params [21840]
+  float* slab;               // [grid, 21840] per-workgroup partial grads
+  float* loss_acc;           // [2]: loss sum, correct count (accumulated)
+  float grad_scale;          // 1 / (global batch)
+  float mean, std_;
+  float drop_p;
+  uint64_t seed;
+  const int64_t* rng_offset; // device counter
+  int grid;
+  int mfma_dtype;
+};
+hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s);
+int64_t lenet_wimg_elems();
+int64_t lenet_param_count();
+// Fused grad reduce + SGD + weight-image refresh.  When `grad_out` is
+// non-null and `apply_sgd` is 0 the reduced gradient is written there (for
+// an all-reduce) and nothing else happens; with apply_sgd=1 and `grad_in`
+// non-null, the SGD consumes grad_in instead of the slab.
+struct LenetUpdateArgs {
+  const float* slab; int grid;
+  const float* grad_in;
+  float* grad_out;
+  float* params; float* momentum; uint16_t* wimg;
+  float lr, mom, dampening, weight_decay; int nesterov;
+  int64_t* step; int* ticket;
+  int64_t* cursor; int64_t* rng_offset;   // bumped by the last block when apply_sgd
+  int apply_sgd;
+  int mfma_dtype;
+};
+hipError_t launch_lenet_update(const LenetUpdateArgs& a, hipStream_t s);
+// Pack fp32 params into the 16-bit weight images (used at init / after a load).
+hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype, hipStream_t s);
+// Fused eval: forward over n images, accumulates [loss_sum, correct] in out.
+hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,
+                             int64_t n, const uint16_t* wimg, const float* params, float mean,
+                             float std_, float* out, float* logp_out, int mfma_dtype, hipStream_t s);
+
+}  // namespace csed

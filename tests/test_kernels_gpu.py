@@ -1,0 +1,246 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to the compute dtype (bf16/fp16) before the fp32 reference
+runs, so the comparison isolates the kernel (accumulation order and output
+rounding), not the input quantisation.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from csed_514_project_distributed_training_using_pytorch_amd import ops
+from csed_514_project_distributed_training_using_pytorch_amd.ops import _native
+from csed_514_project_distributed_training_using_pytorch_amd.ops.rng import philox_uniform_reference
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_loaded():
+    _native.require()
+    yield
+
+
+def q(t, dt=torch.bfloat16):
+    return t.to(dt).float()
+
+
+def close(a, b, rel=2e-2, name=""):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    scale = max(b.abs().max().item(), 1e-6)
+    err = (a - b).abs().max().item()
+    assert err <= rel * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(4, 1, 28, 28, 10, 5, 0), (3, 10, 12, 12, 20, 5, 0), (2, 3, 9, 11, 7, 3, 1),
+                                   (2, 16, 14, 14, 33, 3, 1), (1, 2, 6, 6, 4, 1, 0)])
+def test_conv2d_fwd_bwd(dt, shape):
+    ops.set_compute_dtype(dt)
+    try:
+        N, C, H, W, OC, K, pad = shape
+        torch.manual_seed(0)
+        x = q(torch.randn(N, C, H, W), dt)
+        w = q(torch.randn(OC, C, K, K) * 0.2, dt)
+        b = torch.randn(OC)
+        xg = x.to(DEV, dt).requires_grad_(True)
+        wg = w.to(DEV).requires_grad_(True)
+        bg = b.to(DEV).requires_grad_(True)
+        y = ops.conv2d(xg, wg, bg, padding=pad)
+        xr = x.clone().requires_grad_(True)
+        wr = w.clone().requires_grad_(True)
+        br = b.clone().requires_grad_(True)
+        yr = F.conv2d(xr, wr, br, padding=pad)
+        close(y, yr, name="conv fwd")
+        gy = q(torch.randn(yr.shape), dt)
+        y.backward(gy.to(DEV, dt))
+        yr.backward(gy)
+        close(xg.grad, xr.grad, name="conv dgrad")
+        close(wg.grad, wr.grad, name="conv wgrad")
+        close(bg.grad, br.grad, name="conv bgrad")
+    finally:
+        ops.set_compute_dtype(torch.bfloat16)
+
+
+@pytest.mark.parametrize("shape", [(5, 1, 28, 28, 10), (7, 10, 12, 12, 20), (3, 4, 10, 14, 16)])
+@pytest.mark.parametrize("with_scale", [False, True])
+def test_conv2d_pool_relu(shape, with_scale):
+    N, C, H, W, OC = shape
+    torch.manual_seed(1)
+    x = q(torch.randn(N, C, H, W))
+    w = q(torch.randn(OC, C, 5, 5) * 0.2)
+    b = torch.randn(OC) * 0.1
+    scale = None
+    if with_scale:
+        scale = (torch.rand(N * OC) > 0.5).float() * 2.0
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True)
+    y = ops.conv2d_pool_relu(xg, wg, bg, scale.to(DEV) if scale is not None else None)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    c = F.conv2d(xr, wr, br)
+    if scale is not None:
+        c = c * scale.view(N, OC, 1, 1)
+    yr = F.relu(F.max_pool2d(c, 2))
+    close(y, yr, name="conv_pool fwd")
+    gy = q(torch.randn(yr.shape))
+    y.backward(gy.to(DEV, torch.bfloat16))
+    yr.backward(gy)
+    close(xg.grad, xr.grad, rel=3e-2, name="conv_pool dgrad")
+    close(wg.grad, wr.grad, rel=3e-2, name="conv_pool wgrad")
+    close(bg.grad, br.grad, rel=3e-2, name="conv_pool bgrad")
+
+
+def test_maxpool_relu():
+    torch.manual_seed(2)
+    x = q(torch.randn(3, 5, 8, 12))
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    y = ops.max_pool2d_relu(xg, 2)
+    xr = x.clone().requires_grad_(True)
+    yr = F.relu(F.max_pool2d(xr, 2))
+    close(y, yr, rel=1e-6, name="pool fwd")
+    gy = q(torch.randn(yr.shape))
+    y.backward(gy.to(DEV, torch.bfloat16))
+    yr.backward(gy)
+    close(xg.grad, xr.grad, rel=1e-6, name="pool bwd")
+
+
+@pytest.mark.parametrize("act", ["none", "relu"])
+@pytest.mark.parametrize("mnk", [(64, 50, 320), (8, 10, 50), (1000, 10, 50), (37, 70, 45)])
+def test_linear(act, mnk):
+    M, N, K = mnk
+    torch.manual_seed(3)
+    x = q(torch.randn(M, K))
+    w = q(torch.randn(N, K) * 0.1)
+    b = torch.randn(N)
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    wg, bg = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    y = ops.linear(xg, wg, bg, act=act, out_dtype=torch.float32)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = F.linear(xr, wr, br)
+    if act == "relu":
+        yr = F.relu(yr)
+    close(y, yr, rel=1e-2, name="linear fwd")
+    gy = torch.randn(yr.shape)
+    y.backward(gy.to(DEV))
+    yr.backward(gy)
+    close(xg.grad, xr.grad, rel=2e-2, name="linear dx")
+    close(wg.grad, wr.grad, rel=2e-2, name="linear dw")
+    close(bg.grad, br.grad, rel=2e-2, name="linear db")
+
+
+def test_linear_relu_dropout_mask_matches_philox():
+    M, N, K = 64, 50, 320
+    torch.manual_seed(4)
+    x = q(torch.randn(M, K))
+    w = q(torch.randn(N, K) * 0.1)
+    b = torch.randn(N)
+    ops.rng.manual_seed(1234)
+    seed = ops.rng.default_state.seed
+    y = ops.linear(x.to(DEV, torch.bfloat16), w.to(DEV), b.to(DEV), act="relu_dropout", p=0.5,
+                   out_dtype=torch.float32)
+    u = philox_uniform_reference(seed, 0, np.arange(M * N)).reshape(M, N)
+    keep = torch.from_numpy(u >= 0.5)
+    yr = F.relu(F.linear(x, w, b)) * keep * 2.0
+    close(y, yr, rel=1e-2, name="relu_dropout fwd")
+    frac = keep.float().mean().item()
+    assert 0.4 < frac < 0.6
+
+
+def test_dropout_and_dropout2d():
+    x = torch.randn(16, 20, 8, 8, device=DEV, dtype=torch.bfloat16).requires_grad_(True)
+    y = ops.dropout2d(x, 0.5, True)
+    z = (y.float() / x.float()).detach()
+    per_ch = z.view(16, 20, 64)
+    # whole channels are either 0 or 2
+    assert torch.all((per_ch == 0).all(-1) | (per_ch == 2).all(-1))
+    y.backward(torch.ones_like(y))
+    assert torch.equal((x.grad.float() != 0), (y.detach().float() != 0))
+    x2 = torch.randn(4096, device=DEV).requires_grad_(True)
+    y2 = ops.dropout(x2, 0.3, True)
+    kept = (y2 != 0).float().mean().item()
+    assert 0.65 < kept < 0.75
+    torch.testing.assert_close(y2[y2 != 0], x2[y2 != 0] / 0.7)
+
+
+def test_log_softmax_nll():
+    torch.manual_seed(5)
+    x = torch.randn(100, 10)
+    t = torch.randint(0, 10, (100,))
+    for red in ("mean", "sum", "none"):
+        xg = x.to(DEV).requires_grad_(True)
+        xr = x.clone().requires_grad_(True)
+        lg = ops.nll_loss(ops.log_softmax(xg), t.to(DEV), reduction=red)
+        lr_ = F.nll_loss(F.log_softmax(xr, 1), t, reduction=red)
+        torch.testing.assert_close(lg.cpu(), lr_, rtol=1e-5, atol=1e-5)
+        g = torch.randn(lr_.shape)
+        lg.backward(g.to(DEV))
+        lr_.backward(g)
+        torch.testing.assert_close(xg.grad.cpu(), xr.grad, rtol=1e-5, atol=1e-5)
+    # CrossEntropyLoss on log-probs == nll (ref src/train_dist.py:67)
+    lp = F.log_softmax(x, 1)
+    ce = ops.cross_entropy(lp.to(DEV), t.to(DEV))
+    torch.testing.assert_close(ce.cpu(), F.nll_loss(lp, t), rtol=1e-5, atol=1e-5)
+
+
+def test_sgd_flat_matches_torch():
+    torch.manual_seed(6)
+    n = 21840
+    p0 = torch.randn(n)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.SGD([ref], lr=0.02, momentum=0.5)
+    p = p0.clone().to(DEV)
+    buf = torch.zeros(n, device=DEV)
+    step = torch.zeros(1, dtype=torch.long, device=DEV)
+    ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(3):
+        g = torch.randn(n)
+        ref.grad = g.clone()
+        opt.step()
+        torch.ops.csed.sgd_flat(p, g.to(DEV), buf, 0.02, 0.5, 0.0, 0.0, False, 1.0, step, ticket)
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-6)
+    assert step.item() == 3 and ticket.item() == 0
+
+
+def test_gather_normalize():
+    src = torch.randint(0, 256, (100, 28, 28), dtype=torch.uint8)
+    labels = torch.randint(0, 10, (100,))
+    idx = torch.randperm(100)[:32]
+    out = torch.empty(32, 1, 28, 28, device=DEV, dtype=torch.float32)
+    lab = torch.empty(32, dtype=torch.long, device=DEV)
+    torch.ops.csed.gather_normalize(src.to(DEV), idx.to(DEV), None, 32, 0.1307, 0.3081, out, lab,
+                                    labels.to(DEV))
+    ref = (src[idx].float() / 255.0 - 0.1307) / 0.3081
+    torch.testing.assert_close(out.cpu().view(32, 28, 28), ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(lab.cpu(), labels[idx])
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.bfloat16, 4e-2), (torch.float16, 8e-3)])
+def test_net_matches_reference_forward_backward(dt, tol):
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+    ops.set_compute_dtype(dt)
+    try:
+        torch.manual_seed(1)
+        net = Net().eval()
+        ref = Net().eval()
+        ref.load_state_dict(net.state_dict())
+        net = net.to(DEV)
+        x = q(torch.randn(64, 1, 28, 28), dt)
+        t = torch.randint(0, 10, (64,))
+        out = net(x.to(DEV))
+        loss = ops.nll_loss(out, t.to(DEV))
+        loss.backward()
+        out_r = ref(x)
+        loss_r = F.nll_loss(out_r, t)
+        loss_r.backward()
+        close(out, out_r, rel=tol, name="net logp")
+        for (n1, p1), (_, p2) in zip(net.named_parameters(), ref.named_parameters()):
+            a, b = p1.grad.float().cpu(), p2.grad
+            rel = ((a - b).norm() / b.norm()).item()
+            assert rel < tol, f"grad {n1}: relative L2 error {rel:.3e}"
+    finally:
+        ops.set_compute_dtype(torch.bfloat16)
