@@ -1,0 +1,289 @@
+"""Fused LeNet training engine: the MI355X fast path for ``Net`` (ref src/model.py).
+
+One training step = two HIP kernels (``csed::lenet_train`` + ``csed::lenet_update``,
+see csrc/kernels/lenet_fused.hip), plus -- for data parallelism -- one RCCL
+all-reduce of the 87,360-byte gradient between them:
+
+    lenet_train    per-sample fwd+bwd of the whole network in LDS -> per-WG gradient slabs
+    lenet_update   fixed-order slab reduce (-> flat grad)          [world > 1: reduce only]
+    all_reduce     SUM over ranks on the flat grad (RCCL / xGMI)   [world > 1]
+    lenet_update   SGD-momentum + fp32 master params + 16-bit weight images + counters
+
+All per-step state (batch cursor into this rank's epoch permutation, Philox
+offset, optimizer step) lives on the device, so a sequence of steps is
+captured once into a HIP graph and replayed with no host work per step.
+
+The model's parameters are re-homed into the engine's flat fp32 buffer, so the
+``Net`` module always sees the current weights (checkpointing, evaluation
+through the op library, ``state_dict()``) without copies.
+"""
+from __future__ import annotations
+
+import math
+import sys
+
+import torch
+import torch.distributed as dist
+
+from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
+from ..models.net import N_PARAMS, Net
+from ..ops import _native
+from ..parallel.comm import DistContext
+from ..utils.flat import FlatParams
+
+WIMG_ELEMS = 61312  # 16-bit weight images, see csrc/kernels/lenet_fused.hip (I_END)
+
+
+class FusedLeNetTrainer:
+    def __init__(self, model: Net, train: MNISTData, lr: float = 0.01, momentum: float = 0.5,
+                 dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+                 global_batch: int = 64, ctx: DistContext | None = None,
+                 compute_dtype: torch.dtype = torch.bfloat16, drop_p: float = 0.5, seed: int = 1,
+                 grid: int | None = None, broadcast_init: bool = True):
+        _native.require()
+        self.ctx = ctx or DistContext(device=next(model.parameters()).device)
+        self.device = self.ctx.device
+        if self.device.type != "cuda":
+            raise RuntimeError("FusedLeNetTrainer runs on a GPU")
+        self.model = model
+        self.world = self.ctx.world_size if self.ctx.is_distributed else 1
+        if global_batch % self.world:
+            raise ValueError(f"global batch {global_batch} not divisible by world size {self.world}")
+        self.global_batch = int(global_batch)
+        self.B = self.global_batch // self.world
+        self.grid = int(grid) if grid else min(self.B, 256)
+        self.lr, self.momentum, self.dampening = float(lr), float(momentum), float(dampening)
+        self.weight_decay, self.nesterov = float(weight_decay), bool(nesterov)
+        self.mfma = _native.MFMA_CODE[compute_dtype]
+        self.drop_p = float(drop_p)
+        self.seed = int(seed)  # masks decorrelate across ranks through the rank id in the element index
+        self.train_data = train.to(self.device)
+        dev = self.device
+
+        self.flat = FlatParams(list(model.parameters()))
+        if self.flat.numel != N_PARAMS:
+            raise ValueError("FusedLeNetTrainer needs the reference Net architecture")
+        if broadcast_init and self.world > 1:
+            dist.broadcast(self.flat.data, src=0)  # the DDP-constructor parameter sync (CS4)
+        self.momentum_buf = torch.zeros_like(self.flat.data)
+        self.wimg = torch.zeros(WIMG_ELEMS, dtype=torch.int16, device=dev)
+        self.slab = torch.empty((self._max_grid(), N_PARAMS), dtype=torch.float32, device=dev)
+        self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
+        self.loss_acc = torch.zeros(2, dtype=torch.float32, device=dev)  # running (loss sum, correct)
+        self.step_count = torch.zeros(1, dtype=torch.long, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.cursor = torch.zeros(1, dtype=torch.long, device=dev)
+        self.rng_offset = torch.zeros(1, dtype=torch.long, device=dev)
+        self.eval_parts = torch.zeros(2 * 256, dtype=torch.float32, device=dev)
+        self.perm = torch.arange(self.B, dtype=torch.long, device=dev)
+        self.repack()
+        self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self.capture_comm_ok: bool | None = None
+
+    def _max_grid(self) -> int:
+        return max(self.grid, 1)
+
+    # ----------------------------------------------------------------- state
+    def repack(self) -> None:
+        """Rebuild the 16-bit weight images from the fp32 master parameters."""
+        torch.ops.csed.lenet_pack(self.flat.data, self.wimg, self.mfma)
+
+    def set_epoch_order(self, order: torch.Tensor) -> None:
+        """This rank's sample order for the epoch (int64 indices into the train set)."""
+        order = order.to(self.device, torch.long).contiguous()
+        if order.numel() < self.B:
+            raise ValueError("epoch order shorter than one batch")
+        if self._graphs and order.numel() != self.perm.numel():
+            self._graphs.clear()  # captured pointers refer to the old buffer
+        if order.numel() == self.perm.numel():
+            self.perm.copy_(order)
+        else:
+            self.perm = order
+        self.cursor.zero_()
+
+    def steps_per_epoch(self) -> int:
+        return math.ceil(self.perm.numel() / self.B)
+
+    def full_steps(self) -> int:
+        return self.perm.numel() // self.B
+
+    # ------------------------------------------------------------ launches
+    def _launch_step(self, B: int, grid: int, grad_scale: float, cursor: torch.Tensor | None,
+                     perm: torch.Tensor) -> None:
+        ops = torch.ops.csed
+        ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
+                        self.flat.data, self.slab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD, self.drop_p,
+                        self.seed, self.rng_offset, grid, self.mfma)
+        common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
+                  self.weight_decay, self.nesterov, self.step_count, self.ticket)
+        if self.world > 1:
+            ops.lenet_update(self.slab, grid, None, self.flat.grad, *common, None, None, False, self.loss_parts,
+                             grid, self.loss_acc, self.mfma)
+            dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
+            ops.lenet_update(self.slab, grid, self.flat.grad, None, *common, cursor, self.rng_offset, True, None, 0,
+                             None, self.mfma)
+        else:
+            ops.lenet_update(self.slab, grid, None, None, *common, cursor, self.rng_offset, True, self.loss_parts,
+                             grid, self.loss_acc, self.mfma)
+
+    def step(self) -> None:
+        """One full-batch training step at the device cursor (eager launches)."""
+        self._launch_step(self.B, self.grid, 1.0 / self.global_batch, self.cursor, self.perm)
+
+    def last_partial_step(self) -> None:
+        """The epoch's final short batch (ref DataLoader drop_last=False semantics)."""
+        rem = self.perm.numel() - self.full_steps() * self.B
+        if rem <= 0:
+            return
+        tail = self.perm[self.full_steps() * self.B:].contiguous()
+        gb = rem * self.world  # every rank has the same remainder (sampler pads to a multiple)
+        self._launch_step(rem, min(rem, self.grid), 1.0 / gb, None, tail)
+        # the tail step does not use the cursor; keep it consistent for the next epoch
+        self.cursor.add_(1)
+
+    # --------------------------------------------------------- graph capture
+    def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        # snapshot the state the capture warm-up will advance
+        saved = [t.clone() for t in (self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor,
+                                     self.rng_offset, self.loss_acc)]
+        with torch.cuda.stream(s):
+            self.step()  # warm-up on the capture stream (lazy RCCL init etc.)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        for t, v in zip((self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor,
+                         self.rng_offset, self.loss_acc), saved):
+            t.copy_(v)
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(nsteps):
+                self.step()
+        torch.cuda.synchronize(self.device)
+        return g
+
+    def graph(self, nsteps: int) -> torch.cuda.CUDAGraph | None:
+        key = (nsteps, self.perm.data_ptr(), self.B)
+        if key in self._graphs:
+            return self._graphs[key]
+        try:
+            g = self._capture(nsteps)
+            self.capture_comm_ok = True
+        except Exception as e:  # RCCL capture unsupported -> eager fallback
+            print(f"[csed] HIP graph capture failed ({e!r}); running steps eagerly", file=sys.stderr)
+            self.capture_comm_ok = False
+            torch.cuda.synchronize(self.device)
+            return None
+        self._graphs[key] = g
+        return g
+
+    def prepare(self, steps_per_graph: int = 16) -> None:
+        """Capture the step graphs up front (capture is never inside a timed region)."""
+        if self.graph(max(1, steps_per_graph)) is not None:
+            self.graph(1)
+
+    def run_steps(self, k: int, steps_per_graph: int = 16, use_graph: bool = True) -> None:
+        """Advance k full-batch steps from the current cursor."""
+        if k <= 0:
+            return
+        if not use_graph or self.capture_comm_ok is False:
+            for _ in range(k):
+                self.step()
+            return
+        spg = max(1, steps_per_graph)
+        full, rem = divmod(k, spg)
+        g = self.graph(spg) if full else None
+        if g is None and full:
+            for _ in range(k):
+                self.step()
+            return
+        for _ in range(full):
+            g.replay()
+        if rem:
+            g1 = self.graph(1)
+            for _ in range(rem):
+                if g1 is not None:
+                    g1.replay()
+                else:
+                    self.step()
+
+    def train_epoch(self, order: torch.Tensor, steps_per_graph: int = 16, use_graph: bool = True) -> None:
+        self.set_epoch_order(order)
+        self.run_steps(self.full_steps(), steps_per_graph, use_graph)
+        self.last_partial_step()
+
+    # ---------------------------------------------------------------- metrics
+    def take_loss(self) -> tuple[float, float]:
+        """(sum of per-sample train NLL, correct count) since the last call (one host sync)."""
+        v = self.loss_acc.tolist()
+        self.loss_acc.zero_()
+        return v[0], v[1]
+
+    @torch.no_grad()
+    def evaluate(self, test: MNISTData, order: torch.Tensor | None = None) -> tuple[float, int]:
+        """Forward-only pass over ``test``: (summed NLL, correct).  No dropout."""
+        test = test.to(self.device)
+        n = len(test)
+        order = torch.arange(n, device=self.device) if order is None else order.to(self.device)
+        nparts = min(n, 256)
+        torch.ops.csed.lenet_eval(test.images, test.labels, order, n, self.wimg, self.flat.data, MNIST_MEAN,
+                                  MNIST_STD, self.eval_parts, None, self.mfma)
+        parts = self.eval_parts[: 2 * nparts].view(nparts, 2).double().sum(0).tolist()
+        return parts[0], int(round(parts[1]))
+
+    @torch.no_grad()
+    def eval_logp(self, test: MNISTData) -> torch.Tensor:
+        test = test.to(self.device)
+        n = len(test)
+        out = torch.empty(n, 10, device=self.device)
+        torch.ops.csed.lenet_eval(test.images, test.labels, torch.arange(n, device=self.device), n, self.wimg,
+                                  self.flat.data, MNIST_MEAN, MNIST_STD, self.eval_parts, out, self.mfma)
+        return out
+
+    # ------------------------------------------------------------ optimizer io
+    def optimizer_state_dict(self) -> dict:
+        """torch.optim.SGD-compatible state dict (ref results/optimizer.pth)."""
+        state = {}
+        if int(self.step_count.item()) > 0 and self.momentum != 0:
+            for i in range(len(self.flat.params)):
+                state[i] = {"momentum_buffer": self.flat.view(self.momentum_buf, i).detach().cpu().clone()}
+        group = {"lr": self.lr, "momentum": self.momentum, "dampening": self.dampening,
+                 "weight_decay": self.weight_decay, "nesterov": self.nesterov, "maximize": False,
+                 "foreach": None, "differentiable": False, "fused": None,
+                 "params": list(range(len(self.flat.params)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd: dict) -> None:
+        have = False
+        for i in range(len(self.flat.params)):
+            st = sd.get("state", {}).get(i)
+            if st and st.get("momentum_buffer") is not None:
+                self.flat.view(self.momentum_buf, i).copy_(st["momentum_buffer"])
+                have = True
+        self.step_count.fill_(1 if have else 0)
+        g = sd["param_groups"][0]
+        self.lr, self.momentum = float(g["lr"]), float(g["momentum"])
+        self._graphs.clear()
+
+    def params_changed(self) -> None:
+        """Call after writing the model parameters from outside (e.g. a checkpoint load)."""
+        self.repack()
+
+    # --------------------------------------------------------------- smoke
+    @classmethod
+    def smoke_instance(cls, device) -> "FusedLeNetTrainer":
+        from ..data.mnist import synthetic_mnist
+
+        torch.manual_seed(1)
+        net = Net().to(device)
+        data = synthetic_mnist(64, seed=3)
+        return cls(net, data, lr=0.01, momentum=0.5, global_batch=16)
+
+    def smoke_step(self) -> None:
+        self.set_epoch_order(torch.arange(64))
+        self.step()
+        torch.cuda.synchronize(self.device)
+        loss, _ = self.take_loss()
+        if not math.isfinite(loss):
+            raise RuntimeError("fused smoke step produced a non-finite loss")

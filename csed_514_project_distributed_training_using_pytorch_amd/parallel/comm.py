@@ -1,0 +1,124 @@
+"""Process-group bootstrap and point-to-point helpers.
+
+Ref: ``init_process_group("gloo", rank, world_size)`` with a hard-coded
+``MASTER_ADDR=10.128.0.2`` (src/train_dist.py:144-146) and the 2-machine
+send/recv smoke test (src/run1.py:8-24).
+
+Here one process drives one MI355X.  The backend is RCCL (PyTorch's "nccl"
+backend on ROCm) whenever the process owns a GPU, so collectives run over
+xGMI; gloo remains for CPU-only runs and tests.  Rendezvous follows the
+torchrun environment contract (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR,
+MASTER_PORT) with the reference's ``--local_rank`` convention accepted too,
+and 127.0.0.1 as the default master address.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str | None = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.backend is not None and self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def env_int(name: str, default: int | None) -> int | None:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def _gpu_count() -> int:
+    # device_count() does not initialise the HIP runtime on this image
+    try:
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+def init_distributed(rank: int | None = None, world_size: int | None = None, local_rank: int | None = None,
+                     backend: str | None = None, master_addr: str | None = None, master_port: int | None = None,
+                     device: str | None = None, timeout_s: float = 600.0) -> DistContext:
+    """Initialise the default process group (if world_size > 1) and pick this rank's device."""
+    world_size = world_size if world_size is not None else env_int("WORLD_SIZE", 1)
+    rank = rank if rank is not None else env_int("RANK", None)
+    local_rank = local_rank if local_rank is not None else env_int("LOCAL_RANK", None)
+    if rank is None:
+        rank = local_rank if local_rank is not None else 0
+    if local_rank is None:
+        local_rank = rank
+    ngpu = _gpu_count()
+    if device is None:
+        device = "cuda" if ngpu > 0 else "cpu"
+    if device.startswith("cuda"):
+        if ngpu == 0:
+            raise RuntimeError("device=cuda requested but no GPU is visible")
+        dev = torch.device("cuda", local_rank % ngpu)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    be = None
+    if world_size > 1:
+        be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        os.environ.setdefault("MASTER_ADDR", master_addr or "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(master_port or 29500))
+        if master_addr:
+            os.environ["MASTER_ADDR"] = master_addr
+        if master_port:
+            os.environ["MASTER_PORT"] = str(master_port)
+        if not dist.is_initialized():
+            kw = {}
+            if be == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(be, rank=rank, world_size=world_size,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistContext(rank, world_size, local_rank, dev, be)
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def barrier(ctx: DistContext) -> None:
+    if ctx.is_distributed:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.device.index])
+        else:
+            dist.barrier()
+
+
+def p2p_exchange(ctx: DistContext, src: int = 0, dst: int = 1) -> torch.Tensor:
+    """The reference smoke test (src/run1.py:8-17): rank ``src`` adds 1 to a zeros(1)
+    tensor and sends it; rank ``dst`` receives it.  Returns the local tensor."""
+    t = torch.zeros(1, device=ctx.device)
+    if ctx.rank == src:
+        t += 1
+        dist.send(t, dst=dst)
+    elif ctx.rank == dst:
+        dist.recv(t, src=src)
+    return t
+
+
+def all_reduce_max(ctx: DistContext, value: float) -> float:
+    """Max of a host scalar over ranks (used to report the slowest rank's time)."""
+    if not ctx.is_distributed:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

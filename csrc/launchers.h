@@ -125,30 +125,30 @@ hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int d
 struct LenetTrainArgs {
   const uint8_t* images;     // [n_src, 784] raw MNIST pixels
   const int64_t* labels;     // [n_src]
-  const int64_t* perm;       // sample order for the epoch (global indices)
-  const int64_t* cursor;     // device step counter (batch index into perm)
+  const int64_t* perm;       // this rank's sample order for the epoch
+  const int64_t* cursor;     // device step counter (batch index into perm) or null
   int64_t perm_len;          // valid entries in perm
   int B;                     // per-rank batch for this step
-  int rank_stride;           // unused (sharding is folded into perm)
-  const uint16_t* wimg;      // packed 16-bit weight images (see layout)
+  int rank_stride;           // rank id (decorrelates dropout masks across ranks)
+  const uint16_t* wimg;      // packed 16-bit weight images
   const float* params;       // flat fp32 master params [21840]
   float* slab;               // [grid, 21840] per-workgroup partial grads
-  float* loss_acc;           // [2]: loss sum, correct count (accumulated)
+  float* loss_acc;           // [grid, 2] per-workgroup (loss sum, correct count)
   float grad_scale;          // 1 / (global batch)
   float mean, std_;
   float drop_p;
   uint64_t seed;
-  const int64_t* rng_offset; // device counter
+  const int64_t* rng_offset; // device counter (high bits of the Philox offset)
   int grid;
   int mfma_dtype;
+  uint64_t* dbg;             // optional [grid, 16] stage stamps (diagnostics)
 };
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s);
 int64_t lenet_wimg_elems();
 int64_t lenet_param_count();
-// Fused grad reduce + SGD + weight-image refresh.  When `grad_out` is
-// non-null and `apply_sgd` is 0 the reduced gradient is written there (for
-// an all-reduce) and nothing else happens; with apply_sgd=1 and `grad_in`
-// non-null, the SGD consumes grad_in instead of the slab.
+// Fused slab reduce + SGD + weight-image refresh + counter bump.
+// apply_sgd = 0: write the reduced gradient to grad_out (DDP: all-reduce next).
+// apply_sgd = 1: grad = grad_in if given (after the all-reduce) else the slab sum.
 struct LenetUpdateArgs {
   const float* slab; int grid;
   const float* grad_in;
@@ -156,16 +156,17 @@ struct LenetUpdateArgs {
   float* params; float* momentum; uint16_t* wimg;
   float lr, mom, dampening, weight_decay; int nesterov;
   int64_t* step; int* ticket;
-  int64_t* cursor; int64_t* rng_offset;   // bumped by the last block when apply_sgd
+  int64_t* cursor; int64_t* rng_offset;
   int apply_sgd;
   int mfma_dtype;
 };
-hipError_t launch_lenet_update(const LenetUpdateArgs& a, hipStream_t s);
-// Pack fp32 params into the 16-bit weight images (used at init / after a load).
+// loss_parts [nparts, 2] are summed in a fixed order into loss_acc[2] (optional).
+hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
+                               hipStream_t s);
 hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype, hipStream_t s);
-// Fused eval: forward over n images, accumulates [loss_sum, correct] in out.
+// Forward-only evaluation: out_parts [min(n,256), 2] per-workgroup (loss sum, correct).
 hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,
                              int64_t n, const uint16_t* wimg, const float* params, float mean,
-                             float std_, float* out, float* logp_out, int mfma_dtype, hipStream_t s);
+                             float std_, float* out_parts, float* logp_out, int mfma_dtype, hipStream_t s);
 
 }  // namespace csed

