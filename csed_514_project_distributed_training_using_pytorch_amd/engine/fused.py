@@ -39,7 +39,7 @@ class FusedLeNetTrainer:
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
                  global_batch: int = 64, ctx: DistContext | None = None,
                  compute_dtype: torch.dtype = torch.bfloat16, drop_p: float = 0.5, seed: int = 1,
-                 grid: int | None = None, broadcast_init: bool = True):
+                 grid: int | None = None, broadcast_init: bool = True, comm: bool | None = None):
         _native.require()
         self.ctx = ctx or DistContext(device=next(model.parameters()).device)
         self.device = self.ctx.device
@@ -47,6 +47,9 @@ class FusedLeNetTrainer:
             raise RuntimeError("FusedLeNetTrainer runs on a GPU")
         self.model = model
         self.world = self.ctx.world_size if self.ctx.is_distributed else 1
+        # comm=True forces the all-reduce path even at world size 1 (tests RCCL graph capture
+        # on a single GPU); default: collectives exactly when there is more than one rank
+        self.comm = (self.world > 1) if comm is None else (bool(comm) and dist.is_initialized())
         if global_batch % self.world:
             raise ValueError(f"global batch {global_batch} not divisible by world size {self.world}")
         self.global_batch = int(global_batch)
@@ -116,7 +119,7 @@ class FusedLeNetTrainer:
                         self.seed, self.rng_offset, grid, self.mfma)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
-        if self.world > 1:
+        if self.comm:
             ops.lenet_update(self.slab, grid, None, self.flat.grad, *common, None, None, False, self.loss_parts,
                              grid, self.loss_acc, self.mfma)
             dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
@@ -256,6 +259,7 @@ class FusedLeNetTrainer:
 
     def load_optimizer_state_dict(self, sd: dict) -> None:
         have = False
+        self.momentum_buf.zero_()
         for i in range(len(self.flat.params)):
             st = sd.get("state", {}).get(i)
             if st and st.get("momentum_buffer") is not None:

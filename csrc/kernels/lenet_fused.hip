@@ -155,31 +155,29 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 
   if (a.dbg && tid == 0) a.dbg[g * 16 + 12] = __builtin_amdgcn_s_memtime();
   // ---------------- once per workgroup: weight images, offset tables, fp32 params -> LDS
+  // register-resident conv1 weight fragment, reused for every sample of this WG
+  frag fb1;
   {
-    // all 10 16-byte loads per thread are issued before the first LDS store
+    // Every global load of the preamble (weight images, fp32 params, the conv1
+    // fragment) is issued before the first wait: one memory round trip.
     constexpr int PER = (WIMG_LDS_U4 + NT - 1) / NT;
     const uint4* src = reinterpret_cast<const uint4*>(a.wimg + I_W2C);
-    uint4* dst = reinterpret_cast<uint4*>(W2c);
     uint4 v[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int i = tid + u * NT;
       v[u] = i < WIMG_LDS_U4 ? src[i] : make_uint4(0, 0, 0, 0);
     }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int i = tid + u * NT;
-      if (i < WIMG_LDS_U4) dst[i] = v[u];
-    }
-    for (int i = tid; i < 590; i += NT) {
-      int pi;
-      if (i < 10) pi = O_C1B + i;
-      else if (i < 30) pi = O_C2B + i - 10;
-      else if (i < 80) pi = O_F1B + i - 30;
-      else if (i < 90) pi = O_F2B + i - 80;
-      else pi = O_F2W + i - 90;
-      PAR[i] = a.params[pi];
-    }
+    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, one per thread)
+    int pi = O_F2W + tid - 90;
+    if (tid < 10) pi = O_C1B + tid;
+    else if (tid < 30) pi = O_C2B + tid - 10;
+    else if (tid < 80) pi = O_F1B + tid - 30;
+    else if (tid < 90) pi = O_F2B + tid - 80;
+    const float pv0 = a.params[pi];
+    const float pv1 = tid + NT < 590 ? a.params[O_F2W + tid + NT - 90] : 0.f;
+    fb1 = *reinterpret_cast<const frag*>(a.wimg + I_W1C + l16 * 32 + kb);
+    // work that needs no loaded data overlaps the loads
     if (tid < 256) {
       const int k = tid, ic = k / 25, r = k % 25;
       KO2[k] = (short)(k < 250 ? ic * 144 + (r / 5) * 12 + (r % 5) : 0);
@@ -188,14 +186,23 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       const int k = tid, co = k / 25, r = k % 25;
       KOD[k] = (short)(k < 500 ? co * 256 + (r / 5) * 16 + (r % 5) : 0);
     }
-    // regions whose padding must stay zero across samples
-    for (int i = tid; i < 32 * LD_DC2; i += NT) DC2[i] = 0;
-    for (int i = tid; i < 20 * 256; i += NT) DC2P[i] = 0;
-    for (int i = tid; i < 16 * LD_DC1; i += NT) DC1[i] = 0;
-    if (tid < 64) DZ1B[tid] = 0;
+    // DC2 | DC2P | DC1 are contiguous: zero their padding once with 16-B stores
+    {
+      constexpr int NZ = (S_KO2 - S_DC2) / 16;
+      uint4* z = reinterpret_cast<uint4*>(sm + S_DC2);
+      for (int i = tid; i < NZ; i += NT) z[i] = make_uint4(0, 0, 0, 0);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(W2c);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = tid + u * NT;
+      if (i < WIMG_LDS_U4) dst[i] = v[u];
+    }
+    if (tid < 590) PAR[tid] = pv0;
+    if (tid + NT < 590) PAR[tid + NT] = pv1;
   }
-  // register-resident weight fragments, reused for every sample of this WG
-  const frag fb1 = *reinterpret_cast<const frag*>(a.wimg + I_W1C + l16 * 32 + kb);
+  if (a.dbg && tid == 0) a.dbg[g * 16 + 13] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && tid == 0) a.dbg[g * 16 + 14] = __builtin_amdgcn_s_memtime();
   int koff1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -621,7 +628,9 @@ __global__ void __launch_bounds__(UP_C * UP_S) lenet_update_kernel(LenetUpdateAr
   const int cl = threadIdx.x & (UP_C - 1), sl = threadIdx.x / UP_C;
   const int q4 = blockIdx.x * UP_C + cl;  // float4 column
   constexpr int NQ = NP / 4;
-  const bool first = a.step ? a.step[0] == 0 : false;
+  // with zero dampening a zero-initialised momentum buffer reproduces torch's
+  // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
+  const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
   const bool from_slab = !(a.grad_in && a.apply_sgd);
   if (from_slab) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -700,16 +709,26 @@ __global__ void __launch_bounds__(UP_C * UP_S) lenet_update_kernel(LenetUpdateAr
     }
   }
   if (a.apply_sgd) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // every block has read step[0] above before taking its ticket
-      const int t = atomicAdd(a.ticket, 1);
-      if (t == (int)gridDim.x - 1) {
-        a.ticket[0] = 0;
-        if (a.step) a.step[0] += 1;
-        if (a.cursor) a.cursor[0] += 1;
-        if (a.rng_offset) a.rng_offset[0] += 1;
+    // Device counters.  cursor / rng_offset are never read by this kernel, so
+    // block 0 bumps them directly.  step[0] is read by every block only when
+    // dampening != 0 (the one case where torch's "first step: buf = g" differs
+    // from a zero-initialised buffer); then the last block to take a ticket
+    // bumps it, otherwise block 0 does -- no 342-way atomic on the hot path.
+    if (a.dampening != 0.f) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
+        if (t == (int)gridDim.x - 1) {
+          a.ticket[0] = 0;
+          if (a.step) a.step[0] += 1;
+        }
       }
+    } else if (blockIdx.x == 0 && threadIdx.x == 0 && a.step) {
+      a.step[0] += 1;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (a.cursor) a.cursor[0] += 1;
+      if (a.rng_offset) a.rng_offset[0] += 1;
     }
   }
 }
