@@ -32,6 +32,8 @@ from ..parallel.comm import DistContext
 from ..utils.flat import FlatParams
 
 WIMG_ELEMS = 61312  # 16-bit weight images, see csrc/kernels/lenet_fused.hip (I_END)
+CONV_PARAMS = 5312  # conv1.w/b + conv2.w/b (5280) per WG, in 83 chunks of 64 floats (CNP_PAD)
+VEC_LEN = 464       # per-sample fc vectors P2 | dZ1 | H | dlogits (VEC)
 
 
 class FusedLeNetTrainer:
@@ -70,7 +72,9 @@ class FusedLeNetTrainer:
             dist.broadcast(self.flat.data, src=0)  # the DDP-constructor parameter sync (CS4)
         self.momentum_buf = torch.zeros_like(self.flat.data)
         self.wimg = torch.zeros(WIMG_ELEMS, dtype=torch.int16, device=dev)
-        self.slab = torch.empty((self._max_grid(), N_PARAMS), dtype=torch.float32, device=dev)
+        # per-WG conv partial gradients and per-sample fc vectors (see lenet_fused.hip)
+        self.slab = torch.empty((self._max_grid(), CONV_PARAMS), dtype=torch.float32, device=dev)
+        self.vslab = torch.zeros((self.B, VEC_LEN), dtype=torch.float32, device=dev)
         self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(2, dtype=torch.float32, device=dev)  # running (loss sum, correct)
         self.step_count = torch.zeros(1, dtype=torch.long, device=dev)
@@ -115,19 +119,34 @@ class FusedLeNetTrainer:
                      perm: torch.Tensor) -> None:
         ops = torch.ops.csed
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
-                        self.flat.data, self.slab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD, self.drop_p,
-                        self.seed, self.rng_offset, grid, self.mfma)
+                        self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
+                        self.drop_p, self.seed, self.rng_offset, grid, self.mfma)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
         if self.comm:
-            ops.lenet_update(self.slab, grid, None, self.flat.grad, *common, None, None, False, self.loss_parts,
-                             grid, self.loss_acc, self.mfma)
+            ops.lenet_update(self.slab, grid, self.vslab, B, None, self.flat.grad, *common, None, None, False,
+                             self.loss_parts, grid, self.loss_acc, self.mfma)
             dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
-            ops.lenet_update(self.slab, grid, self.flat.grad, None, *common, cursor, self.rng_offset, True, None, 0,
-                             None, self.mfma)
+            ops.lenet_update(self.slab, grid, self.vslab, B, self.flat.grad, None, *common, cursor, self.rng_offset,
+                             True, None, 0, None, self.mfma)
         else:
-            ops.lenet_update(self.slab, grid, None, None, *common, cursor, self.rng_offset, True, self.loss_parts,
-                             grid, self.loss_acc, self.mfma)
+            ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
+                             self.loss_parts, grid, self.loss_acc, self.mfma)
+
+    def gradient(self, grid: int | None = None, dbg: torch.Tensor | None = None) -> torch.Tensor:
+        """Mean-loss gradient of the batch at the cursor, without updating anything
+        (lenet_train + the reduce-only lenet_update).  Also accumulates the batch's
+        loss / correct count into the running totals."""
+        grid = grid or self.grid
+        g = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
+        ops = torch.ops.csed
+        ops.lenet_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B, self.ctx.rank,
+                        self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts, 1.0 / self.global_batch,
+                        MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg)
+        ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
+                         self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
+                         self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma)
+        return g
 
     def step(self) -> None:
         """One full-batch training step at the device cursor (eager launches)."""

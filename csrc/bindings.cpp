@@ -281,16 +281,19 @@ void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
 }
 
 void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm, const optional<Tensor>& cursor,
-                 int64_t B, int64_t rank, const Tensor& wimg, const Tensor& params, Tensor& slab, Tensor& loss_parts,
+                 int64_t B, int64_t rank, const Tensor& wimg, const Tensor& params, Tensor& slab, Tensor& vslab,
+                 Tensor& loss_parts,
                  double grad_scale, double mean, double std_, double drop_p, int64_t seed,
                  const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
                  const optional<Tensor>& dbg) {
   dev(images, "images"); dev(labels, "labels"); dev(perm, "perm"); dev(wimg, "wimg"); dev(params, "params");
-  dev(slab, "slab"); dev(loss_parts, "loss_parts");
+  dev(slab, "slab"); dev(vslab, "vslab"); dev(loss_parts, "loss_parts");
   TORCH_CHECK(images.scalar_type() == at::kByte && images.numel() == images.size(0) * 784, "images: uint8 [N,28,28]");
   TORCH_CHECK(labels.scalar_type() == at::kLong && perm.scalar_type() == at::kLong);
   TORCH_CHECK(grid >= 1 && grid <= B && grid <= 1024, "lenet_train: 1 <= grid <= B");
-  TORCH_CHECK(slab.numel() >= grid * csed::lenet_param_count() && loss_parts.numel() >= 2 * grid);
+  TORCH_CHECK(slab.numel() >= grid * csed::lenet_conv_param_count() && loss_parts.numel() >= 2 * grid,
+              "lenet_train: slab [grid, 5280] / loss_parts [grid, 2] too small");
+  TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_train: vslab [B, 464] too small");
   if (!cursor.has_value()) TORCH_CHECK(perm.numel() >= B, "perm shorter than the batch");
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0);
   const c10::DeviceGuard gd(images.device());
@@ -298,7 +301,7 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
   a.images = images.data_ptr<uint8_t>(); a.labels = labels.data_ptr<int64_t>(); a.perm = perm.data_ptr<int64_t>();
   a.cursor = optpt<int64_t>(cursor); a.perm_len = perm.numel(); a.B = (int)B; a.rank_stride = (int)rank;
   a.wimg = (const uint16_t*)wimg.data_ptr(); a.params = params.data_ptr<float>(); a.slab = slab.data_ptr<float>();
-  a.loss_acc = loss_parts.data_ptr<float>(); a.grad_scale = (float)grad_scale; a.mean = (float)mean;
+  a.vslab = vslab.data_ptr<float>(); a.loss_acc = loss_parts.data_ptr<float>(); a.grad_scale = (float)grad_scale; a.mean = (float)mean;
   a.std_ = (float)std_; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.rng_offset = optpt<int64_t>(rng_offset);
   a.grid = (int)grid; a.mfma_dtype = mcode(mfma_dtype);
   if (dbg.has_value()) {
@@ -308,23 +311,31 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
   CHECK_HIP(csed::launch_lenet_train(a, cur_stream(images)));
 }
 
-void lenet_update(const Tensor& slab, int64_t grid, const optional<Tensor>& grad_in, const optional<Tensor>& grad_out,
+void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t B, const optional<Tensor>& grad_in, const optional<Tensor>& grad_out,
                   Tensor& params, Tensor& momentum, Tensor& wimg, double lr, double mom, double dampening,
                   double weight_decay, bool nesterov, Tensor& step, Tensor& ticket, const optional<Tensor>& cursor,
                   const optional<Tensor>& rng_offset, bool apply_sgd, const optional<Tensor>& loss_parts,
-                  int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype) {
+                  int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg) {
   dev(slab, "slab"); dev(params, "params"); dev(momentum, "momentum"); dev(wimg, "wimg");
+  TORCH_CHECK(params.numel() == csed::lenet_param_count() && momentum.numel() == params.numel(),
+              "lenet_update: params / momentum must hold the 21840 flat LeNet parameters");
   TORCH_CHECK(apply_sgd || grad_out.has_value(), "lenet_update: reduce-only mode needs grad_out");
   TORCH_CHECK(loss_parts.has_value() == loss_acc.has_value());
   const c10::DeviceGuard gd(params.device());
   csed::LenetUpdateArgs a{};
   a.slab = slab.data_ptr<float>(); a.grid = (int)grid;
+  a.vslab = vslab.data_ptr<float>(); a.B = (int)B;
+  TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_update: vslab too small");
   a.grad_in = optpt<float>(grad_in); a.grad_out = optpt<float>(grad_out);
   a.params = params.data_ptr<float>(); a.momentum = momentum.data_ptr<float>(); a.wimg = (uint16_t*)wimg.data_ptr();
   a.lr = (float)lr; a.mom = (float)mom; a.dampening = (float)dampening; a.weight_decay = (float)weight_decay;
   a.nesterov = nesterov ? 1 : 0; a.step = step.data_ptr<int64_t>(); a.ticket = ticket.data_ptr<int>();
   a.cursor = optpt<int64_t>(cursor); a.rng_offset = optpt<int64_t>(rng_offset);
   a.apply_sgd = apply_sgd ? 1 : 0; a.mfma_dtype = mcode(mfma_dtype);
+  if (dbg.has_value()) {
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 128, "lenet_update: dbg must be int64[>=1024]");
+    a.dbg = (uint64_t*)dbg->data_ptr();
+  }
   CHECK_HIP(csed::launch_lenet_update(a, optpt<float>(loss_parts), (int)nparts, optpt<float>(loss_acc),
                                       cur_stream(params)));
 }
@@ -347,12 +358,13 @@ void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order,
 TORCH_LIBRARY(csed, m) {
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
-        "Tensor params, Tensor(a!) slab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "
+        "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "
         "float drop_p, int seed, Tensor? rng_offset, int grid, int mfma_dtype, Tensor(c!)? dbg=None) -> ()");
-  m.def("lenet_update(Tensor slab, int grid, Tensor? grad_in, Tensor(a!)? grad_out, Tensor(b!) params, "
+  m.def("lenet_update(Tensor slab, int grid, Tensor vslab, int B, Tensor? grad_in, Tensor(a!)? grad_out, Tensor(b!) params, "
         "Tensor(c!) momentum, Tensor(d!) wimg, float lr, float mom, float dampening, float weight_decay, "
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
-        "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype) -> ()");
+        "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
+        "Tensor(j!)? dbg=None) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
         "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "

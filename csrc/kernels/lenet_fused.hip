@@ -52,6 +52,11 @@ constexpr int I_W1C = 0, I_W2C = 512, I_W2D = 8960, I_F1 = 17280, I_F1T = 38272,
 constexpr int LD_W2C = 264, LD_W2D = 520, LD_F1 = 328, LD_F1T = 72;
 constexpr int LD_DC2 = 72, LD_DC1 = 584;
 constexpr int NT = 512, NW = 8;
+// conv partial-gradient slab: params [0, CNP) = conv1.w, conv1.b, conv2.w, conv2.b
+constexpr int CNP = O_F1W;
+constexpr int CNP_PAD = (CNP + 63) / 64 * 64;  // slab row: 83 chunks of 64 floats (see lenet_update)
+// per-sample vector slab (fp32): fc1 input P2 | dL/dz1 | fc1 output H | dL/dlogits
+constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;
 
 // LDS carve (bytes); every region 16-B aligned
 constexpr int S_W2C = 0;                              // u16 32*264
@@ -164,10 +169,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     const uint4* src = reinterpret_cast<const uint4*>(a.wimg + I_W2C);
     uint4 v[PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int i = tid + u * NT;
-      v[u] = i < WIMG_LDS_U4 ? src[i] : make_uint4(0, 0, 0, 0);
-    }
+    for (int u = 0; u < PER; ++u) v[u] = src[min(tid + u * NT, WIMG_LDS_U4 - 1)];  // unconditional: no branches
     // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, one per thread)
     int pi = O_F2W + tid - 90;
     if (tid < 10) pi = O_C1B + tid;
@@ -175,7 +177,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     else if (tid < 80) pi = O_F1B + tid - 30;
     else if (tid < 90) pi = O_F2B + tid - 80;
     const float pv0 = a.params[pi];
-    const float pv1 = tid + NT < 590 ? a.params[O_F2W + tid + NT - 90] : 0.f;
+    const float pv1 = a.params[O_F2W + min(tid + NT, 589) - 90];
     fb1 = *reinterpret_cast<const frag*>(a.wimg + I_W1C + l16 * 32 + kb);
     // work that needs no loaded data overlaps the loads
     if (tid < 256) {
@@ -217,16 +219,15 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc_c2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc_c1 = f32x4{0.f, 0.f, 0.f, 0.f};  // conv1 wgrad tile (wave&1), steps (wave>>1) mod 4
-  float acc_f1[32];                          // fc1 dW, elements tid + 512*j
-#pragma unroll
-  for (int j = 0; j < 32; ++j) acc_f1[j] = 0.f;
-  float acc_f2 = 0.f;                        // fc2 dW element tid (< 500)
-  float acc_b1 = 0.f, acc_b2 = 0.f;          // fc1 bias (tid<50), fc2 bias (tid<10)
   float loss_sum = 0.f, correct = 0.f;
+  // The fc-layer weight gradients are rank-1 per sample (dZ (x) input); instead of
+  // accumulating 16,500 products per sample here, each sample's vectors are written
+  // to the vector slab and lenet_update forms the sums as one GEMM over the batch.
 
   const int nsamp = (a.B - g + G - 1) / G;
   for (int s = 0; s < nsamp; ++s) {
     const int b = g + s * G;
+    float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
     __syncthreads();  // previous sample's readers of Xs / P1 / DC1 are done
     // ---------------- stage 0: gather + normalise the image, dropout masks
     STAMP(0);
@@ -249,7 +250,10 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1
     STAMP(1);
-    for (int mt = wave; mt < 36; mt += NW) {
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {  // 36 tiles over 8 waves, unrolled so all gathers issue up front
+      const int mt = wave + it * NW;
+      if (mt >= 36) break;
       const int m = mt * 16 + l16;
       const int p = m >> 2, q = m & 3;
       const int pb = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       const int pb = (2 * (p >> 2) + (q >> 1)) * 12 + 2 * (p & 3) + (q & 1);
       f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
       const unsigned short* wrow = W2c + (nt * 16 + l16) * LD_W2C + kb;
-#pragma unroll 2
+#pragma unroll 4
       for (int ks = 0; ks < 8; ++ks) {
         const s16x8 o = *reinterpret_cast<const s16x8*>(KO2 + ks * 32 + kb);
         u16x8 raw;
@@ -295,8 +299,10 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         for (int r = 1; r < 4; ++r)
           if (c[r] > best) { best = c[r]; bi = r; }
         const int w = mt * 4 + (lane >> 4);
-        P2[oc * 16 + w] = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
+        const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
+        P2[oc * 16 + w] = hv;
         I2[oc * 16 + w] = (uint8_t)bi;
+        if (TRAIN) vs[V_P2 + oc * 16 + w] = f16v<T>(hv);  // fc1 input, exactly as the forward used it
       }
     }
     __syncthreads();
@@ -313,7 +319,11 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       }
       if (lane < 16) {
         const int o = wave * 16 + lane;
-        if (o < 50) Hs[o] = fmaxf(c[0] + PAR[P_F1B + o], 0.f) * D1S[o];
+        if (o < 50) {
+          const float h = fmaxf(c[0] + PAR[P_F1B + o], 0.f) * D1S[o];
+          Hs[o] = h;
+          if (TRAIN) vs[V_H + o] = h;
+        }
       }
     }
     __syncthreads();
@@ -352,7 +362,11 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         correct += (amax == t) ? 1.f : 0.f;
       }
       if (write_logp && lane < 10) logp_out[(int64_t)b * 10 + lane] = lp;
-      if (TRAIN && lane < 16) DLOG[lane] = lane < 10 ? (__expf(lp) - (lane == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
+      if (TRAIN && lane < 16) {
+        const float dl = lane < 10 ? (__expf(lp) - (lane == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
+        DLOG[lane] = dl;
+        vs[V_DLOG + lane] = dl;
+      }
     }
     if (!TRAIN) continue;
     __syncthreads();
@@ -360,8 +374,6 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 5: fc2 backward, fc1 relu/dropout gate
     STAMP(5);
     {
-      if (tid < 500) acc_f2 = fmaf(DLOG[tid / 50], Hs[tid % 50], acc_f2);
-      if (tid < 10) acc_b2 += DLOG[tid];
       if (tid < 64) {
         float dz = 0.f;
         if (tid < 50) {
@@ -369,25 +381,16 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
           for (int c = 0; c < 10; ++c) dh = fmaf(DLOG[c], PAR[P_F2W + c * 50 + tid], dh);
           dz = Hs[tid] > 0.f ? dh * D1S[tid] : 0.f;
-          acc_b1 += dz;
+          vs[V_DZ1 + tid] = dz;
         }
         DZ1[tid] = dz;
-        DZ1B[tid] = h16<T>(dz);
       }
     }
     __syncthreads();
 
-    // ---------------- stage 6: fc1 dW (registers) and dP2 = W1^T dZ1 (MFMA)
+    // ---------------- stage 6: dP2 = W1^T dZ1 (VALU over the LDS fc1 image)
     STAMP(6);
     {
-      int o = tid / 320, i = tid - o * 320;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        if (o < 50) acc_f1[j] = fmaf(DZ1[o], f16v<T>(P2[i]), acc_f1[j]);
-        i += 192;  // e += 512 = 320 + 192
-        o += 1;
-        if (i >= 320) { i -= 320; o += 1; }
-      }
       // dP2[i] = sum_o dZ1[o] * W1[o][i]: one input feature per thread, lanes read
       // consecutive columns of the LDS fc1 image (conflict-free), 50-long FMA chain
       if (tid < 320) {
@@ -531,7 +534,9 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   }
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
-    float* out = a.slab + (int64_t)g * NP;
+    // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a
+    // chunk ([chunk][WG][64]) so lenet_update reads each chunk contiguously
+    auto out = [&](int e) -> float& { return a.slab[((int64_t)(e >> 6) * G + g) * 64 + (e & 63)]; };
     // conv1: combine the four step-slices of each tile (fixed order)
     __syncthreads();
 #pragma unroll
@@ -544,8 +549,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       for (int q = 0; q < 4; ++q) v += RED[((nt + 2 * q) * 16 + oc) * 16 + col];
       const int k = nt * 16 + col;
       if (oc < 10) {
-        if (k < 25) out[O_C1W + oc * 25 + k] = v;
-        else if (k == 25) out[O_C1B + oc] = v;
+        if (k < 25) out(O_C1W + oc * 25 + k) = v;
+        else if (k == 25) out(O_C1B + oc) = v;
       }
     }
     // conv2
@@ -558,20 +563,11 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         for (int r = 0; r < 4; ++r) {
           const int oc = mt * 16 + 4 * (lane >> 4) + r;
           if (oc < 20) {
-            if (k < 250) out[O_C2W + oc * 250 + k] = acc_c2[mt][jj][r];
-            else if (k == 250) out[O_C2B + oc] = acc_c2[mt][jj][r];
+            if (k < 250) out(O_C2W + oc * 250 + k) = acc_c2[mt][jj][r];
+            else if (k == 250) out(O_C2B + oc) = acc_c2[mt][jj][r];
           }
         }
       }
-    // fc1 / fc2
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const int e = tid + j * NT;
-      if (e < 16000) out[O_F1W + e] = acc_f1[j];
-    }
-    if (tid < 50) out[O_F1B + tid] = acc_b1;
-    if (tid < 500) out[O_F2W + tid] = acc_f2;
-    if (tid < 10) out[O_F2B + tid] = acc_b2;
   }
   if (tid == 0) {
     a.loss_acc[2 * g] = loss_sum;
@@ -606,138 +602,237 @@ __global__ void lenet_pack_kernel(const float* __restrict__ params, unsigned sho
   if (i < NP) write_images<T>(wimg, i, params[i]);
 }
 
-// Reduce the per-workgroup slabs, then either export the gradient (DDP: the
-// all-reduce happens next) or apply SGD + refresh the weight images.
+// ---------------------------------------------------------------------------
+// lenet_update: turn the step's partials into the gradient, then either
+// export it (DDP: the RCCL all-reduce runs next) or apply SGD + refresh the
+// 16-bit weight images.  Two block roles in one launch:
 //
-// Block = 16 float4 columns (64 parameters) x 32 slices = 512 threads, 342
-// blocks: every CU pulls ~16 KB of the 5.6 MB slab (B = 64) with all of its
-// loads in flight -- this kernel is per-CU-latency, not bandwidth, bound.
-// Slice s sums partials g = s, s+32, ... ; the 32 slices are then combined
-// through LDS in a fixed two-level order: bitwise reproducible.
-constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8;
+//   role CONV (blocks [0, NB_CONV)): fixed-order reduction of the per-WG conv
+//     slabs, 16 float4 columns x 32 slices per block so every CU pulls only a
+//     few KB with all loads in flight (latency-, not bandwidth-bound).  Block 0
+//     also folds the loss partials and bumps the device counters.
+//   role FC (blocks [NB_CONV, +NB_FC)): the fc gradients are batch GEMMs of the
+//     per-sample vectors, on the fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32
+//     products), one 16x16 output tile per wave, K = batch:
+//       dW1 | db1 = dZ1^T . [P2 | 1]   (4 x 21 tiles: column 320 = bias grad)
+//       dW2 | db2 = dL^T  . [H  | 1]   (1 x 4 tiles:  column 50  = bias grad)
+//     Each lane issues all of a 64-sample chunk's loads before its 16 MFMAs.
+//
+// Reductions run in a fixed order everywhere: bitwise reproducible.
+// ---------------------------------------------------------------------------
+constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
+constexpr int CNQ = CNP / 4;                        // conv float4 columns (1320)
+constexpr int NB_CONV = (CNQ + UP_C - 1) / UP_C;    // 83
+constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
+constexpr int NB_FC = (FC_TILES + UP_NT / 64 - 1) / (UP_NT / 64);  // 11 blocks x 8 waves
+constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
 }
 
+// Final consumer of one parameter's gradient: export or SGD step.  p / m are
+// params[i] / momentum[i], loaded by the caller at kernel entry so their
+// round trip overlaps the gradient loads instead of following them.
 template <typename T>
-__global__ void __launch_bounds__(UP_C * UP_S) lenet_update_kernel(LenetUpdateArgs a, float* loss_parts, int nparts,
-                                                                   float* loss_acc) {
+__device__ __forceinline__ void finish_param(const LenetUpdateArgs& a, int i, float gsum, bool first, float p,
+                                             float m) {
+  if (!a.apply_sgd) {
+    a.grad_out[i] = gsum;
+    return;
+  }
+  if (a.grad_out) a.grad_out[i] = gsum;
+  const float gj = gsum + a.weight_decay * p;
+  float d = gj;
+  if (a.mom != 0.f) {
+    const float bj = first ? gj : fmaf(a.mom, m, (1.f - a.dampening) * gj);
+    a.momentum[i] = bj;
+    d = a.nesterov ? fmaf(a.mom, bj, gj) : bj;
+  }
+  p = fmaf(-a.lr, d, p);
+  a.params[i] = p;
+  write_images<T>(a.wimg, i, p);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
+                                                             int B, float* loss_parts, int nparts,
+                                                             float* loss_acc) {
   __shared__ float4 part[UP_S][UP_C];
-  __shared__ float4 part2[4][UP_C];
-  const int cl = threadIdx.x & (UP_C - 1), sl = threadIdx.x / UP_C;
-  const int q4 = blockIdx.x * UP_C + cl;  // float4 column
-  constexpr int NQ = NP / 4;
+  __shared__ float part2[4][UP_C * 4];
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
-  const bool from_slab = !(a.grad_in && a.apply_sgd);
-  if (from_slab) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q4 < NQ) {
-      const float4* sp = reinterpret_cast<const float4*>(a.slab) + q4;
-      for (int g0 = sl; g0 < a.grid; g0 += UP_S * UP_MAXL) {
-        float4 v[UP_MAXL];
-#pragma unroll
-        for (int u = 0; u < UP_MAXL; ++u) {
-          const int gg = g0 + u * UP_S;
-          v[u] = gg < a.grid ? sp[(int64_t)gg * NQ] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < UP_MAXL; ++u) add4(acc, v[u]);
-      }
+  const int tid = threadIdx.x, blk = blockIdx.x;
+#define USTAMP(k) \
+  if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+  USTAMP(0);
+
+  if (blk < NB_CONV) {
+    // ---------------- role CONV
+    const int cl = tid & (UP_C - 1), sl = tid / UP_C;
+    // wave 0 owns params blk*64 + tid (16 float4 columns): prefetch p / m now
+    const int pi = blk * (UP_C * 4) + tid;
+    float p0 = 0.f, m0 = 0.f;
+    if (a.apply_sgd && tid < 64) {
+      p0 = a.params[min(pi, NP - 1)];
+      m0 = a.momentum[min(pi, NP - 1)];
     }
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    // Loads are unconditional from a clamped address and masked afterwards: a
+    // per-element "load or zero" select makes hipcc branch around every load
+    // and wait vmcnt(0) each time (dependent round trips instead of one).
+    // chunk blk of the slab is [WG][16 float4]: contiguous for this block
+    const float4* sp = reinterpret_cast<const float4*>(a.slab) + (int64_t)blk * a.grid * UP_C + cl;
+    for (int g0 = sl; g0 < a.grid; g0 += UP_S * UP_MAXL) {
+      float4 v[UP_MAXL];
+#pragma unroll
+      for (int u = 0; u < UP_MAXL; ++u) v[u] = sp[(int64_t)min(g0 + u * UP_S, a.grid - 1) * UP_C];
+#pragma unroll
+      for (int u = 0; u < UP_MAXL; ++u)
+        if (g0 + u * UP_S < a.grid) add4(acc, v[u]);
+    }
+    USTAMP(1);
     part[sl][cl] = acc;
     __syncthreads();
+    USTAMP(2);
     if (sl < 4) {
       float4 t = part[sl * 8][cl];
 #pragma unroll
       for (int q = 1; q < 8; ++q) add4(t, part[sl * 8 + q][cl]);
-      part2[sl][cl] = t;
+      *reinterpret_cast<float4*>(&part2[sl][4 * cl]) = t;
     }
-  }
-  __syncthreads();
-  if (sl == 0 && q4 < NQ) {
-    float4 gs;
-    if (from_slab) {
-      gs = part2[0][cl];
-      add4(gs, part2[1][cl]);
-      add4(gs, part2[2][cl]);
-      add4(gs, part2[3][cl]);
-    } else {
-      gs = reinterpret_cast<const float4*>(a.grad_in)[q4];
+    __syncthreads();
+    USTAMP(3);
+    if (tid < 64 && pi < CNP) {
+      const float g = (part2[0][tid] + part2[1][tid]) + (part2[2][tid] + part2[3][tid]);
+      finish_param<T>(a, pi, g, first, p0, m0);
     }
-    if (!a.apply_sgd) {
-      reinterpret_cast<float4*>(a.grad_out)[q4] = gs;
-    } else {
-      if (a.grad_out) reinterpret_cast<float4*>(a.grad_out)[q4] = gs;
-      float4 pv = reinterpret_cast<const float4*>(a.params)[q4];
-      float4 mv = a.mom != 0.f && !first ? reinterpret_cast<const float4*>(a.momentum)[q4]
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-      float* pp = &pv.x;
-      float* mm = &mv.x;
-      const float* gg = &gs.x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float gj = gg[j] + a.weight_decay * pp[j];
-        float d = gj;
-        if (a.mom != 0.f) {
-          const float bj = first ? gj : fmaf(a.mom, mm[j], (1.f - a.dampening) * gj);
-          mm[j] = bj;
-          d = a.nesterov ? fmaf(a.mom, bj, gj) : bj;
-        }
-        pp[j] = fmaf(-a.lr, d, pp[j]);
-        write_images<T>(a.wimg, 4 * q4 + j, pp[j]);
+    USTAMP(4);
+    if (blk == 0 && loss_parts && tid < 64) {
+      // loss / accuracy partials: lane-strided sums, then a fixed butterfly
+      float s0 = 0.f, s1 = 0.f;
+      for (int q = tid; q < nparts; q += 64) {
+        s0 += loss_parts[2 * q];
+        s1 += loss_parts[2 * q + 1];
       }
-      reinterpret_cast<float4*>(a.params)[q4] = pv;
-      if (a.mom != 0.f) reinterpret_cast<float4*>(a.momentum)[q4] = mv;
+      s0 = wave_sum(s0);
+      s1 = wave_sum(s1);
+      if (tid == 0) {
+        loss_acc[0] += s0;
+        loss_acc[1] += s1;
+      }
+    }
+  } else {
+    // ---------------- role FC: one 16x16 tile of [dW | db] per wave
+    const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
+    const int tile = (blk - NB_CONV) * (UP_NT / 64) + wave;
+    if (tile < FC_TILES) {
+      const bool fc1 = tile < FC1_TILES;
+      const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
+      const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
+      const int a_off = fc1 ? V_DZ1 : V_DLOG, b_off = fc1 ? V_P2 : V_H;
+      const int o = mt * 16 + l16, i = nt * 16 + l16;  // A row (out feature) / B col (in feature)
+      // this lane's 4 outputs (C rows 4*kq + r, column i) and their p / m
+      int pidx[4];
+      float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oo = mt * 16 + 4 * kq + r;
+        pidx[r] = (oo < rows && i <= cols)
+                      ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
+                             : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
+                      : -1;
+        if (a.apply_sgd) {
+          pp[r] = a.params[max(pidx[r], 0)];
+          pm[r] = a.momentum[max(pidx[r], 0)];
+        }
+      }
+      f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+      // K = batch; 16x16x4 f32 MFMA: lane holds A[o][s0 + 4u + kq] and B[s0 + 4u + kq][i]
+      for (int s0 = 0; s0 < B; s0 += 64) {
+        float av[16], bv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int s = s0 + 4 * u + kq;
+          const bool ok = s < B;
+          // unconditional loads from clamped addresses, masked after (see role CONV)
+          const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
+          const float ra = rowc[a_off + min(o, rows - 1)];
+          const float rb = rowc[b_off + min(i, cols - 1)];
+          av[u] = (ok && o < rows) ? ra : 0.f;
+          bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
+        }
+        // keep all 32 loads in flight before the first MFMA (otherwise the
+        // scheduler interleaves them and waits on each pair in turn)
+        __builtin_amdgcn_sched_barrier(0);
+        USTAMP(1);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], c, 0, 0, 0);
+      }
+      USTAMP(2);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (pidx[r] >= 0) finish_param<T>(a, pidx[r], c[r], first, pp[r], pm[r]);
+      USTAMP(4);
     }
   }
-  // loss / accuracy partials (fixed order) -> running totals
-  // (wave 0 of block 0: lane-strided partial sums, then a fixed butterfly)
-  if (loss_parts && blockIdx.x == 0 && threadIdx.x < 64) {
-    float s0 = 0.f, s1 = 0.f;
-    for (int q = threadIdx.x; q < nparts; q += 64) {
-      s0 += loss_parts[2 * q];
-      s1 += loss_parts[2 * q + 1];
-    }
-    s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    if (threadIdx.x == 0) {
-      loss_acc[0] += s0;
-      loss_acc[1] += s1;
-    }
-  }
+
   if (a.apply_sgd) {
     // Device counters.  cursor / rng_offset are never read by this kernel, so
-    // block 0 bumps them directly.  step[0] is read by every block only when
-    // dampening != 0 (the one case where torch's "first step: buf = g" differs
-    // from a zero-initialised buffer); then the last block to take a ticket
-    // bumps it, otherwise block 0 does -- no 342-way atomic on the hot path.
+    // one thread bumps them directly.  step[0] is read by every block only when
+    // dampening != 0; then the last block to take a ticket bumps it.
     if (a.dampening != 0.f) {
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (tid == 0) {
         const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
         if (t == (int)gridDim.x - 1) {
           a.ticket[0] = 0;
           if (a.step) a.step[0] += 1;
         }
       }
-    } else if (blockIdx.x == 0 && threadIdx.x == 0 && a.step) {
+    } else if (blk == 0 && tid == 0 && a.step) {
       a.step[0] += 1;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blk == 0 && tid == 0) {
       if (a.cursor) a.cursor[0] += 1;
       if (a.rng_offset) a.rng_offset[0] += 1;
     }
   }
 }
 
+// SGD from an already-reduced gradient (DDP: after the all-reduce).
+template <typename T>
+__global__ void lenet_sgd_kernel(LenetUpdateArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
+  if (i < NP) finish_param<T>(a, i, a.grad_in[i], first, a.params[i], a.momentum[i]);
+  if (a.dampening != 0.f) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int t = atomicAdd(a.ticket, 1);
+      if (t == (int)gridDim.x - 1) {
+        a.ticket[0] = 0;
+        if (a.step) a.step[0] += 1;
+      }
+    }
+  } else if (i == 0 && a.step) {
+    a.step[0] += 1;
+  }
+  if (i == 0) {
+    if (a.cursor) a.cursor[0] += 1;
+    if (a.rng_offset) a.rng_offset[0] += 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 int64_t lenet_wimg_elems() { return I_END; }
 int64_t lenet_param_count() { return NP; }
+int64_t lenet_conv_param_count() { return CNP_PAD; }
+int64_t lenet_vec_len() { return VEC; }
 
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   if (a.B <= 0 || a.grid <= 0 || a.grid > a.B) return hipErrorInvalidValue;
@@ -753,8 +848,15 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
 
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
                                hipStream_t s) {
+  if (a.apply_sgd && a.grad_in) {
+    CSED_DISPATCH_MFMA(a.mfma_dtype, {
+      hipLaunchKernelGGL(lenet_sgd_kernel<scalar_t>, dim3(cdiv(NP, 256)), dim3(256), 0, s, a);
+    });
+    return hipGetLastError();
+  }
+  if (!a.vslab || a.B <= 0) return hipErrorInvalidValue;
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
-    hipLaunchKernelGGL(lenet_update_kernel<scalar_t>, dim3(cdiv(NP / 4, UP_C)), dim3(UP_C * UP_S), 0, s, a,
+    hipLaunchKernelGGL(lenet_update_kernel<scalar_t>, dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab, a.B,
                        loss_parts, nparts, loss_acc);
   });
   return hipGetLastError();

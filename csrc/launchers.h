@@ -132,7 +132,8 @@ struct LenetTrainArgs {
   int rank_stride;           // rank id (decorrelates dropout masks across ranks)
   const uint16_t* wimg;      // packed 16-bit weight images
   const float* params;       // flat fp32 master params [21840]
-  float* slab;               // [grid, 21840] per-workgroup partial grads
+  float* slab;               // [grid, 5280] per-workgroup partial conv grads
+  float* vslab;              // [B, 464] per-sample fc vectors (P2 | dZ1 | H | dlogits)
   float* loss_acc;           // [grid, 2] per-workgroup (loss sum, correct count)
   float grad_scale;          // 1 / (global batch)
   float mean, std_;
@@ -146,11 +147,14 @@ struct LenetTrainArgs {
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s);
 int64_t lenet_wimg_elems();
 int64_t lenet_param_count();
+int64_t lenet_conv_param_count();  // 5280: conv1.w, conv1.b, conv2.w, conv2.b
+int64_t lenet_vec_len();           // 464 floats of per-sample fc vectors
 // Fused slab reduce + SGD + weight-image refresh + counter bump.
 // apply_sgd = 0: write the reduced gradient to grad_out (DDP: all-reduce next).
 // apply_sgd = 1: grad = grad_in if given (after the all-reduce) else the slab sum.
 struct LenetUpdateArgs {
   const float* slab; int grid;
+  const float* vslab; int B;         // per-sample fc vectors of the step and their count
   const float* grad_in;
   float* grad_out;
   float* params; float* momentum; uint16_t* wimg;
@@ -159,6 +163,7 @@ struct LenetUpdateArgs {
   int64_t* cursor; int64_t* rng_offset;
   int apply_sgd;
   int mfma_dtype;
+  uint64_t* dbg;      // optional [blocks, 8] s_memrealtime stamps (diagnostics)
 };
 // loss_parts [nparts, 2] are summed in a fixed order into loss_acc[2] (optional).
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,

@@ -35,14 +35,7 @@ def test_fused_gradient_matches_reference(dt, tol, B, grid):
                             drop_p=0.0, grid=grid)
     order = torch.randperm(256)[:B]
     eng.set_epoch_order(order)
-    g = torch.empty(21840, device=DEV)
-    ops = torch.ops.csed
-    ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, B, 0, eng.wimg,
-                    eng.flat.data, eng.slab, eng.loss_parts, 1.0 / B, MNIST_MEAN, MNIST_STD, 0.0, 1, None, grid,
-                    eng.mfma)
-    ops.lenet_update(eng.slab, grid, None, g, eng.flat.data, eng.momentum_buf, eng.wimg, 0.01, 0.5, 0.0, 0.0,
-                     False, eng.step_count, eng.ticket, None, None, False, eng.loss_parts, grid, eng.loss_acc,
-                     eng.mfma)
+    g = eng.gradient()
     torch.cuda.synchronize()
     x, t = _ref_batch(data, order, dt)
     ref.eval()  # dropout off, same as drop_p = 0
@@ -98,13 +91,7 @@ def test_fused_matches_modular(dt):
     order = torch.randperm(256)[:B]
     eng = FusedLeNetTrainer(net, data, global_batch=B, compute_dtype=dt, drop_p=0.0)
     eng.set_epoch_order(order)
-    g = torch.empty(21840, device=DEV)
-    ops = torch.ops.csed
-    ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, B, 0, eng.wimg,
-                    eng.flat.data, eng.slab, eng.loss_parts, 1.0 / B, MNIST_MEAN, MNIST_STD, 0.0, 1, None, B,
-                    eng.mfma)
-    ops.lenet_update(eng.slab, B, None, g, eng.flat.data, eng.momentum_buf, eng.wimg, 0.01, 0.5, 0.0, 0.0, False,
-                     eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
+    g = eng.gradient()
     gm = _modular_grads(net, data, order, dt)
     off = 0
     for name, p in net.named_parameters():
@@ -140,13 +127,7 @@ def test_fused_sgd_step_and_counters():
     p0 = eng.flat.data.clone()
     eng.set_epoch_order(torch.arange(128))
     # gradient of the first batch through the reduce-only path
-    g = torch.empty(21840, device=DEV)
-    ops = torch.ops.csed
-    ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, 32, 0, eng.wimg,
-                    eng.flat.data, eng.slab, eng.loss_parts, 1.0 / 32, MNIST_MEAN, MNIST_STD, 0.0, 1, None, 32,
-                    eng.mfma)
-    ops.lenet_update(eng.slab, 32, None, g, eng.flat.data, eng.momentum_buf, eng.wimg, 0.05, 0.5, 0.0, 0.0, False,
-                     eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
+    g = eng.gradient()
     eng.step()
     torch.cuda.synchronize()
     torch.testing.assert_close(eng.flat.data, p0 - 0.05 * g, rtol=1e-5, atol=1e-6)

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist  # noqa: E402
-from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNIST_MEAN, MNIST_STD  # noqa: E402
+
 from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer  # noqa: E402
 from csed_514_project_distributed_training_using_pytorch_amd.models import Net  # noqa: E402
 
@@ -30,9 +30,7 @@ def main():
     eng.set_epoch_order(torch.randperm(4096))
     dbg = torch.zeros(grid * 16, dtype=torch.long, device=dev)
     for _ in range(20):
-        torch.ops.csed.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, B, 0,
-                                   eng.wimg, eng.flat.data, eng.slab, eng.loss_parts, 1.0 / B, MNIST_MEAN,
-                                   MNIST_STD, 0.5, 1, eng.rng_offset, grid, eng.mfma, dbg)
+        eng.gradient(grid, dbg)
     torch.cuda.synchronize()
     st = dbg.view(grid, 16).cpu().double()
     # order: 12 = kernel start, 0..10 = stage starts, 11 = after all samples
