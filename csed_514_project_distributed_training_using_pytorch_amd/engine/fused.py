@@ -31,9 +31,15 @@ from ..ops import _native
 from ..parallel.comm import DistContext
 from ..utils.flat import FlatParams
 
-WIMG_ELEMS = 61312  # 16-bit weight images, see csrc/kernels/lenet_fused.hip (I_END)
-CONV_PARAMS = 5312  # conv1.w/b + conv2.w/b (5280) per WG, in 83 chunks of 64 floats (CNP_PAD)
-VEC_LEN = 464       # per-sample fc vectors P2 | dZ1 | H | dlogits (VEC)
+
+
+def layout() -> tuple[int, int, int]:
+    """Buffer sizes of the fused kernels, from the extension (csrc/kernels/lenet_fused.hip):
+    16-bit weight-image elements (I_END), conv slab row per workgroup (CNP_PAD: conv1.w/b +
+    conv2.w/b = 5280 floats in 64-float chunks) and per-sample fc vector length (VEC)."""
+    wimg, conv, vec, nparams = (int(v) for v in torch.ops.csed.lenet_layout())
+    assert nparams == N_PARAMS
+    return wimg, conv, vec
 
 
 class FusedLeNetTrainer:
@@ -71,10 +77,12 @@ class FusedLeNetTrainer:
         if broadcast_init and self.world > 1:
             dist.broadcast(self.flat.data, src=0)  # the DDP-constructor parameter sync (CS4)
         self.momentum_buf = torch.zeros_like(self.flat.data)
-        self.wimg = torch.zeros(WIMG_ELEMS, dtype=torch.int16, device=dev)
+        wimg_elems, conv_params, vec_len = layout()
+        # zero-initialised: padding rows / columns of the images must stay zero
+        self.wimg = torch.zeros(wimg_elems, dtype=torch.int16, device=dev)
         # per-WG conv partial gradients and per-sample fc vectors (see lenet_fused.hip)
-        self.slab = torch.empty((self._max_grid(), CONV_PARAMS), dtype=torch.float32, device=dev)
-        self.vslab = torch.zeros((self.B, VEC_LEN), dtype=torch.float32, device=dev)
+        self.slab = torch.empty((self._max_grid(), conv_params), dtype=torch.float32, device=dev)
+        self.vslab = torch.zeros((self.B, vec_len), dtype=torch.float32, device=dev)
         self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(2, dtype=torch.float32, device=dev)  # running (loss sum, correct)
         self.step_count = torch.zeros(1, dtype=torch.long, device=dev)

@@ -5,6 +5,7 @@
 // kernel(s) on the current PyTorch HIP stream.  No op allocates, copies to
 // host or synchronises, so every op is safe inside torch.cuda.graph capture
 // (= hipStreamBeginCapture).
+#include <vector>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
@@ -269,7 +270,12 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 }
 
 // ----------------------------------------------------------- fused lenet
-int64_t lenet_wimg_elems() { return csed::lenet_wimg_elems(); }
+// Buffer sizes the fused LeNet kernels expect: [weight-image elements, conv
+// slab row (floats per workgroup), per-sample vector length, flat params].
+std::vector<int64_t> lenet_layout() {
+  return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
+          csed::lenet_param_count()};
+}
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
   dev(params, "params"); dev(wimg, "wimg");
@@ -356,6 +362,7 @@ void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order,
 }  // namespace
 
 TORCH_LIBRARY(csed, m) {
+  m.def("lenet_layout() -> int[]", &lenet_layout);
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
         "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "

@@ -15,25 +15,31 @@
 //
 // Matrix work runs on v_mfma_f32_16x16x32_{bf16,f16}:
 //   conv1 fwd   : [576 px x 25] . [25 x 10]        36 tiles, 1 K-step
-//   conv2 fwd   : [64 px x 250] . [250 x 20]       4x2 tiles, 8 K-steps (one tile per wave)
+//   conv2 fwd   : [64 px x 400] . [400 x 20]       4x2 tiles, 13 K-steps (one tile per wave)
 //   fc1 fwd     : [1 x 320] . [320 x 50]           4 tiles (row 0 live), 10 K-steps
-//   fc1 dX      : 320 x 50 VALU dot products from the LDS F1 image
+//   fc1 dX      : [1 x 50] . [50 x 320]            20 tiles, 2 K-steps; the B operand is the
+//                 fc1 image read column-wise with ds_read_b64_tr_b16 (no transposed copy)
 //   conv2 wgrad : [20 x 64 px] . [64 px x 251]     2x16 tiles (col 250 = bias grad)
-//   conv2 dgrad : [144 px x 500] . [500 x 10]      9 tiles, 16 K-steps (tile 8 split over waves)
+//   conv2 dgrad : [144 px x 600] . [600 x 10]      9 tiles, 19 K-steps (tile 8 split over waves)
 //   conv1 wgrad : [10 x 576 px] . [576 px x 26]    1x2 tiles (col 25 = bias grad), 18 K-steps
-// im2col operands are gathered from LDS through int16 k->offset tables read
-// 8 at a time (ds_read_b128), so a gathered fragment costs 1 + 8 LDS reads
-// and no integer division.  The pool-fused pixel order (m = 4*window +
-// dy*2+dx) puts each 2x2 window in one lane's four accumulators (C row =
-// 4*(lane>>4) + reg): max-pool, argmax, bias, ReLU and the Dropout2d scale
-// are register-only epilogues.
+// The two convolutions whose im2col operand would be a gather (conv2 fwd, conv2
+// dgrad) read it from HWC images instead ([pos][channel], channels padded to a
+// multiple of 8, spatially zero-padded for the dgrad), with K ordered (tap,
+// channel): every 8-wide K slice of a fragment is then one ds_read_b128 at a
+// per-(K-step, lane-group) offset from a small table.  conv1 and the wgrads
+// read contiguous runs and need no table.  The pool-fused pixel order (m =
+// 4*window + dy*2+dx) puts each 2x2 window in one lane's four accumulators (C
+// row = 4*(lane>>4) + reg): max-pool, argmax, bias, ReLU and the Dropout2d
+// scale are register-only epilogues.  Every stage issues all of its LDS reads
+// before its first MFMA: no branches inside the unrolled K loops.
 //
-// Weight-image layout (16-bit, offsets in elements; all 16-B aligned):
+// Weight-image layout (16-bit, offsets in elements; all 16-B aligned); each
+// operand holds its live rows and one zero row that padding rows are clamped to:
 //   W1C  [16][32]   conv1  B operand  (k = kh*5+kw)
-//   W2C  [32][264]  conv2  B operand  (k = ic*25+kh*5+kw), padded rows
-//   W2D  [16][520]  conv2 dgrad B     (k' = oc*25 + (4-kh)*5 + (4-kw))
-//   F1   [64][328]  fc1 B operand     (rows = out features)
-//   F1T  [320][72]  reserved (fc1 dX runs on the VALU from the F1 image in LDS)
+//   W2C  [21][424]  conv2  B operand  (k = (kh*5+kw)*16 + ic)
+//   W2D  [11][616]  conv2 dgrad B     (k = ((4-kh)*5 + (4-kw))*24 + oc)
+//   F1   [51][328]  fc1 B operand     (rows = out features; read transposed for dX)
+// The W2C | W2D | F1 block is copied to LDS by LDS-DMA (global_load_lds_dwordx4).
 // fp32 values used as-is from the flat parameter buffer: all biases and fc2.
 //
 // Flat parameter order (= Net.state_dict() order, 21,840 floats):
@@ -48,8 +54,19 @@ namespace lenet {
 constexpr int NP = 21840;
 constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O_F1B = 21280,
               O_F2W = 21330, O_F2B = 21830;
-constexpr int I_W1C = 0, I_W2C = 512, I_W2D = 8960, I_F1 = 17280, I_F1T = 38272, I_END = 61312;
-constexpr int LD_W2C = 264, LD_W2D = 520, LD_F1 = 328, LD_F1T = 72;
+// 16-bit weight images.  Each operand keeps only its live rows plus ONE zero
+// row; fragment reads of padding rows are clamped onto that zero row.
+constexpr int C2_ICP = 16;  // conv2 fwd HWC: 10 input channels padded to 2 groups of 8
+constexpr int C2_KS = 13;   // conv2 fwd K-steps: 25 taps x 16 channels = 400 -> 416
+constexpr int DG_OCP = 24;  // dgrad HWC: 20 channels padded to 3 groups of 8
+constexpr int DG_KS = 19;   // dgrad K-steps: 25 taps x 24 channels = 600 -> 608
+constexpr int LD_W2C = 424, LD_W2D = 616, LD_F1 = 328;
+constexpr int R_W2C = 20, R_W2D = 10, R_F1 = 50;  // live rows; row R_* is the zero row
+constexpr int I_W1C = 0, I_W2C = 512;
+constexpr int I_W2D = I_W2C + (R_W2C + 1) * LD_W2C;  // 9416
+constexpr int I_F1 = I_W2D + (R_W2D + 1) * LD_W2D;   // 16192
+// padded so the LDS copy is whole 512-thread x 16-byte rounds
+constexpr int I_END = I_W2C + ((I_F1 + (R_F1 + 1) * LD_F1 - I_W2C + 4095) / 4096) * 4096;  // 33280
 constexpr int LD_DC2 = 72, LD_DC1 = 584;
 constexpr int NT = 512, NW = 8;
 // conv partial-gradient slab: params [0, CNP) = conv1.w, conv1.b, conv2.w, conv2.b
@@ -59,38 +76,45 @@ constexpr int CNP_PAD = (CNP + 63) / 64 * 64;  // slab row: 83 chunks of 64 floa
 constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;
 
 // LDS carve (bytes); every region 16-B aligned
-constexpr int S_W2C = 0;                              // u16 32*264
-constexpr int S_W2D = S_W2C + 32 * LD_W2C * 2;        // u16 16*520
-constexpr int S_F1 = S_W2D + 16 * LD_W2D * 2;         // u16 64*328 fc1 weight image
+constexpr int S_W2C = 0;                              // u16 21*424  conv2 B operand [oc][tap*16+ic]
+constexpr int S_W2D = (I_W2D - I_W2C) * 2;            // u16 11*616  dgrad B operand [ic][tap'*24+oc]
+constexpr int S_F1 = (I_F1 - I_W2C) * 2;              // u16 51*328  fc1 weight image [o][i]
 // W2C | W2D | F1 are contiguous here exactly as in the global image: one flat copy
-constexpr int WIMG_LDS_U4 = (I_F1T - I_W2C) / 8;      // 16-byte vectors to stage
-constexpr int S_X = S_F1 + 64 * LD_F1 * 2;            // u16 784 (+16 pad)
+constexpr int WIMG_LDS_U4 = (I_END - I_W2C) / 8;      // 16-byte vectors to stage
+constexpr int S_X = (I_END - I_W2C) * 2;              // u16 784 (+16 pad)
 constexpr int S_P1 = S_X + 800 * 2;                   // u16 1440   [ic][12][12]
 constexpr int S_I1 = S_P1 + 1440 * 2;                 // u8 1440    argmax in window
 constexpr int S_P2 = S_I1 + 1440;                     // u16 320    [oc][4][4] = fc1 input
 constexpr int S_I2 = S_P2 + 320 * 2;                  // u8 320
-constexpr int S_DC2 = S_I2 + 320;                     // u16 32*72  dL/dconv2 [oc][pix]
-constexpr int S_DC2P = S_DC2 + 32 * LD_DC2 * 2;       // u16 20*256 same, zero-padded [oc][16][16]
-constexpr int S_DC1 = S_DC2P + 20 * 256 * 2;          // u16 16*584 dL/dconv1 [oc][pix]
-constexpr int S_KO2 = S_DC1 + 16 * LD_DC1 * 2;        // i16 256    conv2 k -> P1 offset
-constexpr int S_KOD = S_KO2 + 256 * 2;                // i16 512    dgrad k' -> DC2P offset
-constexpr int S_DZ1B = S_KOD + 512 * 2;               // u16 64     dZ1 as the MFMA A row
+constexpr int S_P1H = S_I2 + 320;                     // u16 144*16 P1 again, HWC [12][12][16]
+constexpr int S_DC2 = S_P1H + 144 * C2_ICP * 2;       // u16 32*72  dL/dconv2 [oc][pix]
+constexpr int S_DC2H = S_DC2 + 32 * LD_DC2 * 2;       // u16 256*24 same, HWC, zero-padded [16][16][24]
+constexpr int S_DC1 = S_DC2H + 256 * DG_OCP * 2;      // u16 16*584 dL/dconv1 [oc][pix]
+constexpr int S_COFF = S_DC1 + 16 * LD_DC1 * 2;       // i16 4*16   conv2 (K-step, lane group) -> P1H offset
+constexpr int S_DOFF = S_COFF + 4 * 16 * 2;           // i16 4*24   dgrad (K-step, lane group) -> DC2H offset
+constexpr int S_DZ1B = S_DOFF + 4 * 24 * 2;           // u16 64     dZ1 as the MFMA A row
 constexpr int S_F = S_DZ1B + 64 * 2;                  // f32 scratch
-constexpr int F_D2S = 0, F_D1S = 32, F_H = 96, F_DLOG = 160, F_DZ1 = 176, F_DP2 = 240, F_PAR = 560,
-              F_RED = 1152, F_LAB = 3200, F_END = 3204;
+constexpr int F_D2S = 0, F_D1S = 32, F_H = 96, F_LOGIT = 160, F_PAR = 176, F_RED = 768, F_END = 2816;
 // fp32 params cached in LDS (offsets inside F_PAR): c1b 0, c2b 10, f1b 30, f2b 80, f2w 90 (500) -> 590
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 constexpr int S_TOTAL = S_F + F_END * 4;
-static_assert(S_W2D % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
-static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_DC2 % 16 == 0 && S_DC2P % 16 == 0, "align");
-static_assert(S_DC1 % 16 == 0 && S_KO2 % 16 == 0 && S_KOD % 16 == 0 && S_DZ1B % 16 == 0, "align");
-static_assert(S_F % 16 == 0 && S_TOTAL <= 160 * 1024, "lds");
-static_assert(S_W2D == (I_W2D - I_W2C) * 2 && S_F1 == (I_F1 - I_W2C) * 2, "LDS image must mirror wimg");
+static_assert(S_W2D % 16 == 0 && S_F1 % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
+static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_P1H % 16 == 0 && S_DC2 % 16 == 0 && S_DC2H % 16 == 0, "align");
+static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B % 16 == 0, "align");
+static_assert(S_F % 16 == 0 && (F_RED * 4) % 16 == 0 && S_TOTAL <= 160 * 1024, "lds");
+static_assert(WIMG_LDS_U4 % NT == 0, "whole LDS-DMA rounds");
+static_assert(C2_KS * 32 <= LD_W2C && 25 * C2_ICP <= C2_KS * 32, "conv2 K");
+static_assert(DG_KS * 32 <= LD_W2D && 25 * DG_OCP <= DG_KS * 32, "dgrad K");
 }  // namespace lenet
 
 using namespace lenet;
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
 
 // Diagnostic stage stamps (a.dbg non-null): thread 0 of each workgroup records
 // s_memtime at each stage start of its first sample.  Only for profiling builds
@@ -104,6 +128,19 @@ template <typename T>
 __device__ __forceinline__ unsigned short h16(float v) { return bits_of<T>((T)v); }
 template <typename T>
 __device__ __forceinline__ float f16v(unsigned short b) { return (float)of_bits<T>(b); }
+
+// ds_read_b64_tr_b16: lanes 4q+p of each 16-lane group address row q, columns
+// 4p..4p+3 of a 4x16 block; lane i of the group receives column i (row q in
+// element q).  EXEC must be all ones (the gather crosses lanes).
+__device__ __forceinline__ s16x4 lds_read_tr16(const unsigned short* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+  return ((int64_t)hi << 32) | (uint32_t)lo;
+}
 
 // conv2 dgrad epilogue for one (input channel, P1 pixel): relu gate, then the
 // pool1 backward scatter of the 2x2 window (argmax position gets the value).
@@ -133,43 +170,51 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   uint8_t* I1 = sm + S_I1;
   unsigned short* P2 = (unsigned short*)(sm + S_P2);
   uint8_t* I2 = sm + S_I2;
+  unsigned short* P1H = (unsigned short*)(sm + S_P1H);
   unsigned short* DC2 = (unsigned short*)(sm + S_DC2);
-  unsigned short* DC2P = (unsigned short*)(sm + S_DC2P);
+  unsigned short* DC2H = (unsigned short*)(sm + S_DC2H);
   unsigned short* DC1 = (unsigned short*)(sm + S_DC1);
-  short* KO2 = (short*)(sm + S_KO2);
-  short* KOD = (short*)(sm + S_KOD);
+  short* COFF = (short*)(sm + S_COFF);
+  short* DOFF = (short*)(sm + S_DOFF);
   unsigned short* DZ1B = (unsigned short*)(sm + S_DZ1B);
   unsigned short* F1s = (unsigned short*)(sm + S_F1);
   float* Fs = (float*)(sm + S_F);
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
-  float* DLOG = Fs + F_DLOG;
-  float* DZ1 = Fs + F_DZ1;
-  float* DP2 = Fs + F_DP2;
+  float* LOGIT = Fs + F_LOGIT;
   float* PAR = Fs + F_PAR;
   float* RED = Fs + F_RED;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l16 = lane & 15, kb = 8 * (lane >> 4);
+  const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
   const int G = gridDim.x, g = blockIdx.x;
   const float inv_std = 1.f / a.std_;
   const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
+  const int nsamp = g < a.B ? (a.B - g + G - 1) / G : 0;
+  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
+  auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
   if (a.dbg && tid == 0) a.dbg[g * 16 + 12] = __builtin_amdgcn_s_memtime();
   // ---------------- once per workgroup: weight images, offset tables, fp32 params -> LDS
   // register-resident conv1 weight fragment, reused for every sample of this WG
   frag fb1;
+  // sample pipeline registers: this sample's 4 pixels per thread and label, the
+  // row indices of the next 64 samples (lane s) and their labels
+  uint32_t px = 0;
+  int lab = 0, labv = 0;
+  int64_t rowv = 0;
   {
-    // Every global load of the preamble (weight images, fp32 params, the conv1
-    // fragment) is issued before the first wait: one memory round trip.
-    constexpr int PER = (WIMG_LDS_U4 + NT - 1) / NT;
+    // W2C | W2D | F1 straight into LDS by LDS-DMA: each wave-instruction moves
+    // 1 KB to a wave-uniform base + lane*16, so the image stays lane-linear
     const uint4* src = reinterpret_cast<const uint4*>(a.wimg + I_W2C);
-    uint4 v[PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) v[u] = src[min(tid + u * NT, WIMG_LDS_U4 - 1)];  // unconditional: no branches
+    for (int u = 0; u < WIMG_LDS_U4 / NT; ++u)
+      __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * NT + tid)),
+                                       (lds_void*)(sm + S_W2C + (u * NT + wave * 64) * 16), 16, 0, 0);
     // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, one per thread)
     int pi = O_F2W + tid - 90;
     if (tid < 10) pi = O_C1B + tid;
@@ -179,26 +224,32 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     const float pv0 = a.params[pi];
     const float pv1 = a.params[O_F2W + min(tid + NT, 589) - 90];
     fb1 = *reinterpret_cast<const frag*>(a.wimg + I_W1C + l16 * 32 + kb);
+    // the first sample (cursor -> row -> pixels, label: scalar chain) and the
+    // row indices of samples 0..63 (one per lane), behind the weight loads
+    if (nsamp > 0) {
+      const int64_t row0 = perm_at(0);
+      lab = (int)a.labels[row0];
+      px = reinterpret_cast<const uint32_t*>(a.images + row0 * 784)[min(tid, 195)];
+      rowv = perm_at(min(lane, nsamp - 1));
+    }
     // work that needs no loaded data overlaps the loads
-    if (tid < 256) {
-      const int k = tid, ic = k / 25, r = k % 25;
-      KO2[k] = (short)(k < 250 ? ic * 144 + (r / 5) * 12 + (r % 5) : 0);
+    if (tid < 64) {
+      // conv2 A-fragment offset of K-step ks for lane group q: K slice kg = 4*ks + q
+      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: K >= 400 meets zero weights)
+      const int q = tid >> 4, ks = tid & 15;
+      const int kg = min(4 * ks + q, 49), tap = kg >> 1;
+      COFF[tid] = (short)(((tap / 5) * 12 + tap % 5) * C2_ICP + (kg & 1) * 8);
+    } else if (tid < 160) {
+      // dgrad: K slice kg covers channels 8*(kg%3) .. +7 of tap kg/3 (K >= 600: zero weights)
+      const int q = (tid - 64) / 24, ks = (tid - 64) - 24 * q;
+      const int kg = min(4 * ks + q, 74), tap = kg / 3, ocg = kg - 3 * tap;
+      DOFF[tid - 64] = (short)((((tap / 5) * 16) + tap % 5) * DG_OCP + ocg * 8);
     }
+    // P1H | DC2 | DC2H | DC1 are contiguous: zero their padding once with 16-B stores
     {
-      const int k = tid, co = k / 25, r = k % 25;
-      KOD[k] = (short)(k < 500 ? co * 256 + (r / 5) * 16 + (r % 5) : 0);
-    }
-    // DC2 | DC2P | DC1 are contiguous: zero their padding once with 16-B stores
-    {
-      constexpr int NZ = (S_KO2 - S_DC2) / 16;
-      uint4* z = reinterpret_cast<uint4*>(sm + S_DC2);
+      constexpr int NZ = (S_COFF - S_P1H) / 16;
+      uint4* z = reinterpret_cast<uint4*>(sm + S_P1H);
       for (int i = tid; i < NZ; i += NT) z[i] = make_uint4(0, 0, 0, 0);
-    }
-    uint4* dst = reinterpret_cast<uint4*>(W2c);
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int i = tid + u * NT;
-      if (i < WIMG_LDS_U4) dst[i] = v[u];
     }
     if (tid < 590) PAR[tid] = pv0;
     if (tid + NT < 590) PAR[tid + NT] = pv1;
@@ -211,6 +262,16 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     const int k = kb + j;
     koff1[j] = k < 25 ? (k / 5) * 28 + (k % 5) : 0;
   }
+  // conv2 wgrad B columns k = (wave + 8*jj)*16 + l16 = ic*25 + kh*5 + kw: P1 offset
+  int kwb[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int k = min((wave + 8 * jj) * 16 + l16, 249), ic = k / 25, r = k % 25;
+    kwb[jj] = ic * 144 + (r / 5) * 12 + (r % 5);
+  }
+  // conv1 wgrad B column k = (wave&1)*16 + l16 = kh*5 + kw: X offset
+  const int kc1 = (wave & 1) * 16 + l16;
+  const int koffc1 = kc1 < 25 ? (kc1 / 5) * 28 + (kc1 % 5) : 0;
 
   // ---------------- per-workgroup gradient accumulators (registers)
   f32x4 acc_c2[2][2];   // conv2 wgrad: M-tiles (oc) 0,1 x N-tiles (k) wave, wave+8
@@ -224,17 +285,22 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   // accumulating 16,500 products per sample here, each sample's vectors are written
   // to the vector slab and lenet_update forms the sums as one GEMM over the batch.
 
-  const int nsamp = (a.B - g + G - 1) / G;
   for (int s = 0; s < nsamp; ++s) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
-    __syncthreads();  // previous sample's readers of Xs / P1 / DC1 are done
-    // ---------------- stage 0: gather + normalise the image, dropout masks
+    __syncthreads();  // LDS-DMA drained (first pass); previous sample's readers are done
+    // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
+    // then start the next sample's loads (consumed one sample later)
     STAMP(0);
-    const int64_t row = a.perm[(a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + b];
+    const int t_lab = s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63);
     {
-      const uint8_t* img = a.images + row * 784;
-      for (int i = tid; i < 784; i += NT) Xs[i] = h16<T>(((float)img[i] * (1.f / 255.f) - a.mean) * inv_std);
+      if (tid < 196) {
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = h16<T>(((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std);
+        *reinterpret_cast<u16x4*>(Xs + 4 * tid) = o;
+      }
       if (tid < 70) {
         float sc = 1.f;
         if (TRAIN) {
@@ -244,32 +310,49 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         if (tid < 20) D2S[tid] = sc;
         else D1S[tid - 20] = sc;
       }
-      if (tid == 0) Fs[F_LAB] = __int_as_float((int)a.labels[row]);
+      if (s + 1 < nsamp) {
+        const int sn = s + 1;
+        if ((sn & 63) == 0) rowv = perm_at(min(sn + lane, nsamp - 1));
+        if (s == 0 || (sn & 63) == 0) labv = (int)a.labels[rowv];
+        const int64_t rn = readlane64(rowv, sn & 63);
+        px = reinterpret_cast<const uint32_t*>(a.images + rn * 784)[min(tid, 195)];
+      }
     }
     __syncthreads();
 
-    // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1
+    // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, P1H
     STAMP(1);
+    {
+      // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
+      u16x8 raw[5];
 #pragma unroll
-    for (int it = 0; it < 5; ++it) {  // 36 tiles over 8 waves, unrolled so all gathers issue up front
-      const int mt = wave + it * NW;
-      if (mt >= 36) break;
-      const int m = mt * 16 + l16;
-      const int p = m >> 2, q = m & 3;
-      const int pb = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
-      u16x8 raw;
+      for (int it = 0; it < 5; ++it) {
+        const int mt = min(wave + it * NW, 35);
+        const int m = mt * 16 + l16;
+        const int p = m >> 2, q = m & 3;
+        const int pb = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) raw[j] = Xs[pb + koff1[j]];
-      const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
-      if (l16 < 10) {
-        float best = c[0];
-        int bi = 0;
+        for (int j = 0; j < 8; ++j) raw[it][j] = Xs[pb + koff1[j]];
+      }
+      const float cb = PAR[P_C1B + min(l16, 9)];
 #pragma unroll
-        for (int r = 1; r < 4; ++r)
-          if (c[r] > best) { best = c[r]; bi = r; }
-        const int w = mt * 4 + (lane >> 4);
-        P1[l16 * 144 + w] = h16<T>(fmaxf(best + PAR[P_C1B + l16], 0.f));
-        I1[l16 * 144 + w] = (uint8_t)bi;
+      for (int it = 0; it < 5; ++it) {
+        const int mt = wave + it * NW;
+        if (it < 4 || mt < 36) {
+          const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw[it]), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
+          if (l16 < 10) {
+            float best = c[0];
+            int bi = 0;
+#pragma unroll
+            for (int r = 1; r < 4; ++r)
+              if (c[r] > best) { best = c[r]; bi = r; }
+            const int w = mt * 4 + kq;  // pooled position py*12 + px
+            const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
+            P1[l16 * 144 + w] = hv;
+            I1[l16 * 144 + w] = (uint8_t)bi;
+            P1H[w * C2_ICP + l16] = hv;
+          }
+        }
       }
     }
     __syncthreads();
@@ -277,20 +360,20 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
     STAMP(2);
     {
+      // A[m][k = tap*16 + ic] = P1H[pos(m) + shift(tap)][ic]; one b128 per K slice
       const int mt = wave & 3, nt = wave >> 2;
       const int m = mt * 16 + l16;
       const int p = m >> 2, q = m & 3;
-      const int pb = (2 * (p >> 2) + (q >> 1)) * 12 + 2 * (p & 3) + (q & 1);
+      const int oy = 2 * (p >> 2) + (q >> 1), ox = 2 * (p & 3) + (q & 1);
+      const unsigned short* arow = P1H + (oy * 12 + ox) * C2_ICP;
+      const unsigned short* wrow = W2c + min(nt * 16 + l16, R_W2C) * LD_W2C + kb;
+      const s16x8 co0 = *reinterpret_cast<const s16x8*>(COFF + kq * 16);
+      const s16x8 co1 = *reinterpret_cast<const s16x8*>(COFF + kq * 16 + 8);
       f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-      const unsigned short* wrow = W2c + (nt * 16 + l16) * LD_W2C + kb;
-#pragma unroll 4
-      for (int ks = 0; ks < 8; ++ks) {
-        const s16x8 o = *reinterpret_cast<const s16x8*>(KO2 + ks * 32 + kb);
-        u16x8 raw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[j] = P1[pb + o[j]];
-        c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), *reinterpret_cast<const frag*>(wrow + ks * 32), c);
-      }
+      for (int ks = 0; ks < C2_KS; ++ks)
+        c = Mfma<T>::mma(*reinterpret_cast<const frag*>(arow + (ks < 8 ? co0[ks] : co1[ks - 8])),
+                         *reinterpret_cast<const frag*>(wrow + ks * 32), c);
       const int oc = nt * 16 + l16;
       if (oc < 20) {
         float best = c[0];
@@ -298,7 +381,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
         for (int r = 1; r < 4; ++r)
           if (c[r] > best) { best = c[r]; bi = r; }
-        const int w = mt * 4 + (lane >> 4);
+        const int w = mt * 4 + kq;
         const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
         P2[oc * 16 + w] = hv;
         I2[oc * 16 + w] = (uint8_t)bi;
@@ -310,12 +393,12 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3)
     STAMP(3);
     if (wave < 4) {
+      const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
       f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-      const unsigned short* wrow = F1s + (wave * 16 + l16) * LD_F1 + kb;
-#pragma unroll 5
+#pragma unroll
       for (int ks = 0; ks < 10; ++ks) {
-        const frag fa = l16 == 0 ? *reinterpret_cast<const frag*>(P2 + ks * 32 + kb) : zfrag;
-        c = Mfma<T>::mma(fa, *reinterpret_cast<const frag*>(wrow + ks * 32), c);
+        const frag pa = *reinterpret_cast<const frag*>(P2 + ks * 32 + kb);
+        c = Mfma<T>::mma(l16 == 0 ? pa : zfrag, *reinterpret_cast<const frag*>(wrow + ks * 32), c);
       }
       if (lane < 16) {
         const int o = wave * 16 + lane;
@@ -328,10 +411,11 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     }
     __syncthreads();
 
-    // ---------------- stage 4: fc2 + log_softmax + NLL + dlogits (wave 0)
+    // ---------------- stage 4: fc2 + log_softmax + NLL, then dlogits and the fc1
+    // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
     STAMP(4);
     if (wave == 0) {
-      const int t = __float_as_int(Fs[F_LAB]);
+      const int t = t_lab;
       // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12), then a
       // fixed-order 2-step butterfly inside each aligned 4-lane group
       float zp = 0.f;
@@ -346,147 +430,159 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       }
       zp += __shfl_xor(zp, 1, 64);
       zp += __shfl_xor(zp, 2, 64);
-      const float zc = __shfl(zp, (lane & 15) * 4, 64);
-      const float logit = lane < 10 ? zc + PAR[P_F2B + lane] : -INFINITY;
-      const float mx = wave_max(logit);
-      const float e = lane < 10 ? __expf(logit - mx) : 0.f;
-      const float se = wave_sum(e);
+      if (lane < 40 && (lane & 3) == 0) LOGIT[lane >> 2] = zp + PAR[P_F2B + (lane >> 2)];
+      __builtin_amdgcn_wave_barrier();
+      // every lane reads all 10 logits (same-wave LDS round trip, no barrier) and
+      // does the softmax locally: no cross-lane reductions
+      float lg[10];
+#pragma unroll
+      for (int c = 0; c < 10; ++c) lg[c] = LOGIT[c];
+      float mx = lg[0];
+      int amax = 0;
+#pragma unroll
+      for (int c = 1; c < 10; ++c)
+        if (lg[c] > mx) { mx = lg[c]; amax = c; }  // first index attaining the max (torch argmax)
+      float se = 0.f, lt = 0.f;
+#pragma unroll
+      for (int c = 0; c < 10; ++c) {
+        se += __expf(lg[c] - mx);
+        lt = c == t ? lg[c] : lt;
+      }
       const float lse = mx + __logf(se);
-      const float lp = logit - lse;
-      // first index attaining the max (torch argmax tie rule)
-      const unsigned long long ismax = __ballot(lane < 10 && logit == mx);
-      const int amax = __ffsll((long long)ismax) - 1;
-      const float lt = __shfl(lp, t, 64);
       if (lane == 0) {
-        loss_sum += -lt;
+        loss_sum += lse - lt;
         correct += (amax == t) ? 1.f : 0.f;
       }
-      if (write_logp && lane < 10) logp_out[(int64_t)b * 10 + lane] = lp;
-      if (TRAIN && lane < 16) {
-        const float dl = lane < 10 ? (__expf(lp) - (lane == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
-        DLOG[lane] = dl;
-        vs[V_DLOG + lane] = dl;
+      const float mylg = LOGIT[min(lane, 9)];
+      if (write_logp && lane < 10) logp_out[(int64_t)b * 10 + lane] = mylg - lse;
+      if (TRAIN) {
+        if (lane < 16) vs[V_DLOG + lane] = lane < 10 ? (__expf(mylg - lse) - (lane == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
+        // dZ1[o] = gate(o) * sum_c dl[c] * W2[c][o]   (lane o; every lane has all dl[c])
+        const int o = min(lane, 49);
+        float dh = 0.f;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+          const float dl = (__expf(lg[c] - lse) - (c == t ? 1.f : 0.f)) * a.grad_scale;
+          dh = fmaf(dl, PAR[P_F2W + c * 50 + o], dh);
+        }
+        const float dz = (lane < 50 && Hs[o] > 0.f) ? dh * D1S[o] : 0.f;
+        DZ1B[lane] = h16<T>(dz);
+        if (lane < 50) vs[V_DZ1 + lane] = dz;
       }
     }
     if (!TRAIN) continue;
     __syncthreads();
 
-    // ---------------- stage 5: fc2 backward, fc1 relu/dropout gate
+    // ---------------- stage 5: dP2 = dZ1 . W1 on the MFMA (B = fc1 image read
+    // transposed), fused with the pool2 / relu / Dropout2d backward -> dC2 (2 layouts)
     STAMP(5);
     {
-      if (tid < 64) {
-        float dz = 0.f;
-        if (tid < 50) {
-          float dh = 0.f;
+      // A = dZ1 as row 0 (K = fc1 output o, 64 = 2 steps); tile t = output channel t of P2
+      const frag dz0 = *reinterpret_cast<const frag*>(DZ1B + kb);
+      const frag dz1 = *reinterpret_cast<const frag*>(DZ1B + 32 + kb);
+      const frag fa0 = l16 == 0 ? dz0 : zfrag, fa1 = l16 == 0 ? dz1 : zfrag;
+      // lane 4q+p reads rows o = ks*32 + kb + {0,4} + q (rows >= 50: the zero row)
+      const unsigned short* fc0 = F1s + min(kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
+      const unsigned short* fc1 = F1s + min(kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
+      const unsigned short* fc2 = F1s + min(32 + kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
+      const unsigned short* fc3 = F1s + min(32 + kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
 #pragma unroll
-          for (int c = 0; c < 10; ++c) dh = fmaf(DLOG[c], PAR[P_F2W + c * 50 + tid], dh);
-          dz = Hs[tid] > 0.f ? dh * D1S[tid] : 0.f;
-          vs[V_DZ1 + tid] = dz;
+      for (int tt = 0; tt < 3; ++tt) {
+        const int t = wave + NW * tt;  // wave-uniform: EXEC stays full for the transposed reads
+        if (t < 20) {
+          const s16x4 r0 = lds_read_tr16(fc0 + t * 16), r1 = lds_read_tr16(fc1 + t * 16);
+          const s16x4 r2 = lds_read_tr16(fc2 + t * 16), r3 = lds_read_tr16(fc3 + t * 16);
+          f32x4 c = Mfma<T>::mma(fa0, __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7)),
+                                 f32x4{0.f, 0.f, 0.f, 0.f});
+          c = Mfma<T>::mma(fa1, __builtin_bit_cast(frag, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7)), c);
+          if (lane < 16) {
+            // C row 0: lane w holds dP2[t][w]; unpool window w of channel t
+            const int pi = t * 16 + lane;
+            const float gv = f16v<T>(P2[pi]) > 0.f ? c[0] * D2S[t] : 0.f;
+            const int bi = I2[pi];
+            const int oh0 = 2 * (lane >> 2), ow0 = 2 * (lane & 3);
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) {
+              const int oh = oh0 + (pos >> 1), ow = ow0 + (pos & 1);
+              const unsigned short hb = pos == bi ? h16<T>(gv) : (unsigned short)0;
+              DC2[t * LD_DC2 + oh * 8 + ow] = hb;
+              DC2H[((oh + 4) * 16 + ow + 4) * DG_OCP + t] = hb;
+            }
+          }
         }
-        DZ1[tid] = dz;
       }
     }
     __syncthreads();
 
-    // ---------------- stage 6: dP2 = W1^T dZ1 (VALU over the LDS fc1 image)
+    // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers, and
+    // conv2 dgrad -> dP1 -> relu/pool1 backward -> dC1
     STAMP(6);
     {
-      // dP2[i] = sum_o dZ1[o] * W1[o][i]: one input feature per thread, lanes read
-      // consecutive columns of the LDS fc1 image (conflict-free), 50-long FMA chain
-      if (tid < 320) {
-        float d[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-        const unsigned short* col = F1s + tid;
-#pragma unroll
-        for (int o = 0; o < 50; ++o) d[o % 5] = fmaf(DZ1[o], f16v<T>(col[o * LD_F1]), d[o % 5]);
-        DP2[tid] = ((d[0] + d[1]) + (d[2] + d[3])) + d[4];
-      }
-    }
-    __syncthreads();
-
-    // ---------------- stage 7: pool2 / relu / Dropout2d backward -> dC2 (two layouts)
-    STAMP(7);
-    for (int i = tid; i < 1280; i += NT) {
-      const int oc = i >> 6, pix = i & 63;
-      const int oh = pix >> 3, ow = pix & 7;
-      const int w = (oh >> 1) * 4 + (ow >> 1);
-      const int pos = (oh & 1) * 2 + (ow & 1);
-      const int pi = oc * 16 + w;
-      const float gv = (I2[pi] == pos && f16v<T>(P2[pi]) > 0.f) ? DP2[pi] * D2S[oc] : 0.f;
-      const unsigned short hb = h16<T>(gv);
-      DC2[oc * LD_DC2 + pix] = hb;
-      DC2P[oc * 256 + (oh + 4) * 16 + (ow + 4)] = hb;
-    }
-    __syncthreads();
-
-    // ---------------- stage 8: conv2 wgrad (+bias column 250), accumulate in registers
-    STAMP(8);
-    {
       const unsigned short one = h16<T>(1.f);
+      frag fa[2][2];
+      u16x8 raw[2][2];
 #pragma unroll
       for (int ps = 0; ps < 2; ++ps) {
-        const frag fa0 = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + ps * 32 + kb);
-        const frag fa1 = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + ps * 32 + kb);
+        fa[ps][0] = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + ps * 32 + kb);
+        fa[ps][1] = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + ps * 32 + kb);
         const int ohr = ((ps * 32 + kb) >> 3) * 12;
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int k = (wave + 8 * jj) * 16 + l16;
-          u16x8 raw;
-          if (k < 250) {
-            const int base = KO2[k] + ohr;
+        for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) raw[j] = P1[base + j];
-          } else {
-            const unsigned short v = k == 250 ? one : (unsigned short)0;
+          for (int j = 0; j < 8; ++j) raw[ps][jj][j] = P1[kwb[jj] + ohr + j];
+      }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) raw[j] = v;
-          }
-          const frag fb = __builtin_bit_cast(frag, raw);
-          acc_c2[0][jj] = Mfma<T>::mma(fa0, fb, acc_c2[0][jj]);
-          acc_c2[1][jj] = Mfma<T>::mma(fa1, fb, acc_c2[1][jj]);
+      for (int jj = 0; jj < 2; ++jj) {
+        const int k = (wave + 8 * jj) * 16 + l16;
+        const unsigned short cst = k == 250 ? one : (unsigned short)0;  // bias column / padding
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+          u16x8 rv = raw[ps][jj];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rv[j] = k < 250 ? rv[j] : cst;
+          const frag fb = __builtin_bit_cast(frag, rv);
+          acc_c2[0][jj] = Mfma<T>::mma(fa[ps][0], fb, acc_c2[0][jj]);
+          acc_c2[1][jj] = Mfma<T>::mma(fa[ps][1], fb, acc_c2[1][jj]);
         }
       }
     }
-    // ---------------- stage 9: conv2 dgrad -> dP1 -> relu/pool1 backward -> dC1
-    STAMP(9);
     {
-      const unsigned short* wrow = W2d + l16 * LD_W2D + kb;
-      // full tile `wave` (pixels 16*wave .. +15)
-      {
-        const int m = wave * 16 + l16;
-        const int pb = (m / 12) * 16 + (m % 12);
-        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-        for (int ks = 0; ks < 16; ++ks) {
-          const s16x8 o = *reinterpret_cast<const s16x8*>(KOD + ks * 32 + kb);
-          u16x8 raw;
+      // dP1[px][ic] = sum_{tap, oc} DC2H[px + shift(tap)][oc] * W2D[ic][tap*24 + oc]:
+      // full tile `wave` (pixels 16*wave ..) plus K-steps ks = wave + 8j of tile 8
+      const s16x8 dof0 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24);
+      const s16x8 dof1 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 8);
+      const s16x8 dof2 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 16);
+      const unsigned short* wrow = W2d + min(l16, R_W2D) * LD_W2D + kb;
+      const int mw = wave * 16 + l16, m8 = 128 + l16;
+      const unsigned short* aw = DC2H + ((mw / 12) * 16 + mw % 12) * DG_OCP;
+      const unsigned short* a8 = DC2H + ((m8 / 12) * 16 + m8 % 12) * DG_OCP;
+      // tile-8 share: 3 K-steps, the third only for waves 0-2 (others read the zero row)
+      frag f8a[3], f8b[3];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) raw[j] = DC2P[pb + o[j]];
-          c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), *reinterpret_cast<const frag*>(wrow + ks * 32), c);
-        }
-        if (l16 < 10) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dgrad_out<T>(DC1, P1, I1, l16, wave * 16 + 4 * (lane >> 4) + r, c[r]);
-        }
+      for (int j = 0; j < 3; ++j) {
+        const int ks = wave + 8 * j;
+        const int off = DOFF[kq * 24 + min(ks, DG_KS - 1)];
+        f8a[j] = *reinterpret_cast<const frag*>(a8 + off);
+        f8b[j] = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 32 : W2d + R_W2D * LD_W2D + kb);
       }
-      // tile 8 (pixels 128..143): K-steps 2*wave, 2*wave+1 here, reduced below
-      {
-        const int m = 128 + l16;
-        const int pb = (m / 12) * 16 + (m % 12);
-        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 cw = f32x4{0.f, 0.f, 0.f, 0.f}, c8 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int ks = 2 * wave + kk;
-          const s16x8 o = *reinterpret_cast<const s16x8*>(KOD + ks * 32 + kb);
-          u16x8 raw;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) raw[j] = DC2P[pb + o[j]];
-          c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), *reinterpret_cast<const frag*>(wrow + ks * 32), c);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) RED[wave * 256 + (4 * (lane >> 4) + r) * 16 + l16] = c[r];
+      for (int ks = 0; ks < DG_KS; ++ks) {
+        const int off = ks < 8 ? dof0[ks] : (ks < 16 ? dof1[ks - 8] : dof2[ks - 16]);
+        cw = Mfma<T>::mma(*reinterpret_cast<const frag*>(aw + off), *reinterpret_cast<const frag*>(wrow + ks * 32),
+                          cw);
       }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) c8 = Mfma<T>::mma(f8a[j], f8b[j], c8);
+      if (l16 < 10) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dgrad_out<T>(DC1, P1, I1, l16, wave * 16 + 4 * kq + r, cw[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) RED[wave * 256 + (4 * kq + r) * 16 + l16] = c8[r];
     }
     __syncthreads();
+    STAMP(7);
     if (tid < 256) {
       const int rr = tid >> 4, ci = tid & 15;
       if (ci < 10) {
@@ -498,32 +594,29 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     }
     __syncthreads();
 
-    // ---------------- stage 10: conv1 wgrad (+bias column 25), accumulate in registers
-    STAMP(10);
+    // ---------------- stage 8: conv1 wgrad (+bias column 25), accumulate in registers
+    // (tile wave&1, K-steps ps = (wave>>1) + 4i: 18 steps over 4 wave pairs)
+    STAMP(8);
     {
-      const int nt = wave & 1;
-      const int k = nt * 16 + l16;
-      const unsigned short one = h16<T>(1.f);
-      const int koff = k < 25 ? (k / 5) * 28 + (k % 5) : 0;
+      const unsigned short cst = kc1 == 25 ? h16<T>(1.f) : (unsigned short)0;
+      frag fa[5];
+      u16x8 raw[5];
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int ps = (wave >> 1) + 4 * i;
-        if (ps < 18) {
-          const int p0 = ps * 32 + kb;
-          const frag fa = *reinterpret_cast<const frag*>(DC1 + l16 * LD_DC1 + p0);
-          const int oh = p0 / 24, ow0 = p0 - oh * 24;
-          u16x8 raw;
-          if (k < 25) {
-            const int base = oh * 28 + ow0 + koff;
+        const int ps = min((wave >> 1) + 4 * i, 17);
+        const int p0 = ps * 32 + kb;
+        fa[i] = *reinterpret_cast<const frag*>(DC1 + l16 * LD_DC1 + p0);
+        const int oh = p0 / 24, ow0 = p0 - oh * 24;
+        const int base = oh * 28 + ow0 + koffc1;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) raw[j] = Xs[base + j];
-          } else {
-            const unsigned short v = k == 25 ? one : (unsigned short)0;
+        for (int j = 0; j < 8; ++j) raw[i][j] = Xs[base + j];
+      }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) raw[j] = v;
-          }
-          acc_c1 = Mfma<T>::mma(fa, __builtin_bit_cast(frag, raw), acc_c1);
-        }
+      for (int i = 0; i < 5; ++i) {
+        u16x8 rv = raw[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rv[j] = kc1 < 25 ? rv[j] : cst;
+        if (i < 4 || wave < 4) acc_c1 = Mfma<T>::mma(fa[i], __builtin_bit_cast(frag, rv), acc_c1);
       }
     }
   }
@@ -586,9 +679,9 @@ __device__ __forceinline__ void write_images(unsigned short* wimg, int i, float 
   } else if (i >= O_C2W && i < O_C2B) {
     const int j = i - O_C2W;
     const int oc = j / 250, k = j % 250;
-    wimg[I_W2C + oc * LD_W2C + k] = h;
     const int ic = k / 25, r = k % 25, kh = r / 5, kw = r % 5;
-    wimg[I_W2D + ic * LD_W2D + oc * 25 + (4 - kh) * 5 + (4 - kw)] = h;
+    wimg[I_W2C + oc * LD_W2C + r * C2_ICP + ic] = h;
+    wimg[I_W2D + ic * LD_W2D + ((4 - kh) * 5 + (4 - kw)) * DG_OCP + oc] = h;
   } else if (i >= O_F1W && i < O_F1B) {
     const int j = i - O_F1W;
     const int o = j / 320, ii = j % 320;
@@ -878,7 +971,7 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   // into `out` (2*G floats); the caller reduces them in a fixed order.
   if (n <= 0) return hipSuccess;
   LenetTrainArgs a{};
-  a.images = images; a.labels = labels; a.perm = order; a.cursor = nullptr;
+  a.images = images; a.labels = labels; a.perm = order; a.cursor = nullptr; a.perm_len = n;
   a.B = (int)n; a.wimg = wimg; a.params = params; a.slab = nullptr; a.loss_acc = out;
   a.grad_scale = 0.f; a.mean = mean; a.std_ = std_; a.drop_p = 0.f; a.seed = 0; a.rng_offset = nullptr;
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
