@@ -57,6 +57,7 @@ constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O
 // 16-bit weight images.  Each operand keeps only its live rows plus ONE zero
 // row; fragment reads of padding rows are clamped onto that zero row.
 constexpr int C2_ICP = 16;  // conv2 fwd HWC: 10 input channels padded to 2 groups of 8
+constexpr int LD_P1H = 24;  // P1H position stride (elements): 12 dwords, conflict-free b128 rows
 constexpr int C2_KS = 13;   // conv2 fwd K-steps: 25 taps x 16 channels = 400 -> 416
 constexpr int DG_OCP = 24;  // dgrad HWC: 20 channels padded to 3 groups of 8
 constexpr int DG_KS = 19;   // dgrad K-steps: 25 taps x 24 channels = 600 -> 608
@@ -86,8 +87,8 @@ constexpr int S_P1 = S_X + 800 * 2;                   // u16 1440   [ic][12][12]
 constexpr int S_I1 = S_P1 + 1440 * 2;                 // u8 1440    argmax in window
 constexpr int S_P2 = S_I1 + 1440;                     // u16 320    [oc][4][4] = fc1 input
 constexpr int S_I2 = S_P2 + 320 * 2;                  // u8 320
-constexpr int S_P1H = S_I2 + 320;                     // u16 144*16 P1 again, HWC [12][12][16]
-constexpr int S_DC2 = S_P1H + 144 * C2_ICP * 2;       // u16 32*72  dL/dconv2 [oc][pix]
+constexpr int S_P1H = S_I2 + 320;                     // u16 144*24 P1 again, HWC [12][12][24] (16 used)
+constexpr int S_DC2 = S_P1H + 144 * LD_P1H * 2;       // u16 32*72  dL/dconv2 [oc][pix]
 constexpr int S_DC2H = S_DC2 + 32 * LD_DC2 * 2;       // u16 256*24 same, HWC, zero-padded [16][16][24]
 constexpr int S_DC1 = S_DC2H + 256 * DG_OCP * 2;      // u16 16*584 dL/dconv1 [oc][pix]
 constexpr int S_COFF = S_DC1 + 16 * LD_DC1 * 2;       // i16 4*16   conv2 (K-step, lane group) -> P1H offset
@@ -134,6 +135,14 @@ __device__ __forceinline__ float f16v(unsigned short b) { return (float)of_bits<
 // element q).  EXEC must be all ones (the gather crosses lanes).
 __device__ __forceinline__ s16x4 lds_read_tr16(const unsigned short* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+// An LDS index the compiler cannot relate to its neighbours: keeps a run of
+// 16-bit reads at a sliding (2-byte aligned) window as single ds_read_u16s
+// instead of one merged, misaligned ds_read_b128 (replayed at ~64 cycles).
+__device__ __forceinline__ int opaque(int x) {
+  asm("" : "+v"(x));
+  return x;
 }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
@@ -238,7 +247,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: K >= 400 meets zero weights)
       const int q = tid >> 4, ks = tid & 15;
       const int kg = min(4 * ks + q, 49), tap = kg >> 1;
-      COFF[tid] = (short)(((tap / 5) * 12 + tap % 5) * C2_ICP + (kg & 1) * 8);
+      COFF[tid] = (short)(((tap / 5) * 12 + tap % 5) * LD_P1H + (kg & 1) * 8);
     } else if (tid < 160) {
       // dgrad: K slice kg covers channels 8*(kg%3) .. +7 of tap kg/3 (K >= 600: zero weights)
       const int q = (tid - 64) / 24, ks = (tid - 64) - 24 * q;
@@ -350,7 +359,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
             P1[l16 * 144 + w] = hv;
             I1[l16 * 144 + w] = (uint8_t)bi;
-            P1H[w * C2_ICP + l16] = hv;
+            P1H[w * LD_P1H + l16] = hv;
           }
         }
       }
@@ -365,7 +374,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       const int m = mt * 16 + l16;
       const int p = m >> 2, q = m & 3;
       const int oy = 2 * (p >> 2) + (q >> 1), ox = 2 * (p & 3) + (q & 1);
-      const unsigned short* arow = P1H + (oy * 12 + ox) * C2_ICP;
+      const unsigned short* arow = P1H + (oy * 12 + ox) * LD_P1H;
       const unsigned short* wrow = W2c + min(nt * 16 + l16, R_W2C) * LD_W2C + kb;
       const s16x8 co0 = *reinterpret_cast<const s16x8*>(COFF + kq * 16);
       const s16x8 co1 = *reinterpret_cast<const s16x8*>(COFF + kq * 16 + 8);
@@ -529,7 +538,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) raw[ps][jj][j] = P1[kwb[jj] + ohr + j];
+          for (int j = 0; j < 8; ++j) raw[ps][jj][j] = P1[opaque(kwb[jj] + ohr + j)];
       }
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -609,7 +618,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         const int oh = p0 / 24, ow0 = p0 - oh * 24;
         const int base = oh * 28 + ow0 + koffc1;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[i][j] = Xs[base + j];
+        for (int j = 0; j < 8; ++j) raw[i][j] = Xs[opaque(base + j)];
       }
 #pragma unroll
       for (int i = 0; i < 5; ++i) {

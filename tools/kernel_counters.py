@@ -1,0 +1,52 @@
+"""Launch the fused step's two kernels N times each (no graph), for rocprofv3 --pmc runs.
+
+    rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU ... --output-format csv -d OUT -o run -- \
+        python3 tools/kernel_counters.py [B] [N]
+
+then `python tools/kernel_counters.py --summarize OUT/run_counter_collection.csv` prints the
+per-dispatch mean of every counter for lenet_train / lenet_update.
+"""
+import csv
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(B: int, n: int):
+    import torch
+
+    from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+    from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    eng = FusedLeNetTrainer(Net().to(dev), synthetic_mnist(4096, seed=1), global_batch=B)
+    eng.set_epoch_order(torch.randperm(4096))
+    for _ in range(n):
+        eng.step()
+    torch.cuda.synchronize()
+
+
+def summarize(path: str):
+    acc = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        name = r.get("Kernel_Name", "")
+        short = "lenet_train" if "lenet_train" in name else ("lenet_update" if "lenet_update" in name else None)
+        if short is None:
+            continue
+        acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, cs in acc.items():
+        print(f"== {k}")
+        for c, v in sorted(cs.items()):
+            print(f"  {c:28s} {sum(v) / len(v):14.1f}   (n={len(v)})")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--summarize":
+        for p in sys.argv[2:]:
+            summarize(p)
+    else:
+        run(int(sys.argv[1]) if len(sys.argv) > 1 else 64, int(sys.argv[2]) if len(sys.argv) > 2 else 200)
