@@ -123,6 +123,7 @@ def main() -> int:
         epoch_s = all_reduce_max(ctx, time.perf_counter() - te)
         val = {"val_loss": vloss / len(test), "val_acc": vcorrect / len(test)}
 
+    comm_err = eng.comm_errors()
     n = ctx.world_size
     value = args.steps * args.global_batch / elapsed
     base = BASELINE_EPOCH_S.get(n)
@@ -143,12 +144,18 @@ def main() -> int:
             "data": "synthetic (60000 x 1x28x28 uint8, class-conditional; random-init weights)",
             "config": {"model": "Net (ref src/model.py, 21,840 params)", "global_batch": args.global_batch,
                        "seq_len": None, "parallelism": f"dp{n}", "optimizer": "SGD lr=0.02 momentum=0.5",
-                       "engine": "fused HIP (lenet_train + lenet_update" + (" + RCCL all-reduce" if n > 1 else "")
-                                 + ")", "hip_graph": (not args.no_graph) and bool(eng.capture_comm_ok)},
+                       "engine": "fused HIP (lenet_train + lenet_update" + (" + gradient all-reduce" if n > 1 else "")
+                                 + ")", "hip_graph": (not args.no_graph) and bool(eng.capture_comm_ok),
+                       "allreduce": eng.allreduce_kind},
             "epoch_s": round(epoch_s, 4) if epoch_s is not None else None,
             "baseline_epoch_s": base,
             "train_loss_timed_rank0": round(loss_sum / max(1, args.steps * eng.B), 4),
         }
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc
+        if _ipc.LAST_TIMING:
+            rec["config"]["allreduce_select_us"] = _ipc.LAST_TIMING
+        if comm_err:
+            rec["comm_error"] = "IPC all-reduce timed out waiting for a peer: results invalid"
         if val:
             rec.update({k: round(v, 4) for k, v in val.items()})
         print(json.dumps(rec), flush=True)

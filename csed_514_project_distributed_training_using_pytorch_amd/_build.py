@@ -72,7 +72,7 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-r
 
 
 def _sources() -> tuple[list[Path], list[Path]]:
-    kernels = sorted((CSRC / "kernels").glob("*.hip"))
+    kernels = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "comm").glob("*.hip"))
     hosts = sorted(CSRC.glob("*.cpp"))
     return kernels, hosts
 

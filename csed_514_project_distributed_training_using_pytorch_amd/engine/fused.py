@@ -29,6 +29,7 @@ from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
 from ..parallel.comm import DistContext
+from ..parallel.ipc import make_allreduce
 from ..utils.flat import FlatParams
 
 
@@ -74,8 +75,13 @@ class FusedLeNetTrainer:
         self.flat = FlatParams(list(model.parameters()))
         if self.flat.numel != N_PARAMS:
             raise ValueError("FusedLeNetTrainer needs the reference Net architecture")
-        if broadcast_init and self.world > 1:
-            dist.broadcast(self.flat.data, src=0)  # the DDP-constructor parameter sync (CS4)
+        if broadcast_init and self.world > 1:  # the DDP-constructor parameter sync (CS4)
+            if self.ctx.backend == "nccl":
+                dist.broadcast(self.flat.data, src=0)
+            else:  # gloo bootstrap (tests): host copy
+                host = self.flat.data.cpu()
+                dist.broadcast(host, src=0)
+                self.flat.data.copy_(host)
         self.momentum_buf = torch.zeros_like(self.flat.data)
         wimg_elems, conv_params, vec_len = layout()
         # zero-initialised: padding rows / columns of the images must stay zero
@@ -92,8 +98,21 @@ class FusedLeNetTrainer:
         self.eval_parts = torch.zeros(2 * 256, dtype=torch.float32, device=dev)
         self.perm = torch.arange(self.B, dtype=torch.long, device=dev)
         self.repack()
+        # gradient all-reduce: the one-shot IPC kernel (csrc/comm) when every rank
+        # passes its self-test, else RCCL (see parallel/ipc.py)
+        self.allreduce = make_allreduce(self.ctx, N_PARAMS) if (self.comm and self.world > 1) else None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.capture_comm_ok: bool | None = None
+
+    @property
+    def allreduce_kind(self) -> str:
+        if not self.comm:
+            return "none"
+        return "ipc-oneshot" if self.allreduce is not None else "rccl"
+
+    def comm_errors(self) -> int:
+        """Nonzero if the IPC all-reduce ever timed out waiting for a peer (synchronous)."""
+        return self.allreduce.error() if self.allreduce is not None else 0
 
     def _max_grid(self) -> int:
         return max(self.grid, 1)
@@ -134,7 +153,10 @@ class FusedLeNetTrainer:
         if self.comm:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, self.flat.grad, *common, None, None, False,
                              self.loss_parts, grid, self.loss_acc, self.mfma)
-            dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
+            if self.allreduce is not None:
+                self.allreduce(self.flat.grad)
+            else:
+                dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
             ops.lenet_update(self.slab, grid, self.vslab, B, self.flat.grad, None, *common, cursor, self.rng_offset,
                              True, None, 0, None, self.mfma)
         else:

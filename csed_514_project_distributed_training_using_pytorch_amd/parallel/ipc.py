@@ -1,0 +1,194 @@
+"""One-shot gradient all-reduce over HIP-IPC peer mappings (native: csrc/comm/).
+
+Replaces, for the fused engine's single 87 KB gradient (ref
+src/train_dist.py:83 -> DDP Reducer all-reduce), the ring/tree collective by a
+kernel that reads every peer's buffer directly over its own xGMI link: one hop,
+all 7 links of an MI355X at once, no host work, graph-capturable.
+
+Bring-up is defensive.  Every rank creates its exchange buffer, the IPC handles
+are all-gathered over the existing process group, each rank maps its peers and
+runs a self-test: exact integer-valued sums over several rounds, the timeout
+error word, and bitwise agreement with the process group's own all-reduce.  The
+ranks then agree (MIN over the process group) and the path is enabled only if
+every rank passed; otherwise callers keep using RCCL.  In ``auto`` mode the two
+are then timed on the real buffer and the faster one is kept (the slowest
+rank's numbers decide, so all ranks agree).  ``CSED_ALLREDUCE`` = ``auto``
+(default) | ``ipc`` (use it; fail if unusable) | ``rccl`` (never try).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _native
+from .comm import DistContext
+
+
+# latencies measured by the last auto selection (us per call, max over ranks), for reports
+LAST_TIMING: dict | None = None
+
+
+def _gather_handles(ctx: DistContext, h: torch.Tensor) -> torch.Tensor:
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    mine = h.to(dev)
+    out = [torch.empty_like(mine) for _ in range(ctx.world_size)]
+    dist.all_gather(out, mine)
+    return torch.stack([t.cpu() for t in out]).contiguous()
+
+
+def _all_ok(ctx: DistContext, ok: bool) -> bool:
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+class IpcAllReduce:
+    """SUM all-reduce of one fp32 buffer of ``n`` elements across the process group.
+
+    Construction is split so that every rank issues the same collectives even when
+    a local step fails: :meth:`create` (local), :meth:`exchange` (collective:
+    all-gather of the handles), :meth:`open` (local).  Use :func:`make_allreduce`.
+    """
+
+    def __init__(self, ctx: DistContext, n: int, blocks: int = 32, timeout_s: float = 2.0):
+        self.ctx = ctx
+        self.n = int(n)
+        self.n_pad = (self.n + 3) // 4 * 4
+        self.blocks = int(blocks)
+        self.timeout_s = float(timeout_s)
+        self.id = -1
+        self.measured_us: dict | None = None
+        self._pad_in = self._pad_out = None
+        if self.n_pad != self.n:
+            self._pad_in = torch.zeros(self.n_pad, dtype=torch.float32, device=ctx.device)
+            self._pad_out = torch.zeros_like(self._pad_in)
+
+    def create(self) -> torch.Tensor:
+        """Allocate the exchange buffer; returns this rank's IPC handle (CPU uint8)."""
+        _native.require()
+        with torch.cuda.device(self.ctx.device):
+            self.id = int(torch.ops.csed.ipc_create(self.n_pad, self.blocks))
+            return torch.ops.csed.ipc_handle(self.id)
+
+    def exchange(self, handle: torch.Tensor) -> torch.Tensor:
+        return _gather_handles(self.ctx, handle)
+
+    def open(self, handles: torch.Tensor) -> None:
+        with torch.cuda.device(self.ctx.device):
+            torch.ops.csed.ipc_open(self.id, handles, self.ctx.rank)
+
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """out = sum over ranks of x (in place when ``out`` is None).  Graph-capturable."""
+        out = x if out is None else out
+        ops = torch.ops.csed
+        if self._pad_in is None:
+            ops.ipc_allreduce(self.id, x, out, self.timeout_s)
+        else:
+            self._pad_in[: self.n].copy_(x)
+            ops.ipc_allreduce(self.id, self._pad_in, self._pad_out, self.timeout_s)
+            out.copy_(self._pad_out[: self.n])
+        return out
+
+    def error(self, reset: bool = False) -> int:
+        return int(torch.ops.csed.ipc_error(self.id, reset))
+
+    def self_test(self, rounds: int = 4) -> bool:
+        """Exact sums of integer-valued data over several rounds (both slot parities),
+        no timeout, and bitwise agreement with the process group's all-reduce.
+
+        Every rank must call it.  The process-group reductions run first, so a local
+        failure in the IPC rounds cannot desynchronise the ranks' collectives; a rank
+        that fails before its kernel makes its peers time out (error word), not hang.
+        """
+        ctx = self.ctx
+        dev = ctx.device
+        idx = torch.arange(self.n, device=dev, dtype=torch.float32)
+        cases = []
+        pg_dev = dev if ctx.backend == "nccl" else torch.device("cpu")
+        for r in range(rounds):
+            x = torch.remainder(idx * (ctx.rank + 1) + r, 97.0)  # small integers: sums are exact in fp32
+            z = x.to(pg_dev, copy=True)
+            dist.all_reduce(z)
+            z = z.to(dev)
+            exact = sum(torch.remainder(idx * (k + 1) + r, 97.0) for k in range(ctx.world_size))
+            cases.append((x, z, exact))
+        try:
+            ok = True
+            for x, z, exact in cases:
+                y = self(x.clone())
+                ok &= bool(torch.equal(y, exact)) and bool(torch.equal(y, z))
+            torch.cuda.synchronize(dev)
+            ok &= self.error(reset=True) == 0
+        except Exception:
+            ok = False
+        return ok
+
+
+def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
+    """The IPC all-reduce if every rank can use it (see module docstring), else None.
+
+    Every rank runs the same sequence of collectives whatever fails locally:
+    create -> vote -> all-gather handles -> open -> vote -> self-test -> vote.
+    """
+    mode = os.environ.get("CSED_ALLREDUCE", "auto").lower()
+    if mode == "rccl" or not ctx.is_distributed or ctx.device.type != "cuda":
+        return None
+    ar = IpcAllReduce(ctx, n)
+    why = ""
+    handle = None
+    try:
+        handle = ar.create()
+    except Exception as e:
+        why = f"create: {type(e).__name__}: {e}"
+    ok = _all_ok(ctx, handle is not None)
+    if ok:
+        handles = ar.exchange(handle)
+        try:
+            ar.open(handles)
+        except Exception as e:
+            why, ok = f"open: {type(e).__name__}: {e}", False
+        ok = _all_ok(ctx, ok)
+    if ok:
+        ok = _all_ok(ctx, ar.self_test())
+        why = why or ("" if ok else "self-test mismatch or timeout on some rank")
+    if not ok:
+        if mode == "ipc":
+            raise RuntimeError(f"CSED_ALLREDUCE=ipc but the IPC all-reduce is unusable ({why or 'a peer failed'})")
+        return None
+    if mode == "auto" and ctx.backend == "nccl":
+        # keep whichever is faster on this machine (slowest rank decides, all ranks agree)
+        global LAST_TIMING
+        t_ipc, t_pg = _time_both(ctx, ar)
+        ar.measured_us = LAST_TIMING = {"ipc_us": round(t_ipc, 2), "rccl_us": round(t_pg, 2)}
+        if t_pg < t_ipc:
+            return None
+    return ar
+
+
+def _time_both(ctx: DistContext, ar: IpcAllReduce, calls: int = 50) -> tuple[float, float]:
+    """Per-call latency (us, max over ranks) of the IPC kernel and of the process group's
+    all-reduce on the same 87 KB buffer, eager launches back to back."""
+    dev = ctx.device
+    x = torch.randn(ar.n, device=dev)
+
+    def run(fn) -> float:
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier(device_ids=[dev.index])
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(calls):
+            fn()
+        b.record()
+        b.synchronize()
+        t = torch.tensor([a.elapsed_time(b) * 1e3 / calls], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_ipc = run(lambda: ar(x))
+    t_pg = run(lambda: dist.all_reduce(x))
+    return t_ipc, t_pg

@@ -1,0 +1,24 @@
+// Host API of the one-shot IPC all-reduce (csrc/comm/ipc_allreduce.hip).
+// No torch headers: the ATen-facing wrappers live in csrc/comm_bindings.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace csed {
+namespace comm {
+
+// Allocate an IPC-exportable (uncached) exchange buffer for up to n floats
+// (n % 4 == 0) on the current device; `blocks` workgroups per all-reduce.
+hipError_t ipc_create(int64_t n, int blocks, int* id_out);
+// Serialised hipIpcMemHandle_t of this rank's buffer (ipc_handle_bytes() bytes).
+hipError_t ipc_get_handle(int id, void* handle_out);
+int ipc_handle_bytes();
+// Map every peer's buffer; `handles` is [world][ipc_handle_bytes()] in rank order.
+hipError_t ipc_open(int id, const void* handles, int world, int rank);
+// out = sum over ranks of in (n floats, n % 4 == 0); in == out is allowed.
+hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double timeout_s, hipStream_t s);
+// Error word: nonzero if a wait ever timed out (synchronous read).
+hipError_t ipc_error(int id, int* err_out, bool reset);
+
+}  // namespace comm
+}  // namespace csed

@@ -1,0 +1,117 @@
+"""Native one-shot IPC all-reduce (csrc/comm/ipc_allreduce.hip, parallel/ipc.py).
+
+Two ranks share the box's single GPU: the handle exchange, the peer mapping,
+the flag protocol (both slot parities, graph replay) and the fused engine's
+data-parallel step all run for real; only the transport is local HBM rather
+than xGMI.  The bootstrap process group is gloo (CPU), as on a CPU-only host.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CSED_ALLREDUCE="ipc")
+        import torch.distributed as dist
+
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import DistContext
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.ipc import make_allreduce
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        ctx = DistContext(rank, world, 0, dev, "gloo")
+        res = {}
+        n = 21840
+        ar = make_allreduce(ctx, n)
+        res["enabled"] = ar is not None
+        # random data vs the process group's reduction (2 ranks: a + b in either order)
+        g = torch.Generator(device="cpu").manual_seed(100 + rank)
+        ok = True
+        for _ in range(5):
+            x = torch.randn(n, generator=g).to(dev)
+            ref = x.cpu().clone()
+            dist.all_reduce(ref)
+            y = ar(x.clone())
+            ok &= torch.equal(y.cpu(), ref)
+        res["eager"] = ok
+        # inside a graph: 3 calls per replay, new inputs each replay
+        buf = torch.zeros(n, device=dev)
+        out = [torch.zeros(n, device=dev) for _ in range(3)]
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            for k in range(3):
+                ar(buf + k, out[k])
+        ok = True
+        for rep in range(3):
+            x = torch.randn(n, generator=g)
+            buf.copy_(x.to(dev))
+            graph.replay()
+            torch.cuda.synchronize(dev)
+            for k in range(3):
+                ref = (x + k).clone()
+                dist.all_reduce(ref)
+                ok &= torch.allclose(out[k].cpu(), ref, rtol=0, atol=1e-5)
+        res["graph"] = ok
+        res["errors"] = ar.error()
+
+        # fused data-parallel engine: identical parameters on both ranks after graph steps
+        from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+        from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
+        from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
+
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(dev), synthetic_mnist(2048, seed=3), lr=0.05, global_batch=64, ctx=ctx)
+        smp = ShardSampler(2048, world, rank, shuffle=True, seed=42)
+        smp.set_epoch(0)
+        eng.set_epoch_order(smp.indices())
+        eng.run_steps(12, steps_per_graph=4)
+        torch.cuda.synchronize(dev)
+        p = eng.flat.data.cpu()
+        other = p.clone()
+        dist.broadcast(other, src=0)
+        res["kind"] = eng.allreduce_kind
+        res["params_equal"] = torch.equal(p, other)
+        res["engine_errors"] = eng.comm_errors()
+        res["finite"] = bool(torch.isfinite(p).all())
+        q.put((rank, res))
+        dist.destroy_process_group()
+    except Exception as e:  # report, do not hang the parent
+        q.put((rank, {"exception": repr(e)}))
+
+
+def test_ipc_allreduce_two_ranks_one_gpu():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(2):
+        r, res = q.get(timeout=300)
+        results[r] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        res = results[r]
+        assert "exception" not in res, res
+        assert res["enabled"] and res["eager"] and res["graph"], res
+        assert res["errors"] == 0 and res["engine_errors"] == 0, res
+        assert res["kind"] == "ipc-oneshot" and res["params_equal"] and res["finite"], res
