@@ -237,12 +237,15 @@ class _Linear(torch.autograd.Function):
             dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
             _ops().gemm(dy2, w, dx, None, 1.0, 0.0, 0, 0.0, 0, 0, None, gate, gs, mf)
             dx = dx.view(*ctx.lead, x2.shape[1])
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if want_db:
+            db = torch.empty((w.shape[0],), device=w.device, dtype=torch.float32)
         if ctx.needs_input_grad[1]:
+            # dW = gate(dY)^T X; the bias gradient rides along as the GEMM's ones column
             dw = torch.empty(w.shape, device=w.device, dtype=torch.float32)
             _ops().gemm(dy2.t(), x2, dw, None, 1.0, 0.0, 0, 0.0, 0, 0, None,
-                        gate.t() if gate is not None else None, gs, mf)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.empty((w.shape[0],), device=w.device, dtype=torch.float32)
+                        gate.t() if gate is not None else None, gs, mf, db if want_db else None)
+        elif want_db:
             _ops().colsum(dy2, gate, gs, db, 0.0)
         return dx, dw, db, None, None, None, None, None, None
 

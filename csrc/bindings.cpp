@@ -177,7 +177,7 @@ void gate_bwd(const Tensor& dout, const Tensor& y, Tensor& dx, double s) {
 // arbitrary strides (e.g. .t() views); strides are read from the tensors.
 void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, double alpha, double beta,
           int64_t act, double drop_p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev,
-          const optional<Tensor>& gate, double gate_scale, int64_t mfma_dtype) {
+          const optional<Tensor>& gate, double gate_scale, int64_t mfma_dtype, const optional<Tensor>& rowsum) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2);
   TORCH_CHECK(A.size(1) == B.size(0) && C.size(0) == A.size(0) && C.size(1) == B.size(1), "gemm: shape mismatch");
@@ -201,6 +201,18 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
   a.act = (int)act; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset;
   a.offset_dev = optpt<int64_t>(offset_dev);
   a.mfma_dtype = mcode(mfma_dtype);
+  if (rowsum.has_value()) {
+    TORCH_CHECK(rowsum->scalar_type() == at::kFloat && rowsum->is_contiguous() && rowsum->numel() == a.M,
+                "gemm: rowsum must be fp32 [M]");
+    a.rowsum = rowsum->data_ptr<float>();
+  }
+  // split-K workspace (stream-ordered caching allocation: legal inside graph capture)
+  Tensor ws;
+  const int splits = csed::gemm_splits(a);
+  if (splits > 1) {
+    ws = at::empty({(int64_t)splits * a.M * (a.N + (a.rowsum ? 1 : 0))}, A.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+  }
   CHECK_HIP(csed::launch_gemm(a, cur_stream(A)));
 }
 
@@ -389,7 +401,8 @@ TORCH_LIBRARY(csed, m) {
   m.def("channel_mask(Tensor(a!) scale, float p, int seed, int offset, Tensor? offset_dev) -> ()");
   m.def("gate_bwd(Tensor dout, Tensor y, Tensor(a!) dx, float s) -> ()");
   m.def("gemm(Tensor A, Tensor B, Tensor(a!) C, Tensor? bias, float alpha, float beta, int act, float drop_p, "
-        "int seed, int offset, Tensor? offset_dev, Tensor? gate, float gate_scale, int mfma_dtype) -> ()");
+        "int seed, int offset, Tensor? offset_dev, Tensor? gate, float gate_scale, int mfma_dtype, "
+        "Tensor(b!)? rowsum=None) -> ()");
   m.def("colsum(Tensor x, Tensor? gate, float gate_scale, Tensor(a!) out, float beta) -> ()");
   m.def("conv2d_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, int pad, Tensor(b!)? idx, Tensor? chscale, "
         "int pool_k, int mfma_dtype) -> ()");

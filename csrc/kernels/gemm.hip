@@ -1,14 +1,27 @@
-// Strided small-GEMM on gfx950 MFMA (v_mfma_f32_16x16x32_{bf16,f16}).
+// Strided GEMM on gfx950 MFMA (v_mfma_f32_16x16x32_{bf16,f16}) for nn.Linear.
 //
-// Serves nn.Linear forward (fused bias / ReLU / dropout epilogue) and both
-// backward GEMMs (dX = dY.W, dW = dY^T.X with the ReLU+dropout gate fused into
-// the operand staging) -- ref src/model.py:12-13,19-21.
+// Serves the forward (fused bias / ReLU / dropout epilogue) and both backward
+// GEMMs: dX = dY.W and dW = dY^T.X with the ReLU+dropout gate of the forward
+// fused into the operand staging, plus the bias gradient as a "ones column":
+// with `rowsum` set the B operand gets a virtual extra column of 1.0, so
+// C[:, N] = sum_k A(m, k) falls out of the same MFMAs (ref src/model.py:12-13,
+// 19-21).
 //
 // Tiling: 64x64 block tile, BK = 32 (= one MFMA K), 256 threads = 4 waves as
 // 2(M) x 2(N); each wave owns a 32x32 sub-tile = 2x2 MFMA 16x16 fragments.
-// Operands are staged global -> registers -> LDS as 16-bit values ([row][k]
-// images with an 8-element pad: 80-B rows keep the 16-lane ds_read_b128
-// groups on distinct banks) and read back as 16-byte fragments.
+// Operands are loaded global -> registers with 16-byte vector loads along
+// whichever dimension is contiguous (k for row-major operands, rows for
+// transposed ones), converted/gated in registers and written to one of two LDS
+// buffers as [row][k] 16-bit images (8-element pad: 80-B rows keep the 16-lane
+// ds_read_b128 groups on distinct banks).  The next K-tile's global loads are
+// in flight while the current one is on the MFMAs: one barrier per K-tile.
+//
+// Split-K: when the M x N tile grid cannot fill the chip (the fc weight
+// gradients: M = 50, N = 320, K = batch), blockIdx.z splits K; each split
+// writes fp32 partials to a workspace and gemm_splitk_reduce sums them in a
+// fixed order and applies the epilogue (bitwise reproducible).
+#include <algorithm>
+
 #include "common.h"
 #include "dispatch.h"
 
@@ -17,7 +30,9 @@ namespace csed {
 namespace {
 constexpr int BM = 64, BN = 64, BK = 32, LDK = BK + 8;
 
-template <typename T>
+// operand staging modes (chosen on the host)
+enum : int { kScalar = 0, kKContig = 1, kRContig = 2 };
+
 __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
   switch (dt) {
     case kF32: return ((const float*)p)[i];
@@ -27,84 +42,187 @@ __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
   }
 }
 
-// Stage one 64 x 32 operand tile (rows = M or N index, cols = k) into LDS.
-// X(r, k) = X[r*s_r + k*s_k], optional gate X *= (G(r,k) > 0) * gs.
+// Eight operand values of one thread, in registers between load and LDS store:
+// packed 16-bit (8 x T in r[0]) when the operand already has the MFMA type,
+// else 8 floats in r[0..1].
+struct Raw {
+  float4 r[2];
+};
+
 template <typename T>
-__device__ __forceinline__ void stage_tile(unsigned short* lds, const void* X, int xdt, int64_t s_r,
-                                           int64_t s_k, const void* G, int gdt, float gs, int r0,
-                                           int R, int k0, int K) {
+__device__ __forceinline__ bool packed(int dt) {
+  constexpr int code = __is_same(T, __bf16) ? kBF16 : kF16;
+  return dt == code;
+}
+
+// Thread -> element mapping of a 64 x 32 tile:
+//   kKContig / kScalar : row = t >> 2, k = (t & 3) * 8 + j
+//   kRContig           : row = (t & 7) * 8 + j, k = t >> 3
+template <typename T>
+__device__ __forceinline__ void load_raw(Raw& raw, const void* X, int dt, int mode, int64_t s_r, int64_t s_k, int r0,
+                                         int R, int k0, int K) {
   const int t = threadIdx.x;
-  if (s_k == 1 || s_r != 1) {
-    // thread -> (row, 8 consecutive k)
-    const int r = t >> 2, kq = (t & 3) * 8;
-    const int gr = r0 + r;
+  const bool pk = packed<T>(dt);
+  if (mode == kKContig) {
+    const int gr = r0 + (t >> 2), gk = k0 + (t & 3) * 8;
+    if (gr < R && gk + 8 <= K) {
+      const int64_t off = (int64_t)gr * s_r + gk;
+      if (pk) {
+        raw.r[0] = *reinterpret_cast<const float4*>((const unsigned short*)X + off);
+      } else {  // fp32
+        raw.r[0] = *reinterpret_cast<const float4*>((const float*)X + off);
+        raw.r[1] = *reinterpret_cast<const float4*>((const float*)X + off + 4);
+      }
+      return;
+    }
+  } else if (mode == kRContig) {
+    const int gr = r0 + (t & 7) * 8, gk = k0 + (t >> 3);
+    if (gr + 8 <= R && gk < K) {
+      const int64_t off = gr + (int64_t)gk * s_k;
+      if (pk) {
+        raw.r[0] = *reinterpret_cast<const float4*>((const unsigned short*)X + off);
+      } else {
+        raw.r[0] = *reinterpret_cast<const float4*>((const float*)X + off);
+        raw.r[1] = *reinterpret_cast<const float4*>((const float*)X + off + 4);
+      }
+      return;
+    }
+  }
+  // scalar path (any layout / dtype, and the ragged edges of the vector modes)
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int gr, gk;
+    if (mode == kRContig) {
+      gr = r0 + (t & 7) * 8 + j;
+      gk = k0 + (t >> 3);
+    } else {
+      gr = r0 + (t >> 2);
+      gk = k0 + (t & 3) * 8 + j;
+    }
+    f[j] = (gr < R && gk < K) ? ld_any(X, dt, (int64_t)gr * s_r + (int64_t)gk * s_k) : 0.f;
+  }
+  if (pk) {
     u16x8 v;
 #pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bits_of<T>((T)f[j]);
+    raw.r[0] = __builtin_bit_cast(float4, v);
+  } else {
+    raw.r[0] = make_float4(f[0], f[1], f[2], f[3]);
+    raw.r[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ float raw_at(const Raw& raw, bool pk, int j) {
+  if (pk) return (float)of_bits<T>(__builtin_bit_cast(u16x8, raw.r[0])[j]);
+  const float4 q = raw.r[j >> 2];
+  return (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+}
+
+// Convert (+ gate, + ones row) and write the thread's 8 values into the LDS image.
+template <typename T>
+__device__ __forceinline__ void store_tile(unsigned short* lds, const Raw& raw, int dt, int mode, const Raw* graw,
+                                           int gdt, float gs, int r0, int ones_row, int k0, int K) {
+  const int t = threadIdx.x;
+  const bool pk = packed<T>(dt);
+  u16x8 v;
+  if (pk && !graw && ones_row < 0) {
+    v = __builtin_bit_cast(u16x8, raw.r[0]);
+  } else {
+    const bool gpk = graw ? packed<T>(gdt) : false;
+#pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int gk = k0 + kq + j;
-      float f = 0.f;
-      if (gr < R && gk < K) {
-        const int64_t off = (int64_t)gr * s_r + (int64_t)gk * s_k;
-        f = ld_any<T>(X, xdt, off);
-        if (G) f = ld_any<T>(G, gdt, off) > 0.f ? f * gs : 0.f;
+      float f = raw_at<T>(raw, pk, j);
+      if (graw) f = raw_at<T>(*graw, gpk, j) > 0.f ? f * gs : 0.f;
+      if (ones_row >= 0) {
+        const int gr = r0 + (mode == kRContig ? (t & 7) * 8 + j : (t >> 2));
+        const int gk = k0 + (mode == kRContig ? (t >> 3) : (t & 3) * 8 + j);
+        if (gr == ones_row && gk < K) f = 1.f;
       }
       v[j] = bits_of<T>((T)f);
     }
-    *reinterpret_cast<u16x8*>(lds + r * LDK + kq) = v;
-  } else {
-    // row-contiguous operand (s_r == 1): thread -> (k, 8 consecutive rows)
+  }
+  if (mode == kRContig) {
     const int k = t >> 3, rq = (t & 7) * 8;
-    const int gk = k0 + k;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int gr = r0 + rq + j;
-      float f = 0.f;
-      if (gr < R && gk < K) {
-        const int64_t off = (int64_t)gr + (int64_t)gk * s_k;
-        f = ld_any<T>(X, xdt, off);
-        if (G) f = ld_any<T>(G, gdt, off) > 0.f ? f * gs : 0.f;
-      }
-      lds[(rq + j) * LDK + k] = bits_of<T>((T)f);
-    }
+    for (int j = 0; j < 8; ++j) lds[(rq + j) * LDK + k] = v[j];
+  } else {
+    *reinterpret_cast<u16x8*>(lds + (t >> 2) * LDK + (t & 3) * 8) = v;
+  }
+}
+
+// Epilogue of one output element (acc = sum over K).
+template <typename T>
+__device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale) {
+  if (n == a.N) {  // ones column -> row sums of A (bias gradient)
+    a.rowsum[m] = a.alpha * acc;
+    return;
+  }
+  const int64_t co = (int64_t)m * a.scm + (int64_t)n * a.scn;
+  float v = a.alpha * acc;
+  if (a.beta != 0.f) v += a.beta * ld_any(a.C, a.c_dtype, co);
+  if (a.bias) v += a.bias[n];
+  if (a.act >= 1) v = fmaxf(v, 0.f);
+  if (a.act == 2) v = dropout_keep(a.seed, off, (uint64_t)m * a.N + n, a.drop_p) ? v * dscale : 0.f;
+  switch (a.c_dtype) {
+    case kF32: ((float*)a.C)[co] = v; break;
+    case kBF16: ((__bf16*)a.C)[co] = (__bf16)v; break;
+    default: ((_Float16*)a.C)[co] = (_Float16)v; break;
   }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short As[BM * LDK];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[BN * LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][BN * LDK];
   typedef typename Mfma<T>::frag frag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  const int ones_row = a.rowsum ? a.N : -1;
+  // this split's K-tiles
+  const int ktiles = (a.K + BK - 1) / BK;
+  const int per = (ktiles + gridDim.z - 1) / gridDim.z;
+  const int kt0 = blockIdx.z * per, kt1 = min(ktiles, kt0 + per);
+
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 < a.K; k0 += BK) {
-    stage_tile<T>(As, a.A, a.a_dtype, a.sam, a.sak, a.G, a.g_dtype, a.gate_scale, m0, a.M, k0, a.K);
-    stage_tile<T>(Bs, a.B, a.b_dtype, a.sbn, a.sbk, nullptr, 0, 1.f, n0, a.N, k0, a.K);
+  Raw ra, rb, rg;
+  if (kt0 < kt1) {
+    load_raw<T>(ra, a.A, a.a_dtype, a.a_mode, a.sam, a.sak, m0, a.M, kt0 * BK, a.K);
+    if (a.G) load_raw<T>(rg, a.G, a.g_dtype, a.a_mode, a.sam, a.sak, m0, a.M, kt0 * BK, a.K);
+    load_raw<T>(rb, a.B, a.b_dtype, a.b_mode, a.sbn, a.sbk, n0, a.N, kt0 * BK, a.K);
+  }
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1, k0 = kt * BK;
+    store_tile<T>(As[buf], ra, a.a_dtype, a.a_mode, a.G ? &rg : nullptr, a.g_dtype, a.gate_scale, m0, -1, k0, a.K);
+    store_tile<T>(Bs[buf], rb, a.b_dtype, a.b_mode, nullptr, 0, 1.f, n0, ones_row, k0, a.K);
     __syncthreads();
+    if (kt + 1 < kt1) {  // next tile's global loads overlap this tile's MFMAs
+      load_raw<T>(ra, a.A, a.a_dtype, a.a_mode, a.sam, a.sak, m0, a.M, k0 + BK, a.K);
+      if (a.G) load_raw<T>(rg, a.G, a.g_dtype, a.a_mode, a.sam, a.sak, m0, a.M, k0 + BK, a.K);
+      load_raw<T>(rb, a.B, a.b_dtype, a.b_mode, a.sbn, a.sbk, n0, a.N, k0 + BK, a.K);
+    }
     frag fa[2], fb[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wm * 32 + i * 16 + (lane & 15);
-      fa[i] = *reinterpret_cast<const frag*>(As + r * LDK + 8 * (lane >> 4));
-    }
+    for (int i = 0; i < 2; ++i)
+      fa[i] = *reinterpret_cast<const frag*>(As[buf] + (wm * 32 + i * 16 + (lane & 15)) * LDK + 8 * (lane >> 4));
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = wn * 32 + j * 16 + (lane & 15);
-      fb[j] = *reinterpret_cast<const frag*>(Bs + c * LDK + 8 * (lane >> 4));
-    }
+    for (int j = 0; j < 2; ++j)
+      fb[j] = *reinterpret_cast<const frag*>(Bs[buf] + (wn * 32 + j * 16 + (lane & 15)) * LDK + 8 * (lane >> 4));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = Mfma<T>::mma(fa[i], fb[j], acc[i][j]);
-    __syncthreads();
   }
 
+  const bool split = gridDim.z > 1;
   const uint64_t off = rng_offset(a.offset, a.offset_dev);
   const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
 #pragma unroll
@@ -115,19 +233,23 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
         const int n = n0 + wn * 32 + j * 16 + (lane & 15);
-        if (m >= a.M || n >= a.N) continue;
-        const int64_t co = (int64_t)m * a.scm + (int64_t)n * a.scn;
-        float v = a.alpha * acc[i][j][r];
-        if (a.beta != 0.f) v += a.beta * ld_any<T>(a.C, a.c_dtype, co);
-        if (a.bias) v += a.bias[n];
-        if (a.act >= 1) v = fmaxf(v, 0.f);
-        if (a.act == 2) v = dropout_keep(a.seed, off, (uint64_t)m * a.N + n, a.drop_p) ? v * dscale : 0.f;
-        switch (a.c_dtype) {
-          case kF32: ((float*)a.C)[co] = v; break;
-          case kBF16: ((__bf16*)a.C)[co] = (__bf16)v; break;
-          default: ((_Float16*)a.C)[co] = (_Float16)v; break;
-        }
+        if (m >= a.M || n >= Np) continue;
+        if (split) a.ws[((int64_t)blockIdx.z * a.M + m) * Np + n] = acc[i][j][r];
+        else epilogue<T>(a, m, n, acc[i][j][r], off, dscale);
       }
+}
+
+// Fixed-order sum of the split-K partials + the epilogue.
+template <typename T>
+__global__ void gemm_splitk_reduce(GemmArgs a, int splits) {
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.M * Np) return;
+  const int m = (int)(i / Np), n = (int)(i - (int64_t)m * Np);
+  const int64_t stride = (int64_t)a.M * Np;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += a.ws[z * stride + i];
+  epilogue<T>(a, m, n, s, rng_offset(a.offset, a.offset_dev), a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f);
 }
 
 // Column sum with an optional ReLU/dropout gate, fixed reduction order.
@@ -156,13 +278,45 @@ __global__ void colsum_kernel(const TX* __restrict__ x, const TG* __restrict__ g
     out[c] = beta != 0.f ? fmaf(beta, out[c], t) : t;
   }
 }
+
+int esize(int dt) { return dt == kF32 ? 4 : dt == kU8 ? 1 : 2; }
+
+// Vector staging needs 16-byte aligned 8-element runs along the contiguous dim.
+int pick_mode(const void* X, int dt, int64_t s_r, int64_t s_k, int mfma) {
+  const bool vec_dt = dt == kF32 || dt == mfma;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(X);
+  if (!vec_dt || base % 16) return kScalar;
+  const int es = esize(dt);
+  if (s_k == 1 && (s_r * es) % 16 == 0) return kKContig;
+  if (s_r == 1 && (s_k * es) % 16 == 0) return kRContig;
+  return kScalar;
+}
 }  // namespace
 
-hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.N <= 0) return hipSuccess;
-  dim3 grid(cdiv(a.N, BN), cdiv(a.M, BM));
+int gemm_splits(const GemmArgs& a) {
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  const int tiles = cdiv(Np, BN) * cdiv(a.M, BM);
+  const int ktiles = cdiv(a.K, BK);
+  if (tiles >= 256 || ktiles < 8) return 1;
+  int s = std::min(cdiv(512, tiles), ktiles / 4);
+  return std::max(1, std::min(s, 64));
+}
+
+hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
+  if (in.M <= 0 || in.N <= 0) return hipSuccess;
+  GemmArgs a = in;
+  a.a_mode = pick_mode(a.A, a.a_dtype, a.sam, a.sak, a.mfma_dtype);
+  a.b_mode = pick_mode(a.B, a.b_dtype, a.sbn, a.sbk, a.mfma_dtype);
+  // the gate is loaded with A's mode: it must allow the same vector access
+  if (a.G && pick_mode(a.G, a.g_dtype, a.sam, a.sak, a.mfma_dtype) != a.a_mode) a.a_mode = kScalar;
+  const int splits = a.ws ? gemm_splits(a) : 1;
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  dim3 grid(cdiv(Np, BN), cdiv(a.M, BM), splits);
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     hipLaunchKernelGGL(gemm_kernel<scalar_t>, grid, dim3(256), 0, s, a);
+    if (splits > 1)
+      hipLaunchKernelGGL(gemm_splitk_reduce<scalar_t>, dim3(cdiv((int64_t)a.M * Np, 256)), dim3(256), 0, s, a,
+                         splits);
   });
   return hipGetLastError();
 }

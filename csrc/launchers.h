@@ -85,7 +85,12 @@ struct GemmArgs {
   int act;            // 0 none, 1 relu, 2 relu + dropout
   float drop_p; uint64_t seed, offset; const int64_t* offset_dev;
   int mfma_dtype;     // kBF16 or kF16
+  float* rowsum;      // optional [M]: alpha * sum_k A(m,k) (bias gradient via a ones column of B)
+  float* ws;          // optional split-K workspace, >= gemm_splits(a) * M * (N + (rowsum != 0)) floats
+  int a_mode, b_mode; // set by launch_gemm (operand staging modes)
 };
+// Number of K splits launch_gemm will use for these shapes (1 = no workspace needed).
+int gemm_splits(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 
 // Column sums of a (gated) [rows, cols] matrix -> fp32 out[cols] (fixed order).

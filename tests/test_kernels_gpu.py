@@ -109,7 +109,8 @@ def test_maxpool_relu():
 
 
 @pytest.mark.parametrize("act", ["none", "relu"])
-@pytest.mark.parametrize("mnk", [(64, 50, 320), (8, 10, 50), (1000, 10, 50), (37, 70, 45)])
+@pytest.mark.parametrize("mnk", [(64, 50, 320), (8, 10, 50), (1000, 10, 50), (37, 70, 45),
+                                 (4096, 50, 320), (8192, 10, 50), (33, 64, 1000)])
 def test_linear(act, mnk):
     M, N, K = mnk
     torch.manual_seed(3)
