@@ -34,13 +34,14 @@ from ..utils.flat import FlatParams
 
 
 
-def layout() -> tuple[int, int, int]:
+def layout() -> tuple[int, int, int, int]:
     """Buffer sizes of the fused kernels, from the extension (csrc/kernels/lenet_fused.hip):
     16-bit weight-image elements (I_END), conv slab row per workgroup (CNP_PAD: conv1.w/b +
-    conv2.w/b = 5280 floats in 64-float chunks) and per-sample fc vector length (VEC)."""
-    wimg, conv, vec, nparams = (int(v) for v in torch.ops.csed.lenet_layout())
+    conv2.w/b = 5280 floats in 64-float chunks), per-sample fc vector length (VEC) and the
+    largest per-rank batch that uses batch staging (STAGE_MAXB)."""
+    wimg, conv, vec, nparams, stage_max = (int(v) for v in torch.ops.csed.lenet_layout())
     assert nparams == N_PARAMS
-    return wimg, conv, vec
+    return wimg, conv, vec, stage_max
 
 
 class FusedLeNetTrainer:
@@ -83,7 +84,7 @@ class FusedLeNetTrainer:
                 dist.broadcast(host, src=0)
                 self.flat.data.copy_(host)
         self.momentum_buf = torch.zeros_like(self.flat.data)
-        wimg_elems, conv_params, vec_len = layout()
+        wimg_elems, conv_params, vec_len, stage_max = layout()
         # zero-initialised: padding rows / columns of the images must stay zero
         self.wimg = torch.zeros(wimg_elems, dtype=torch.int16, device=dev)
         # per-WG conv partial gradients and per-sample fc vectors (see lenet_fused.hip)
@@ -97,6 +98,11 @@ class FusedLeNetTrainer:
         self.rng_offset = torch.zeros(1, dtype=torch.long, device=dev)
         self.eval_parts = torch.zeros(2 * 256, dtype=torch.float32, device=dev)
         self.perm = torch.arange(self.B, dtype=torch.long, device=dev)
+        # batch staging (per-rank batch <= stage_max): lenet_update gathers the next step's
+        # pixels + labels one step ahead, so lenet_train starts with no dependent index chain
+        self.staged = self.B <= stage_max and self.grid == self.B
+        self.xstage = torch.zeros((self.B, 784), dtype=torch.uint8, device=dev) if self.staged else None
+        self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
         self.repack()
         # gradient all-reduce: the one-shot IPC kernel (csrc/comm) when every rank
         # passes its self-test, else RCCL (see parallel/ipc.py)
@@ -134,6 +140,15 @@ class FusedLeNetTrainer:
         else:
             self.perm = order
         self.cursor.zero_()
+        self._stage_current()
+
+    def _stage_current(self) -> None:
+        """Gather the batch at the cursor into the staging buffers (epoch start)."""
+        if self.staged:
+            torch.ops.csed.lenet_stage(self.train_data.images, self.train_data.labels, self.perm, self.cursor,
+                                       self.B, self.xstage, self.lstage)
+
+
 
     def steps_per_epoch(self) -> int:
         return math.ceil(self.perm.numel() / self.B)
@@ -145,9 +160,12 @@ class FusedLeNetTrainer:
     def _launch_step(self, B: int, grid: int, grad_scale: float, cursor: torch.Tensor | None,
                      perm: torch.Tensor) -> None:
         ops = torch.ops.csed
+        # full steps read the staged batch and stage the next one; the epoch's short tail uses perm
+        st = self.staged and cursor is not None
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
                         self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
-                        self.drop_p, self.seed, self.rng_offset, grid, self.mfma)
+                        self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,
+                        self.xstage if st else None, self.lstage if st else None, st)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
         if self.comm:
@@ -172,7 +190,8 @@ class FusedLeNetTrainer:
         ops = torch.ops.csed
         ops.lenet_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B, self.ctx.rank,
                         self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts, 1.0 / self.global_batch,
-                        MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg)
+                        MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg,
+                        self.xstage if grid == self.B else None, self.lstage if grid == self.B else None, False)
         ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
                          self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma)
@@ -197,16 +216,17 @@ class FusedLeNetTrainer:
     def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
+        # snapshot the state the capture warm-up will advance; the side stream must
+        # wait for the snapshot copies too (they are enqueued on the current stream)
+        state = [self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor, self.rng_offset,
+                 self.loss_acc] + ([self.xstage, self.lstage] if self.staged else [])
+        saved = [t.clone() for t in state]
         s.wait_stream(torch.cuda.current_stream(self.device))
-        # snapshot the state the capture warm-up will advance
-        saved = [t.clone() for t in (self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor,
-                                     self.rng_offset, self.loss_acc)]
         with torch.cuda.stream(s):
             self.step()  # warm-up on the capture stream (lazy RCCL init etc.)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        for t, v in zip((self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor,
-                         self.rng_offset, self.loss_acc), saved):
+        for t, v in zip(state, saved):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
         with torch.cuda.graph(g, stream=s):

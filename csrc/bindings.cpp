@@ -283,10 +283,11 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 
 // ----------------------------------------------------------- fused lenet
 // Buffer sizes the fused LeNet kernels expect: [weight-image elements, conv
-// slab row (floats per workgroup), per-sample vector length, flat params].
+// slab row (floats per workgroup), per-sample vector length, flat params,
+// largest per-rank batch the batch-staging path handles].
 std::vector<int64_t> lenet_layout() {
   return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
-          csed::lenet_param_count()};
+          csed::lenet_param_count(), csed::lenet_stage_max_batch()};
 }
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
@@ -303,7 +304,8 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
                  Tensor& loss_parts,
                  double grad_scale, double mean, double std_, double drop_p, int64_t seed,
                  const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
-                 const optional<Tensor>& dbg) {
+                 const optional<Tensor>& dbg, const optional<Tensor>& xstage, const optional<Tensor>& lstage,
+                 bool stage_next) {
   dev(images, "images"); dev(labels, "labels"); dev(perm, "perm"); dev(wimg, "wimg"); dev(params, "params");
   dev(slab, "slab"); dev(vslab, "vslab"); dev(loss_parts, "loss_parts");
   TORCH_CHECK(images.scalar_type() == at::kByte && images.numel() == images.size(0) * 784, "images: uint8 [N,28,28]");
@@ -326,7 +328,45 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 16 * grid, "dbg: int64 [grid*16]");
     a.dbg = (uint64_t*)dbg->data_ptr<int64_t>();
   }
+  TORCH_CHECK(xstage.has_value() == lstage.has_value(), "lenet_train: xstage and lstage go together");
+  if (xstage.has_value()) {
+    TORCH_CHECK(xstage->scalar_type() == at::kByte && xstage->numel() >= B * 784 && lstage->scalar_type() == at::kLong &&
+                    lstage->numel() >= B && xstage->is_contiguous() && lstage->is_contiguous(),
+                "lenet_train: staged batch must be uint8 [B, 784] + int64 [B]");
+    a.xstage = xstage->data_ptr<uint8_t>();
+    a.lstage = lstage->data_ptr<int64_t>();
+    if (stage_next) {
+      TORCH_CHECK(cursor.has_value() && grid == B, "lenet_train: stage_next needs the cursor and grid == B");
+      a.stage_next = 1;
+    }
+  }
   CHECK_HIP(csed::launch_lenet_train(a, cur_stream(images)));
+}
+
+csed::LenetStageArgs stage_args(const Tensor& images, const Tensor& labels, const Tensor& perm, int64_t B,
+                                const Tensor& xstage, const Tensor& lstage) {
+  TORCH_CHECK(B >= 1 && B <= csed::lenet_stage_max_batch(), "staged batch must be 1..", csed::lenet_stage_max_batch());
+  TORCH_CHECK(images.scalar_type() == at::kByte && images.is_contiguous() && labels.scalar_type() == at::kLong &&
+                  perm.scalar_type() == at::kLong && perm.numel() >= 1,
+              "staging: images uint8 [N,28,28], labels / perm int64");
+  TORCH_CHECK(xstage.scalar_type() == at::kByte && xstage.numel() >= B * 784 && xstage.is_contiguous() &&
+                  lstage.scalar_type() == at::kLong && lstage.numel() >= B && lstage.is_contiguous(),
+              "staging: xstage uint8 [B, 784], lstage int64 [B]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(images.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(xstage.data_ptr()) % 16 == 0, "staging: 16-byte aligned buffers");
+  csed::LenetStageArgs st{};
+  st.images = images.data_ptr<uint8_t>(); st.labels = labels.data_ptr<int64_t>();
+  st.perm = perm.data_ptr<int64_t>(); st.perm_len = perm.numel(); st.B = (int)B;
+  st.xstage = xstage.data_ptr<uint8_t>(); st.lstage = lstage.data_ptr<int64_t>();
+  return st;
+}
+
+void lenet_stage(const Tensor& images, const Tensor& labels, const Tensor& perm, const Tensor& cursor, int64_t B,
+                 Tensor& xstage, Tensor& lstage) {
+  dev(images, "images"); dev(perm, "perm"); dev(cursor, "cursor"); dev(xstage, "xstage");
+  const c10::DeviceGuard gd(images.device());
+  CHECK_HIP(csed::launch_lenet_stage(stage_args(images, labels, perm, B, xstage, lstage),
+                                     cursor.data_ptr<int64_t>(), cur_stream(images)));
 }
 
 void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t B, const optional<Tensor>& grad_in, const optional<Tensor>& grad_out,
@@ -354,6 +394,7 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 128, "lenet_update: dbg must be int64[>=1024]");
     a.dbg = (uint64_t*)dbg->data_ptr();
   }
+
   CHECK_HIP(csed::launch_lenet_update(a, optpt<float>(loss_parts), (int)nparts, optpt<float>(loss_acc),
                                       cur_stream(params)));
 }
@@ -378,7 +419,10 @@ TORCH_LIBRARY(csed, m) {
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
         "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "
-        "float drop_p, int seed, Tensor? rng_offset, int grid, int mfma_dtype, Tensor(c!)? dbg=None) -> ()");
+        "float drop_p, int seed, Tensor? rng_offset, int grid, int mfma_dtype, Tensor(c!)? dbg=None, "
+        "Tensor(e!)? xstage=None, Tensor(f!)? lstage=None, bool stage_next=False) -> ()");
+  m.def("lenet_stage(Tensor images, Tensor labels, Tensor perm, Tensor cursor, int B, Tensor(a!) xstage, "
+        "Tensor(b!) lstage) -> ()");
   m.def("lenet_update(Tensor slab, int grid, Tensor vslab, int B, Tensor? grad_in, Tensor(a!)? grad_out, Tensor(b!) params, "
         "Tensor(c!) momentum, Tensor(d!) wimg, float lr, float mom, float dampening, float weight_decay, "
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
@@ -431,5 +475,6 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);
   m.impl("lenet_update", &lenet_update);
+  m.impl("lenet_stage", &lenet_stage);
   m.impl("lenet_eval", &lenet_eval);
 }

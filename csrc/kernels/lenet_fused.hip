@@ -216,7 +216,23 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   uint32_t px = 0;
   int lab = 0, labv = 0;
   int64_t rowv = 0;
+  // next-step staging (one sample per workgroup): its row, pixels and label are
+  // loaded during this step's stages and stored at the end
+  const bool stage_next = TRAIN && a.xstage && a.stage_next && nsamp == 1;
+  int64_t nrow = 0;
+  uint32_t px_next = 0;
+  int64_t lab_next = 0;
+  // fp32 params land in LDS at the first loop-top barrier: waiting for them (and
+  // for the weight DMA) there lets the loop-invariant address math that hipcc
+  // hoists into the preheader run under the load latency instead of after it
+  float par0 = 0.f, par1 = 0.f;
   {
+    // a staged batch (lenet_update gathered it last step): the first sample's
+    // pixels and the labels of samples 0..63 need no dependent loads at all
+    if (a.xstage && nsamp > 0) {
+      px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(tid, 195)];
+      labv = (int)a.lstage[min(g + lane * G, a.B - 1)];
+    }
     // W2C | W2D | F1 straight into LDS by LDS-DMA: each wave-instruction moves
     // 1 KB to a wave-uniform base + lane*16, so the image stays lane-linear
     const uint4* src = reinterpret_cast<const uint4*>(a.wimg + I_W2C);
@@ -235,7 +251,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     fb1 = *reinterpret_cast<const frag*>(a.wimg + I_W1C + l16 * 32 + kb);
     // the first sample (cursor -> row -> pixels, label: scalar chain) and the
     // row indices of samples 0..63 (one per lane), behind the weight loads
-    if (nsamp > 0) {
+    if (!a.xstage && nsamp > 0) {
       const int64_t row0 = perm_at(0);
       lab = (int)a.labels[row0];
       px = reinterpret_cast<const uint32_t*>(a.images + row0 * 784)[min(tid, 195)];
@@ -260,8 +276,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       uint4* z = reinterpret_cast<uint4*>(sm + S_P1H);
       for (int i = tid; i < NZ; i += NT) z[i] = make_uint4(0, 0, 0, 0);
     }
-    if (tid < 590) PAR[tid] = pv0;
-    if (tid + NT < 590) PAR[tid + NT] = pv1;
+    par0 = pv0;
+    par1 = pv1;
   }
   if (a.dbg && tid == 0) a.dbg[g * 16 + 13] = __builtin_amdgcn_s_memtime();
   if (a.dbg && tid == 0) a.dbg[g * 16 + 14] = __builtin_amdgcn_s_memtime();
@@ -297,11 +313,15 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   for (int s = 0; s < nsamp; ++s) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
+    if (s == 0) {
+      if (tid < 590) PAR[tid] = par0;
+      if (tid + NT < 590) PAR[tid + NT] = par1;
+    }
     __syncthreads();  // LDS-DMA drained (first pass); previous sample's readers are done
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
     // then start the next sample's loads (consumed one sample later)
     STAMP(0);
-    const int t_lab = s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63);
+    const int t_lab = (s == 0 && !a.xstage) ? lab : __builtin_amdgcn_readlane(labv, s & 63);
     {
       if (tid < 196) {
         u16x4 o;
@@ -321,16 +341,24 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       }
       if (s + 1 < nsamp) {
         const int sn = s + 1;
-        if ((sn & 63) == 0) rowv = perm_at(min(sn + lane, nsamp - 1));
-        if (s == 0 || (sn & 63) == 0) labv = (int)a.labels[rowv];
-        const int64_t rn = readlane64(rowv, sn & 63);
-        px = reinterpret_cast<const uint32_t*>(a.images + rn * 784)[min(tid, 195)];
+        if (a.xstage) {
+          if ((sn & 63) == 0) labv = (int)a.lstage[min(g + (sn + lane) * G, a.B - 1)];
+          px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)(g + sn * G) * 784)[min(tid, 195)];
+        } else {
+          if ((sn & 63) == 0) rowv = perm_at(min(sn + lane, nsamp - 1));
+          if (s == 0 || (sn & 63) == 0) labv = (int)a.labels[rowv];
+          const int64_t rn = readlane64(rowv, sn & 63);
+          px = reinterpret_cast<const uint32_t*>(a.images + rn * 784)[min(tid, 195)];
+        }
       }
     }
     __syncthreads();
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, P1H
     STAMP(1);
+    if (stage_next)  // a relaxed atomic keeps this a vector load (no scalar-queue wait)
+      nrow = __hip_atomic_load(a.perm + min(pbase + a.B, a.perm_len - 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     {
       // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
       u16x8 raw[5];
@@ -401,6 +429,10 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3)
     STAMP(3);
+    if (stage_next) {
+      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid, 195)];
+      lab_next = a.labels[nrow];
+    }
     if (wave < 4) {
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
       f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -634,6 +666,10 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     const int s = 0;
     STAMP(11);
   }
+  if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
+    if (tid < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid] = px_next;
+    if (tid == 0) a.lstage[g] = lab_next;
+  }
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
     // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a
@@ -733,6 +769,48 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
 }
 
+// ---------------------------------------------------------------------------
+// Batch staging: the pixels and labels of one step, gathered through the epoch
+// permutation into a dense [B][784] buffer, so lenet_train loads its sample with
+// no dependent cursor -> perm -> image chain in its preamble.  lenet_train
+// itself stages the NEXT step (each workgroup its own sample, loads issued
+// mid-kernel, stored at its end); this kernel fills the buffer at epoch start.
+// One block; every thread issues all of its loads before its first store.
+// ---------------------------------------------------------------------------
+constexpr int STAGE_MAXB = 512;
+constexpr int IMG_U4 = 784 / 16;  // 49 16-byte chunks per image
+
+__device__ __forceinline__ void gather_batch(const LenetStageArgs& st, int64_t step, int64_t* rows_sh) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int b = tid; b < st.B; b += nt) {
+    const int64_t row = st.perm[min(step * st.B + b, st.perm_len - 1)];
+    rows_sh[b] = row;
+    st.lstage[b] = st.labels[row];
+  }
+  __syncthreads();
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(st.images);
+  uint4* __restrict__ dst = reinterpret_cast<uint4*>(st.xstage);
+  const int total = st.B * IMG_U4;
+  constexpr int U = 8;
+  for (int i0 = tid; i0 < total; i0 += nt * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * nt, total - 1);
+      const int b = i / IMG_U4;
+      v[u] = src[rows_sh[b] * IMG_U4 + (i - b * IMG_U4)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * nt < total) dst[i0 + u * nt] = v[u];
+  }
+}
+
+__global__ void __launch_bounds__(512) lenet_stage_kernel(LenetStageArgs st, const int64_t* cursor) {
+  __shared__ int64_t rows_sh[STAGE_MAXB];
+  gather_batch(st, cursor ? cursor[0] : 0, rows_sh);
+}
+
 // Final consumer of one parameter's gradient: export or SGD step.  p / m are
 // params[i] / momentum[i], loaded by the caller at kernel entry so their
 // round trip overlaps the gradient loads instead of following them.
@@ -762,6 +840,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
                                                              float* loss_acc) {
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
+
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
@@ -961,6 +1040,14 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     hipLaunchKernelGGL(lenet_update_kernel<scalar_t>, dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab, a.B,
                        loss_parts, nparts, loss_acc);
   });
+  return hipGetLastError();
+}
+
+int lenet_stage_max_batch() { return STAGE_MAXB; }
+
+hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hipStream_t s) {
+  if (a.B <= 0 || a.B > STAGE_MAXB || !a.xstage || !a.lstage) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lenet_stage_kernel, dim3(1), dim3(512), 0, s, a, cursor);
   return hipGetLastError();
 }
 

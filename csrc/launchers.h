@@ -148,8 +148,20 @@ struct LenetTrainArgs {
   int grid;
   int mfma_dtype;
   uint64_t* dbg;             // optional [grid, 16] stage stamps (diagnostics)
+  uint8_t* xstage;           // optional staged batch [B, 784] (grid == B): sample b = workgroup b
+  int64_t* lstage;           // its labels [B]
+  int stage_next;            // with xstage: also stage step cursor+1 (perm / cursor are read for it)
 };
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s);
+// Batch staging: pixels + labels of one step, gathered through the epoch permutation.
+struct LenetStageArgs {
+  const uint8_t* images; const int64_t* labels; const int64_t* perm; int64_t perm_len;
+  int B;                     // <= lenet_stage_max_batch()
+  uint8_t* xstage; int64_t* lstage;
+};
+int lenet_stage_max_batch();
+// Gather the batch of step cursor[0] (no counter change).
+hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hipStream_t s);
 int64_t lenet_wimg_elems();
 int64_t lenet_param_count();
 int64_t lenet_conv_param_count();  // 5280: conv1.w, conv1.b, conv2.w, conv2.b

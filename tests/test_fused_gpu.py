@@ -177,3 +177,29 @@ def test_fused_training_converges_with_dropout_and_graphs():
     assert c1 > 700
     assert eng.capture_comm_ok is True
     assert eng.step_count.item() == 2 * 64
+
+
+@pytest.mark.parametrize("B", [64, 24])
+def test_batch_staging_is_bitwise_transparent(B):
+    """lenet_update gathering the next batch one step ahead (and lenet_train reading it)
+    must give exactly the parameters of the perm/cursor path, eager and graph-replayed,
+    across an epoch boundary."""
+    data = synthetic_mnist(B * 6 + 5, seed=5)
+    finals = []
+    for staged in (True, False):
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B)
+        assert eng.staged
+        eng.staged = staged
+        g = torch.Generator().manual_seed(7)
+        eng.set_epoch_order(torch.randperm(len(data), generator=g))
+        eng.run_steps(2, use_graph=False)
+        eng.run_steps(3, steps_per_graph=3)
+        eng.last_partial_step()
+        eng.set_epoch_order(torch.randperm(len(data), generator=g))
+        eng.run_steps(4, steps_per_graph=2)
+        torch.cuda.synchronize()
+        finals.append((eng.flat.data.clone(), eng.loss_acc.clone(), eng.cursor.item()))
+    assert torch.equal(finals[0][0], finals[1][0])
+    assert torch.equal(finals[0][1], finals[1][1])
+    assert finals[0][2] == finals[1][2] == 4
