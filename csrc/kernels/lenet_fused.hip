@@ -310,7 +310,12 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   // accumulating 16,500 products per sample here, each sample's vectors are written
   // to the vector slab and lenet_update forms the sums as one GEMM over the batch.
 
-  for (int s = 0; s < nsamp; ++s) {
+  // The per-sample body takes the lane indices as arguments that are opaque per
+  // iteration: otherwise hipcc hoists every lane-dependent LDS address of every
+  // stage out of the sample loop, where they sit in ~100 long-lived registers
+  // (scratch spills at 256 VGPRs) and run as one serial VALU block in front of
+  // the first sample instead of inside the stages' latency bubbles.
+  auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
     if (s == 0) {
@@ -511,7 +516,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         if (lane < 50) vs[V_DZ1 + lane] = dz;
       }
     }
-    if (!TRAIN) continue;
+    if (!TRAIN) return;
     __syncthreads();
 
     // ---------------- stage 5: dP2 = dZ1 . W1 on the MFMA (B = fc1 image read
@@ -660,6 +665,11 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         if (i < 4 || wave < 4) acc_c1 = Mfma<T>::mma(fa[i], __builtin_bit_cast(frag, rv), acc_c1);
       }
     }
+  };
+  for (int s = 0; s < nsamp; ++s) {
+    const int t = opaque(tid);
+    const int ln = t & 63;
+    sample(s, t, ln, ln & 15, ln >> 4, 8 * (ln >> 4));
   }
 
   {
