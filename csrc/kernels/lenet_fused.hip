@@ -151,21 +151,26 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   return ((int64_t)hi << 32) | (uint32_t)lo;
 }
 
-// conv2 dgrad epilogue for one (input channel, P1 pixel): relu gate, then the
-// pool1 backward scatter of the 2x2 window (argmax position gets the value).
+// pool1 backward scatter of one already-gated dP1 value of (input channel ci,
+// P1 pixel mm): the 2x2 window's argmax position bi gets it, the others 0.
 template <typename T>
-__device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned short* P1, const uint8_t* I1,
-                                          int ci, int mm, float v) {
+__device__ __forceinline__ void dgrad_store(unsigned short* DC1, int ci, int mm, float v, int bi) {
   const int ih = mm / 12, iw = mm - ih * 12;
-  const int pi = ci * 144 + mm;
-  v = f16v<T>(P1[pi]) > 0.f ? v : 0.f;
-  const int bi = I1[pi];
   unsigned short* d = DC1 + ci * LD_DC1 + (2 * ih) * 24 + 2 * iw;
   const unsigned short hv = h16<T>(v), z = 0;
   d[0] = bi == 0 ? hv : z;
   d[1] = bi == 1 ? hv : z;
   d[24] = bi == 2 ? hv : z;
   d[25] = bi == 3 ? hv : z;
+}
+
+// conv2 dgrad epilogue for one (input channel, P1 pixel): relu gate, then the
+// pool1 backward scatter.
+template <typename T>
+__device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned short* P1, const uint8_t* I1,
+                                          int ci, int mm, float v) {
+  const int pi = ci * 144 + mm;
+  dgrad_store<T>(DC1, ci, mm, f16v<T>(P1[pi]) > 0.f ? v : 0.f, I1[pi]);
 }
 
 template <typename T, bool TRAIN>
@@ -411,11 +416,15 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       const unsigned short* wrow = W2c + min(nt * 16 + l16, R_W2C) * LD_W2C + kb;
       const s16x8 co0 = *reinterpret_cast<const s16x8*>(COFF + kq * 16);
       const s16x8 co1 = *reinterpret_cast<const s16x8*>(COFF + kq * 16 + 8);
-      f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;  // even / odd K-step chains
 #pragma unroll
-      for (int ks = 0; ks < C2_KS; ++ks)
-        c = Mfma<T>::mma(*reinterpret_cast<const frag*>(arow + (ks < 8 ? co0[ks] : co1[ks - 8])),
-                         *reinterpret_cast<const frag*>(wrow + ks * 32), c);
+      for (int ks = 0; ks < C2_KS; ++ks) {
+        const frag fa = *reinterpret_cast<const frag*>(arow + (ks < 8 ? co0[ks] : co1[ks - 8]));
+        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 32);
+        if (ks & 1) c1 = Mfma<T>::mma(fa, fb, c1);
+        else c0 = Mfma<T>::mma(fa, fb, c0);
+      }
+      const f32x4 c = c0 + c1;
       const int oc = nt * 16 + l16;
       if (oc < 20) {
         float best = c[0];
@@ -440,12 +449,15 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     }
     if (wave < 4) {
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
-      f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;  // even / odd K-step chains
 #pragma unroll
       for (int ks = 0; ks < 10; ++ks) {
         const frag pa = *reinterpret_cast<const frag*>(P2 + ks * 32 + kb);
-        c = Mfma<T>::mma(l16 == 0 ? pa : zfrag, *reinterpret_cast<const frag*>(wrow + ks * 32), c);
+        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 32);
+        if (ks & 1) c1 = Mfma<T>::mma(l16 == 0 ? pa : zfrag, fb, c1);
+        else c0 = Mfma<T>::mma(l16 == 0 ? pa : zfrag, fb, c0);
       }
+      const f32x4 c = c0 + c1;
       if (lane < 16) {
         const int o = wave * 16 + lane;
         if (o < 50) {
@@ -611,18 +623,36 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         f8a[j] = *reinterpret_cast<const frag*>(a8 + off);
         f8b[j] = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 32 : W2d + R_W2D * LD_W2D + kb);
       }
-      f32x4 cw = f32x4{0.f, 0.f, 0.f, 0.f}, c8 = f32x4{0.f, 0.f, 0.f, 0.f};
+      // the pool1/ReLU gate of this lane's 4 outputs does not depend on the MFMAs:
+      // read it first so its LDS latency hides under the K loop
+      const int ci = min(l16, 9);
+      unsigned short gp[4];
+      uint8_t gi[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pi = ci * 144 + wave * 16 + 4 * kq + r;
+        gp[r] = P1[pi];
+        gi[r] = I1[pi];
+      }
+      // two accumulator chains (even / odd K-steps) halve the dependent-MFMA latency
+      f32x4 cw0 = f32x4{0.f, 0.f, 0.f, 0.f}, cw1 = cw0, c8 = cw0;
 #pragma unroll
       for (int ks = 0; ks < DG_KS; ++ks) {
         const int off = ks < 8 ? dof0[ks] : (ks < 16 ? dof1[ks - 8] : dof2[ks - 16]);
-        cw = Mfma<T>::mma(*reinterpret_cast<const frag*>(aw + off), *reinterpret_cast<const frag*>(wrow + ks * 32),
-                          cw);
+        const frag fa = *reinterpret_cast<const frag*>(aw + off);
+        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 32);
+        if (ks & 1) cw1 = Mfma<T>::mma(fa, fb, cw1);
+        else cw0 = Mfma<T>::mma(fa, fb, cw0);
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j) c8 = Mfma<T>::mma(f8a[j], f8b[j], c8);
       if (l16 < 10) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dgrad_out<T>(DC1, P1, I1, l16, wave * 16 + 4 * kq + r, cw[r]);
+        for (int r = 0; r < 4; ++r) {
+          const int mm = wave * 16 + 4 * kq + r;
+          const float v = f16v<T>(gp[r]) > 0.f ? cw0[r] + cw1[r] : 0.f;
+          dgrad_store<T>(DC1, l16, mm, v, gi[r]);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) RED[wave * 256 + (4 * kq + r) * 16 + l16] = c8[r];
