@@ -604,6 +604,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
+    STAMP(9);
     {
       // dP1[px][ic] = sum_{tap, oc} DC2H[px + shift(tap)][oc] * W2D[ic][tap*24 + oc]:
       // full tile `wave` (pixels 16*wave ..) plus K-steps ks = wave + 8j of tile 8

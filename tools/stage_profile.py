@@ -17,7 +17,7 @@ from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import
 from csed_514_project_distributed_training_using_pytorch_amd.models import Net  # noqa: E402
 
 NAMES = ["start->first stage", "pixels+masks+prefetch", "conv1", "conv2", "fc1", "fc2+loss+dZ1",
-         "dP2 (MFMA-tr)+pool2 bwd", "conv2 wgrad+dgrad", "dgrad tile-8 reduce", "conv1 wgrad"]
+         "dP2 (MFMA-tr)+pool2 bwd", "conv2 wgrad", "conv2 dgrad", "dgrad tile-8 reduce", "conv1 wgrad"]
 
 
 def main():
@@ -33,8 +33,8 @@ def main():
         eng.gradient(grid, dbg)
     torch.cuda.synchronize()
     st = dbg.view(grid, 16).cpu().double()
-    # order: 12 = kernel start, 0..8 = stage starts, 11 = after all samples
-    seq = [12, 0, 1, 2, 3, 4, 5, 6, 7, 8, 11]
+    # order: 12 = kernel start, 0..8 = stage starts (9 = dgrad inside stage 6), 11 = after all samples
+    seq = [12, 0, 1, 2, 3, 4, 5, 6, 9, 7, 8, 11]
     d = torch.stack([st[:, seq[i + 1]] - st[:, seq[i]] for i in range(len(seq) - 1)], 1)
     med = d.median(0).values
     tot = (st[:, 11] - st[:, 12]).median().item()
