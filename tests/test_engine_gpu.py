@@ -79,3 +79,26 @@ def test_train_dist_cli_single_gpu_rank(tmp_path):
     lines = [l for l in r.stdout.splitlines() if l.startswith("Epoch=")]
     assert len(lines) == 2
     assert (tmp_path / "model.pt").exists()
+
+
+def test_bench_contract_json():
+    """bench.py prints exactly one JSON line with the driver's fields (short run)."""
+    import json
+
+    r = _run(["bench.py", "--steps", "40", "--warmup", "8", "--steps-per-graph", "8", "--no-epoch"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == 1 and rec["steps"] == 40 and rec["warmup"] == 8 and rec["dtype"] == "bf16"
+    assert rec["config"]["global_batch"] == 64 and rec["value"] > 0 and rec["higher_is_better"] is True
+    assert abs(rec["value"] - 64 / (rec["ms_per_step"] * 1e-3)) / rec["value"] < 0.01
+
+
+def test_graft_smoke_entry():
+    r = _run(["-c", "import __graft_entry__ as g; g.smoke()"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "smoke ok" in r.stdout
