@@ -786,11 +786,11 @@ __global__ void lenet_pack_kernel(const float* __restrict__ params, unsigned sho
 // export it (DDP: the RCCL all-reduce runs next) or apply SGD + refresh the
 // 16-bit weight images.  Two block roles in one launch:
 //
-//   role CONV (blocks [0, NB_CONV)): fixed-order reduction of the per-WG conv
+//   role CONV (blocks [NB_FC, NB_UPDATE)): fixed-order reduction of the per-WG conv
 //     slabs, 16 float4 columns x 32 slices per block so every CU pulls only a
 //     few KB with all loads in flight (latency-, not bandwidth-bound).  Block 0
 //     also folds the loss partials and bumps the device counters.
-//   role FC (blocks [NB_CONV, +NB_FC)): the fc gradients are batch GEMMs of the
+//   role FC (blocks [0, NB_FC)): the fc gradients are batch GEMMs of the
 //     per-sample vectors, on the fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32
 //     products), one 16x16 output tile per wave, K = batch:
 //       dW1 | db1 = dZ1^T . [P2 | 1]   (4 x 21 tiles: column 320 = bias grad)
@@ -890,11 +890,13 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
 
-  if (blk < NB_CONV) {
-    // ---------------- role CONV
+  if (blk >= NB_FC) {
+    // ---------------- role CONV (after the FC blocks: those have the longer path, so
+    // they are dispatched first)
+    const int cblk = blk - NB_FC;
     const int cl = tid & (UP_C - 1), sl = tid / UP_C;
-    // wave 0 owns params blk*64 + tid (16 float4 columns): prefetch p / m now
-    const int pi = blk * (UP_C * 4) + tid;
+    // wave 0 owns params cblk*64 + tid (16 float4 columns): prefetch p / m now
+    const int pi = cblk * (UP_C * 4) + tid;
     float p0 = 0.f, m0 = 0.f;
     if (a.apply_sgd && tid < 64) {
       p0 = a.params[min(pi, NP - 1)];
@@ -905,7 +907,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
     // per-element "load or zero" select makes hipcc branch around every load
     // and wait vmcnt(0) each time (dependent round trips instead of one).
     // chunk blk of the slab is [WG][16 float4]: contiguous for this block
-    const float4* sp = reinterpret_cast<const float4*>(a.slab) + (int64_t)blk * a.grid * UP_C + cl;
+    const float4* sp = reinterpret_cast<const float4*>(a.slab) + (int64_t)cblk * a.grid * UP_C + cl;
     for (int g0 = sl; g0 < a.grid; g0 += UP_S * UP_MAXL) {
       float4 v[UP_MAXL];
 #pragma unroll
@@ -931,7 +933,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       finish_param<T>(a, pi, g, first, p0, m0);
     }
     USTAMP(4);
-    if (blk == 0 && loss_parts && tid < 64) {
+    if (cblk == 0 && loss_parts && tid < 64) {
       // loss / accuracy partials: lane-strided sums, then a fixed butterfly
       float s0 = 0.f, s1 = 0.f;
       for (int q = tid; q < nparts; q += 64) {
@@ -948,7 +950,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   } else {
     // ---------------- role FC: one 16x16 tile of [dW | db] per wave
     const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
-    const int tile = (blk - NB_CONV) * (UP_NT / 64) + wave;
+    const int tile = blk * (UP_NT / 64) + wave;
     if (tile < FC_TILES) {
       const bool fc1 = tile < FC1_TILES;
       const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;

@@ -80,10 +80,10 @@ def main():
                          eng.grid, eng.loss_acc, eng.mfma, dbg)
         torch.cuda.synchronize()
     st = dbg.view(128, 8).cpu().double()
-    nconv = 83
+    nfc = 11  # blocks [0, 11) FC role, [11, 94) CONV role
     t0 = st[:94, 0].min()
     rel = (st - t0) * 0.01  # us
-    for role, sl, ks in [("CONV", slice(0, nconv), [0, 1, 2, 3, 4]), ("FC", slice(nconv, 94), [0, 1, 2, 4])]:
+    for role, sl, ks in [("CONV", slice(nfc, 94), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 4])]:
         r = rel[sl]
         desc = "  ".join(f"s{k} med {r[:, k].median().item():.2f} max {r[:, k].max().item():.2f}" for k in ks)
         print(f"stamps {role}: {desc}")
