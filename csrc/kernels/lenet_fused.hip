@@ -61,14 +61,18 @@ constexpr int LD_P1H = 24;  // P1H position stride (elements): 12 dwords, confli
 constexpr int C2_KS = 13;   // conv2 fwd K-steps: 25 taps x 16 channels = 400 -> 416
 constexpr int DG_OCP = 24;  // dgrad HWC: 20 channels padded to 3 groups of 8
 constexpr int DG_KS = 19;   // dgrad K-steps: 25 taps x 24 channels = 600 -> 608
-constexpr int LD_W2C = 424, LD_W2D = 616, LD_F1 = 328;
-constexpr int R_W2C = 20, R_W2D = 10, R_F1 = 50;  // live rows; row R_* is the zero row
+constexpr int LD_W2C = 432, LD_F1 = 328;   // row strides chosen bank-conflict-free (tools/lds_bank_model.py)
+constexpr int R_W2C = 20, R_F1 = 50;       // live rows; row R_* is the zero row
+// dgrad B operand, chunk-major: [DG_CH chunks of 8 K][16 rows (ic; 10..15 zero)][8]; chunk
+// DG_CH-1 is all zero.  Every 16-lane ds_read_b128 group then hits 16 distinct 16-byte slots
+// (row-major rows collide between the kq0 / kq1 halves of a group whatever the stride).
+constexpr int DG_CH = 4 * DG_KS + 1;
 constexpr int I_W1C = 0, I_W2C = 512;
-constexpr int I_W2D = I_W2C + (R_W2C + 1) * LD_W2C;  // 9416
-constexpr int I_F1 = I_W2D + (R_W2D + 1) * LD_W2D;   // 16192
+constexpr int I_W2D = I_W2C + (R_W2C + 1) * LD_W2C;  // 9584
+constexpr int I_F1 = I_W2D + DG_CH * 16 * 8;         // 19440
 // padded so the LDS copy is whole 512-thread x 16-byte rounds
 constexpr int I_END = I_W2C + ((I_F1 + (R_F1 + 1) * LD_F1 - I_W2C + 4095) / 4096) * 4096;  // 33280
-constexpr int LD_DC2 = 72, LD_DC1 = 584;
+constexpr int LD_DC2 = 72, LD_DC1 = 592;
 constexpr int NT = 512, NW = 8;
 // conv partial-gradient slab: params [0, CNP) = conv1.w, conv1.b, conv2.w, conv2.b
 constexpr int CNP = O_F1W;
@@ -78,7 +82,7 @@ constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;
 
 // LDS carve (bytes); every region 16-B aligned
 constexpr int S_W2C = 0;                              // u16 21*424  conv2 B operand [oc][tap*16+ic]
-constexpr int S_W2D = (I_W2D - I_W2C) * 2;            // u16 11*616  dgrad B operand [ic][tap'*24+oc]
+constexpr int S_W2D = (I_W2D - I_W2C) * 2;            // u16 77*16*8 dgrad B operand [chunk][ic][8]
 constexpr int S_F1 = (I_F1 - I_W2C) * 2;              // u16 51*328  fc1 weight image [o][i]
 // W2C | W2D | F1 are contiguous here exactly as in the global image: one flat copy
 constexpr int WIMG_LDS_U4 = (I_END - I_W2C) / 8;      // 16-byte vectors to stage
@@ -105,7 +109,7 @@ static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B 
 static_assert(S_F % 16 == 0 && (F_RED * 4) % 16 == 0 && S_TOTAL <= 160 * 1024, "lds");
 static_assert(WIMG_LDS_U4 % NT == 0, "whole LDS-DMA rounds");
 static_assert(C2_KS * 32 <= LD_W2C && 25 * C2_ICP <= C2_KS * 32, "conv2 K");
-static_assert(DG_KS * 32 <= LD_W2D && 25 * DG_OCP <= DG_KS * 32, "dgrad K");
+static_assert(25 * DG_OCP <= DG_KS * 32, "dgrad K");
 }  // namespace lenet
 
 using namespace lenet;
@@ -611,7 +615,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       const s16x8 dof0 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24);
       const s16x8 dof1 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 8);
       const s16x8 dof2 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 16);
-      const unsigned short* wrow = W2d + min(l16, R_W2D) * LD_W2D + kb;
+      // B fragment of K-step ks: chunk 4*ks + kq, row l16 (ic)
+      const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
       const int mw = wave * 16 + l16, m8 = 128 + l16;
       const unsigned short* aw = DC2H + ((mw / 12) * 16 + mw % 12) * DG_OCP;
       const unsigned short* a8 = DC2H + ((m8 / 12) * 16 + m8 % 12) * DG_OCP;
@@ -622,7 +627,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         const int ks = wave + 8 * j;
         const int off = DOFF[kq * 24 + min(ks, DG_KS - 1)];
         f8a[j] = *reinterpret_cast<const frag*>(a8 + off);
-        f8b[j] = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 32 : W2d + R_W2D * LD_W2D + kb);
+        f8b[j] = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 512 : W2d + ((DG_CH - 1) * 16 + l16) * 8);
       }
       // the pool1/ReLU gate of this lane's 4 outputs does not depend on the MFMAs:
       // read it first so its LDS latency hides under the K loop
@@ -641,7 +646,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       for (int ks = 0; ks < DG_KS; ++ks) {
         const int off = ks < 8 ? dof0[ks] : (ks < 16 ? dof1[ks - 8] : dof2[ks - 16]);
         const frag fa = *reinterpret_cast<const frag*>(aw + off);
-        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 32);
+        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 512);
         if (ks & 1) cw1 = Mfma<T>::mma(fa, fb, cw1);
         else cw0 = Mfma<T>::mma(fa, fb, cw0);
       }
@@ -767,7 +772,8 @@ __device__ __forceinline__ void write_images(unsigned short* wimg, int i, float 
     const int oc = j / 250, k = j % 250;
     const int ic = k / 25, r = k % 25, kh = r / 5, kw = r % 5;
     wimg[I_W2C + oc * LD_W2C + r * C2_ICP + ic] = h;
-    wimg[I_W2D + ic * LD_W2D + ((4 - kh) * 5 + (4 - kw)) * DG_OCP + oc] = h;
+    const int kd = ((4 - kh) * 5 + (4 - kw)) * DG_OCP + oc;  // dgrad K index
+    wimg[I_W2D + ((kd >> 3) * 16 + ic) * 8 + (kd & 7)] = h;
   } else if (i >= O_F1W && i < O_F1B) {
     const int j = i - O_F1W;
     const int o = j / 320, ii = j % 320;

@@ -1,0 +1,255 @@
+"""Offline LDS bank-conflict model of lenet_train's hot LDS accesses (gfx950 rules).
+
+Replays the exact per-lane byte addresses of each LDS instruction of the fused
+train kernel (csrc/kernels/lenet_fused.hip) for every wave, applies the CDNA4
+banking rules (MI355X_MICROARCH.md §LDS: lane groups per instruction width, bank
+= (addr/4) mod 64 for b64/b128/tr_b16 reads, mod 32 otherwise) and reports the
+extra LDS cycles per access site, i.e. what SQ_LDS_BANK_CONFLICT attributes to
+each.  Used to choose layouts without a GPU run.
+
+    python tools/lds_bank_model.py
+"""
+from collections import defaultdict
+
+# ---- layout constants (mirror lenet_fused.hip)
+LD_W2C, LD_F1 = 432, 328
+LD_P1H, DG_OCP, LD_DC2, LD_DC1 = 24, 24, 72, 592
+DG_CH = 77  # dgrad B image is chunk-major [chunk][16 rows][8]
+S_W2C = 0
+S_W2D = 21 * LD_W2C * 2
+S_F1 = S_W2D + DG_CH * 16 * 16
+S_X = 73728
+S_P1 = S_X + 1600
+S_I1 = S_P1 + 2880
+S_P2 = S_I1 + 1440
+S_I2 = S_P2 + 640
+S_P1H = S_I2 + 320
+S_DC2 = S_P1H + 144 * LD_P1H * 2
+S_DC2H = S_DC2 + 32 * LD_DC2 * 2
+S_DC1 = S_DC2H + 256 * DG_OCP * 2
+
+B128_GROUPS = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+               [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31],
+               [32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59],
+               [36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63]]
+HALVES = [list(range(32)), list(range(32, 64))]
+
+
+def extra_cycles(addrs, width, kind="read", active=None):
+    """Extra LDS cycles of one wave-instruction (addrs: 64 byte addresses or None)."""
+    if width == 16:
+        groups, nb = (B128_GROUPS, 64) if kind == "read" else ([list(range(i, i + 8)) for i in range(0, 64, 8)], 32)
+    elif width == 8:
+        groups, nb = HALVES, (64 if kind == "read" else 32)
+    else:
+        groups, nb = HALVES, 32
+    ndw = max(1, width // 4)
+    extra = 0
+    for g in groups:
+        banks = defaultdict(set)
+        for l in g:
+            if active is not None and not active[l]:
+                continue
+            a = addrs[l]
+            if a is None:
+                continue
+            for d in range(ndw):
+                dw = a // 4 + d
+                banks[dw % nb].add(dw)
+        worst = max((len(v) for v in banks.values()), default=1)
+        extra += worst - 1
+    return extra
+
+
+def lanes():
+    for lane in range(64):
+        yield lane, lane & 15, lane >> 4
+
+
+def dgrad_offsets():
+    tab = {}
+    for q in range(4):
+        for ks in range(24):
+            kg = min(4 * ks + q, 74)
+            tap, ocg = kg // 3, kg % 3
+            tab[q, ks] = ((tap // 5) * 16 + tap % 5) * DG_OCP + ocg * 8
+    return tab
+
+
+def conv2_offsets():
+    tab = {}
+    for q in range(4):
+        for ks in range(16):
+            kg = min(4 * ks + q, 49)
+            tap = kg >> 1
+            tab[q, ks] = ((tap // 5) * 12 + tap % 5) * LD_P1H + (kg & 1) * 8
+    return tab
+
+
+def site_dgrad_A():
+    tab = dgrad_offsets()
+    tot = 0
+    for wave in range(8):
+        for ks in range(19):
+            addrs = []
+            for lane, l16, kq in lanes():
+                m = wave * 16 + l16
+                base = ((m // 12) * 16 + m % 12) * DG_OCP
+                addrs.append(S_DC2H + 2 * (base + tab[kq, ks]))
+            tot += extra_cycles(addrs, 16)
+    return tot
+
+
+def site_dgrad_B():
+    tot = 0
+    for wave in range(8):
+        for ks in range(19):
+            addrs = [S_W2D + 2 * (((4 * ks + kq) * 16 + l16) * 8) for lane, l16, kq in lanes()]
+            tot += extra_cycles(addrs, 16)
+    return tot
+
+
+def site_conv2_A():
+    tab = conv2_offsets()
+    tot = 0
+    for wave in range(8):
+        mt = wave & 3
+        for ks in range(13):
+            addrs = []
+            for lane, l16, kq in lanes():
+                m = mt * 16 + l16
+                p, q = m >> 2, m & 3
+                oy, ox = 2 * (p >> 2) + (q >> 1), 2 * (p & 3) + (q & 1)
+                addrs.append(S_P1H + 2 * ((oy * 12 + ox) * LD_P1H + tab[kq, ks]))
+            tot += extra_cycles(addrs, 16)
+    return tot
+
+
+def site_conv2_B():
+    tot = 0
+    for wave in range(8):
+        nt = wave >> 2
+        for ks in range(13):
+            addrs = [S_W2C + 2 * (min(nt * 16 + l16, 20) * LD_W2C + 8 * kq + ks * 32) for lane, l16, kq in lanes()]
+            tot += extra_cycles(addrs, 16)
+    return tot
+
+
+def site_conv1_gather():
+    koff = [(k // 5) * 28 + (k % 5) if k < 25 else 0 for k in range(32)]
+    tot = 0
+    for wave in range(8):
+        for it in range(5):
+            mt = min(wave + 8 * it, 35)
+            for j in range(8):
+                addrs = []
+                for lane, l16, kq in lanes():
+                    m = mt * 16 + l16
+                    p, q = m >> 2, m & 3
+                    pb = (2 * (p // 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1)
+                    addrs.append(S_X + 2 * (pb + koff[8 * kq + j]))
+                tot += extra_cycles(addrs, 2)
+    return tot
+
+
+def site_conv1_epilogue():
+    tot = 0
+    for wave in range(8):
+        for it in range(5):
+            mt = wave + 8 * it
+            if mt >= 36:
+                continue
+            act = [l16 < 10 for lane, l16, kq in lanes()]
+            w = [mt * 4 + kq for lane, l16, kq in lanes()]
+            p1 = [S_P1 + 2 * (l16 * 144 + w[lane]) for lane, l16, kq in lanes()]
+            i1 = [S_I1 + (l16 * 144 + w[lane]) for lane, l16, kq in lanes()]
+            p1h = [S_P1H + 2 * (w[lane] * LD_P1H + l16) for lane, l16, kq in lanes()]
+            tot += extra_cycles(p1, 2, "write", act) + extra_cycles(i1, 1, "write", act) + \
+                extra_cycles(p1h, 2, "write", act)
+    return tot
+
+
+def site_conv2_wgrad_gather():
+    tot = 0
+    for wave in range(8):
+        kwb = []
+        for jj in range(2):
+            row = []
+            for lane, l16, kq in lanes():
+                k = min((wave + 8 * jj) * 16 + l16, 249)
+                ic, r = k // 25, k % 25
+                row.append(ic * 144 + (r // 5) * 12 + r % 5)
+            kwb.append(row)
+        for ps in range(2):
+            for jj in range(2):
+                for j in range(8):
+                    addrs = []
+                    for lane, l16, kq in lanes():
+                        ohr = ((ps * 32 + 8 * kq) >> 3) * 12
+                        addrs.append(S_P1 + 2 * (kwb[jj][lane] + ohr + j))
+                    tot += extra_cycles(addrs, 2)
+    return tot
+
+
+def site_conv1_wgrad():
+    tot = 0
+    for wave in range(8):
+        kc1 = [(wave & 1) * 16 + l16 for lane, l16, kq in lanes()]
+        koffc = [(k // 5) * 28 + (k % 5) if k < 25 else 0 for k in kc1]
+        for i in range(5):
+            ps = min((wave >> 1) + 4 * i, 17)
+            dc1 = [S_DC1 + 2 * (l16 * LD_DC1 + ps * 32 + 8 * kq) for lane, l16, kq in lanes()]
+            tot += extra_cycles(dc1, 16)
+            for j in range(8):
+                addrs = []
+                for lane, l16, kq in lanes():
+                    p0 = ps * 32 + 8 * kq
+                    oh, ow0 = p0 // 24, p0 % 24
+                    addrs.append(S_X + 2 * (oh * 28 + ow0 + koffc[lane] + j))
+                tot += extra_cycles(addrs, 2)
+    return tot
+
+
+def site_stage5_writes():
+    tot = 0
+    for t in range(20):
+        for pos in range(4):
+            act = [lane < 16 for lane in range(64)]
+            dc2, dc2h = [], []
+            for lane in range(64):
+                w = lane & 15
+                oh, ow = 2 * (w >> 2) + (pos >> 1), 2 * (w & 3) + (pos & 1)
+                dc2.append(S_DC2 + 2 * (t * LD_DC2 + oh * 8 + ow))
+                dc2h.append(S_DC2H + 2 * (((oh + 4) * 16 + ow + 4) * DG_OCP + t))
+            tot += extra_cycles(dc2, 2, "write", act) + extra_cycles(dc2h, 2, "write", act)
+    return tot
+
+
+def site_dgrad_store():
+    tot = 0
+    for wave in range(8):
+        for r in range(4):
+            act = [l16 < 10 for lane, l16, kq in lanes()]
+            for d in (0, 1, 24, 25):
+                addrs = []
+                for lane, l16, kq in lanes():
+                    mm = wave * 16 + 4 * kq + r
+                    ih, iw = mm // 12, mm % 12
+                    addrs.append(S_DC1 + 2 * (l16 * LD_DC1 + 2 * ih * 24 + 2 * iw + d))
+                tot += extra_cycles(addrs, 2, "write", act)
+    return tot
+
+
+SITES = [("dgrad A (b128)", site_dgrad_A), ("dgrad B (b128)", site_dgrad_B), ("conv2 A (b128)", site_conv2_A),
+         ("conv2 B (b128)", site_conv2_B), ("conv1 gathers (u16)", site_conv1_gather),
+         ("conv1 epilogue writes", site_conv1_epilogue), ("conv2 wgrad gathers (u16)", site_conv2_wgrad_gather),
+         ("conv1 wgrad A b128 + gathers", site_conv1_wgrad), ("stage5 DC2/DC2H writes", site_stage5_writes),
+         ("dgrad DC1 scatter", site_dgrad_store)]
+
+if __name__ == "__main__":
+    total = 0
+    for name, fn in SITES:
+        v = fn()
+        total += v
+        print(f"{name:32s} {v:6d} extra LDS cycles / sample / workgroup")
+    print(f"{'total (modelled sites)':32s} {total:6d}")
