@@ -36,8 +36,9 @@
 // Weight-image layout (16-bit, offsets in elements; all 16-B aligned); each
 // operand holds its live rows and one zero row that padding rows are clamped to:
 //   W1C  [16][32]   conv1  B operand  (k = kh*5+kw)
-//   W2C  [21][424]  conv2  B operand  (k = (kh*5+kw)*16 + ic)
-//   W2D  [11][616]  conv2 dgrad B     (k = ((4-kh)*5 + (4-kw))*24 + oc)
+//   W2C  [21][432]  conv2  B operand  (8-channel K slices (kh*5+kw, ic/8) in kC2Order)
+//   W2D  [77][16][8] conv2 dgrad B, chunk-major: chunk = K slice of 8 channels
+//                   (slice order kDgOrder over (tap = (4-kh)*5 + (4-kw), oc/8))
 //   F1   [51][328]  fc1 B operand     (rows = out features; read transposed for dX)
 // The W2C | W2D | F1 block is copied to LDS by LDS-DMA (global_load_lds_dwordx4).
 // fp32 values used as-is from the flat parameter buffer: all biases and fc2.
@@ -59,8 +60,57 @@ constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O
 constexpr int C2_ICP = 16;  // conv2 fwd HWC: 10 input channels padded to 2 groups of 8
 constexpr int LD_P1H = 24;  // P1H position stride (elements): 12 dwords, conflict-free b128 rows
 constexpr int C2_KS = 13;   // conv2 fwd K-steps: 25 taps x 16 channels = 400 -> 416
+constexpr int P1H_RP = 320; // P1H row pitch (elements): 12 positions x 24 + 32
 constexpr int DG_OCP = 24;  // dgrad HWC: 20 channels padded to 3 groups of 8
 constexpr int DG_KS = 19;   // dgrad K-steps: 25 taps x 24 channels = 600 -> 608
+// DC2H (zero-padded HWC dL/dconv2) row pitch in elements: 16 positions x 24 + 32.  With the
+// K-slice order below it makes the dgrad A reads (16 output pixels crossing a 12-wide row,
+// two K slices per ds_read_b128 lane group) nearly conflict-free: 30 modelled extra LDS
+// cycles per sample instead of 1200 (pitch 384, natural order).
+constexpr int DC2H_RP = 16 * 24 + 32;
+// dgrad K-slice order: K-step ks, lane group q reads slice DG_ORDER[4*ks + q] = tap*3 + ocg
+// (channels 8*ocg .. +7 of tap); slice 75 is padding (zero weights).  Found by local search
+// in tools/lds_bank_model.py (which parses this table).
+struct DgOrder {
+  uint8_t fwd[75], inv[75];
+};
+// conv2 forward K-slice order: K-step ks, lane group q reads slice C2_ORDER[4*ks + q] =
+// tap*2 + icg (channels 8*icg .. +7 of tap); with P1H_RP it makes the conv2 A reads
+// conflict-free (416 modelled extra cycles per sample before).  Slices 50, 51 are padding.
+struct C2Order {
+  uint8_t fwd[50], inv[50];
+};
+constexpr C2Order make_c2_order() {
+  C2Order o{{42, 2, 43, 41, 27, 37, 26, 31, 5, 1, 29, 19, 34, 24, 33, 18, 48, 13, 14, 16, 12, 10, 38, 28, 23,
+             3, 22, 32, 17, 47, 39, 49, 20, 30, 35, 15, 8, 6, 21, 46, 36, 11, 4, 0, 25, 45, 7, 9, 44, 40},
+            {}};
+  for (int i = 0; i < 50; ++i) o.inv[o.fwd[i]] = (uint8_t)i;
+  return o;
+}
+constexpr bool c2_order_is_permutation() {
+  const C2Order o = make_c2_order();
+  for (int c = 0; c < 50; ++c)
+    if (o.fwd[o.inv[c]] != c) return false;
+  return true;
+}
+static_assert(c2_order_is_permutation(), "C2_ORDER must be a permutation of the 50 K slices");
+__constant__ C2Order kC2Order = make_c2_order();
+constexpr DgOrder make_dg_order() {
+  DgOrder o{{10, 70, 33, 22, 35, 46, 63, 52, 49, 27, 66, 6, 7, 56, 11, 71, 64, 53, 47, 74, 36, 42, 51, 40, 16,
+             54, 68, 57, 65, 5, 24, 21, 45, 12, 67, 18, 55, 17, 50, 1, 28, 19, 9, 58, 60, 0, 20, 29, 59, 32,
+             13, 73, 38, 44, 61, 39, 8, 30, 41, 3, 14, 25, 69, 31, 23, 72, 4, 15, 62, 2, 26, 48, 43, 34, 37},
+            {}};
+  for (int i = 0; i < 75; ++i) o.inv[o.fwd[i]] = (uint8_t)i;
+  return o;
+}
+constexpr bool dg_order_is_permutation() {
+  const DgOrder o = make_dg_order();
+  for (int c = 0; c < 75; ++c)
+    if (o.fwd[o.inv[c]] != c) return false;
+  return true;
+}
+static_assert(dg_order_is_permutation(), "DG_ORDER must be a permutation of the 75 K slices");
+__constant__ DgOrder kDgOrder = make_dg_order();
 constexpr int LD_W2C = 432, LD_F1 = 328;   // row strides chosen bank-conflict-free (tools/lds_bank_model.py)
 constexpr int R_W2C = 20, R_F1 = 50;       // live rows; row R_* is the zero row
 // dgrad B operand, chunk-major: [DG_CH chunks of 8 K][16 rows (ic; 10..15 zero)][8]; chunk
@@ -91,10 +141,10 @@ constexpr int S_P1 = S_X + 800 * 2;                   // u16 1440   [ic][12][12]
 constexpr int S_I1 = S_P1 + 1440 * 2;                 // u8 1440    argmax in window
 constexpr int S_P2 = S_I1 + 1440;                     // u16 320    [oc][4][4] = fc1 input
 constexpr int S_I2 = S_P2 + 320 * 2;                  // u8 320
-constexpr int S_P1H = S_I2 + 320;                     // u16 144*24 P1 again, HWC [12][12][24] (16 used)
-constexpr int S_DC2 = S_P1H + 144 * LD_P1H * 2;       // u16 32*72  dL/dconv2 [oc][pix]
-constexpr int S_DC2H = S_DC2 + 32 * LD_DC2 * 2;       // u16 256*24 same, HWC, zero-padded [16][16][24]
-constexpr int S_DC1 = S_DC2H + 256 * DG_OCP * 2;      // u16 16*584 dL/dconv1 [oc][pix]
+constexpr int S_P1H = S_I2 + 320;                     // u16 12*320 P1 again, HWC [12][P1H_RP] (16 of 24 used)
+constexpr int S_DC2 = S_P1H + 12 * P1H_RP * 2;       // u16 32*72  dL/dconv2 [oc][pix]
+constexpr int S_DC2H = S_DC2 + 32 * LD_DC2 * 2;       // u16 16*416 same, HWC, zero-padded [16][DC2H_RP]
+constexpr int S_DC1 = S_DC2H + 16 * DC2H_RP * 2;      // u16 16*592 dL/dconv1 [oc][pix]
 constexpr int S_COFF = S_DC1 + 16 * LD_DC1 * 2;       // i16 4*16   conv2 (K-step, lane group) -> P1H offset
 constexpr int S_DOFF = S_COFF + 4 * 16 * 2;           // i16 4*24   dgrad (K-step, lane group) -> DC2H offset
 constexpr int S_DZ1B = S_DOFF + 4 * 24 * 2;           // u16 64     dZ1 as the MFMA A row
@@ -160,12 +210,11 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 template <typename T>
 __device__ __forceinline__ void dgrad_store(unsigned short* DC1, int ci, int mm, float v, int bi) {
   const int ih = mm / 12, iw = mm - ih * 12;
-  unsigned short* d = DC1 + ci * LD_DC1 + (2 * ih) * 24 + 2 * iw;
-  const unsigned short hv = h16<T>(v), z = 0;
-  d[0] = bi == 0 ? hv : z;
-  d[1] = bi == 1 ? hv : z;
-  d[24] = bi == 2 ? hv : z;
-  d[25] = bi == 3 ? hv : z;
+  // the window's two rows are two aligned 32-bit pairs: 2 ds_write_b32, not 4 x b16
+  uint32_t* d = reinterpret_cast<uint32_t*>(DC1 + ci * LD_DC1 + (2 * ih) * 24 + 2 * iw);
+  const uint32_t hv = h16<T>(v);
+  d[0] = bi == 0 ? hv : (bi == 1 ? hv << 16 : 0u);
+  d[12] = bi == 2 ? hv : (bi == 3 ? hv << 16 : 0u);
 }
 
 // conv2 dgrad epilogue for one (input channel, P1 pixel): relu gate, then the
@@ -268,16 +317,17 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     }
     // work that needs no loaded data overlaps the loads
     if (tid < 64) {
-      // conv2 A-fragment offset of K-step ks for lane group q: K slice kg = 4*ks + q
-      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: K >= 400 meets zero weights)
+      // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
+      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
       const int q = tid >> 4, ks = tid & 15;
-      const int kg = min(4 * ks + q, 49), tap = kg >> 1;
-      COFF[tid] = (short)(((tap / 5) * 12 + tap % 5) * LD_P1H + (kg & 1) * 8);
+      const int kg = kC2Order.fwd[min(4 * ks + q, 49)], tap = kg >> 1;
+      COFF[tid] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
     } else if (tid < 160) {
-      // dgrad: K slice kg covers channels 8*(kg%3) .. +7 of tap kg/3 (K >= 600: zero weights)
+      // dgrad: K slice 4*ks + q is channels 8*ocg .. +7 of tap (kDgOrder; slice 75 and the
+      // clamped steps >= DG_KS meet zero weights, their A offset only has to be in bounds)
       const int q = (tid - 64) / 24, ks = (tid - 64) - 24 * q;
-      const int kg = min(4 * ks + q, 74), tap = kg / 3, ocg = kg - 3 * tap;
-      DOFF[tid - 64] = (short)((((tap / 5) * 16) + tap % 5) * DG_OCP + ocg * 8);
+      const int kg = kDgOrder.fwd[min(4 * ks + q, 74)], tap = kg / 3, ocg = kg - 3 * tap;
+      DOFF[tid - 64] = (short)((tap / 5) * DC2H_RP + (tap % 5) * DG_OCP + ocg * 8);
     }
     // P1H | DC2 | DC2H | DC1 are contiguous: zero their padding once with 16-B stores
     {
@@ -401,7 +451,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
             P1[l16 * 144 + w] = hv;
             I1[l16 * 144 + w] = (uint8_t)bi;
-            P1H[w * LD_P1H + l16] = hv;
+            P1H[(w / 12) * P1H_RP + (w % 12) * LD_P1H + l16] = hv;
           }
         }
       }
@@ -416,7 +466,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       const int m = mt * 16 + l16;
       const int p = m >> 2, q = m & 3;
       const int oy = 2 * (p >> 2) + (q >> 1), ox = 2 * (p & 3) + (q & 1);
-      const unsigned short* arow = P1H + (oy * 12 + ox) * LD_P1H;
+      const unsigned short* arow = P1H + oy * P1H_RP + ox * LD_P1H;
       const unsigned short* wrow = W2c + min(nt * 16 + l16, R_W2C) * LD_W2C + kb;
       const s16x8 co0 = *reinterpret_cast<const s16x8*>(COFF + kq * 16);
       const s16x8 co1 = *reinterpret_cast<const s16x8*>(COFF + kq * 16 + 8);
@@ -563,12 +613,15 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
             const float gv = f16v<T>(P2[pi]) > 0.f ? c[0] * D2S[t] : 0.f;
             const int bi = I2[pi];
             const int oh0 = 2 * (lane >> 2), ow0 = 2 * (lane & 3);
+            const uint32_t hg = h16<T>(gv);
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)  // window rows: aligned 32-bit pairs of DC2
+              reinterpret_cast<uint32_t*>(DC2 + t * LD_DC2 + (oh0 + dy) * 8 + ow0)[0] =
+                  bi == 2 * dy ? hg : (bi == 2 * dy + 1 ? hg << 16 : 0u);
 #pragma unroll
             for (int pos = 0; pos < 4; ++pos) {
               const int oh = oh0 + (pos >> 1), ow = ow0 + (pos & 1);
-              const unsigned short hb = pos == bi ? h16<T>(gv) : (unsigned short)0;
-              DC2[t * LD_DC2 + oh * 8 + ow] = hb;
-              DC2H[((oh + 4) * 16 + ow + 4) * DG_OCP + t] = hb;
+              DC2H[(oh + 4) * DC2H_RP + (ow + 4) * DG_OCP + t] = pos == bi ? (unsigned short)hg : (unsigned short)0;
             }
           }
         }
@@ -618,8 +671,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
       // B fragment of K-step ks: chunk 4*ks + kq, row l16 (ic)
       const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
       const int mw = wave * 16 + l16, m8 = 128 + l16;
-      const unsigned short* aw = DC2H + ((mw / 12) * 16 + mw % 12) * DG_OCP;
-      const unsigned short* a8 = DC2H + ((m8 / 12) * 16 + m8 % 12) * DG_OCP;
+      const unsigned short* aw = DC2H + (mw / 12) * DC2H_RP + (mw % 12) * DG_OCP;
+      const unsigned short* a8 = DC2H + (m8 / 12) * DC2H_RP + (m8 % 12) * DG_OCP;
       // tile-8 share: 3 K-steps, the third only for waves 0-2 (others read the zero row)
       frag f8a[3], f8b[3];
 #pragma unroll
@@ -771,9 +824,9 @@ __device__ __forceinline__ void write_images(unsigned short* wimg, int i, float 
     const int j = i - O_C2W;
     const int oc = j / 250, k = j % 250;
     const int ic = k / 25, r = k % 25, kh = r / 5, kw = r % 5;
-    wimg[I_W2C + oc * LD_W2C + r * C2_ICP + ic] = h;
-    const int kd = ((4 - kh) * 5 + (4 - kw)) * DG_OCP + oc;  // dgrad K index
-    wimg[I_W2D + ((kd >> 3) * 16 + ic) * 8 + (kd & 7)] = h;
+    wimg[I_W2C + oc * LD_W2C + kC2Order.inv[r * 2 + (ic >> 3)] * 8 + (ic & 7)] = h;
+    const int slice = kDgOrder.inv[((4 - kh) * 5 + (4 - kw)) * 3 + (oc >> 3)];  // dgrad K slice
+    wimg[I_W2D + (slice * 16 + ic) * 8 + (oc & 7)] = h;
   } else if (i >= O_F1W && i < O_F1B) {
     const int j = i - O_F1W;
     const int o = j / 320, ii = j % 320;
