@@ -144,8 +144,9 @@ def main() -> int:
             "data": "synthetic (60000 x 1x28x28 uint8, class-conditional; random-init weights)",
             "config": {"model": "Net (ref src/model.py, 21,840 params)", "global_batch": args.global_batch,
                        "seq_len": None, "parallelism": f"dp{n}", "optimizer": "SGD lr=0.02 momentum=0.5",
-                       "engine": "fused HIP (lenet_train + lenet_update" + (" + gradient all-reduce" if n > 1 else "")
-                                 + ")", "hip_graph": (not args.no_graph) and bool(eng.capture_comm_ok),
+                       "engine": "fused HIP (lenet_train + lenet_update"
+                                 + {"fused-ipc": " with in-kernel xGMI gradient exchange", "none": ""}.get(
+                                     eng.allreduce_kind, " + gradient all-reduce") + ")", "hip_graph": (not args.no_graph) and bool(eng.capture_comm_ok),
                        "allreduce": eng.allreduce_kind},
             "epoch_s": round(epoch_s, 4) if epoch_s is not None else None,
             "baseline_epoch_s": base,
@@ -154,6 +155,8 @@ def main() -> int:
         from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc
         if _ipc.LAST_TIMING:
             rec["config"]["allreduce_select_us"] = _ipc.LAST_TIMING
+        if eng.path_timing_us:
+            rec["config"]["step_path_select_us"] = eng.path_timing_us
         if comm_err:
             rec["comm_error"] = "IPC all-reduce timed out waiting for a peer: results invalid"
         if val:

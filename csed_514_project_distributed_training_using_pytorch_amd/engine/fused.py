@@ -1,13 +1,21 @@
 """Fused LeNet training engine: the MI355X fast path for ``Net`` (ref src/model.py).
 
 One training step = two HIP kernels (``csed::lenet_train`` + ``csed::lenet_update``,
-see csrc/kernels/lenet_fused.hip), plus -- for data parallelism -- one RCCL
-all-reduce of the 87,360-byte gradient between them:
+see csrc/kernels/lenet_fused.hip) at any world size:
 
     lenet_train    per-sample fwd+bwd of the whole network in LDS -> per-WG gradient slabs
-    lenet_update   fixed-order slab reduce (-> flat grad)          [world > 1: reduce only]
-    all_reduce     SUM over ranks on the flat grad (RCCL / xGMI)   [world > 1]
-    lenet_update   SGD-momentum + fp32 master params + 16-bit weight images + counters
+    lenet_update   fixed-order slab reduce -> [world > 1: in-kernel exchange with every
+                   peer over xGMI, rank-ordered sum] -> SGD-momentum + fp32 master params
+                   + 16-bit weight images + device counters
+
+The data-parallel gradient all-reduce (ref src/train_dist.py:83, DDP's one
+87,360-byte bucket) is fused into lenet_update: each update lane pushes its
+rank-local gradient value straight into every peer's IPC-mapped receive buffer
+and sums what the peers pushed (csrc/comm buffers, LL-tagged words).  It is
+enabled after a collective bring-up and an exact self-test, and (in ``auto``
+mode, RCCL process group) only if it times faster than the fallback step:
+
+    lenet_update (reduce only) -> all-reduce (one-shot IPC kernel or RCCL) -> SGD kernel
 
 All per-step state (batch cursor into this rank's epoch permutation, Philox
 offset, optimizer step) lives on the device, so a sequence of steps is
@@ -29,7 +37,7 @@ from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
 from ..parallel.comm import DistContext
-from ..parallel.ipc import make_allreduce
+from ..parallel.ipc import allreduce_mode, make_allreduce, open_exchange
 from ..utils.flat import FlatParams
 
 
@@ -39,9 +47,14 @@ def layout() -> tuple[int, int, int, int]:
     16-bit weight-image elements (I_END), conv slab row per workgroup (CNP_PAD: conv1.w/b +
     conv2.w/b = 5280 floats in 64-float chunks), per-sample fc vector length (VEC) and the
     largest per-rank batch that uses batch staging (STAGE_MAXB)."""
-    wimg, conv, vec, nparams, stage_max = (int(v) for v in torch.ops.csed.lenet_layout())
+    wimg, conv, vec, nparams, stage_max, _exch = (int(v) for v in torch.ops.csed.lenet_layout())
     assert nparams == N_PARAMS
     return wimg, conv, vec, stage_max
+
+
+def exch_words() -> int:
+    """8-byte words per sender of lenet_update's fused exchange buffer."""
+    return int(torch.ops.csed.lenet_layout()[5])
 
 
 class FusedLeNetTrainer:
@@ -104,21 +117,119 @@ class FusedLeNetTrainer:
         self.xstage = torch.zeros((self.B, 784), dtype=torch.uint8, device=dev) if self.staged else None
         self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
         self.repack()
-        # gradient all-reduce: the one-shot IPC kernel (csrc/comm) when every rank
-        # passes its self-test, else RCCL (see parallel/ipc.py)
-        self.allreduce = make_allreduce(self.ctx, N_PARAMS) if (self.comm and self.world > 1) else None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.capture_comm_ok: bool | None = None
+        # gradient all-reduce.  Fallback step (3 kernels): the one-shot IPC kernel
+        # (csrc/comm) when every rank passes its self-test, else RCCL (parallel/ipc.py).
+        # Preferred: the exchange fused into lenet_update (1 kernel), see module docstring.
+        self.exch = None
+        self.exch_timeout_s = 2.0
+        self.path_timing_us: dict | None = None
+        multi = self.comm and self.world > 1
+        mode = allreduce_mode() if multi else "rccl"
+        self.allreduce = make_allreduce(self.ctx, N_PARAMS) if multi and mode != "fused" else None
+        if multi and mode in ("auto", "fused"):
+            self._enable_exchange(required=(mode == "fused"))
 
     @property
     def allreduce_kind(self) -> str:
         if not self.comm:
             return "none"
+        if self.exch is not None:
+            return "fused-ipc"
         return "ipc-oneshot" if self.allreduce is not None else "rccl"
 
+    # ------------------------------------------------- fused gradient exchange
+    def _enable_exchange(self, required: bool) -> None:
+        """Bring up lenet_update's in-kernel exchange (collective on every rank):
+        open the IPC buffers, self-test them with the update kernel itself, and in
+        auto mode on RCCL keep it only if a captured step is faster than the fallback's."""
+        ex, why = open_exchange(self.ctx, exch_words())
+        ok = ex is not None
+        if ok:
+            self.exch = ex
+            ok = self._vote(self._exchange_self_test())
+            if not ok:
+                why = "self-test mismatch or timeout on some rank"
+        if not ok:
+            self.exch = None
+            if required:
+                raise RuntimeError(f"CSED_ALLREDUCE=fused but the fused exchange is unusable ({why})")
+            return
+        if not required and self.ctx.backend == "nccl":
+            t_fused = self._time_steps()
+            saved, self.exch = self.exch, None
+            t_fallback = self._time_steps()
+            self.exch = saved if t_fused <= t_fallback else None
+            self.path_timing_us = {"fused_step_us": round(t_fused, 2), "fallback_step_us": round(t_fallback, 2),
+                                   "fallback": "ipc-oneshot" if self.allreduce is not None else "rccl"}
+
+    def _vote(self, ok: bool) -> bool:
+        dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def _exchange_self_test(self, rounds: int = 4) -> bool:
+        """Integer-valued slabs through lenet_update with and without the exchange: the
+        exchanged gradient must equal the process group's sum of the local ones exactly
+        (both slot parities, every rank).  Runs the same collectives on every rank."""
+        ops = torch.ops.csed
+        gen = torch.Generator(device="cpu").manual_seed(977 + 31 * self.ctx.rank)
+        pg_dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
+        common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
+                  self.weight_decay, self.nesterov, self.step_count, self.ticket, None, None, False, None, 0, None,
+                  self.mfma)
+        ok = True
+        for _ in range(rounds):
+            self.slab.copy_(torch.randint(-8, 9, self.slab.shape, generator=gen, dtype=torch.float32))
+            self.vslab.copy_(torch.randint(-4, 5, self.vslab.shape, generator=gen, dtype=torch.float32))
+            local = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
+            fused = torch.empty_like(local)
+            ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, local, *common)
+            ref = local.to(pg_dev, copy=True)
+            dist.all_reduce(ref)
+            try:
+                ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, fused, *common, None,
+                                 self.exch.id, self.exch_timeout_s)
+                ok &= bool(torch.equal(fused, ref.to(self.device)))
+            except Exception:
+                ok = False
+        torch.cuda.synchronize(self.device)
+        try:
+            ok &= self.exch.error(reset=True) == 0
+        except Exception:
+            ok = False
+        self.vslab.zero_()
+        return ok
+
+    def _time_steps(self, nsteps: int = 16, reps: int = 5) -> float:
+        """us per training step of a captured graph (max over ranks); engine state is restored."""
+        state = self._state()
+        saved = [t.clone() for t in state]
+        g = self._capture(nsteps)
+        g.replay()
+        torch.cuda.synchronize(self.device)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            g.replay()
+        b.record()
+        b.synchronize()
+        us = a.elapsed_time(b) * 1e3 / (reps * nsteps)
+        del g
+        for t, v in zip(state, saved):
+            t.copy_(v)
+        torch.cuda.synchronize(self.device)
+        dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([us], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     def comm_errors(self) -> int:
-        """Nonzero if the IPC all-reduce ever timed out waiting for a peer (synchronous)."""
-        return self.allreduce.error() if self.allreduce is not None else 0
+        """Nonzero if an IPC exchange ever timed out waiting for a peer (synchronous)."""
+        e = self.exch.error() if self.exch is not None else 0
+        return e | (self.allreduce.error() if self.allreduce is not None else 0)
 
     def _max_grid(self) -> int:
         return max(self.grid, 1)
@@ -168,7 +279,10 @@ class FusedLeNetTrainer:
                         self.xstage if st else None, self.lstage if st else None, st)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
-        if self.comm:
+        if self.exch is not None:
+            ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
+                             self.loss_parts, grid, self.loss_acc, self.mfma, None, self.exch.id, self.exch_timeout_s)
+        elif self.comm:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, self.flat.grad, *common, None, None, False,
                              self.loss_parts, grid, self.loss_acc, self.mfma)
             if self.allreduce is not None:
@@ -213,13 +327,17 @@ class FusedLeNetTrainer:
         self.cursor.add_(1)
 
     # --------------------------------------------------------- graph capture
+    def _state(self) -> list[torch.Tensor]:
+        """Device tensors a training step advances."""
+        return [self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor, self.rng_offset,
+                self.loss_acc] + ([self.xstage, self.lstage] if self.staged else [])
+
     def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
         # snapshot the state the capture warm-up will advance; the side stream must
         # wait for the snapshot copies too (they are enqueued on the current stream)
-        state = [self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor, self.rng_offset,
-                 self.loss_acc] + ([self.xstage, self.lstage] if self.staged else [])
+        state = self._state()
         saved = [t.clone() for t in state]
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

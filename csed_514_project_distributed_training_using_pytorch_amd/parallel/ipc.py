@@ -13,7 +13,14 @@ ranks then agree (MIN over the process group) and the path is enabled only if
 every rank passed; otherwise callers keep using RCCL.  In ``auto`` mode the two
 are then timed on the real buffer and the faster one is kept (the slowest
 rank's numbers decide, so all ranks agree).  ``CSED_ALLREDUCE`` = ``auto``
-(default) | ``ipc`` (use it; fail if unusable) | ``rccl`` (never try).
+(default) | ``ipc`` (use it; fail if unusable) | ``rccl`` (never try) | ``fused``
+(the fused engine's in-kernel exchange, engine/fused.py; this kernel is then only
+its fallback).
+
+The same IPC buffers also back the fused engine's in-kernel exchange
+(:func:`open_exchange`): lenet_update pushes its reduced gradient to every peer
+and sums all ranks itself, so a data-parallel step is one kernel fewer than
+reduce + all-reduce + SGD.
 """
 from __future__ import annotations
 
@@ -127,16 +134,18 @@ class IpcAllReduce:
         return ok
 
 
-def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
-    """The IPC all-reduce if every rank can use it (see module docstring), else None.
-
-    Every rank runs the same sequence of collectives whatever fails locally:
-    create -> vote -> all-gather handles -> open -> vote -> self-test -> vote.
-    """
+def allreduce_mode() -> str:
+    """``CSED_ALLREDUCE``: auto (default) | fused | ipc | rccl (see engine/fused.py)."""
     mode = os.environ.get("CSED_ALLREDUCE", "auto").lower()
-    if mode == "rccl" or not ctx.is_distributed or ctx.device.type != "cuda":
-        return None
-    ar = IpcAllReduce(ctx, n)
+    if mode not in ("auto", "fused", "ipc", "rccl"):
+        raise ValueError(f"CSED_ALLREDUCE={mode!r}: expected auto, fused, ipc or rccl")
+    return mode
+
+
+def _open(ctx: DistContext, n: int, blocks: int) -> tuple[IpcAllReduce | None, str]:
+    """create -> vote -> all-gather handles -> open -> vote (every rank issues the same
+    collectives whatever fails locally).  Returns the opened buffer, or None + why."""
+    ar = IpcAllReduce(ctx, n, blocks=blocks)
     why = ""
     handle = None
     try:
@@ -151,6 +160,29 @@ def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
         except Exception as e:
             why, ok = f"open: {type(e).__name__}: {e}", False
         ok = _all_ok(ctx, ok)
+    return (ar if ok else None), (why or ("" if ok else "a peer failed to create / map its buffer"))
+
+
+def open_exchange(ctx: DistContext, words: int) -> tuple[IpcAllReduce | None, str]:
+    """An opened IPC exchange buffer of ``words`` 8-byte words per sender for a kernel that
+    carries its own LL exchange (lenet_update's fused gradient all-reduce).  The caller
+    self-tests it with that kernel.  Collective."""
+    if not ctx.is_distributed or ctx.device.type != "cuda":
+        return None, "not distributed on a GPU"
+    return _open(ctx, (words + 3) // 4 * 4, blocks=1)
+
+
+def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
+    """The IPC all-reduce if every rank can use it (see module docstring), else None.
+
+    Every rank runs the same sequence of collectives whatever fails locally:
+    create -> vote -> all-gather handles -> open -> vote -> self-test -> vote.
+    """
+    mode = allreduce_mode()
+    if mode == "rccl" or not ctx.is_distributed or ctx.device.type != "cuda":
+        return None
+    ar, why = _open(ctx, n, blocks=32)
+    ok = ar is not None
     if ok:
         ok = _all_ok(ctx, ar.self_test())
         why = why or ("" if ok else "self-test mismatch or timeout on some rank")

@@ -287,7 +287,7 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 // largest per-rank batch the batch-staging path handles].
 std::vector<int64_t> lenet_layout() {
   return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
-          csed::lenet_param_count(), csed::lenet_stage_max_batch()};
+          csed::lenet_param_count(), csed::lenet_stage_max_batch(), csed::lenet_exch_words()};
 }
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
@@ -373,7 +373,8 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
                   Tensor& params, Tensor& momentum, Tensor& wimg, double lr, double mom, double dampening,
                   double weight_decay, bool nesterov, Tensor& step, Tensor& ticket, const optional<Tensor>& cursor,
                   const optional<Tensor>& rng_offset, bool apply_sgd, const optional<Tensor>& loss_parts,
-                  int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg) {
+                  int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg,
+                  int64_t exch_id, double exch_timeout_s) {
   dev(slab, "slab"); dev(params, "params"); dev(momentum, "momentum"); dev(wimg, "wimg");
   TORCH_CHECK(params.numel() == csed::lenet_param_count() && momentum.numel() == params.numel(),
               "lenet_update: params / momentum must hold the 21840 flat LeNet parameters");
@@ -394,6 +395,9 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 128, "lenet_update: dbg must be int64[>=1024]");
     a.dbg = (uint64_t*)dbg->data_ptr();
   }
+  // exch_id >= 0: csrc/comm buffer of the fused gradient exchange (checked by the launcher)
+  TORCH_CHECK(exch_id < 0 || !a.grad_in, "lenet_update: the fused exchange reduces the slabs itself (no grad_in)");
+  a.exch_id = (int)exch_id; a.exch_timeout_s = exch_timeout_s;
 
   CHECK_HIP(csed::launch_lenet_update(a, optpt<float>(loss_parts), (int)nparts, optpt<float>(loss_acc),
                                       cur_stream(params)));
@@ -427,7 +431,7 @@ TORCH_LIBRARY(csed, m) {
         "Tensor(c!) momentum, Tensor(d!) wimg, float lr, float mom, float dampening, float weight_decay, "
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
         "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
-        "Tensor(j!)? dbg=None) -> ()");
+        "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
         "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "

@@ -20,5 +20,21 @@ hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double 
 // Error word: nonzero if a wait ever timed out (synchronous read).
 hipError_t ipc_error(int id, int* err_out, bool reset);
 
+// Device view of an opened exchange buffer, for kernels that carry their own
+// LL exchange (lenet_update's fused gradient all-reduce).  Layout of rank r's
+// receive buffer: base[r] + slot * kIpcMaxRanks * cap + sender * cap + word;
+// slot = tag & 1; each 8-byte word is {fp32 value, 32-bit tag}.  counters[blk]
+// is the last tag used by workgroup blk of the kernel that owns the buffer.
+constexpr int kIpcMaxRanks = 8;
+constexpr int kIpcMaxBlocks = 128;
+struct IpcPeers {
+  uint64_t* base[kIpcMaxRanks];
+  int64_t* counters;  // [kIpcMaxBlocks]
+  int* err;
+  int64_t cap;        // words per sender per slot
+  int world, rank;
+};
+hipError_t ipc_peers(int id, IpcPeers* out);
+
 }  // namespace comm
 }  // namespace csed

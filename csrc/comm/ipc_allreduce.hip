@@ -29,8 +29,8 @@
 namespace csed {
 namespace comm {
 
-constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 64;
+constexpr int kMaxRanks = kIpcMaxRanks;
+constexpr int kMaxBlocks = kIpcMaxBlocks;
 constexpr int kThreads = 256;
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -199,6 +199,18 @@ hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double 
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(c->blocks), dim3(kThreads), 0, s, in, out, n / 2, c->cap,
                      c->world, c->rank, c->peers, c->counters, c->err, ticks);
   return hipGetLastError();
+}
+
+hipError_t ipc_peers(int id, IpcPeers* out) {
+  IpcComm* c = get(id);
+  if (!c || c->world < 1) return hipErrorInvalidValue;
+  for (int r = 0; r < kMaxRanks; ++r) out->base[r] = c->peers.base[r];
+  out->counters = c->counters;
+  out->err = c->err;
+  out->cap = c->cap;
+  out->world = c->world;
+  out->rank = c->rank;
+  return hipSuccess;
 }
 
 hipError_t ipc_error(int id, int* err_out, bool reset) {

@@ -46,6 +46,7 @@
 // Flat parameter order (= Net.state_dict() order, 21,840 floats):
 //   conv1.w 0, conv1.b 250, conv2.w 260, conv2.b 5260, fc1.w 5280,
 //   fc1.b 21280, fc2.w 21330, fc2.b 21830.
+#include "comm/ipc_allreduce.h"
 #include "common.h"
 #include "dispatch.h"
 
@@ -934,10 +935,86 @@ __device__ __forceinline__ void finish_param(const LenetUpdateArgs& a, int i, fl
   write_images<T>(a.wimg, i, p);
 }
 
-template <typename T>
+// ---------------------------------------------------------------------------
+// Data-parallel exchange fused into lenet_update (EXCH = true).
+//
+// Every gradient value is final in exactly one lane of one workgroup of the
+// update kernel (conv role: one parameter per lane of wave 0; fc role: four
+// [dW | db] tile entries per lane).  With EXCH that lane pushes its rank-local
+// sum to every peer's receive buffer (csrc/comm IPC mapping, one xGMI link per
+// peer, all links at once), polls its own receive buffer for the peers' values
+// of the same word, and sums all ranks in rank order 0..N-1 -- so every rank
+// gets bitwise-identical gradients -- before the SGD step.  No reduce-only
+// launch, no separate all-reduce kernel, no SGD-only launch: one kernel per
+// step for any world size.
+//
+// Words are LL-tagged ({fp32 value, 32-bit tag}, one 8-byte store), so the data
+// carries its own synchronisation; the tag is a per-workgroup call counter that
+// advances identically on every rank, and two slots alternate by tag parity
+// (see csrc/comm/ipc_allreduce.hip for why a peer cannot get two calls ahead).
+// Exchange word of a value: conv parameter i -> i; fc tile entry (tile, r,
+// lane) -> CNP_PAD + tile*256 + r*64 + lane, so each wave's stores to a peer
+// are 512-byte contiguous runs.  Every wait is bounded by a wall-clock timeout
+// that raises the comm error word instead of hanging the GPU.
+// ---------------------------------------------------------------------------
+constexpr int EXCH_WORDS = CNP_PAD + FC_TILES * 256;  // 27840
+
+__device__ __forceinline__ uint64_t ll_word(float v, uint32_t t) {
+  return ((uint64_t)t << 32) | (uint64_t)__float_as_uint(v);
+}
+
+// v[k] (this rank's value of exchange word idx[k], for live[k]) := sum over ranks.
+template <int K>
+__device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t t, const int (&idx)[K],
+                                             const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
+                                             bool& timed_out) {
+  constexpr int R = comm::kIpcMaxRanks;
+  const int64_t slot = (int64_t)(t & 1) * R * px.cap;
+#pragma unroll
+  for (int p = 0; p < R; ++p) {
+    if (p < px.world && p != px.rank) {
+      uint64_t* dst = px.base[p] + slot + (int64_t)px.rank * px.cap;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (live[k]) dst[idx[k]] = ll_word(v[k], t);
+    }
+  }
+  const uint64_t* mine = px.base[px.rank] + slot;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t w[R][K];
+  while (true) {
+    // relaxed system-scope loads: never cached or hoisted, all issued before the first wait
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        w[p][k] = __hip_atomic_load(mine + (int64_t)min(p, px.world - 1) * px.cap + idx[k], __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_SYSTEM);
+    bool ready = true;
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (p < px.world && p != px.rank && live[k]) ready = ready && (uint32_t)(w[p][k] >> 32) == t;
+    if (ready || timed_out) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) timed_out = true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+      if (p < px.world) s += p == px.rank ? v[k] : __uint_as_float((uint32_t)w[p][k]);
+    v[k] = s;
+  }
+}
+
+template <typename T, bool EXCH>
 __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
                                                              int B, float* loss_parts, int nparts,
-                                                             float* loss_acc) {
+                                                             float* loss_acc, comm::IpcPeers px,
+                                                             uint64_t timeout_ticks) {
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
 
@@ -945,6 +1022,9 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
   const int tid = threadIdx.x, blk = blockIdx.x;
+  // exchange tag of this call (uniform load; written back after the block's last poll)
+  const uint32_t xt = EXCH ? (uint32_t)(px.counters[blk] + 1) : 0u;
+  bool timed_out = false;
 #define USTAMP(k) \
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
@@ -988,8 +1068,13 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
     __syncthreads();
     USTAMP(3);
     if (tid < 64 && pi < CNP) {
-      const float g = (part2[0][tid] + part2[1][tid]) + (part2[2][tid] + part2[3][tid]);
-      finish_param<T>(a, pi, g, first, p0, m0);
+      float g[1] = {(part2[0][tid] + part2[1][tid]) + (part2[2][tid] + part2[3][tid])};
+      if (EXCH) {
+        const int idx[1] = {pi};
+        const bool live[1] = {true};
+        ll_allreduce<1>(px, xt, idx, live, g, timeout_ticks, timed_out);
+      }
+      finish_param<T>(a, pi, g[0], first, p0, m0);
     }
     USTAMP(4);
     if (cblk == 0 && loss_parts && tid < 64) {
@@ -1054,13 +1139,29 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
         for (int u = 0; u < 16; ++u) c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], c, 0, 0, 0);
       }
       USTAMP(2);
+      float g[4] = {c[0], c[1], c[2], c[3]};
+      if (EXCH) {
+        int idx[4];
+        bool live[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          idx[r] = CNP_PAD + tile * 256 + r * 64 + lane;
+          live[r] = pidx[r] >= 0;
+        }
+        ll_allreduce<4>(px, xt, idx, live, g, timeout_ticks, timed_out);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (pidx[r] >= 0) finish_param<T>(a, pidx[r], c[r], first, pp[r], pm[r]);
+        if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r]);
       USTAMP(4);
     }
   }
 
+  if (EXCH) {
+    if (timed_out) atomicOr(px.err, 1);
+    __syncthreads();  // every wave has read counters[blk]
+    if (tid == 0) px.counters[blk] = xt;
+  }
   if (a.apply_sgd) {
     // Device counters.  cursor / rng_offset are never read by this kernel, so
     // one thread bumps them directly.  step[0] is read by every block only when
@@ -1138,12 +1239,28 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     return hipGetLastError();
   }
   if (!a.vslab || a.B <= 0) return hipErrorInvalidValue;
+  comm::IpcPeers px{};
+  if (a.exch_id >= 0) {
+    // fused data-parallel exchange: the buffer must hold this kernel's word layout
+    static_assert(NB_UPDATE <= comm::kIpcMaxBlocks, "one exchange counter per update workgroup");
+    const hipError_t e = comm::ipc_peers(a.exch_id, &px);
+    if (e != hipSuccess) return e;
+    if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
+    const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    CSED_DISPATCH_MFMA(a.mfma_dtype, {
+      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+                         a.B, loss_parts, nparts, loss_acc, px, ticks);
+    });
+    return hipGetLastError();
+  }
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
-    hipLaunchKernelGGL(lenet_update_kernel<scalar_t>, dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab, a.B,
-                       loss_parts, nparts, loss_acc);
+    hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+                       a.B, loss_parts, nparts, loss_acc, px, (uint64_t)0);
   });
   return hipGetLastError();
 }
+
+int64_t lenet_exch_words() { return EXCH_WORDS; }
 
 int lenet_stage_max_batch() { return STAGE_MAXB; }
 

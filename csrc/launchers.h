@@ -181,7 +181,13 @@ struct LenetUpdateArgs {
   int apply_sgd;
   int mfma_dtype;
   uint64_t* dbg;      // optional [blocks, 8] s_memrealtime stamps (diagnostics)
+  // Fused data-parallel gradient exchange (csrc/comm IPC buffer id, -1 = none):
+  // the reduced gradient of this kernel is summed over all ranks in-kernel
+  // before SGD / export.  The buffer needs lenet_exch_words() words per sender.
+  int exch_id;
+  double exch_timeout_s;
 };
+int64_t lenet_exch_words();
 // loss_parts [nparts, 2] are summed in a fixed order into loss_acc[2] (optional).
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
                                hipStream_t s);

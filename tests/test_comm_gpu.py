@@ -1,4 +1,5 @@
-"""Native one-shot IPC all-reduce (csrc/comm/ipc_allreduce.hip, parallel/ipc.py).
+"""Native one-shot IPC all-reduce (csrc/comm/ipc_allreduce.hip, parallel/ipc.py) and the
+gradient exchange fused into lenet_update (csrc/kernels/lenet_fused.hip, engine/fused.py).
 
 Two ranks share the box's single GPU: the handle exchange, the peer mapping,
 the flag protocol (both slot parities, graph replay) and the fused engine's
@@ -74,20 +75,33 @@ def _worker(rank, world, port, q):
         from csed_514_project_distributed_training_using_pytorch_amd.models import Net
         from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
 
-        torch.manual_seed(1)
-        eng = FusedLeNetTrainer(Net().to(dev), synthetic_mnist(2048, seed=3), lr=0.05, global_batch=64, ctx=ctx)
-        smp = ShardSampler(2048, world, rank, shuffle=True, seed=42)
-        smp.set_epoch(0)
-        eng.set_epoch_order(smp.indices())
-        eng.run_steps(12, steps_per_graph=4)
-        torch.cuda.synchronize(dev)
-        p = eng.flat.data.cpu()
-        other = p.clone()
-        dist.broadcast(other, src=0)
-        res["kind"] = eng.allreduce_kind
-        res["params_equal"] = torch.equal(p, other)
-        res["engine_errors"] = eng.comm_errors()
-        res["finite"] = bool(torch.isfinite(p).all())
+        data = synthetic_mnist(2048, seed=3)
+
+        def train(mode):
+            # ipc: reduce-only update -> one-shot IPC all-reduce kernel -> SGD kernel;
+            # fused: lenet_update exchanges with the peer itself (one kernel)
+            os.environ["CSED_ALLREDUCE"] = mode
+            torch.manual_seed(1)
+            eng = FusedLeNetTrainer(Net().to(dev), data, lr=0.05, global_batch=64, ctx=ctx)
+            smp = ShardSampler(2048, world, rank, shuffle=True, seed=42)
+            smp.set_epoch(0)
+            eng.set_epoch_order(smp.indices())
+            eng.run_steps(12, steps_per_graph=4)
+            eng.step()  # one eager step after the graph replays
+            torch.cuda.synchronize(dev)
+            p = eng.flat.data.cpu()
+            other = p.clone()
+            dist.broadcast(other, src=0)
+            res[f"kind_{mode}"] = eng.allreduce_kind
+            res[f"params_equal_{mode}"] = torch.equal(p, other)
+            res[f"engine_errors_{mode}"] = eng.comm_errors()
+            res[f"finite_{mode}"] = bool(torch.isfinite(p).all())
+            return p
+
+        p_ipc = train("ipc")
+        p_fused = train("fused")
+        # both sum the same rank-local gradients in rank order: bitwise-identical training
+        res["fused_equals_ipc"] = torch.equal(p_ipc, p_fused)
         q.put((rank, res))
         dist.destroy_process_group()
     except Exception as e:  # report, do not hang the parent
@@ -113,5 +127,9 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         res = results[r]
         assert "exception" not in res, res
         assert res["enabled"] and res["eager"] and res["graph"], res
-        assert res["errors"] == 0 and res["engine_errors"] == 0, res
-        assert res["kind"] == "ipc-oneshot" and res["params_equal"] and res["finite"], res
+        assert res["errors"] == 0, res
+        for mode, kind in (("ipc", "ipc-oneshot"), ("fused", "fused-ipc")):
+            assert res[f"kind_{mode}"] == kind, res
+            assert res[f"params_equal_{mode}"] and res[f"finite_{mode}"], res
+            assert res[f"engine_errors_{mode}"] == 0, res
+        assert res["fused_equals_ipc"], res
