@@ -48,6 +48,9 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-epoch", action="store_true", help="skip the extra measured full epoch")
     ap.add_argument("--grid", type=int, default=0, help="workgroups per step (0 = per-rank batch, max 256)")
+    ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
+                    help="process group: auto = RCCL ('nccl') on GPUs; gloo lets ranks share one GPU "
+                         "(rehearsal of the multi-rank path; the gradient exchange still runs on the GPU)")
     args = ap.parse_args()
 
     import torch
@@ -63,7 +66,7 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    ctx = init_distributed(world_size=world, device="cuda")
+    ctx = init_distributed(world_size=world, device="cuda", backend=None if args.backend == "auto" else args.backend)
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
 
     train = synthetic_mnist(60000, seed=0, train=True)

@@ -12,6 +12,7 @@ compete for it, and the transport is local HBM, not xGMI).
 import argparse
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -51,13 +52,22 @@ def main():
         smp.set_epoch(0)
         eng.set_epoch_order(smp.indices())
         us = eng._time_steps(nsteps=args.steps, reps=10)
-        out[mode] = (eng.allreduce_kind, round(us, 2), eng.comm_errors())
+        # the same steps the way bench.py runs them: cached graphs, wall clock
+        eng.prepare(args.steps)
+        eng.run_steps(4 * args.steps, args.steps)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        eng.run_steps(16 * args.steps, args.steps)
+        torch.cuda.synchronize(dev)
+        wall_us = (time.perf_counter() - t0) * 1e6 / (16 * args.steps)
+        out[mode] = (eng.allreduce_kind, round(us, 2), eng.comm_errors(), round(wall_us, 2))
         del eng
         torch.cuda.synchronize(dev)
     if rank == 0:
-        for mode, (kind, us, err) in out.items():
+        for mode, (kind, us, err, wall) in out.items():
             print(f"world={world} backend={ctx.backend} global_batch={args.global_batch} path={mode:5s} "
-                  f"kind={kind:11s} step_us={us:7.2f} comm_errors={err}", flush=True)
+                  f"kind={kind:11s} step_us={us:7.2f} run_steps_wall_us={wall:7.2f} comm_errors={err}", flush=True)
     dist.destroy_process_group()
 
 
