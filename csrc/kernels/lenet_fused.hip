@@ -153,7 +153,9 @@ constexpr int S_F = S_DZ1B + 64 * 2;                  // f32 scratch
 constexpr int F_D2S = 0, F_D1S = 32, F_H = 96, F_LOGIT = 160, F_PAR = 176, F_RED = 768, F_END = 2816;
 // fp32 params cached in LDS (offsets inside F_PAR): c1b 0, c2b 10, f1b 30, f2b 80, f2w 90 (500) -> 590
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
-constexpr int S_TOTAL = S_F + F_END * 4;
+constexpr int S_W1C = S_F + F_END * 4;                // u16 16*32  conv1 B operand (copy of W1C)
+constexpr int S_LABEL = S_W1C + 16 * 32 * 2;          // i32 [4]   staged sample's label
+constexpr int S_TOTAL = S_LABEL + 16;
 static_assert(S_W2D % 16 == 0 && S_F1 % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
 static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_P1H % 16 == 0 && S_DC2 % 16 == 0 && S_DC2H % 16 == 0, "align");
 static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B % 16 == 0, "align");
@@ -200,6 +202,13 @@ __device__ __forceinline__ int opaque(int x) {
   return x;
 }
 
+// Workgroup barrier for LDS traffic only: this wave's LDS operations complete,
+// then s_barrier; a compiler memory barrier too.  Unlike __syncthreads() it does
+// not wait for an in-flight LDS-DMA (the legaliser makes an LDS release fence
+// wait vmcnt(0) while one is outstanding), so stages that do not read the DMA'd
+// weights run under it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
   const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
@@ -229,24 +238,34 @@ __device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned sh
 
 template <typename T, bool TRAIN>
 __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
+  // per-sample activations (dynamic).  Being distinct objects, accesses to the
+  // activations are provably disjoint from the in-flight DMA, so the compiler's
+  // LDS-DMA wait lands at the first weight read (conv2), not at the first LDS
+  // access of the preamble: the 72 KB weight copy overlaps stages 0-1.
+  __shared__ __attribute__((aligned(16))) unsigned char wsm[S_X];
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  // activation region at its layout offset (S_X ... S_TOTAL)
+#define ACT(off) (dsm + ((off) - S_X))
   typedef typename Mfma<T>::frag frag;
-  unsigned short* W2c = (unsigned short*)(sm + S_W2C);
-  unsigned short* W2d = (unsigned short*)(sm + S_W2D);
-  unsigned short* Xs = (unsigned short*)(sm + S_X);
-  unsigned short* P1 = (unsigned short*)(sm + S_P1);
-  uint8_t* I1 = sm + S_I1;
-  unsigned short* P2 = (unsigned short*)(sm + S_P2);
-  uint8_t* I2 = sm + S_I2;
-  unsigned short* P1H = (unsigned short*)(sm + S_P1H);
-  unsigned short* DC2 = (unsigned short*)(sm + S_DC2);
-  unsigned short* DC2H = (unsigned short*)(sm + S_DC2H);
-  unsigned short* DC1 = (unsigned short*)(sm + S_DC1);
-  short* COFF = (short*)(sm + S_COFF);
-  short* DOFF = (short*)(sm + S_DOFF);
-  unsigned short* DZ1B = (unsigned short*)(sm + S_DZ1B);
-  unsigned short* F1s = (unsigned short*)(sm + S_F1);
-  float* Fs = (float*)(sm + S_F);
+  unsigned short* W2c = (unsigned short*)(wsm + S_W2C);
+  unsigned short* W2d = (unsigned short*)(wsm + S_W2D);
+  unsigned short* Xs = (unsigned short*)ACT(S_X);
+  unsigned short* P1 = (unsigned short*)ACT(S_P1);
+  uint8_t* I1 = ACT(S_I1);
+  unsigned short* P2 = (unsigned short*)ACT(S_P2);
+  uint8_t* I2 = ACT(S_I2);
+  unsigned short* P1H = (unsigned short*)ACT(S_P1H);
+  unsigned short* DC2 = (unsigned short*)ACT(S_DC2);
+  unsigned short* DC2H = (unsigned short*)ACT(S_DC2H);
+  unsigned short* DC1 = (unsigned short*)ACT(S_DC1);
+  short* COFF = (short*)ACT(S_COFF);
+  short* DOFF = (short*)ACT(S_DOFF);
+  unsigned short* DZ1B = (unsigned short*)ACT(S_DZ1B);
+  unsigned short* F1s = (unsigned short*)(wsm + S_F1);
+  float* Fs = (float*)ACT(S_F);
+  unsigned short* W1Cs = (unsigned short*)ACT(S_W1C);
+  int* LABEL = (int*)ACT(S_LABEL);
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
@@ -268,76 +287,110 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 
   if (a.dbg && tid == 0) a.dbg[g * 16 + 12] = __builtin_amdgcn_s_memtime();
   // ---------------- once per workgroup: weight images, offset tables, fp32 params -> LDS
-  // register-resident conv1 weight fragment, reused for every sample of this WG
-  frag fb1;
-  // sample pipeline registers: this sample's 4 pixels per thread and label, the
-  // row indices of the next 64 samples (lane s) and their labels
+  // sample pipeline registers (non-staged batches): this sample's 4 pixels per
+  // thread and label, the row indices of the next 64 samples (lane s) and their labels
   uint32_t px = 0;
   int lab = 0, labv = 0;
   int64_t rowv = 0;
-  // next-step staging (one sample per workgroup): its row, pixels and label are
-  // loaded during this step's stages and stored at the end
+  // next-step staging (one sample per workgroup): its pixels and label are loaded
+  // at stage 3 by waves 4-7 and stored at the end
   const bool stage_next = TRAIN && a.xstage && a.stage_next && nsamp == 1;
   int64_t nrow = 0;
   uint32_t px_next = 0;
   int64_t lab_next = 0;
-  // fp32 params land in LDS at the first loop-top barrier: waiting for them (and
-  // for the weight DMA) there lets the loop-invariant address math that hipcc
-  // hoists into the preheader run under the load latency instead of after it
-  float par0 = 0.f, par1 = 0.f;
-  {
-    // a staged batch (lenet_update gathered it last step): the first sample's
-    // pixels and the labels of samples 0..63 need no dependent loads at all
+  // Wave roles.  Waves 0-3 stream the 72 KB of weight images into LDS (LDS-DMA);
+  // waves 4-7 fetch every small operand (pixels, label, fp32 params, conv1
+  // weights, K-order tables), zero the padded activation images and write the
+  // operands to LDS.  Vector memory operations complete in issue order, so a wave that had
+  // both would wait for the whole DMA at its first use of a small operand; split
+  // this way, no wave waits for the DMA before conv2 (stage 2) reads the images,
+  // and stages 0-1 run while it streams.  (The staged batch has one sample per
+  // workgroup; the non-staged path keeps its per-thread pixel pipeline below.)
+  // Waves 4-7 issue their loads first and then meet waves 0-3 at a barrier, so
+  // that the CU's vector memory pipeline (FIFO) serves them ahead of the DMA.
+  uint32_t px0 = 0;
+  int lab0 = 0, kg = 0;
+  float pv[3] = {0.f, 0.f, 0.f};
+  uint4 w1 = make_uint4(0, 0, 0, 0);
+  if (wave >= 4) {
+    const int t = tid - NT / 2;
+    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread)
+    auto par_index = [](int q) {
+      return q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30 : q < 90 ? O_F2B + q - 80
+                                                                                          : O_F2W + q - 90;
+    };
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * (NT / 2), 589))];
+    w1 = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t & 63];
     if (a.xstage && nsamp > 0) {
-      px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(tid, 195)];
-      labv = (int)a.lstage[min(g + lane * G, a.B - 1)];
+      px0 = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(t, 195)];
+      lab0 = (int)a.lstage[g];
     }
-    // W2C | W2D | F1 straight into LDS by LDS-DMA: each wave-instruction moves
-    // 1 KB to a wave-uniform base + lane*16, so the image stays lane-linear
+    // K-slice orders (constant memory) for the conv2 / dgrad A-offset tables
+    const int tq = t < 64 ? t >> 4 : (t - 64) / 24;
+    const int tks = t < 64 ? t & 15 : (t - 64) - 24 * tq;
+    kg = t < 64 ? (int)kC2Order.fwd[min(4 * tks + tq, 49)] : (int)kDgOrder.fwd[min(4 * tks + tq, 74)];
+    // the next step's row (batch staging); an opaque lane offset keeps it a VGPR (a
+    // uniform load is moved to an SGPR right away, i.e. waited for here)
+    if (stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
+    if (a.dbg && t == 0) a.dbg[g * 16 + 10 + 5] = __builtin_amdgcn_s_memtime();
+  }
+  lds_barrier();
+  if (wave < 4) {
+    // W2C | W2D | F1 by LDS-DMA: each wave-instruction moves 1 KB to a wave-uniform
+    // base + lane*16, so the image stays lane-linear
+    constexpr int DMA_NT = NT / 2;
+    static_assert(WIMG_LDS_U4 % DMA_NT == 0, "whole LDS-DMA rounds over waves 0-3");
     const uint4* src = reinterpret_cast<const uint4*>(a.wimg + I_W2C);
 #pragma unroll
-    for (int u = 0; u < WIMG_LDS_U4 / NT; ++u)
-      __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * NT + tid)),
-                                       (lds_void*)(sm + S_W2C + (u * NT + wave * 64) * 16), 16, 0, 0);
-    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, one per thread)
-    int pi = O_F2W + tid - 90;
-    if (tid < 10) pi = O_C1B + tid;
-    else if (tid < 30) pi = O_C2B + tid - 10;
-    else if (tid < 80) pi = O_F1B + tid - 30;
-    else if (tid < 90) pi = O_F2B + tid - 80;
-    const float pv0 = a.params[pi];
-    const float pv1 = a.params[O_F2W + min(tid + NT, 589) - 90];
-    fb1 = *reinterpret_cast<const frag*>(a.wimg + I_W1C + l16 * 32 + kb);
-    // the first sample (cursor -> row -> pixels, label: scalar chain) and the
-    // row indices of samples 0..63 (one per lane), behind the weight loads
-    if (!a.xstage && nsamp > 0) {
-      const int64_t row0 = perm_at(0);
-      lab = (int)a.labels[row0];
-      px = reinterpret_cast<const uint32_t*>(a.images + row0 * 784)[min(tid, 195)];
-      rowv = perm_at(min(lane, nsamp - 1));
-    }
-    // work that needs no loaded data overlaps the loads
-    if (tid < 64) {
-      // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
-      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
-      const int q = tid >> 4, ks = tid & 15;
-      const int kg = kC2Order.fwd[min(4 * ks + q, 49)], tap = kg >> 1;
-      COFF[tid] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
-    } else if (tid < 160) {
-      // dgrad: K slice 4*ks + q is channels 8*ocg .. +7 of tap (kDgOrder; slice 75 and the
-      // clamped steps >= DG_KS meet zero weights, their A offset only has to be in bounds)
-      const int q = (tid - 64) / 24, ks = (tid - 64) - 24 * q;
-      const int kg = kDgOrder.fwd[min(4 * ks + q, 74)], tap = kg / 3, ocg = kg - 3 * tap;
-      DOFF[tid - 64] = (short)((tap / 5) * DC2H_RP + (tap % 5) * DG_OCP + ocg * 8);
-    }
-    // P1H | DC2 | DC2H | DC1 are contiguous: zero their padding once with 16-B stores
+    for (int u = 0; u < WIMG_LDS_U4 / DMA_NT; ++u)
+      __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * DMA_NT + tid)),
+                                       (lds_void*)(wsm + S_W2C + (u * DMA_NT + wave * 64) * 16), 16, 0, 0);
+    if (a.dbg && tid == 0) a.dbg[g * 16 + 10] = __builtin_amdgcn_s_memtime();
+  } else {
+    const int t = tid - NT / 2;
+    // under the load latency: P1H | DC2 | DC2H | DC1 are contiguous, zero their
+    // padding once with 16-B stores (in these waves: the compiler makes an LDS
+    // store loop wait for any LDS-DMA still in flight)
     {
       constexpr int NZ = (S_COFF - S_P1H) / 16;
-      uint4* z = reinterpret_cast<uint4*>(sm + S_P1H);
-      for (int i = tid; i < NZ; i += NT) z[i] = make_uint4(0, 0, 0, 0);
+      uint4* z = reinterpret_cast<uint4*>(ACT(S_P1H));
+      for (int i = t; i < NZ; i += NT / 2) z[i] = make_uint4(0, 0, 0, 0);
     }
-    par0 = pv0;
-    par1 = pv1;
+    if (t < 64) {
+      // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
+      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
+      const int tap = kg >> 1;
+      COFF[t] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
+      reinterpret_cast<uint4*>(W1Cs)[t] = w1;
+    } else if (t < 160) {
+      // dgrad: K slice 4*ks + q is channels 8*ocg .. +7 of tap (kDgOrder; slice 75 and the
+      // clamped steps >= DG_KS meet zero weights, their A offset only has to be in bounds)
+      const int tap = kg / 3, ocg = kg - 3 * tap;
+      DOFF[t - 64] = (short)((tap / 5) * DC2H_RP + (tap % 5) * DG_OCP + ocg * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (t + j * (NT / 2) < 590) PAR[t + j * (NT / 2)] = pv[j];
+    if (a.xstage && nsamp > 0) {
+      if (t < 196) {  // the staged sample's pixels (stage 0 of sample 0)
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = h16<T>(((float)((px0 >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std);
+        *reinterpret_cast<u16x4*>(Xs + 4 * t) = o;
+      }
+      if (t == 0) LABEL[0] = lab0;
+    }
+  }
+  // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
+  // chain) and the row indices of samples 0..63 (one per lane); these waits do
+  // include the DMA in waves 0-3 (the large-batch path amortises it over samples)
+  if (!a.xstage && nsamp > 0) {
+    const int64_t row0 = perm_at(0);
+    lab = (int)a.labels[row0];
+    px = reinterpret_cast<const uint32_t*>(a.images + row0 * 784)[min(tid, 195)];
+    rowv = perm_at(min(lane, nsamp - 1));
   }
   if (a.dbg && tid == 0) a.dbg[g * 16 + 13] = __builtin_amdgcn_s_memtime();
   if (a.dbg && tid == 0) a.dbg[g * 16 + 14] = __builtin_amdgcn_s_memtime();
@@ -378,17 +431,14 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
-    if (s == 0) {
-      if (tid < 590) PAR[tid] = par0;
-      if (tid + NT < 590) PAR[tid + NT] = par1;
-    }
-    __syncthreads();  // LDS-DMA drained (first pass); previous sample's readers are done
+    lds_barrier();  // previous sample's readers are done (first pass: preamble LDS writes)
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
     // then start the next sample's loads (consumed one sample later)
     STAMP(0);
-    const int t_lab = (s == 0 && !a.xstage) ? lab : __builtin_amdgcn_readlane(labv, s & 63);
+    // label of this sample: staged -> LDS (preamble), else the register pipeline
+    const int t_lab = a.xstage ? 0 : (s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63));
     {
-      if (tid < 196) {
+      if (tid < 196 && !a.xstage) {  // staged sample: done in the preamble
         u16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -417,13 +467,10 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, P1H
     STAMP(1);
-    if (stage_next)  // a relaxed atomic keeps this a vector load (no scalar-queue wait)
-      nrow = __hip_atomic_load(a.perm + min(pbase + a.B, a.perm_len - 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
     {
       // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
       u16x8 raw[5];
@@ -437,6 +484,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         for (int j = 0; j < 8; ++j) raw[it][j] = Xs[pb + koff1[j]];
       }
       const float cb = PAR[P_C1B + min(l16, 9)];
+      const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
 #pragma unroll
       for (int it = 0; it < 5; ++it) {
         const int mt = wave + it * NW;
@@ -457,7 +505,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
-    __syncthreads();
+    __syncthreads();  // also the weight DMA (first pass): conv2 reads W2C next
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
     STAMP(2);
@@ -498,8 +546,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3)
     STAMP(3);
-    if (stage_next) {
-      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid, 195)];
+    if (stage_next && tid >= NT / 2) {  // waves 4-7: they hold nrow
+      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid - NT / 2, 195)];
       lab_next = a.labels[nrow];
     }
     if (wave < 4) {
@@ -528,7 +576,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
     STAMP(4);
     if (wave == 0) {
-      const int t = t_lab;
+      const int t = a.xstage ? LABEL[0] : t_lab;
       // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12), then a
       // fixed-order 2-step butterfly inside each aligned 4-lane group
       float zp = 0.f;
@@ -767,8 +815,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     STAMP(11);
   }
   if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
-    if (tid < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid] = px_next;
-    if (tid == 0) a.lstage[g] = lab_next;
+    if (tid >= NT / 2 && tid - NT / 2 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - NT / 2] = px_next;
+    if (tid == NT / 2) a.lstage[g] = lab_next;
   }
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
@@ -812,6 +860,8 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     a.loss_acc[2 * g + 1] = correct;
   }
 }
+
+#undef ACT
 
 // ---------------------------------------------------------------------------
 // Weight images from fp32 params (element i of the flat buffer).
@@ -1220,7 +1270,7 @@ int64_t lenet_vec_len() { return VEC; }
 
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   if (a.B <= 0 || a.grid <= 0 || a.grid > a.B) return hipErrorInvalidValue;
-  const size_t lds = (size_t)S_TOTAL;
+  const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1290,7 +1340,7 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   a.B = (int)n; a.wimg = wimg; a.params = params; a.slab = nullptr; a.loss_acc = out;
   a.grad_scale = 0.f; a.mean = mean; a.std_ = std_; a.drop_p = 0.f; a.seed = 0; a.rng_offset = nullptr;
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
-  const size_t lds = (size_t)S_TOTAL;
+  const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
     hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -39,9 +39,12 @@ def main():
     med = d.median(0).values
     tot = (st[:, 11] - st[:, 12]).median().item()
     print(f"B={B} grid={grid}: median total {tot:.0f} cycles (s_memtime ticks)")
-    pre = [(st[:, 13] - st[:, 12]).median().item(), (st[:, 14] - st[:, 13]).median().item(),
-           (st[:, 0] - st[:, 14]).median().item()]
-    print(f"  preamble: weight copy {pre[0]:.0f}, params/tables/zero {pre[1]:.0f}, to stage0 {pre[2]:.0f}")
+    # preamble stamps: 12 kernel start (wave 0), 10 LDS-DMA issued (wave 0), 15 small
+    # loads issued (wave 4), 13 = 14 preamble end (wave 0), 0 first stage (after the barrier)
+    pre = [(st[:, 10] - st[:, 12]).median().item(), (st[:, 15] - st[:, 12]).median().item(),
+           (st[:, 13] - st[:, 12]).median().item(), (st[:, 0] - st[:, 14]).median().item()]
+    print(f"  preamble (from kernel start): DMA issued {pre[0]:.0f}, small loads issued {pre[1]:.0f}, "
+          f"wave 0 done {pre[2]:.0f}; then to stage0 (barrier) {pre[3]:.0f}")
     for n, v in zip(NAMES, med.tolist()):
         print(f"  {n:24s} {v:8.0f}  {100 * v / tot:5.1f}%")
 
