@@ -179,7 +179,7 @@ typedef __attribute__((address_space(1))) void glb_void;
 // of the step; read the shares, not the absolute time.
 #define STAMP(i)                                                              \
   do {                                                                        \
-    if (a.dbg && tid == 0 && s == 0) a.dbg[g * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (a.dbg && tid == 0 && s == (nsamp > 1 ? 1 : 0)) a.dbg[g * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
 template <typename T>
@@ -237,7 +237,7 @@ __device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned sh
 }
 
 template <typename T, bool TRAIN>
-__global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
+__global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
   // per-sample activations (dynamic).  Being distinct objects, accesses to the
   // activations are provably disjoint from the in-flight DMA, so the compiler's
@@ -393,7 +393,6 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     rowv = perm_at(min(lane, nsamp - 1));
   }
   if (a.dbg && tid == 0) a.dbg[g * 16 + 13] = __builtin_amdgcn_s_memtime();
-  if (a.dbg && tid == 0) a.dbg[g * 16 + 14] = __builtin_amdgcn_s_memtime();
   int koff1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -803,6 +802,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
         if (i < 4 || wave < 4) acc_c1 = Mfma<T>::mma(fa[i], __builtin_bit_cast(frag, rv), acc_c1);
       }
     }
+    STAMP(14);
   };
   for (int s = 0; s < nsamp; ++s) {
     const int t = opaque(tid);
@@ -810,10 +810,7 @@ __global__ void __launch_bounds__(NT, 2) lenet_train_kernel(LenetTrainArgs a, in
     sample(s, t, ln, ln & 15, ln >> 4, 8 * (ln >> 4));
   }
 
-  {
-    const int s = 0;
-    STAMP(11);
-  }
+  if (a.dbg && tid == 0) a.dbg[g * 16 + 11] = __builtin_amdgcn_s_memtime();
   if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
     if (tid >= NT / 2 && tid - NT / 2 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - NT / 2] = px_next;
     if (tid == NT / 2) a.lstage[g] = lab_next;

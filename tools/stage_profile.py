@@ -16,7 +16,7 @@ from csed_514_project_distributed_training_using_pytorch_amd.data import synthet
 from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer  # noqa: E402
 from csed_514_project_distributed_training_using_pytorch_amd.models import Net  # noqa: E402
 
-NAMES = ["start->first stage", "pixels+masks+prefetch", "conv1", "conv2", "fc1", "fc2+loss+dZ1",
+NAMES = ["preamble end->stage 0", "pixels+masks+prefetch", "conv1", "conv2", "fc1", "fc2+loss+dZ1",
          "dP2 (MFMA-tr)+pool2 bwd", "conv2 wgrad", "conv2 dgrad", "dgrad tile-8 reduce", "conv1 wgrad"]
 
 
@@ -24,29 +24,33 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     grid = int(sys.argv[2]) if len(sys.argv) > 2 else B
     dev = torch.device("cuda")
-    data = synthetic_mnist(4096, seed=1)
+    n = max(4096, 2 * B)
+    data = synthetic_mnist(n, seed=1)
     torch.manual_seed(1)
     eng = FusedLeNetTrainer(Net().to(dev), data, global_batch=B, grid=grid)
-    eng.set_epoch_order(torch.randperm(4096))
+    eng.set_epoch_order(torch.randperm(n))
     dbg = torch.zeros(grid * 16, dtype=torch.long, device=dev)
     for _ in range(20):
         eng.gradient(grid, dbg)
     torch.cuda.synchronize()
     st = dbg.view(grid, 16).cpu().double()
-    # order: 12 = kernel start, 0..8 = stage starts (9 = dgrad inside stage 6), 11 = after all samples
-    seq = [12, 0, 1, 2, 3, 4, 5, 6, 9, 7, 8, 11]
+    # Stamps (thread 0): 12 kernel start, 10 LDS-DMA issued, 15 small loads issued (wave 4),
+    # 13 preamble end, 0..8 stage starts of the stamped sample (9 = dgrad inside stage 6),
+    # 14 end of the stamped sample, 11 after all samples.  The stamped sample is sample 1
+    # when a workgroup has several (steady state), else sample 0.
+    seq = [13, 0, 1, 2, 3, 4, 5, 6, 9, 7, 8, 14]
     d = torch.stack([st[:, seq[i + 1]] - st[:, seq[i]] for i in range(len(seq) - 1)], 1)
     med = d.median(0).values
     tot = (st[:, 11] - st[:, 12]).median().item()
-    print(f"B={B} grid={grid}: median total {tot:.0f} cycles (s_memtime ticks)")
-    # preamble stamps: 12 kernel start (wave 0), 10 LDS-DMA issued (wave 0), 15 small
-    # loads issued (wave 4), 13 = 14 preamble end (wave 0), 0 first stage (after the barrier)
+    per = (st[:, 14] - st[:, 0]).median().item()
+    print(f"B={B} grid={grid}: median kernel {tot:.0f} cycles (s_memtime ticks), stamped sample {per:.0f}")
     pre = [(st[:, 10] - st[:, 12]).median().item(), (st[:, 15] - st[:, 12]).median().item(),
-           (st[:, 13] - st[:, 12]).median().item(), (st[:, 0] - st[:, 14]).median().item()]
+           (st[:, 13] - st[:, 12]).median().item()]
     print(f"  preamble (from kernel start): DMA issued {pre[0]:.0f}, small loads issued {pre[1]:.0f}, "
-          f"wave 0 done {pre[2]:.0f}; then to stage0 (barrier) {pre[3]:.0f}")
-    for n, v in zip(NAMES, med.tolist()):
-        print(f"  {n:24s} {v:8.0f}  {100 * v / tot:5.1f}%")
+          f"wave 0 done {pre[2]:.0f}")
+    span = (st[:, 14] - st[:, 13]).median().item()
+    for name, v in zip(NAMES, med.tolist()):
+        print(f"  {name:24s} {v:8.0f}  {100 * v / span:5.1f}%")
 
 
 if __name__ == "__main__":
