@@ -325,7 +325,7 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
   a.std_ = (float)std_; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.rng_offset = optpt<int64_t>(rng_offset);
   a.grid = (int)grid; a.mfma_dtype = mcode(mfma_dtype);
   if (dbg.has_value()) {
-    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 16 * grid, "dbg: int64 [grid*16]");
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 32 * grid, "dbg: int64 [grid*32]");
     a.dbg = (uint64_t*)dbg->data_ptr<int64_t>();
   }
   TORCH_CHECK(xstage.has_value() == lstage.has_value(), "lenet_train: xstage and lstage go together");

@@ -155,7 +155,8 @@ constexpr int F_D2S = 0, F_D1S = 32, F_H = 96, F_LOGIT = 160, F_PAR = 176, F_RED
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 constexpr int S_W1C = S_F + F_END * 4;                // u16 16*32  conv1 B operand (copy of W1C)
 constexpr int S_LABEL = S_W1C + 16 * 32 * 2;          // i32 [4]   staged sample's label
-constexpr int S_TOTAL = S_LABEL + 16;
+constexpr int S_DBG = S_LABEL + 16;                   // u64 [32]  stage stamps (diagnostics)
+constexpr int S_TOTAL = S_DBG + 32 * 8;
 static_assert(S_W2D % 16 == 0 && S_F1 % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
 static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_P1H % 16 == 0 && S_DC2 % 16 == 0 && S_DC2H % 16 == 0, "align");
 static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B % 16 == 0, "align");
@@ -175,11 +176,14 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
 // Diagnostic stage stamps (a.dbg non-null): thread 0 of each workgroup records
-// s_memtime at each stage start of its first sample.  Only for profiling builds
+// s_memtime at each stage start of its first sample, into LDS (a global store
+// would make the next VGPR reuse wait for vmcnt, i.e. for an in-flight LDS-DMA,
+// in every build); the slots are copied out at the end.  Only for profiling builds
 // of the step; read the shares, not the absolute time.
+constexpr int DBG_W = 32;  // stamp slots per workgroup (a.dbg: int64 [grid][32])
 #define STAMP(i)                                                              \
   do {                                                                        \
-    if (a.dbg && tid == 0 && s == (nsamp > 1 ? 1 : 0)) a.dbg[g * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (a.dbg && tid == 0 && s == (nsamp > 1 ? 1 : 0)) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
 template <typename T>
@@ -236,7 +240,12 @@ __device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned sh
   dgrad_store<T>(DC1, ci, mm, f16v<T>(P1[pi]) > 0.f ? v : 0.f, I1[pi]);
 }
 
-template <typename T, bool TRAIN>
+// STAGED: the batch was staged (a.xstage) and every workgroup owns exactly one
+// sample (grid == B).  A separate instantiation, so that the staged step carries
+// no code of the multi-sample pixel pipeline: its branches would merge register
+// state into the staged path and make hipcc wait for loads (and so for the LDS
+// DMA) that the staged path never issued.
+template <typename T, bool TRAIN, bool STAGED>
 __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
   // per-sample activations (dynamic).  Being distinct objects, accesses to the
@@ -266,6 +275,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   float* Fs = (float*)ACT(S_F);
   unsigned short* W1Cs = (unsigned short*)ACT(S_W1C);
   int* LABEL = (int*)ACT(S_LABEL);
+  uint64_t* DBGS = (uint64_t*)ACT(S_DBG);
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
@@ -281,11 +291,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
-  const int nsamp = g < a.B ? (a.B - g + G - 1) / G : 0;
+  const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
   const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
   auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
-  if (a.dbg && tid == 0) a.dbg[g * 16 + 12] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && tid == 0) DBGS[12] = __builtin_amdgcn_s_memtime();
   // ---------------- once per workgroup: weight images, offset tables, fp32 params -> LDS
   // sample pipeline registers (non-staged batches): this sample's 4 pixels per
   // thread and label, the row indices of the next 64 samples (lane s) and their labels
@@ -294,7 +304,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   int64_t rowv = 0;
   // next-step staging (one sample per workgroup): its pixels and label are loaded
   // at stage 3 by waves 4-7 and stored at the end
-  const bool stage_next = TRAIN && a.xstage && a.stage_next && nsamp == 1;
+  const bool stage_next = TRAIN && STAGED && a.stage_next;
   int64_t nrow = 0;
   uint32_t px_next = 0;
   int64_t lab_next = 0;
@@ -314,6 +324,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   uint4 w1 = make_uint4(0, 0, 0, 0);
   if (wave >= 4) {
     const int t = tid - NT / 2;
+    if (a.dbg && t == 0) DBGS[17] = __builtin_amdgcn_s_memtime();
     // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread)
     auto par_index = [](int q) {
       return q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30 : q < 90 ? O_F2B + q - 80
@@ -322,7 +333,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
     for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * (NT / 2), 589))];
     w1 = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t & 63];
-    if (a.xstage && nsamp > 0) {
+    if (STAGED) {
       px0 = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(t, 195)];
       lab0 = (int)a.lstage[g];
     }
@@ -333,7 +344,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // the next step's row (batch staging); an opaque lane offset keeps it a VGPR (a
     // uniform load is moved to an SGPR right away, i.e. waited for here)
     if (stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
-    if (a.dbg && t == 0) a.dbg[g * 16 + 10 + 5] = __builtin_amdgcn_s_memtime();
+    if (a.dbg && t == 0) DBGS[10 + 5] = __builtin_amdgcn_s_memtime();
   }
   lds_barrier();
   if (wave < 4) {
@@ -346,7 +357,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     for (int u = 0; u < WIMG_LDS_U4 / DMA_NT; ++u)
       __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * DMA_NT + tid)),
                                        (lds_void*)(wsm + S_W2C + (u * DMA_NT + wave * 64) * 16), 16, 0, 0);
-    if (a.dbg && tid == 0) a.dbg[g * 16 + 10] = __builtin_amdgcn_s_memtime();
+    if (a.dbg && lane == 0) DBGS[(wave == 0 ? 10 : 17 + wave)] = __builtin_amdgcn_s_memtime();
   } else {
     const int t = tid - NT / 2;
     // under the load latency: P1H | DC2 | DC2H | DC1 are contiguous, zero their
@@ -372,7 +383,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       if (t + j * (NT / 2) < 590) PAR[t + j * (NT / 2)] = pv[j];
-    if (a.xstage && nsamp > 0) {
+    if (STAGED) {
       if (t < 196) {  // the staged sample's pixels (stage 0 of sample 0)
         u16x4 o;
 #pragma unroll
@@ -382,17 +393,23 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       }
       if (t == 0) LABEL[0] = lab0;
     }
+    if (a.dbg && t == 0) DBGS[16] = __builtin_amdgcn_s_memtime();
+    // Retire every load of this branch here, in every lane (an empty asm reading the
+    // registers): the merge below would otherwise inherit them as pending, and the
+    // first reuse of their registers would make waves 0-3 wait vmcnt(0) -- for the DMA.
+    asm volatile("" ::"v"(pv[0]), "v"(pv[1]), "v"(pv[2]), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(px0),
+                 "v"(lab0), "v"(kg));
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
   // include the DMA in waves 0-3 (the large-batch path amortises it over samples)
-  if (!a.xstage && nsamp > 0) {
+  if (!STAGED && nsamp > 0) {
     const int64_t row0 = perm_at(0);
     lab = (int)a.labels[row0];
     px = reinterpret_cast<const uint32_t*>(a.images + row0 * 784)[min(tid, 195)];
     rowv = perm_at(min(lane, nsamp - 1));
   }
-  if (a.dbg && tid == 0) a.dbg[g * 16 + 13] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && tid == 0) DBGS[13] = __builtin_amdgcn_s_memtime();
   int koff1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -430,14 +447,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
+    if (a.dbg && lane == 0 && s == 0) DBGS[24 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
     lds_barrier();  // previous sample's readers are done (first pass: preamble LDS writes)
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
     // then start the next sample's loads (consumed one sample later)
     STAMP(0);
     // label of this sample: staged -> LDS (preamble), else the register pipeline
-    const int t_lab = a.xstage ? 0 : (s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63));
+    const int t_lab = STAGED ? 0 : (s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63));
     {
-      if (tid < 196 && !a.xstage) {  // staged sample: done in the preamble
+      if (tid < 196 && !STAGED) {  // staged sample: done in the preamble
         u16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -453,17 +471,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (tid < 20) D2S[tid] = sc;
         else D1S[tid - 20] = sc;
       }
-      if (s + 1 < nsamp) {
+      if (!STAGED && s + 1 < nsamp) {
         const int sn = s + 1;
-        if (a.xstage) {
-          if ((sn & 63) == 0) labv = (int)a.lstage[min(g + (sn + lane) * G, a.B - 1)];
-          px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)(g + sn * G) * 784)[min(tid, 195)];
-        } else {
-          if ((sn & 63) == 0) rowv = perm_at(min(sn + lane, nsamp - 1));
-          if (s == 0 || (sn & 63) == 0) labv = (int)a.labels[rowv];
-          const int64_t rn = readlane64(rowv, sn & 63);
-          px = reinterpret_cast<const uint32_t*>(a.images + rn * 784)[min(tid, 195)];
-        }
+        if ((sn & 63) == 0) rowv = perm_at(min(sn + lane, nsamp - 1));
+        if (s == 0 || (sn & 63) == 0) labv = (int)a.labels[rowv];
+        const int64_t rn = readlane64(rowv, sn & 63);
+        px = reinterpret_cast<const uint32_t*>(a.images + rn * 784)[min(tid, 195)];
       }
     }
     lds_barrier();
@@ -575,7 +588,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
     STAMP(4);
     if (wave == 0) {
-      const int t = a.xstage ? LABEL[0] : t_lab;
+      const int t = STAGED ? LABEL[0] : t_lab;
       // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12), then a
       // fixed-order 2-step butterfly inside each aligned 4-lane group
       float zp = 0.f;
@@ -810,7 +823,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     sample(s, t, ln, ln & 15, ln >> 4, 8 * (ln >> 4));
   }
 
-  if (a.dbg && tid == 0) a.dbg[g * 16 + 11] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
   if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
     if (tid >= NT / 2 && tid - NT / 2 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - NT / 2] = px_next;
     if (tid == NT / 2) a.lstage[g] = lab_next;
@@ -855,6 +868,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   if (tid == 0) {
     a.loss_acc[2 * g] = loss_sum;
     a.loss_acc[2 * g + 1] = correct;
+  }
+  if (a.dbg) {
+    __syncthreads();
+    if (tid < DBG_W) a.dbg[g * DBG_W + tid] = DBGS[tid];
   }
 }
 
@@ -1267,12 +1284,21 @@ int64_t lenet_vec_len() { return VEC; }
 
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   if (a.B <= 0 || a.grid <= 0 || a.grid > a.B) return hipErrorInvalidValue;
+  // a staged batch has one sample per workgroup (the STAGED instantiation relies on it)
+  if (a.xstage && (a.grid != a.B || !a.lstage)) return hipErrorInvalidValue;
   const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
-    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true>), dim3(a.grid), dim3(NT), lds, s, a, 0,
-                       (float*)nullptr);
+    if (a.xstage) {
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true>), dim3(a.grid), dim3(NT), lds, s, a, 0,
+                         (float*)nullptr);
+    } else {
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false>), dim3(a.grid), dim3(NT), lds, s, a, 0,
+                         (float*)nullptr);
+    }
   });
   return hipGetLastError();
 }
@@ -1339,9 +1365,9 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
-    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false>,
+    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false>), dim3(a.grid), dim3(NT), lds, s, a,
+    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false>), dim3(a.grid), dim3(NT), lds, s, a,
                        logp_out ? 1 : 0, logp_out);
   });
   return hipGetLastError();
