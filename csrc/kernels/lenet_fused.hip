@@ -589,24 +589,29 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     STAMP(4);
     if (wave == 0) {
       const int t = STAGED ? LABEL[0] : t_lab;
-      // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12), then a
-      // fixed-order 2-step butterfly inside each aligned 4-lane group
-      float zp = 0.f;
+      // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12, two FMA chains),
+      // then a fixed-order 2-step butterfly inside each aligned 4-lane group
+      float zp0 = 0.f, zp1 = 0.f;
       if (lane < 40) {
         const int c = lane >> 2, q = lane & 3;
         const float* wr = PAR + P_F2W + c * 50;
 #pragma unroll
         for (int u = 0; u < 13; ++u) {
           const int o = q * 13 + u;
-          if (o < 50) zp = fmaf(wr[o], Hs[o], zp);
+          if (o < 50) {
+            if (u & 1) zp1 = fmaf(wr[o], Hs[o], zp1);
+            else zp0 = fmaf(wr[o], Hs[o], zp0);
+          }
         }
       }
+      float zp = zp0 + zp1;
       zp += __shfl_xor(zp, 1, 64);
       zp += __shfl_xor(zp, 2, 64);
       if (lane < 40 && (lane & 3) == 0) LOGIT[lane >> 2] = zp + PAR[P_F2B + (lane >> 2)];
       __builtin_amdgcn_wave_barrier();
       // every lane reads all 10 logits (same-wave LDS round trip, no barrier) and
-      // does the softmax locally: no cross-lane reductions
+      // does the softmax locally: no cross-lane reductions.  The 10 exponentials
+      // serve the log-sum-exp and the softmax gradient alike.
       float lg[10];
 #pragma unroll
       for (int c = 0; c < 10; ++c) lg[c] = LOGIT[c];
@@ -615,10 +620,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
       for (int c = 1; c < 10; ++c)
         if (lg[c] > mx) { mx = lg[c]; amax = c; }  // first index attaining the max (torch argmax)
-      float se = 0.f, lt = 0.f;
+      float ex[10], se = 0.f, lt = 0.f;
 #pragma unroll
       for (int c = 0; c < 10; ++c) {
-        se += __expf(lg[c] - mx);
+        ex[c] = __expf(lg[c] - mx);
+        se += ex[c];
         lt = c == t ? lg[c] : lt;
       }
       const float lse = mx + __logf(se);
@@ -626,19 +632,28 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         loss_sum += lse - lt;
         correct += (amax == t) ? 1.f : 0.f;
       }
-      const float mylg = LOGIT[min(lane, 9)];
-      if (write_logp && lane < 10) logp_out[(int64_t)b * 10 + lane] = mylg - lse;
+      if (write_logp && lane < 10) logp_out[(int64_t)b * 10 + lane] = LOGIT[lane] - lse;
       if (TRAIN) {
-        if (lane < 16) vs[V_DLOG + lane] = lane < 10 ? (__expf(mylg - lse) - (lane == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
+        // dlogits = softmax - onehot, scaled by 1 / global batch
+        const float gs = a.grad_scale * (1.f / se);
+        float dl[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
+        if (lane < 16) {
+          float mine = 0.f;
+#pragma unroll
+          for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
+          vs[V_DLOG + lane] = mine;
+        }
         // dZ1[o] = gate(o) * sum_c dl[c] * W2[c][o]   (lane o; every lane has all dl[c])
         const int o = min(lane, 49);
-        float dh = 0.f;
+        float dh0 = 0.f, dh1 = 0.f;
 #pragma unroll
         for (int c = 0; c < 10; ++c) {
-          const float dl = (__expf(lg[c] - lse) - (c == t ? 1.f : 0.f)) * a.grad_scale;
-          dh = fmaf(dl, PAR[P_F2W + c * 50 + o], dh);
+          if (c & 1) dh1 = fmaf(dl[c], PAR[P_F2W + c * 50 + o], dh1);
+          else dh0 = fmaf(dl[c], PAR[P_F2W + c * 50 + o], dh0);
         }
-        const float dz = (lane < 50 && Hs[o] > 0.f) ? dh * D1S[o] : 0.f;
+        const float dz = (lane < 50 && Hs[o] > 0.f) ? (dh0 + dh1) * D1S[o] : 0.f;
         DZ1B[lane] = h16<T>(dz);
         if (lane < 50) vs[V_DZ1 + lane] = dz;
       }
