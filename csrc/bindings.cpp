@@ -392,7 +392,7 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
   a.cursor = optpt<int64_t>(cursor); a.rng_offset = optpt<int64_t>(rng_offset);
   a.apply_sgd = apply_sgd ? 1 : 0; a.mfma_dtype = mcode(mfma_dtype);
   if (dbg.has_value()) {
-    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 128, "lenet_update: dbg must be int64[>=1024]");
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 256, "lenet_update: dbg must be int64[>=2048]");
     a.dbg = (uint64_t*)dbg->data_ptr();
   }
   // exch_id >= 0: csrc/comm buffer of the fused gradient exchange (checked by the launcher)

@@ -931,10 +931,13 @@ __global__ void lenet_pack_kernel(const float* __restrict__ params, unsigned sho
 //     also folds the loss partials and bumps the device counters.
 //   role FC (blocks [0, NB_FC)): the fc gradients are batch GEMMs of the
 //     per-sample vectors, on the fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32
-//     products), one 16x16 output tile per wave, K = batch:
+//     products), one 16x16 output tile per block, K = batch split over the 8
+//     waves (fixed-order LDS combine):
 //       dW1 | db1 = dZ1^T . [P2 | 1]   (4 x 21 tiles: column 320 = bias grad)
 //       dW2 | db2 = dL^T  . [H  | 1]   (1 x 4 tiles:  column 50  = bias grad)
-//     Each lane issues all of a 64-sample chunk's loads before its 16 MFMAs.
+//     Each lane issues a whole 64-sample chunk's loads before its 16 MFMAs, and
+//     the next chunk's loads before the current chunk's MFMAs (ping-pong), so a
+//     large batch streams instead of paying one memory round trip per chunk.
 //
 // Reductions run in a fixed order everywhere: bitwise reproducible.
 // ---------------------------------------------------------------------------
@@ -942,7 +945,7 @@ constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
 constexpr int CNQ = CNP / 4;                        // conv float4 columns (1320)
 constexpr int NB_CONV = (CNQ + UP_C - 1) / UP_C;    // 83
 constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
-constexpr int NB_FC = (FC_TILES + UP_NT / 64 - 1) / (UP_NT / 64);  // 11 blocks x 8 waves
+constexpr int NB_FC = FC_TILES;                     // 88 blocks, one tile each
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
@@ -1171,54 +1174,85 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       }
     }
   } else {
-    // ---------------- role FC: one 16x16 tile of [dW | db] per wave
+    // ---------------- role FC: one 16x16 tile of [dW | db] per block, K split over waves
     const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
-    const int tile = blk * (UP_NT / 64) + wave;
-    if (tile < FC_TILES) {
-      const bool fc1 = tile < FC1_TILES;
-      const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
-      const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
-      const int a_off = fc1 ? V_DZ1 : V_DLOG, b_off = fc1 ? V_P2 : V_H;
-      const int o = mt * 16 + l16, i = nt * 16 + l16;  // A row (out feature) / B col (in feature)
-      // this lane's 4 outputs (C rows 4*kq + r, column i) and their p / m
-      int pidx[4];
-      float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
+    const int tile = blk;
+    const bool fc1 = tile < FC1_TILES;
+    const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
+    const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
+    const int a_off = fc1 ? V_DZ1 : V_DLOG, b_off = fc1 ? V_P2 : V_H;
+    const int o = mt * 16 + l16, i = nt * 16 + l16;  // A row (out feature) / B col (in feature)
+    // wave 0 finishes the tile: this lane's 4 outputs (C rows 4*kq + r, column i), their p / m
+    int pidx[4];
+    float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int oo = mt * 16 + 4 * kq + r;
-        pidx[r] = (oo < rows && i <= cols)
-                      ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
-                             : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
-                      : -1;
-        if (a.apply_sgd) {
-          pp[r] = a.params[max(pidx[r], 0)];
-          pm[r] = a.momentum[max(pidx[r], 0)];
-        }
+    for (int r = 0; r < 4; ++r) {
+      const int oo = mt * 16 + 4 * kq + r;
+      pidx[r] = (oo < rows && i <= cols)
+                    ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
+                           : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
+                    : -1;
+      if (a.apply_sgd && wave == 0) {
+        pp[r] = a.params[max(pidx[r], 0)];
+        pm[r] = a.momentum[max(pidx[r], 0)];
       }
-      f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-      // K = batch; 16x16x4 f32 MFMA: lane holds A[o][s0 + 4u + kq] and B[s0 + 4u + kq][i]
-      for (int s0 = 0; s0 < B; s0 += 64) {
-        float av[16], bv[16];
+    }
+    // this wave's samples [k0, k1): a multiple-of-4 share of the batch
+    const int kw = ((B + UP_NT / 64 - 1) / (UP_NT / 64) + 3) & ~3;
+    const int k0 = min(B, wave * kw), k1 = min(B, k0 + kw);
+    // K = samples; 16x16x4 f32 MFMA: lane holds A[o][s0 + 4u + kq] and B[s0 + 4u + kq][i]
+    auto load = [&](int s0, float (&av)[16], float (&bv)[16]) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int s = s0 + 4 * u + kq;
-          const bool ok = s < B;
-          // unconditional loads from clamped addresses, masked after (see role CONV)
-          const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
-          const float ra = rowc[a_off + min(o, rows - 1)];
-          const float rb = rowc[b_off + min(i, cols - 1)];
-          av[u] = (ok && o < rows) ? ra : 0.f;
-          bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
-        }
-        // keep all 32 loads in flight before the first MFMA (otherwise the
-        // scheduler interleaves them and waits on each pair in turn)
+      for (int u = 0; u < 16; ++u) {
+        const int s = s0 + 4 * u + kq;
+        const bool ok = s < k1;
+        // unconditional loads from clamped addresses, masked after (see role CONV)
+        const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
+        const float ra = rowc[a_off + min(o, rows - 1)];
+        const float rb = rowc[b_off + min(i, cols - 1)];
+        av[u] = (ok && o < rows) ? ra : 0.f;
+        bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
+      }
+    };
+    auto mfma16 = [&](f32x4 c, const float (&av)[16], const float (&bv)[16]) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], c, 0, 0, 0);
+      return c;
+    };
+    f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (k0 < k1) {
+      float a0[16], b0[16], a1[16], b1[16];
+      load(k0, a0, b0);
+      for (int s0 = k0; s0 < k1; s0 += 128) {
+        const bool more = s0 + 64 < k1;
+        if (more) load(s0 + 64, a1, b1);
+        // keep each chunk's loads in flight before the MFMAs (otherwise the scheduler
+        // interleaves them and waits on each pair in turn)
         __builtin_amdgcn_sched_barrier(0);
         USTAMP(1);
-#pragma unroll
-        for (int u = 0; u < 16; ++u) c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], c, 0, 0, 0);
+        c = mfma16(c, a0, b0);
+        if (more) {
+          if (s0 + 128 < k1) load(s0 + 128, a0, b0);
+          __builtin_amdgcn_sched_barrier(0);
+          c = mfma16(c, a1, b1);
+        }
       }
-      USTAMP(2);
-      float g[4] = {c[0], c[1], c[2], c[3]};
+    }
+    USTAMP(2);
+    // fixed-order combine of the 8 wave partials (reuses the CONV role's LDS)
+    float* pfc = reinterpret_cast<float*>(&part[0][0]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pfc[wave * 256 + r * 64 + lane] = c[r];
+    __syncthreads();
+    if (wave == 0) {
+      float g[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = pfc[r * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < UP_NT / 64; ++w) v += pfc[w * 256 + r * 64 + lane];
+        g[r] = v;
+      }
       if (EXCH) {
         int idx[4];
         bool live[4];

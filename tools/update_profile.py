@@ -72,18 +72,18 @@ def main():
 
     # s_memrealtime stamps (100 MHz) of one full update, relative to the
     # earliest block entry: shows dispatch skew and per-phase cost per role
-    dbg = torch.zeros(8 * 128, dtype=torch.long, device=dev)
+    dbg = torch.zeros(8 * 256, dtype=torch.long, device=dev)
     for _ in range(3):
         train()
         dbg.zero_()
         ops.lenet_update(eng.slab, eng.grid, eng.vslab, B, None, None, *common(), None, None, True, eng.loss_parts,
                          eng.grid, eng.loss_acc, eng.mfma, dbg)
         torch.cuda.synchronize()
-    st = dbg.view(128, 8).cpu().double()
-    nfc = 11  # blocks [0, 11) FC role, [11, 94) CONV role
-    t0 = st[:94, 0].min()
+    st = dbg.view(256, 8).cpu().double()
+    nfc, nb = 88, 88 + 83  # blocks [0, 88) FC role (one tile each), [88, 171) CONV role
+    t0 = st[:nb, 0].min()
     rel = (st - t0) * 0.01  # us
-    for role, sl, ks in [("CONV", slice(nfc, 94), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 4])]:
+    for role, sl, ks in [("CONV", slice(nfc, nb), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 4])]:
         r = rel[sl]
         desc = "  ".join(f"s{k} med {r[:, k].median().item():.2f} max {r[:, k].max().item():.2f}" for k in ks)
         print(f"stamps {role}: {desc}")
