@@ -895,23 +895,39 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 // ---------------------------------------------------------------------------
 // Weight images from fp32 params (element i of the flat buffer).
 // ---------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void write_images(unsigned short* wimg, int i, float v) {
-  const unsigned short h = h16<T>(v);
+// Destinations of parameter i in the 16-bit weight images (-1: none).  The
+// conv2 slots go through the K-order tables (constant memory): callers on the
+// step's critical path compute them at kernel entry, so that table round trip
+// overlaps their gradient loads instead of following the SGD math.
+__device__ __forceinline__ void image_slots(int i, int& d0, int& d1) {
+  d0 = d1 = -1;
   if (i < O_C1B) {
-    wimg[I_W1C + (i / 25) * 32 + (i % 25)] = h;
+    d0 = I_W1C + (i / 25) * 32 + (i % 25);
   } else if (i >= O_C2W && i < O_C2B) {
     const int j = i - O_C2W;
     const int oc = j / 250, k = j % 250;
     const int ic = k / 25, r = k % 25, kh = r / 5, kw = r % 5;
-    wimg[I_W2C + oc * LD_W2C + kC2Order.inv[r * 2 + (ic >> 3)] * 8 + (ic & 7)] = h;
+    d0 = I_W2C + oc * LD_W2C + kC2Order.inv[r * 2 + (ic >> 3)] * 8 + (ic & 7);
     const int slice = kDgOrder.inv[((4 - kh) * 5 + (4 - kw)) * 3 + (oc >> 3)];  // dgrad K slice
-    wimg[I_W2D + (slice * 16 + ic) * 8 + (oc & 7)] = h;
+    d1 = I_W2D + (slice * 16 + ic) * 8 + (oc & 7);
   } else if (i >= O_F1W && i < O_F1B) {
     const int j = i - O_F1W;
-    const int o = j / 320, ii = j % 320;
-    wimg[I_F1 + o * LD_F1 + ii] = h;
+    d0 = I_F1 + (j / 320) * LD_F1 + (j % 320);
   }
+}
+
+template <typename T>
+__device__ __forceinline__ void write_slots(unsigned short* wimg, int d0, int d1, float v) {
+  const unsigned short h = h16<T>(v);
+  if (d0 >= 0) wimg[d0] = h;
+  if (d1 >= 0) wimg[d1] = h;
+}
+
+template <typename T>
+__device__ __forceinline__ void write_images(unsigned short* wimg, int i, float v) {
+  int d0, d1;
+  image_slots(i, d0, d1);
+  write_slots<T>(wimg, d0, d1, v);
 }
 
 template <typename T>
@@ -999,7 +1015,7 @@ __global__ void __launch_bounds__(512) lenet_stage_kernel(LenetStageArgs st, con
 // round trip overlaps the gradient loads instead of following them.
 template <typename T>
 __device__ __forceinline__ void finish_param(const LenetUpdateArgs& a, int i, float gsum, bool first, float p,
-                                             float m) {
+                                             float m, int d0, int d1) {
   if (!a.apply_sgd) {
     a.grad_out[i] = gsum;
     return;
@@ -1014,7 +1030,7 @@ __device__ __forceinline__ void finish_param(const LenetUpdateArgs& a, int i, fl
   }
   p = fmaf(-a.lr, d, p);
   a.params[i] = p;
-  write_images<T>(a.wimg, i, p);
+  write_slots<T>(a.wimg, d0, d1, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -1119,9 +1135,11 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
     // wave 0 owns params cblk*64 + tid (16 float4 columns): prefetch p / m now
     const int pi = cblk * (UP_C * 4) + tid;
     float p0 = 0.f, m0 = 0.f;
+    int d0 = -1, d1 = -1;
     if (a.apply_sgd && tid < 64) {
       p0 = a.params[min(pi, NP - 1)];
       m0 = a.momentum[min(pi, NP - 1)];
+      image_slots(pi, d0, d1);
     }
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     // Loads are unconditional from a clamped address and masked afterwards: a
@@ -1156,7 +1174,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
         const bool live[1] = {true};
         ll_allreduce<1>(px, xt, idx, live, g, timeout_ticks, timed_out);
       }
-      finish_param<T>(a, pi, g[0], first, p0, m0);
+      finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
     USTAMP(4);
     if (cblk == 0 && loss_parts && tid < 64) {
@@ -1196,6 +1214,14 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
         pp[r] = a.params[max(pidx[r], 0)];
         pm[r] = a.momentum[max(pidx[r], 0)];
       }
+    }
+    // fc destinations in the weight images (no table lookups for fc)
+    int fd[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int d1;
+      image_slots(max(pidx[r], 0), fd[r], d1);
+      if (pidx[r] < 0) fd[r] = -1;
     }
     // this wave's samples [k0, k1): a multiple-of-4 share of the batch
     const int kw = ((B + UP_NT / 64 - 1) / (UP_NT / 64) + 3) & ~3;
@@ -1265,7 +1291,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r]);
+        if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
       USTAMP(4);
     }
   }
@@ -1303,7 +1329,11 @@ template <typename T>
 __global__ void lenet_sgd_kernel(LenetUpdateArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
-  if (i < NP) finish_param<T>(a, i, a.grad_in[i], first, a.params[i], a.momentum[i]);
+  if (i < NP) {
+    int d0, d1;
+    image_slots(i, d0, d1);
+    finish_param<T>(a, i, a.grad_in[i], first, a.params[i], a.momentum[i], d0, d1);
+  }
   if (a.dampening != 0.f) {
     __syncthreads();
     if (threadIdx.x == 0) {
