@@ -35,7 +35,7 @@
 //
 // Weight-image layout (16-bit, offsets in elements; all 16-B aligned); each
 // operand holds its live rows and one zero row that padding rows are clamped to:
-//   W1C  [16][32]   conv1  B operand  (k = kh*5+kw)
+//   W1C  [16][32]   conv1  B operand  (K slots: see w1c_slot)
 //   W2C  [21][432]  conv2  B operand  (8-channel K slices (kh*5+kw, ic/8) in kC2Order)
 //   W2D  [77][16][8] conv2 dgrad B, chunk-major: chunk = K slice of 8 channels
 //                   (slice order kDgOrder over (tap = (4-kh)*5 + (4-kw), oc/8))
@@ -119,6 +119,16 @@ constexpr int R_W2C = 20, R_F1 = 50;       // live rows; row R_* is the zero row
 // (row-major rows collide between the kq0 / kq1 halves of a group whatever the stride).
 constexpr int DG_CH = 4 * DG_KS + 1;
 constexpr int I_W1C = 0, I_W2C = 512;
+// conv1 K slot of tap (kh, kw): lane group q of the MFMA A fragment owns slots
+// 8q..8q+7; slots 8q+j (j < 5) are row q's taps, so every group reads its row as
+// base + 28q + {0..4} (immediate LDS offsets), and the five row-4 taps fill slots
+// 8q+5..8q+7 of groups 0 and 1 as base + 112 + e_q + {0,1,2} (e_0 = 0, e_1 = 2;
+// slot 7 of group 0 duplicates tap (4,2) with a zero weight; groups 2, 3 read
+// (4,0..2) with zero weights).
+constexpr int w1c_slot(int kh, int kw) {
+  return kh < 4 ? kh * 8 + kw : (kw < 2 ? 5 + kw : 8 + 5 + (kw - 2));
+}
+constexpr int W1_E1 = 2;  // row-4 column offset of lane group 1's extra slots
 constexpr int I_W2D = I_W2C + (R_W2C + 1) * LD_W2C;  // 9584
 constexpr int I_F1 = I_W2D + DG_CH * 16 * 8;         // 19440
 // padded so the LDS copy is whole 512-thread x 16-byte rounds
@@ -212,6 +222,22 @@ __device__ __forceinline__ int opaque(int x) {
 // wait vmcnt(0) while one is outstanding), so stages that do not read the DMA'd
 // weights run under it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One ds_read_u16 at an immediate offset (OFF elements) from p.  Inline asm keeps
+// neighbouring 16-bit reads at a sliding, 2-byte-aligned window from being merged
+// into misaligned ds_read_b32/b64 (replayed at ~64 cycles); the compiler does not
+// track these reads, so their consumer must wait with lds_wait8 first.
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_u16(const unsigned short* p) {
+  uint32_t v;
+  asm volatile("ds_read_u16 %0, %1 offset:%2" : "=v"(v) : "v"((uint32_t)reinterpret_cast<uintptr_t>(p)), "i"(OFF * 2));
+  return v;
+}
+// lgkmcnt(0), threading the eight values through the asm so no use is hoisted above it
+__device__ __forceinline__ void lds_wait8(uint32_t (&v)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+}
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
@@ -410,12 +436,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     rowv = perm_at(min(lane, nsamp - 1));
   }
   if (a.dbg && tid == 0) DBGS[13] = __builtin_amdgcn_s_memtime();
-  int koff1[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = kb + j;
-    koff1[j] = k < 25 ? (k / 5) * 28 + (k % 5) : 0;
-  }
   // conv2 wgrad B columns k = (wave + 8*jj)*16 + l16 = ic*25 + kh*5 + kw: P1 offset
   int kwb[2];
 #pragma unroll
@@ -485,15 +505,31 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     STAMP(1);
     {
       // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
-      u16x8 raw[5];
+      uint32_t rv[5][8];
 #pragma unroll
       for (int it = 0; it < 5; ++it) {
         const int mt = min(wave + it * NW, 35);
         const int m = mt * 16 + l16;
         const int p = m >> 2, q = m & 3;
         const int pb = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
+        // K slots of lane group kq (see w1c_slot): row kq, then 3 taps of row 4
+        const unsigned short* r1 = Xs + pb + 28 * kq;
+        const unsigned short* r2 = Xs + pb + 112 + (kq == 1 ? W1_E1 : 0);
+        rv[it][0] = lds_u16<0>(r1);
+        rv[it][1] = lds_u16<1>(r1);
+        rv[it][2] = lds_u16<2>(r1);
+        rv[it][3] = lds_u16<3>(r1);
+        rv[it][4] = lds_u16<4>(r1);
+        rv[it][5] = lds_u16<0>(r2);
+        rv[it][6] = lds_u16<1>(r2);
+        rv[it][7] = lds_u16<2>(r2);
+      }
+      u16x8 raw[5];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[it][j] = Xs[pb + koff1[j]];
+      for (int it = 0; it < 5; ++it) {
+        lds_wait8(rv[it]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[it][j] = (unsigned short)rv[it][j];
       }
       const float cb = PAR[P_C1B + min(l16, 9)];
       const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
@@ -902,7 +938,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 __device__ __forceinline__ void image_slots(int i, int& d0, int& d1) {
   d0 = d1 = -1;
   if (i < O_C1B) {
-    d0 = I_W1C + (i / 25) * 32 + (i % 25);
+    d0 = I_W1C + (i / 25) * 32 + w1c_slot((i % 25) / 5, (i % 25) % 5);
   } else if (i >= O_C2W && i < O_C2B) {
     const int j = i - O_C2W;
     const int oc = j / 250, k = j % 250;
