@@ -166,7 +166,9 @@ constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 constexpr int S_W1C = S_F + F_END * 4;                // u16 16*32  conv1 B operand (copy of W1C)
 constexpr int S_LABEL = S_W1C + 16 * 32 * 2;          // i32 [4]   staged sample's label
 constexpr int S_DBG = S_LABEL + 16;                   // u64 [32]  stage stamps (diagnostics)
-constexpr int S_TOTAL = S_DBG + 32 * 8;
+constexpr int S_C1T = S_DBG + 32 * 8;                 // u16 [512][8] conv1 per-thread X offsets (tiles 0..4)
+constexpr int S_C1H = S_C1T + 512 * 16;               // u16 [512][8] conv1 per-thread P1H offsets
+constexpr int S_TOTAL = S_C1H + 512 * 16;
 static_assert(S_W2D % 16 == 0 && S_F1 % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
 static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_P1H % 16 == 0 && S_DC2 % 16 == 0 && S_DC2H % 16 == 0, "align");
 static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B % 16 == 0, "align");
@@ -302,6 +304,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   unsigned short* W1Cs = (unsigned short*)ACT(S_W1C);
   int* LABEL = (int*)ACT(S_LABEL);
   uint64_t* DBGS = (uint64_t*)ACT(S_DBG);
+  u16x8* C1T = (u16x8*)ACT(S_C1T);
+  u16x8* C1H = (u16x8*)ACT(S_C1H);
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
@@ -384,6 +388,24 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * DMA_NT + tid)),
                                        (lds_void*)(wsm + S_W2C + (u * DMA_NT + wave * 64) * 16), 16, 0, 0);
     if (a.dbg && lane == 0) DBGS[(wave == 0 ? 10 : 17 + wave)] = __builtin_amdgcn_s_memtime();
+    // while the DMA streams: conv1's per-thread address tables (stage 1 reads them
+    // back with two ds_read_b128 instead of ~100 VALU of index math per thread)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tt = tid + h * DMA_NT, tw = tt >> 6, tl16 = tt & 15, tkq = (tt & 63) >> 4;
+      u16x8 xo, ho;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int mt = min(tw + min(it, 4) * NW, 35);
+        const int m = mt * 16 + tl16;
+        const int p = m >> 2, q = m & 3;
+        xo[it] = (unsigned short)((2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1));
+        const int w = mt * 4 + tkq;  // pooled position py*12 + px
+        ho[it] = (unsigned short)((w / 12) * P1H_RP + (w % 12) * LD_P1H);
+      }
+      C1T[tt] = xo;
+      C1H[tt] = ho;
+    }
   } else {
     const int t = tid - NT / 2;
     // under the load latency: P1H | DC2 | DC2H | DC1 are contiguous, zero their
@@ -506,12 +528,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     {
       // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
       uint32_t rv[5][8];
+      const u16x8 xo = C1T[tid];  // per-thread tables (preamble, waves 0-3)
+      const u16x8 ho = C1H[tid];
 #pragma unroll
       for (int it = 0; it < 5; ++it) {
-        const int mt = min(wave + it * NW, 35);
-        const int m = mt * 16 + l16;
-        const int p = m >> 2, q = m & 3;
-        const int pb = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
+        const int pb = xo[it];
         // K slots of lane group kq (see w1c_slot): row kq, then 3 taps of row 4
         const unsigned short* r1 = Xs + pb + 28 * kq;
         const unsigned short* r2 = Xs + pb + 112 + (kq == 1 ? W1_E1 : 0);
@@ -548,7 +569,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
             P1[l16 * 144 + w] = hv;
             I1[l16 * 144 + w] = (uint8_t)bi;
-            P1H[(w / 12) * P1H_RP + (w % 12) * LD_P1H + l16] = hv;
+            P1H[ho[it] + l16] = hv;
           }
         }
       }
