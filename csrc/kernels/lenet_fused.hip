@@ -134,7 +134,7 @@ constexpr int I_F1 = I_W2D + DG_CH * 16 * 8;         // 19440
 // padded so the LDS copy is whole 512-thread x 16-byte rounds
 constexpr int I_END = I_W2C + ((I_F1 + (R_F1 + 1) * LD_F1 - I_W2C + 4095) / 4096) * 4096;  // 33280
 constexpr int LD_DC2 = 72, LD_DC1 = 592;
-constexpr int NT = 512, NW = 8;
+constexpr int NT = 1024, NW = 16;  // 16 waves, 4 per SIMD
 // conv partial-gradient slab: params [0, CNP) = conv1.w, conv1.b, conv2.w, conv2.b
 constexpr int CNP = O_F1W;
 constexpr int CNP_PAD = (CNP + 63) / 64 * 64;  // slab row: 83 chunks of 64 floats (see lenet_update)
@@ -166,14 +166,14 @@ constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 constexpr int S_W1C = S_F + F_END * 4;                // u16 16*32  conv1 B operand (copy of W1C)
 constexpr int S_LABEL = S_W1C + 16 * 32 * 2;          // i32 [4]   staged sample's label
 constexpr int S_DBG = S_LABEL + 16;                   // u64 [32]  stage stamps (diagnostics)
-constexpr int S_C1T = S_DBG + 32 * 8;                 // u16 [512][8] conv1 per-thread X offsets (tiles 0..4)
-constexpr int S_C1H = S_C1T + 512 * 16;               // u16 [512][8] conv1 per-thread P1H offsets
-constexpr int S_TOTAL = S_C1H + 512 * 16;
+constexpr int S_C1T = S_DBG + 32 * 8;                 // u16 [1024][4] conv1 per-thread X offsets (tiles 0..2)
+constexpr int S_C1H = S_C1T + 1024 * 8;               // u16 [1024][4] conv1 per-thread P1H offsets
+constexpr int S_TOTAL = S_C1H + 1024 * 8;
 static_assert(S_W2D % 16 == 0 && S_F1 % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
 static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_P1H % 16 == 0 && S_DC2 % 16 == 0 && S_DC2H % 16 == 0, "align");
 static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B % 16 == 0, "align");
 static_assert(S_F % 16 == 0 && (F_RED * 4) % 16 == 0 && S_TOTAL <= 160 * 1024, "lds");
-static_assert(WIMG_LDS_U4 % NT == 0, "whole LDS-DMA rounds");
+static_assert(WIMG_LDS_U4 % 256 == 0, "whole LDS-DMA rounds over waves 0-3");
 static_assert(C2_KS * 32 <= LD_W2C && 25 * C2_ICP <= C2_KS * 32, "conv2 K");
 static_assert(25 * DG_OCP <= DG_KS * 32, "dgrad K");
 }  // namespace lenet
@@ -304,8 +304,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   unsigned short* W1Cs = (unsigned short*)ACT(S_W1C);
   int* LABEL = (int*)ACT(S_LABEL);
   uint64_t* DBGS = (uint64_t*)ACT(S_DBG);
-  u16x8* C1T = (u16x8*)ACT(S_C1T);
-  u16x8* C1H = (u16x8*)ACT(S_C1H);
+  u16x4* C1T = (u16x4*)ACT(S_C1T);
+  u16x4* C1H = (u16x4*)ACT(S_C1H);
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
@@ -340,8 +340,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   int64_t lab_next = 0;
   // Wave roles.  Waves 0-3 stream the 72 KB of weight images into LDS (LDS-DMA);
   // waves 4-7 fetch every small operand (pixels, label, fp32 params, conv1
-  // weights, K-order tables), zero the padded activation images and write the
-  // operands to LDS.  Vector memory operations complete in issue order, so a wave that had
+  // weights, K-order tables), write them to LDS and zero the padded activation
+  // images; waves 8-15 build conv1's address tables.  Vector memory operations complete in issue order, so a wave that had
   // both would wait for the whole DMA at its first use of a small operand; split
   // this way, no wave waits for the DMA before conv2 (stage 2) reads the images,
   // and stages 0-1 run while it streams.  (The staged batch has one sample per
@@ -352,8 +352,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   int lab0 = 0, kg = 0;
   float pv[3] = {0.f, 0.f, 0.f};
   uint4 w1 = make_uint4(0, 0, 0, 0);
-  if (wave >= 4) {
-    const int t = tid - NT / 2;
+  if (wave >= 4 && wave < 8) {
+    const int t = tid - 256;
     if (a.dbg && t == 0) DBGS[17] = __builtin_amdgcn_s_memtime();
     // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread)
     auto par_index = [](int q) {
@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
                                                                                           : O_F2W + q - 90;
     };
 #pragma unroll
-    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * (NT / 2), 589))];
+    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * 256, 589))];
     w1 = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t & 63];
     if (STAGED) {
       px0 = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(t, 195)];
@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   if (wave < 4) {
     // W2C | W2D | F1 by LDS-DMA: each wave-instruction moves 1 KB to a wave-uniform
     // base + lane*16, so the image stays lane-linear
-    constexpr int DMA_NT = NT / 2;
+    constexpr int DMA_NT = 256;  // waves 0-3
     static_assert(WIMG_LDS_U4 % DMA_NT == 0, "whole LDS-DMA rounds over waves 0-3");
     const uint4* src = reinterpret_cast<const uint4*>(a.wimg + I_W2C);
 #pragma unroll
@@ -388,34 +388,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * DMA_NT + tid)),
                                        (lds_void*)(wsm + S_W2C + (u * DMA_NT + wave * 64) * 16), 16, 0, 0);
     if (a.dbg && lane == 0) DBGS[(wave == 0 ? 10 : 17 + wave)] = __builtin_amdgcn_s_memtime();
-    // while the DMA streams: conv1's per-thread address tables (stage 1 reads them
-    // back with two ds_read_b128 instead of ~100 VALU of index math per thread)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int tt = tid + h * DMA_NT, tw = tt >> 6, tl16 = tt & 15, tkq = (tt & 63) >> 4;
-      u16x8 xo, ho;
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int mt = min(tw + min(it, 4) * NW, 35);
-        const int m = mt * 16 + tl16;
-        const int p = m >> 2, q = m & 3;
-        xo[it] = (unsigned short)((2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1));
-        const int w = mt * 4 + tkq;  // pooled position py*12 + px
-        ho[it] = (unsigned short)((w / 12) * P1H_RP + (w % 12) * LD_P1H);
-      }
-      C1T[tt] = xo;
-      C1H[tt] = ho;
-    }
-  } else {
-    const int t = tid - NT / 2;
-    // under the load latency: P1H | DC2 | DC2H | DC1 are contiguous, zero their
-    // padding once with 16-B stores (in these waves: the compiler makes an LDS
-    // store loop wait for any LDS-DMA still in flight)
-    {
-      constexpr int NZ = (S_COFF - S_P1H) / 16;
-      uint4* z = reinterpret_cast<uint4*>(ACT(S_P1H));
-      for (int i = t; i < NZ; i += NT / 2) z[i] = make_uint4(0, 0, 0, 0);
-    }
+  } else if (wave < 8) {
+    const int t = tid - 256;
     if (t < 64) {
       // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
       // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
@@ -430,7 +404,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      if (t + j * (NT / 2) < 590) PAR[t + j * (NT / 2)] = pv[j];
+      if (t + j * 256 < 590) PAR[t + j * 256] = pv[j];
     if (STAGED) {
       if (t < 196) {  // the staged sample's pixels (stage 0 of sample 0)
         u16x4 o;
@@ -447,6 +421,30 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // first reuse of their registers would make waves 0-3 wait vmcnt(0) -- for the DMA.
     asm volatile("" ::"v"(pv[0]), "v"(pv[1]), "v"(pv[2]), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(px0),
                  "v"(lab0), "v"(kg));
+    // then zero the padded activation images (P1H | DC2 | DC2H | DC1 are contiguous)
+    constexpr int NZ = (S_COFF - S_P1H) / 16;
+    uint4* z = reinterpret_cast<uint4*>(ACT(S_P1H));
+    for (int i = t; i < NZ; i += 256) z[i] = make_uint4(0, 0, 0, 0);
+  } else {
+    // waves 8-15: conv1's per-thread address tables, so stage 1 reads two 8-byte
+    // rows instead of redoing the index math
+    const int t = tid - 512;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tt = t + h * 512, tw = tt >> 6, tl16 = tt & 15, tkq = (tt & 63) >> 4;
+      u16x4 xo = {0, 0, 0, 0}, ho = {0, 0, 0, 0};
+#pragma unroll
+      for (int it = 0; it < 3; ++it) {
+        const int mt = min(tw + it * NW, 35);
+        const int m = mt * 16 + tl16;
+        const int p = m >> 2, q = m & 3;
+        xo[it] = (unsigned short)((2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1));
+        const int w = mt * 4 + tkq;  // pooled position py*12 + px
+        ho[it] = (unsigned short)((w / 12) * P1H_RP + (w % 12) * LD_P1H);
+      }
+      C1T[tt] = xo;
+      C1H[tt] = ho;
+    }
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
@@ -459,22 +457,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   }
   if (a.dbg && tid == 0) DBGS[13] = __builtin_amdgcn_s_memtime();
   // conv2 wgrad B columns k = (wave + 8*jj)*16 + l16 = ic*25 + kh*5 + kw: P1 offset
-  int kwb[2];
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int k = min((wave + 8 * jj) * 16 + l16, 249), ic = k / 25, r = k % 25;
-    kwb[jj] = ic * 144 + (r / 5) * 12 + (r % 5);
+  int kwb[1];
+  {
+    const int k = min(wave * 16 + l16, 249), ic = k / 25, r = k % 25;
+    kwb[0] = ic * 144 + (r / 5) * 12 + (r % 5);
   }
   // conv1 wgrad B column k = (wave&1)*16 + l16 = kh*5 + kw: X offset
   const int kc1 = (wave & 1) * 16 + l16;
   const int koffc1 = kc1 < 25 ? (kc1 / 5) * 28 + (kc1 % 5) : 0;
 
   // ---------------- per-workgroup gradient accumulators (registers)
-  f32x4 acc_c2[2][2];   // conv2 wgrad: M-tiles (oc) 0,1 x N-tiles (k) wave, wave+8
+  f32x4 acc_c2[2][1];   // conv2 wgrad: M-tiles (oc) 0,1 x N-tile (k) `wave`
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc_c2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 2; ++i) acc_c2[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc_c1 = f32x4{0.f, 0.f, 0.f, 0.f};  // conv1 wgrad tile (wave&1), steps (wave>>1) mod 4
   float loss_sum = 0.f, correct = 0.f;
   // The fc-layer weight gradients are rank-1 per sample (dZ (x) input); instead of
@@ -489,7 +484,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
-    if (a.dbg && lane == 0 && s == 0) DBGS[24 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
+    if (a.dbg && lane == 0 && s == 0 && wave < 8) DBGS[24 + wave] = __builtin_amdgcn_s_memtime();
     lds_barrier();  // previous sample's readers are done (first pass: preamble LDS writes)
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
     // then start the next sample's loads (consumed one sample later)
@@ -527,11 +522,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     STAMP(1);
     {
       // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
-      uint32_t rv[5][8];
-      const u16x8 xo = C1T[tid];  // per-thread tables (preamble, waves 0-3)
-      const u16x8 ho = C1H[tid];
+      // 36 tiles over 16 waves: at most 3 per wave
+      uint32_t rv[3][8];
+      const u16x4 xo = C1T[tid];  // per-thread tables (preamble, waves 8-15)
+      const u16x4 ho = C1H[tid];
 #pragma unroll
-      for (int it = 0; it < 5; ++it) {
+      for (int it = 0; it < 3; ++it) {
         const int pb = xo[it];
         // K slots of lane group kq (see w1c_slot): row kq, then 3 taps of row 4
         const unsigned short* r1 = Xs + pb + 28 * kq;
@@ -545,9 +541,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         rv[it][6] = lds_u16<1>(r2);
         rv[it][7] = lds_u16<2>(r2);
       }
-      u16x8 raw[5];
+      u16x8 raw[3];
 #pragma unroll
-      for (int it = 0; it < 5; ++it) {
+      for (int it = 0; it < 3; ++it) {
         lds_wait8(rv[it]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) raw[it][j] = (unsigned short)rv[it][j];
@@ -555,9 +551,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       const float cb = PAR[P_C1B + min(l16, 9)];
       const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
 #pragma unroll
-      for (int it = 0; it < 5; ++it) {
+      for (int it = 0; it < 3; ++it) {
         const int mt = wave + it * NW;
-        if (it < 4 || mt < 36) {
+        if (mt < 36) {
           const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw[it]), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
           if (l16 < 10) {
             float best = c[0];
@@ -578,7 +574,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
     STAMP(2);
-    {
+    if (wave < 8) {
       // A[m][k = tap*16 + ic] = P1H[pos(m) + shift(tap)][ic]; one b128 per K slice
       const int mt = wave & 3, nt = wave >> 2;
       const int m = mt * 16 + l16;
@@ -615,8 +611,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3)
     STAMP(3);
-    if (stage_next && tid >= NT / 2) {  // waves 4-7: they hold nrow
-      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid - NT / 2, 195)];
+    if (stage_next && wave >= 4 && wave < 8) {  // waves 4-7: they hold nrow
+      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid - 256, 195)];
       lab_next = a.labels[nrow];
     }
     if (wave < 4) {
@@ -732,7 +728,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       const unsigned short* fc2 = F1s + min(32 + kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc3 = F1s + min(32 + kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt) {
+      for (int tt = 0; tt < 2; ++tt) {
         const int t = wave + NW * tt;  // wave-uniform: EXEC stays full for the transposed reads
         if (t < 20) {
           const s16x4 r0 = lds_read_tr16(fc0 + t * 16), r1 = lds_read_tr16(fc1 + t * 16);
@@ -767,21 +763,20 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     STAMP(6);
     {
       const unsigned short one = h16<T>(1.f);
+      // 16 waves x 16 columns cover the 251 B columns (k = wave*16 + l16) in one pass
       frag fa[2][2];
-      u16x8 raw[2][2];
+      u16x8 raw[2][1];
 #pragma unroll
       for (int ps = 0; ps < 2; ++ps) {
         fa[ps][0] = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + ps * 32 + kb);
         fa[ps][1] = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + ps * 32 + kb);
         const int ohr = ((ps * 32 + kb) >> 3) * 12;
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) raw[ps][jj][j] = P1[opaque(kwb[jj] + ohr + j)];
+        for (int j = 0; j < 8; ++j) raw[ps][0][j] = P1[opaque(kwb[0] + ohr + j)];
       }
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int k = (wave + 8 * jj) * 16 + l16;
+      for (int jj = 0; jj < 1; ++jj) {
+        const int k = wave * 16 + l16;
         const unsigned short cst = k == 250 ? one : (unsigned short)0;  // bias column / padding
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
@@ -795,26 +790,17 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       }
     }
     STAMP(9);
-    {
+    if (wave < 8) {
       // dP1[px][ic] = sum_{tap, oc} DC2H[px + shift(tap)][oc] * W2D[ic][tap*24 + oc]:
-      // full tile `wave` (pixels 16*wave ..) plus K-steps ks = wave + 8j of tile 8
+      // tile `wave` = pixels 16*wave .. +15, all 19 K-steps (tile 8 is split over waves
+      // 8-15 below, so each SIMD carries ~43 of the 171 MFMAs)
       const s16x8 dof0 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24);
       const s16x8 dof1 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 8);
       const s16x8 dof2 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 16);
       // B fragment of K-step ks: chunk 4*ks + kq, row l16 (ic)
       const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
-      const int mw = wave * 16 + l16, m8 = 128 + l16;
+      const int mw = wave * 16 + l16;
       const unsigned short* aw = DC2H + (mw / 12) * DC2H_RP + (mw % 12) * DG_OCP;
-      const unsigned short* a8 = DC2H + (m8 / 12) * DC2H_RP + (m8 % 12) * DG_OCP;
-      // tile-8 share: 3 K-steps, the third only for waves 0-2 (others read the zero row)
-      frag f8a[3], f8b[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int ks = wave + 8 * j;
-        const int off = DOFF[kq * 24 + min(ks, DG_KS - 1)];
-        f8a[j] = *reinterpret_cast<const frag*>(a8 + off);
-        f8b[j] = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 512 : W2d + ((DG_CH - 1) * 16 + l16) * 8);
-      }
       // the pool1/ReLU gate of this lane's 4 outputs does not depend on the MFMAs:
       // read it first so its LDS latency hides under the K loop
       const int ci = min(l16, 9);
@@ -827,7 +813,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         gi[r] = I1[pi];
       }
       // two accumulator chains (even / odd K-steps) halve the dependent-MFMA latency
-      f32x4 cw0 = f32x4{0.f, 0.f, 0.f, 0.f}, cw1 = cw0, c8 = cw0;
+      f32x4 cw0 = f32x4{0.f, 0.f, 0.f, 0.f}, cw1 = cw0;
 #pragma unroll
       for (int ks = 0; ks < DG_KS; ++ks) {
         const int off = ks < 8 ? dof0[ks] : (ks < 16 ? dof1[ks - 8] : dof2[ks - 16]);
@@ -836,8 +822,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (ks & 1) cw1 = Mfma<T>::mma(fa, fb, cw1);
         else cw0 = Mfma<T>::mma(fa, fb, cw0);
       }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) c8 = Mfma<T>::mma(f8a[j], f8b[j], c8);
       if (l16 < 10) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -846,32 +830,46 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           dgrad_store<T>(DC1, l16, mm, v, gi[r]);
         }
       }
+    } else {
+      // tile 8 (pixels 128..143), K-steps ks = (wave - 8) + 8j: a split-K share
+      const int w8 = wave - 8, m8 = 128 + l16;
+      const unsigned short* a8 = DC2H + (m8 / 12) * DC2H_RP + (m8 % 12) * DG_OCP;
+      const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
+      f32x4 c8 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) RED[wave * 256 + (4 * kq + r) * 16 + l16] = c8[r];
+      for (int j = 0; j < 3; ++j) {
+        const int ks = w8 + 8 * j;  // the third share only for w8 < 3 (others read the zero chunk)
+        const int off = DOFF[kq * 24 + min(ks, DG_KS - 1)];
+        const frag fa = *reinterpret_cast<const frag*>(a8 + off);
+        const frag fb = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 512 : W2d + ((DG_CH - 1) * 16 + l16) * 8);
+        c8 = Mfma<T>::mma(fa, fb, c8);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) RED[w8 * 256 + (4 * kq + r) * 16 + l16] = c8[r];
     }
     __syncthreads();
     STAMP(7);
-    if (tid < 256) {
+    if (tid < 256) {  // tile 8: fixed-order sum of the 8 shares, then the pool1/relu backward
       const int rr = tid >> 4, ci = tid & 15;
       if (ci < 10) {
         float v = 0.f;
 #pragma unroll
-        for (int q = 0; q < NW; ++q) v += RED[q * 256 + rr * 16 + ci];
+        for (int q = 0; q < 8; ++q) v += RED[q * 256 + rr * 16 + ci];
         dgrad_out<T>(DC1, P1, I1, ci, 128 + rr, v);
       }
     }
     __syncthreads();
 
     // ---------------- stage 8: conv1 wgrad (+bias column 25), accumulate in registers
-    // (tile wave&1, K-steps ps = (wave>>1) + 4i: 18 steps over 4 wave pairs)
+    // (tile wave&1, K-steps ps = (wave>>1) + 8i: 18 steps over 8 wave pairs)
     STAMP(8);
     {
       const unsigned short cst = kc1 == 25 ? h16<T>(1.f) : (unsigned short)0;
-      frag fa[5];
-      u16x8 raw[5];
+      frag fa[3];
+      u16x8 raw[3];
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const int ps = min((wave >> 1) + 4 * i, 17);
+      for (int i = 0; i < 3; ++i) {
+        const int ps = min((wave >> 1) + 8 * i, 17);
         const int p0 = ps * 32 + kb;
         fa[i] = *reinterpret_cast<const frag*>(DC1 + l16 * LD_DC1 + p0);
         const int oh = p0 / 24, ow0 = p0 - oh * 24;
@@ -880,11 +878,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         for (int j = 0; j < 8; ++j) raw[i][j] = Xs[opaque(base + j)];
       }
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
+      for (int i = 0; i < 3; ++i) {
         u16x8 rv = raw[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) rv[j] = kc1 < 25 ? rv[j] : cst;
-        if (i < 4 || wave < 4) acc_c1 = Mfma<T>::mma(fa[i], __builtin_bit_cast(frag, rv), acc_c1);
+        if ((wave >> 1) + 8 * i < 18) acc_c1 = Mfma<T>::mma(fa[i], __builtin_bit_cast(frag, rv), acc_c1);
       }
     }
     STAMP(14);
@@ -897,8 +895,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 
   if (a.dbg && tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
   if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
-    if (tid >= NT / 2 && tid - NT / 2 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - NT / 2] = px_next;
-    if (tid == NT / 2) a.lstage[g] = lab_next;
+    if (tid >= 256 && tid - 256 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 256] = px_next;
+    if (tid == 256) a.lstage[g] = lab_next;
   }
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
@@ -907,14 +905,16 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     auto out = [&](int e) -> float& { return a.slab[((int64_t)(e >> 6) * G + g) * 64 + (e & 63)]; };
     // conv1: combine the four step-slices of each tile (fixed order)
     __syncthreads();
+    // partial of wave w at part(w): RED for waves 0-7, the dead DC2H image for 8-15
+    auto part = [&](int w) { return w < 8 ? RED + w * 256 : reinterpret_cast<float*>(DC2H) + (w - 8) * 256; };
 #pragma unroll
-    for (int r = 0; r < 4; ++r) RED[(wave * 16 + 4 * (lane >> 4) + r) * 16 + l16] = acc_c1[r];
+    for (int r = 0; r < 4; ++r) part(wave)[(4 * (lane >> 4) + r) * 16 + l16] = acc_c1[r];
     __syncthreads();
-    {
+    if (tid < 512) {
       const int nt = tid >> 8, oc = (tid >> 4) & 15, col = tid & 15;
       float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v += RED[((nt + 2 * q) * 16 + oc) * 16 + col];
+      for (int q = 0; q < 8; ++q) v += part(nt + 2 * q)[oc * 16 + col];
       const int k = nt * 16 + col;
       if (oc < 10) {
         if (k < 25) out(O_C1W + oc * 25 + k) = v;
@@ -925,8 +925,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int k = (wave + 8 * jj) * 16 + l16;
+      for (int jj = 0; jj < 1; ++jj) {
+        const int k = wave * 16 + l16;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int oc = mt * 16 + 4 * (lane >> 4) + r;
