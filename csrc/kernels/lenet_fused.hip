@@ -340,14 +340,32 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   int64_t lab_next = 0;
   // Wave roles.  Waves 0-3 stream the 72 KB of weight images into LDS (LDS-DMA);
   // waves 4-7 fetch every small operand (pixels, label, fp32 params, conv1
-  // weights, K-order tables), write them to LDS and zero the padded activation
-  // images; waves 8-15 build conv1's address tables.  Vector memory operations complete in issue order, so a wave that had
+  // weights, K-order tables) and write them to LDS; waves 8-15 build conv1's
+  // address tables.  (The zero padding of the im2col images is written by idle
+  // waves inside the sample, see stages 0 and 3.)  Vector memory operations complete in issue order, so a wave that had
   // both would wait for the whole DMA at its first use of a small operand; split
   // this way, no wave waits for the DMA before conv2 (stage 2) reads the images,
   // and stages 0-1 run while it streams.  (The staged batch has one sample per
   // workgroup; the non-staged path keeps its per-thread pixel pipeline below.)
   // Waves 4-7 issue their loads first and then meet waves 0-3 at a barrier, so
   // that the CU's vector memory pipeline (FIFO) serves them ahead of the DMA.
+  // conv1's per-thread address tables (thread tt's X offsets and P1H offsets for its
+  // tiles 0..2), so stage 1 reads two 8-byte rows instead of redoing the index math
+  auto conv1_tables = [&](int tt) {
+    const int tw = tt >> 6, tl16 = tt & 15, tkq = (tt & 63) >> 4;
+    u16x4 xo = {0, 0, 0, 0}, ho = {0, 0, 0, 0};
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int mt = min(tw + it * NW, 35);
+      const int m = mt * 16 + tl16;
+      const int p = m >> 2, q = m & 3;
+      xo[it] = (unsigned short)((2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1));
+      const int w = mt * 4 + tkq;  // pooled position py*12 + px
+      ho[it] = (unsigned short)((w / 12) * P1H_RP + (w % 12) * LD_P1H);
+    }
+    C1T[tt] = xo;
+    C1H[tt] = ho;
+  };
   uint32_t px0 = 0;
   int lab0 = 0, kg = 0;
   float pv[3] = {0.f, 0.f, 0.f};
@@ -421,30 +439,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // first reuse of their registers would make waves 0-3 wait vmcnt(0) -- for the DMA.
     asm volatile("" ::"v"(pv[0]), "v"(pv[1]), "v"(pv[2]), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(px0),
                  "v"(lab0), "v"(kg));
-    // then zero the padded activation images (P1H | DC2 | DC2H | DC1 are contiguous)
-    constexpr int NZ = (S_COFF - S_P1H) / 16;
-    uint4* z = reinterpret_cast<uint4*>(ACT(S_P1H));
-    for (int i = t; i < NZ; i += 256) z[i] = make_uint4(0, 0, 0, 0);
   } else {
-    // waves 8-15: conv1's per-thread address tables, so stage 1 reads two 8-byte
-    // rows instead of redoing the index math
-    const int t = tid - 512;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int tt = t + h * 512, tw = tt >> 6, tl16 = tt & 15, tkq = (tt & 63) >> 4;
-      u16x4 xo = {0, 0, 0, 0}, ho = {0, 0, 0, 0};
-#pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        const int mt = min(tw + it * NW, 35);
-        const int m = mt * 16 + tl16;
-        const int p = m >> 2, q = m & 3;
-        xo[it] = (unsigned short)((2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1));
-        const int w = mt * 4 + tkq;  // pooled position py*12 + px
-        ho[it] = (unsigned short)((w / 12) * P1H_RP + (w % 12) * LD_P1H);
-      }
-      C1T[tt] = xo;
-      C1H[tt] = ho;
-    }
+    // waves 8-15 (otherwise idle here): conv1's address tables of all 1024 threads
+    conv1_tables(tid - 512);
+    conv1_tables(tid);
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
@@ -489,6 +487,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
     // then start the next sample's loads (consumed one sample later)
     STAMP(0);
+    if (wave >= 8) {
+      // idle waves: zero the HWC conv1 image.  conv1 writes channels 0-9 of each
+      // position at stage 1; channels 10-15 meet zero conv2 weights in the K sum, so
+      // they must hold finite values (zero), not whatever the LDS last held.  (DC2 /
+      // DC1 rows >= 20 / >= 10 only feed discarded output rows and need no init.)
+      constexpr int NZ = (S_DC2 - S_P1H) / 16;
+      uint4* z = reinterpret_cast<uint4*>(P1H);
+      for (int i = tid - 512; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
+    }
     // label of this sample: staged -> LDS (preamble), else the register pipeline
     const int t_lab = STAGED ? 0 : (s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63));
     {
@@ -614,6 +621,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     if (stage_next && wave >= 4 && wave < 8) {  // waves 4-7: they hold nrow
       px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid - 256, 195)];
       lab_next = a.labels[nrow];
+    }
+    if (wave >= 8) {
+      // idle waves: zero the dgrad input image (its 4-pixel border and channels 20-23
+      // are the convolution's zero padding; stage 5 writes the interior)
+      constexpr int NZ = (S_DC1 - S_DC2H) / 16;
+      uint4* z = reinterpret_cast<uint4*>(DC2H);
+      for (int i = tid - 512; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
     }
     if (wave < 4) {
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
