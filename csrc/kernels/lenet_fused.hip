@@ -1341,6 +1341,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
 #pragma unroll
     for (int r = 0; r < 4; ++r) pfc[wave * 256 + r * 64 + lane] = c[r];
     __syncthreads();
+    USTAMP(3);
     if (wave == 0) {
       float g[4];
 #pragma unroll

@@ -83,7 +83,7 @@ def main():
     nfc, nb = 88, 88 + 83  # blocks [0, 88) FC role (one tile each), [88, 171) CONV role
     t0 = st[:nb, 0].min()
     rel = (st - t0) * 0.01  # us
-    for role, sl, ks in [("CONV", slice(nfc, nb), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 4])]:
+    for role, sl, ks in [("CONV", slice(nfc, nb), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 3, 4])]:
         r = rel[sl]
         desc = "  ".join(f"s{k} med {r[:, k].median().item():.2f} max {r[:, k].max().item():.2f}" for k in ks)
         print(f"stamps {role}: {desc}")
