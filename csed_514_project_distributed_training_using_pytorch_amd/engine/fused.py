@@ -37,7 +37,7 @@ from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
 from ..parallel.comm import DistContext
-from ..parallel.ipc import allreduce_mode, make_allreduce, open_exchange
+from ..parallel.ipc import allreduce_mode, make_allreduce, open_exchange, wait_timeout_s
 from ..utils.flat import FlatParams
 
 
@@ -123,7 +123,7 @@ class FusedLeNetTrainer:
         # (csrc/comm) when every rank passes its self-test, else RCCL (parallel/ipc.py).
         # Preferred: the exchange fused into lenet_update (1 kernel), see module docstring.
         self.exch = None
-        self.exch_timeout_s = 2.0
+        self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"

@@ -60,12 +60,12 @@ class IpcAllReduce:
     all-gather of the handles), :meth:`open` (local).  Use :func:`make_allreduce`.
     """
 
-    def __init__(self, ctx: DistContext, n: int, blocks: int = 32, timeout_s: float = 2.0):
+    def __init__(self, ctx: DistContext, n: int, blocks: int = 32, timeout_s: float | None = None):
         self.ctx = ctx
         self.n = int(n)
         self.n_pad = (self.n + 3) // 4 * 4
         self.blocks = int(blocks)
-        self.timeout_s = float(timeout_s)
+        self.timeout_s = float(timeout_s if timeout_s is not None else wait_timeout_s())
         self.id = -1
         self.measured_us: dict | None = None
         self._pad_in = self._pad_out = None
@@ -132,6 +132,13 @@ class IpcAllReduce:
         except Exception:
             ok = False
         return ok
+
+
+def wait_timeout_s() -> float:
+    """Wall-clock bound of every peer wait inside the exchange kernels (``CSED_IPC_TIMEOUT_S``,
+    default 2 s): on expiry a kernel raises the comm error word and finishes instead of
+    hanging the GPU."""
+    return float(os.environ.get("CSED_IPC_TIMEOUT_S", "2.0"))
 
 
 def allreduce_mode() -> str:

@@ -1012,7 +1012,7 @@ __global__ void lenet_pack_kernel(const float* __restrict__ params, unsigned sho
 // export it (DDP: the RCCL all-reduce runs next) or apply SGD + refresh the
 // 16-bit weight images.  Two block roles in one launch:
 //
-//   role CONV (blocks [NB_FC, NB_UPDATE)): fixed-order reduction of the per-WG conv
+//   role CONV (blocks [fc_blocks(B), +NB_CONV)): fixed-order reduction of the per-WG conv
 //     slabs, 16 float4 columns x 32 slices per block so every CU pulls only a
 //     few KB with all loads in flight (latency-, not bandwidth-bound).  Block 0
 //     also folds the loss partials and bumps the device counters.
@@ -1032,7 +1032,14 @@ constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
 constexpr int CNQ = CNP / 4;                        // conv float4 columns (1320)
 constexpr int NB_CONV = (CNQ + UP_C - 1) / UP_C;    // 83
 constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
-constexpr int NB_FC = FC_TILES;                     // 88 blocks, one tile each
+// FC role: wpt waves per tile (K split over them), 8 / wpt tiles per block.  A
+// small batch uses one wave per tile (no combine, no barrier: the tile's K is one
+// or two 64-sample chunks); a large batch streams K over 8 waves.
+__host__ __device__ constexpr int fc_waves_per_tile(int B) {
+  return B <= 128 ? 1 : (B <= 256 ? 2 : (B <= 512 ? 4 : 8));
+}
+__host__ __device__ constexpr int fc_blocks(int B) { return FC_TILES / (8 / fc_waves_per_tile(B)); }
+constexpr int NB_FC = FC_TILES;                     // FC blocks at most (one tile each)
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
@@ -1198,10 +1205,11 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
 
-  if (blk >= NB_FC) {
+  const int nb_fc = fc_blocks(B);
+  if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first)
-    const int cblk = blk - NB_FC;
+    const int cblk = blk - nb_fc;
     const int cl = tid & (UP_C - 1), sl = tid / UP_C;
     // wave 0 owns params cblk*64 + tid (16 float4 columns): prefetch p / m now
     const int pi = cblk * (UP_C * 4) + tid;
@@ -1263,15 +1271,17 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       }
     }
   } else {
-    // ---------------- role FC: one 16x16 tile of [dW | db] per block, K split over waves
+    // ---------------- role FC: 16x16 tiles of [dW | db], K split over wpt waves per tile
     const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
-    const int tile = blk;
+    const int wpt = fc_waves_per_tile(B);
+    const int tile = blk * (UP_NT / 64 / wpt) + wave / wpt, sub = wave % wpt;
     const bool fc1 = tile < FC1_TILES;
     const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
     const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
     const int a_off = fc1 ? V_DZ1 : V_DLOG, b_off = fc1 ? V_P2 : V_H;
     const int o = mt * 16 + l16, i = nt * 16 + l16;  // A row (out feature) / B col (in feature)
-    // wave 0 finishes the tile: this lane's 4 outputs (C rows 4*kq + r, column i), their p / m
+    // the tile's first wave (sub 0) finishes it: this lane's 4 outputs (C rows 4*kq + r,
+    // column i), their p / m
     int pidx[4];
     float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1281,7 +1291,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
                     ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
                            : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
                     : -1;
-      if (a.apply_sgd && wave == 0) {
+      if (a.apply_sgd && sub == 0) {
         pp[r] = a.params[max(pidx[r], 0)];
         pm[r] = a.momentum[max(pidx[r], 0)];
       }
@@ -1295,8 +1305,8 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       if (pidx[r] < 0) fd[r] = -1;
     }
     // this wave's samples [k0, k1): a multiple-of-4 share of the batch
-    const int kw = ((B + UP_NT / 64 - 1) / (UP_NT / 64) + 3) & ~3;
-    const int k0 = min(B, wave * kw), k1 = min(B, k0 + kw);
+    const int kw = ((B + wpt - 1) / wpt + 3) & ~3;
+    const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
     // K = samples; 16x16x4 f32 MFMA: lane holds A[o][s0 + 4u + kq] and B[s0 + 4u + kq][i]
     auto load = [&](int s0, float (&av)[16], float (&bv)[16]) {
 #pragma unroll
@@ -1336,19 +1346,25 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       }
     }
     USTAMP(2);
-    // fixed-order combine of the 8 wave partials (reuses the CONV role's LDS)
+    // Retire the p / m prefetch now: after the first finish_param's stores, hipcc would
+    // wait for them with vmcnt(0), i.e. for those stores too (one store round trip per
+    // output, four in a row).
+    asm volatile("" ::"v"(pp[0]), "v"(pp[1]), "v"(pp[2]), "v"(pp[3]), "v"(pm[0]), "v"(pm[1]), "v"(pm[2]),
+                 "v"(pm[3]));
+    // fixed-order combine of the tile's wpt partials (reuses the CONV role's LDS)
     float* pfc = reinterpret_cast<float*>(&part[0][0]);
+    if (wpt > 1) {  // uniform
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pfc[wave * 256 + r * 64 + lane] = c[r];
-    __syncthreads();
+      for (int r = 0; r < 4; ++r) pfc[wave * 256 + r * 64 + lane] = c[r];
+      __syncthreads();
+    }
     USTAMP(3);
-    if (wave == 0) {
+    if (sub == 0) {
       float g[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = pfc[r * 64 + lane];
-#pragma unroll
-        for (int w = 1; w < UP_NT / 64; ++w) v += pfc[w * 256 + r * 64 + lane];
+        float v = c[r];
+        for (int w = 1; w < wpt; ++w) v += pfc[(wave + w) * 256 + r * 64 + lane];
         g[r] = v;
       }
       if (EXCH) {
@@ -1463,6 +1479,7 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     return hipGetLastError();
   }
   if (!a.vslab || a.B <= 0) return hipErrorInvalidValue;
+  const int nblocks = fc_blocks(a.B) + NB_CONV;
   comm::IpcPeers px{};
   if (a.exch_id >= 0) {
     // fused data-parallel exchange: the buffer must hold this kernel's word layout
@@ -1472,13 +1489,13 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
     CSED_DISPATCH_MFMA(a.mfma_dtype, {
-      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
                          a.B, loss_parts, nparts, loss_acc, px, ticks);
     });
     return hipGetLastError();
   }
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
-    hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+    hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
                        a.B, loss_parts, nparts, loss_acc, px, (uint64_t)0);
   });
   return hipGetLastError();

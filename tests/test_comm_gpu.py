@@ -23,7 +23,11 @@ def _free_port() -> int:
 
 def _worker(rank, world, port, q):
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CSED_ALLREDUCE="ipc")
+        # two processes share one GPU here, and how the GPU interleaves their queues is
+        # not ours to control: give the peer waits a generous bound (the kernels still
+        # report a timeout through the error word, checked below)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CSED_ALLREDUCE="ipc",
+                          CSED_IPC_TIMEOUT_S="30")
         import torch.distributed as dist
 
         from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import DistContext
@@ -126,8 +130,8 @@ def test_ipc_allreduce_two_ranks_one_gpu():
     for r in range(2):
         res = results[r]
         assert "exception" not in res, res
+        assert res["errors"] == 0, res  # first: a timed-out wait explains any mismatch below
         assert res["enabled"] and res["eager"] and res["graph"], res
-        assert res["errors"] == 0, res
         for mode, kind in (("ipc", "ipc-oneshot"), ("fused", "fused-ipc")):
             assert res[f"kind_{mode}"] == kind, res
             assert res[f"params_equal_{mode}"] and res[f"finite_{mode}"], res

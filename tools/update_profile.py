@@ -80,7 +80,9 @@ def main():
                          eng.grid, eng.loss_acc, eng.mfma, dbg)
         torch.cuda.synchronize()
     st = dbg.view(256, 8).cpu().double()
-    nfc, nb = 88, 88 + 83  # blocks [0, 88) FC role (one tile each), [88, 171) CONV role
+    wpt = 1 if B <= 128 else (2 if B <= 256 else (4 if B <= 512 else 8))  # fc_waves_per_tile
+    nfc = 88 // (8 // wpt)  # blocks [0, nfc) FC role, then 83 CONV role blocks
+    nb = nfc + 83
     t0 = st[:nb, 0].min()
     rel = (st - t0) * 0.01  # us
     for role, sl, ks in [("CONV", slice(nfc, nb), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 3, 4])]:
