@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--gloo", action="store_true")
     ap.add_argument("--global-batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--no-time-steps", action="store_true", help="skip engine._time_steps (bench.py's order)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
@@ -51,7 +52,7 @@ def main():
         smp = ShardSampler(len(data), world, rank, shuffle=True, seed=42)
         smp.set_epoch(0)
         eng.set_epoch_order(smp.indices())
-        us = eng._time_steps(nsteps=args.steps, reps=10)
+        us = float("nan") if args.no_time_steps else eng._time_steps(nsteps=args.steps, reps=10)
         # the same steps the way bench.py runs them: cached graphs, wall clock
         eng.prepare(args.steps)
         eng.run_steps(4 * args.steps, args.steps)
