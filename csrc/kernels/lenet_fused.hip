@@ -168,7 +168,10 @@ constexpr int S_LABEL = S_W1C + 16 * 32 * 2;          // i32 [4]   staged sample
 constexpr int S_DBG = S_LABEL + 16;                   // u64 [32]  stage stamps (diagnostics)
 constexpr int S_C1T = S_DBG + 32 * 8;                 // u16 [1024][4] conv1 per-thread X offsets (tiles 0..2)
 constexpr int S_C1H = S_C1T + 1024 * 8;               // u16 [1024][4] conv1 per-thread P1H offsets
-constexpr int S_TOTAL = S_C1H + 1024 * 8;
+constexpr int S_XC = S_C1H + 1024 * 8;                // u16 3 x [800]  X shifted by 1, 2, 3 elements
+constexpr int XC_LD = 800;
+constexpr int S_CONSTB = S_XC + 3 * XC_LD * 2;         // u16 [16]   8 zeros, 8 ones (wgrad bias / padding columns)
+constexpr int S_TOTAL = S_CONSTB + 16 * 2;
 static_assert(S_W2D % 16 == 0 && S_F1 % 16 == 0 && S_X % 16 == 0 && S_P1 % 16 == 0 && S_I1 % 16 == 0, "align");
 static_assert(S_P2 % 16 == 0 && S_I2 % 16 == 0 && S_P1H % 16 == 0 && S_DC2 % 16 == 0 && S_DC2H % 16 == 0, "align");
 static_assert(S_DC1 % 16 == 0 && S_COFF % 16 == 0 && S_DOFF % 16 == 0 && S_DZ1B % 16 == 0, "align");
@@ -306,6 +309,16 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   uint64_t* DBGS = (uint64_t*)ACT(S_DBG);
   u16x4* C1T = (u16x4*)ACT(S_C1T);
   u16x4* C1H = (u16x4*)ACT(S_C1H);
+  unsigned short* XC = (unsigned short*)ACT(S_XC);
+  unsigned short* CONSTB = (unsigned short*)ACT(S_CONSTB);
+  // Pixels X[e .. e+7] as an aligned run: copy c = e & 3 holds X shifted by c (X_c[m] =
+  // X[m + c]), so X[e + j] = X_c[e - c + j] with e - c a multiple of 4 (8-byte aligned).
+  auto xrun = [&](int e) -> const unsigned short* {
+    const int c = e & 3;
+    return (c == 0 ? Xs : XC + (c - 1) * XC_LD) + (e - c);
+  };
+  // normalised pixels X[4q .. 4q+3] (the shifted copies are made at stage 3)
+  auto put_x = [&](int q, const u16x4& o) { *reinterpret_cast<u16x4*>(Xs + 4 * q) = o; };
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
@@ -429,7 +442,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           o[j] = h16<T>(((float)((px0 >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std);
-        *reinterpret_cast<u16x4*>(Xs + 4 * t) = o;
+        put_x(t, o);
       }
       if (t == 0) LABEL[0] = lab0;
     }
@@ -443,6 +456,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // waves 8-15 (otherwise idle here): conv1's address tables of all 1024 threads
     conv1_tables(tid - 512);
     conv1_tables(tid);
+    if (tid - 512 < 16) CONSTB[tid - 512] = tid - 512 < 8 ? (unsigned short)0 : h16<T>(1.f);
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
@@ -504,7 +518,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           o[j] = h16<T>(((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std);
-        *reinterpret_cast<u16x4*>(Xs + 4 * tid) = o;
+        put_x(tid, o);
       }
       if (tid < 70) {
         float sc = 1.f;
@@ -624,10 +638,17 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
     if (wave >= 8) {
       // idle waves: zero the dgrad input image (its 4-pixel border and channels 20-23
-      // are the convolution's zero padding; stage 5 writes the interior)
+      // are the convolution's zero padding; stage 5 writes the interior), and make the
+      // shifted copies of X that conv1 wgrad reads as aligned runs (stage 8)
       constexpr int NZ = (S_DC1 - S_DC2H) / 16;
       uint4* z = reinterpret_cast<uint4*>(DC2H);
       for (int i = tid - 512; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
+      for (int m = tid - 512; m < 784; m += 512) {
+        const unsigned short v = Xs[m];
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+          if (m - k >= 0) XC[(k - 1) * XC_LD + m - k] = v;
+      }
     }
     if (wave < 4) {
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
@@ -878,26 +899,23 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // (tile wave&1, K-steps ps = (wave>>1) + 8i: 18 steps over 8 wave pairs)
     STAMP(8);
     {
-      const unsigned short cst = kc1 == 25 ? h16<T>(1.f) : (unsigned short)0;
-      frag fa[3];
-      u16x8 raw[3];
+      // B fragment = X[base + 0..7] (one output row run of 8 pixels), two aligned b64
+      // reads from the shifted copy; columns past the 25 taps read a constant run instead
+      // (ones for the bias column 25, zeros beyond), so nothing is masked per element
+      frag fa[3], fbv[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int ps = min((wave >> 1) + 8 * i, 17);
         const int p0 = ps * 32 + kb;
         fa[i] = *reinterpret_cast<const frag*>(DC1 + l16 * LD_DC1 + p0);
         const int oh = p0 / 24, ow0 = p0 - oh * 24;
-        const int base = oh * 28 + ow0 + koffc1;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) raw[i][j] = Xs[opaque(base + j)];
+        const unsigned short* src = kc1 < 25 ? xrun(oh * 28 + ow0 + koffc1) : CONSTB + (kc1 == 25 ? 8 : 0);
+        const uint2 lo = reinterpret_cast<const uint2*>(src)[0], hi = reinterpret_cast<const uint2*>(src)[1];
+        fbv[i] = __builtin_bit_cast(frag, uint4{lo.x, lo.y, hi.x, hi.y});
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        u16x8 rv = raw[i];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rv[j] = kc1 < 25 ? rv[j] : cst;
-        if ((wave >> 1) + 8 * i < 18) acc_c1 = Mfma<T>::mma(fa[i], __builtin_bit_cast(frag, rv), acc_c1);
-      }
+      for (int i = 0; i < 3; ++i)
+        if ((wave >> 1) + 8 * i < 18) acc_c1 = Mfma<T>::mma(fa[i], fbv[i], acc_c1);
     }
     STAMP(14);
   };
