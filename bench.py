@@ -150,7 +150,7 @@ def main() -> int:
                        "engine": "fused HIP (lenet_train + lenet_update"
                                  + {"fused-ipc": " with in-kernel xGMI gradient exchange", "none": ""}.get(
                                      eng.allreduce_kind, " + gradient all-reduce") + ")", "hip_graph": (not args.no_graph) and bool(eng.capture_comm_ok),
-                       "allreduce": eng.allreduce_kind},
+                       "allreduce": eng.allreduce_kind, "step": eng.step_kind},
             "epoch_s": round(epoch_s, 4) if epoch_s is not None else None,
             "baseline_epoch_s": base,
             "train_loss_timed_rank0": round(loss_sum / max(1, args.steps * eng.B), 4),

@@ -28,6 +28,7 @@ through the op library, ``state_dict()``) without copies.
 from __future__ import annotations
 
 import math
+import os
 import sys
 
 import torch
@@ -47,9 +48,14 @@ def layout() -> tuple[int, int, int, int]:
     16-bit weight-image elements (I_END), conv slab row per workgroup (CNP_PAD: conv1.w/b +
     conv2.w/b = 5280 floats in 64-float chunks), per-sample fc vector length (VEC) and the
     largest per-rank batch that uses batch staging (STAGE_MAXB)."""
-    wimg, conv, vec, nparams, stage_max, _exch = (int(v) for v in torch.ops.csed.lenet_layout())
+    wimg, conv, vec, nparams, stage_max, _exch, _fmax, _bar = (int(v) for v in torch.ops.csed.lenet_layout())
     assert nparams == N_PARAMS
     return wimg, conv, vec, stage_max
+
+
+def fused_max_batch() -> int:
+    """Largest per-rank batch of the one-kernel step (csed::lenet_step)."""
+    return int(torch.ops.csed.lenet_layout()[6])
 
 
 def exch_words() -> int:
@@ -116,6 +122,13 @@ class FusedLeNetTrainer:
         self.staged = self.B <= stage_max and self.grid == self.B
         self.xstage = torch.zeros((self.B, 784), dtype=torch.uint8, device=dev) if self.staged else None
         self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
+        # one-kernel step (csed::lenet_step): training workgroups + trailing update
+        # workgroups that wait on a device counter, instead of two launches.  bar:
+        # its synchronisation words ([2] != 0: a timed-out wait); CSED_ONE_KERNEL_STEP=0
+        # keeps two kernels.
+        self.one_kernel = (self.staged and self.B <= fused_max_batch()
+                           and os.environ.get("CSED_ONE_KERNEL_STEP", "1") != "0")
+        self.bar = torch.zeros(int(torch.ops.csed.lenet_layout()[7]), dtype=torch.int32, device=dev)
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.capture_comm_ok: bool | None = None
@@ -237,6 +250,7 @@ class FusedLeNetTrainer:
     def comm_errors(self) -> int:
         """Nonzero if an IPC exchange ever timed out waiting for a peer (synchronous)."""
         e = self.exch.error() if self.exch is not None else 0
+        e |= int(self.bar[2].item())  # a one-kernel step's update workgroups timed out
         return e | (self.allreduce.error() if self.allreduce is not None else 0)
 
     def _max_grid(self) -> int:
@@ -269,6 +283,13 @@ class FusedLeNetTrainer:
 
 
 
+    @property
+    def step_kind(self) -> str:
+        """How a full (staged) training step is launched."""
+        if self.one_kernel and (not self.comm or self.exch is not None):
+            return "one kernel (lenet_step)"
+        return "two kernels" if (not self.comm or self.exch is not None) else "update split around an all-reduce"
+
     def steps_per_epoch(self) -> int:
         return math.ceil(self.perm.numel() / self.B)
 
@@ -281,6 +302,14 @@ class FusedLeNetTrainer:
         ops = torch.ops.csed
         # full steps read the staged batch and stage the next one; the epoch's short tail uses perm
         st = self.staged and cursor is not None
+        if st and self.one_kernel and (not self.comm or self.exch is not None):
+            ops.lenet_step(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
+                           self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
+                           self.drop_p, self.seed, self.rng_offset, self.mfma, self.xstage, self.lstage,
+                           self.momentum_buf, self.lr, self.momentum, self.dampening, self.weight_decay,
+                           self.nesterov, self.step_count, self.ticket, self.loss_acc, self.bar, None, None,
+                           self.exch.id if self.exch is not None else -1, self.exch_timeout_s)
+            return
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
                         self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
                         self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,

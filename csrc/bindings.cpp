@@ -287,7 +287,8 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 // largest per-rank batch the batch-staging path handles].
 std::vector<int64_t> lenet_layout() {
   return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
-          csed::lenet_param_count(), csed::lenet_stage_max_batch(), csed::lenet_exch_words()};
+          csed::lenet_param_count(), csed::lenet_stage_max_batch(), csed::lenet_exch_words(),
+          csed::lenet_fused_max_batch(), csed::lenet_step_bar_ints()};
 }
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
@@ -299,13 +300,13 @@ void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
                                     cur_stream(params)));
 }
 
-void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm, const optional<Tensor>& cursor,
-                 int64_t B, int64_t rank, const Tensor& wimg, const Tensor& params, Tensor& slab, Tensor& vslab,
-                 Tensor& loss_parts,
-                 double grad_scale, double mean, double std_, double drop_p, int64_t seed,
-                 const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
-                 const optional<Tensor>& dbg, const optional<Tensor>& xstage, const optional<Tensor>& lstage,
-                 bool stage_next) {
+csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, const Tensor& perm,
+                                const optional<Tensor>& cursor, int64_t B, int64_t rank, const Tensor& wimg,
+                                const Tensor& params, Tensor& slab, Tensor& vslab, Tensor& loss_parts,
+                                double grad_scale, double mean, double std_, double drop_p, int64_t seed,
+                                const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
+                                const optional<Tensor>& dbg, const optional<Tensor>& xstage,
+                                const optional<Tensor>& lstage, bool stage_next) {
   dev(images, "images"); dev(labels, "labels"); dev(perm, "perm"); dev(wimg, "wimg"); dev(params, "params");
   dev(slab, "slab"); dev(vslab, "vslab"); dev(loss_parts, "loss_parts");
   TORCH_CHECK(images.scalar_type() == at::kByte && images.numel() == images.size(0) * 784, "images: uint8 [N,28,28]");
@@ -316,7 +317,6 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
   TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_train: vslab [B, 464] too small");
   if (!cursor.has_value()) TORCH_CHECK(perm.numel() >= B, "perm shorter than the batch");
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0);
-  const c10::DeviceGuard gd(images.device());
   csed::LenetTrainArgs a{};
   a.images = images.data_ptr<uint8_t>(); a.labels = labels.data_ptr<int64_t>(); a.perm = perm.data_ptr<int64_t>();
   a.cursor = optpt<int64_t>(cursor); a.perm_len = perm.numel(); a.B = (int)B; a.rank_stride = (int)rank;
@@ -340,6 +340,20 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
       a.stage_next = 1;
     }
   }
+  return a;
+}
+
+void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm, const optional<Tensor>& cursor,
+                 int64_t B, int64_t rank, const Tensor& wimg, const Tensor& params, Tensor& slab, Tensor& vslab,
+                 Tensor& loss_parts,
+                 double grad_scale, double mean, double std_, double drop_p, int64_t seed,
+                 const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
+                 const optional<Tensor>& dbg, const optional<Tensor>& xstage, const optional<Tensor>& lstage,
+                 bool stage_next) {
+  const c10::DeviceGuard gd(images.device());
+  const csed::LenetTrainArgs a = train_args(images, labels, perm, cursor, B, rank, wimg, params, slab, vslab,
+                                            loss_parts, grad_scale, mean, std_, drop_p, seed, rng_offset, grid,
+                                            mfma_dtype, dbg, xstage, lstage, stage_next);
   CHECK_HIP(csed::launch_lenet_train(a, cur_stream(images)));
 }
 
@@ -369,18 +383,19 @@ void lenet_stage(const Tensor& images, const Tensor& labels, const Tensor& perm,
                                      cursor.data_ptr<int64_t>(), cur_stream(images)));
 }
 
-void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t B, const optional<Tensor>& grad_in, const optional<Tensor>& grad_out,
-                  Tensor& params, Tensor& momentum, Tensor& wimg, double lr, double mom, double dampening,
-                  double weight_decay, bool nesterov, Tensor& step, Tensor& ticket, const optional<Tensor>& cursor,
-                  const optional<Tensor>& rng_offset, bool apply_sgd, const optional<Tensor>& loss_parts,
-                  int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg,
-                  int64_t exch_id, double exch_timeout_s) {
+csed::LenetUpdateArgs update_args(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t B,
+                                  const optional<Tensor>& grad_in, const optional<Tensor>& grad_out, Tensor& params,
+                                  Tensor& momentum, Tensor& wimg, double lr, double mom, double dampening,
+                                  double weight_decay, bool nesterov, Tensor& step, Tensor& ticket,
+                                  const optional<Tensor>& cursor, const optional<Tensor>& rng_offset, bool apply_sgd,
+                                  const optional<Tensor>& loss_parts, const optional<Tensor>& loss_acc,
+                                  int64_t mfma_dtype, const optional<Tensor>& dbg, int64_t exch_id,
+                                  double exch_timeout_s) {
   dev(slab, "slab"); dev(params, "params"); dev(momentum, "momentum"); dev(wimg, "wimg");
   TORCH_CHECK(params.numel() == csed::lenet_param_count() && momentum.numel() == params.numel(),
               "lenet_update: params / momentum must hold the 21840 flat LeNet parameters");
   TORCH_CHECK(apply_sgd || grad_out.has_value(), "lenet_update: reduce-only mode needs grad_out");
   TORCH_CHECK(loss_parts.has_value() == loss_acc.has_value());
-  const c10::DeviceGuard gd(params.device());
   csed::LenetUpdateArgs a{};
   a.slab = slab.data_ptr<float>(); a.grid = (int)grid;
   a.vslab = vslab.data_ptr<float>(); a.B = (int)B;
@@ -398,9 +413,46 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
   // exch_id >= 0: csrc/comm buffer of the fused gradient exchange (checked by the launcher)
   TORCH_CHECK(exch_id < 0 || !a.grad_in, "lenet_update: the fused exchange reduces the slabs itself (no grad_in)");
   a.exch_id = (int)exch_id; a.exch_timeout_s = exch_timeout_s;
+  return a;
+}
 
+void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t B, const optional<Tensor>& grad_in, const optional<Tensor>& grad_out,
+                  Tensor& params, Tensor& momentum, Tensor& wimg, double lr, double mom, double dampening,
+                  double weight_decay, bool nesterov, Tensor& step, Tensor& ticket, const optional<Tensor>& cursor,
+                  const optional<Tensor>& rng_offset, bool apply_sgd, const optional<Tensor>& loss_parts,
+                  int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg,
+                  int64_t exch_id, double exch_timeout_s) {
+  const c10::DeviceGuard gd(params.device());
+  const csed::LenetUpdateArgs a =
+      update_args(slab, grid, vslab, B, grad_in, grad_out, params, momentum, wimg, lr, mom, dampening, weight_decay,
+                  nesterov, step, ticket, cursor, rng_offset, apply_sgd, loss_parts, loss_acc, mfma_dtype, dbg,
+                  exch_id, exch_timeout_s);
   CHECK_HIP(csed::launch_lenet_update(a, optpt<float>(loss_parts), (int)nparts, optpt<float>(loss_acc),
                                       cur_stream(params)));
+}
+
+// One-kernel training step on a staged batch (csed::launch_lenet_step): lenet_train
+// with stage_next, then lenet_update with SGD, in one launch.
+void lenet_step(const Tensor& images, const Tensor& labels, const Tensor& perm, Tensor& cursor, int64_t B,
+                int64_t rank, Tensor& wimg, Tensor& params, Tensor& slab, Tensor& vslab, Tensor& loss_parts,
+                double grad_scale, double mean, double std_, double drop_p, int64_t seed, Tensor& rng_offset,
+                int64_t mfma_dtype, Tensor& xstage, Tensor& lstage, Tensor& momentum, double lr, double mom,
+                double dampening, double weight_decay, bool nesterov, Tensor& step, Tensor& ticket,
+                Tensor& loss_acc, Tensor& bar, const optional<Tensor>& dbg, const optional<Tensor>& udbg,
+                int64_t exch_id, double exch_timeout_s) {
+  dev(bar, "bar");
+  TORCH_CHECK(bar.scalar_type() == at::kInt && bar.numel() >= csed::lenet_step_bar_ints(),
+              "lenet_step: bar must be int32[", csed::lenet_step_bar_ints(), "]");
+  const c10::DeviceGuard gd(images.device());
+  const csed::LenetTrainArgs t = train_args(images, labels, perm, cursor, B, rank, wimg, params, slab, vslab,
+                                            loss_parts, grad_scale, mean, std_, drop_p, seed, rng_offset, B,
+                                            mfma_dtype, dbg, xstage, lstage, true);
+  const csed::LenetUpdateArgs u =
+      update_args(slab, B, vslab, B, c10::nullopt, c10::nullopt, params, momentum, wimg, lr, mom, dampening,
+                  weight_decay, nesterov, step, ticket, cursor, rng_offset, true, loss_parts, loss_acc, mfma_dtype,
+                  udbg, exch_id, exch_timeout_s);
+  CHECK_HIP(csed::launch_lenet_step(t, u, loss_parts.data_ptr<float>(), (int)B, loss_acc.data_ptr<float>(),
+                                    bar.data_ptr<int>(), cur_stream(images)));
 }
 
 void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order, int64_t n, const Tensor& wimg,
@@ -432,6 +484,12 @@ TORCH_LIBRARY(csed, m) {
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
         "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
         "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
+  m.def("lenet_step(Tensor images, Tensor labels, Tensor perm, Tensor(a!) cursor, int B, int rank, Tensor(b!) wimg, "
+        "Tensor(c!) params, Tensor(d!) slab, Tensor(e!) vslab, Tensor(f!) loss_parts, float grad_scale, float mean, "
+        "float std, float drop_p, int seed, Tensor(g!) rng_offset, int mfma_dtype, Tensor(h!) xstage, "
+        "Tensor(i!) lstage, Tensor(j!) momentum, float lr, float mom, float dampening, float weight_decay, "
+        "bool nesterov, Tensor(k!) step, Tensor(l!) ticket, Tensor(m!) loss_acc, Tensor(n!) bar, "
+        "Tensor(o!)? dbg=None, Tensor(p!)? udbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
         "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "
@@ -479,6 +537,7 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);
   m.impl("lenet_update", &lenet_update);
+  m.impl("lenet_step", &lenet_step);
   m.impl("lenet_stage", &lenet_stage);
   m.impl("lenet_eval", &lenet_eval);
 }

@@ -276,8 +276,83 @@ __device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned sh
 // no code of the multi-sample pixel pipeline: its branches would merge register
 // state into the staged path and make hipcc wait for loads (and so for the LDS
 // DMA) that the staged path never issued.
-template <typename T, bool TRAIN, bool STAGED>
-__global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
+// One-kernel training step (FUSE > 0): workgroups [0, a.grid) train as below, then
+// signal a device counter; workgroups [a.grid, a.grid + nupd) run lenet_update's roles
+// (update_role) once every training workgroup has signalled.  The update workgroups
+// come after the training ones in dispatch order and training never waits on them,
+// so the step cannot deadlock whatever the occupancy; they load their parameters and
+// momenta while training runs, and the kernel boundary between the two phases is
+// gone.  FUSE = 2 adds the in-kernel data-parallel exchange.
+// lenet_update workgroup shape (see the update kernel below)
+constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
+
+// Cross-XCD hand-off of the fused step without cache maintenance: the training
+// workgroups write their outputs with device-coherent stores (global_store sc1,
+// written through to memory) and the update workgroups read them with
+// device-coherent loads (sc1), so neither side needs an L2 write-back or
+// invalidate (buffer_wbl2 / buffer_inv walk the whole 4 MB L2 of the XCD).
+template <bool C>
+__device__ __forceinline__ void st_c(float* p, float v) {
+  if (C) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool C>
+__device__ __forceinline__ float ld_c(const float* p) {
+  if (C) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <bool C>
+__device__ __forceinline__ float4 ld4_c(const float4* p) {
+  if (C) {
+    uint64_t* q = reinterpret_cast<uint64_t*>(const_cast<float4*>(p));
+    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
+                       __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
+  }
+  return *p;
+}
+
+// Fused-step synchronisation words (int32, zero-initialised, one 128-byte line each
+// where polled).  The training workgroups count themselves in BAR_CNT; the last one
+// re-arms BAR_CNT and raises every update workgroup's own go flag (BAR_GO + 32*blk),
+// so each update workgroup polls a line of its own (94 pollers on one address queue
+// behind each other at the memory side: ~4 us); the update workgroup clears its flag
+// once seen.  Nothing is read back at the end of the launch (a re-arm that needs an
+// atomic's return value there costs ~1.5 us on the critical path).
+constexpr int BAR_CNT = 0, BAR_ERR = 2, BAR_GO = 32;
+constexpr int BAR_INTS = BAR_GO + 32 * 256;
+__device__ __forceinline__ int sys_load(const int* p) {
+  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct StepFuse {
+  LenetUpdateArgs u;
+  float* loss_parts;
+  int nparts;
+  float* loss_acc;
+  comm::IpcPeers px;
+  uint64_t timeout_ticks;
+  int* bar;  // BAR_INTS synchronisation words (BAR_ERR != 0: a wait timed out)
+  int nupd;  // update workgroups
+};
+
+// FUSED_MAXB: the fused step's batch limit -- one 64-sample chunk per fc wave, so the
+// update role fits the training kernel's 128 VGPRs (no second load buffer).  With
+// FUSED, update_role also reads the training outputs with device-coherent loads.
+constexpr int FUSED_MAXB = 64;
+constexpr int UPD_NTH = 512;  // threads of a fused-step update role (UP_NT or NT)
+template <typename T, bool EXCH, bool FUSED, int NTH>
+__device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
+                            int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
+                            int nblk, int tid, float4* part, float* part2, const int* ready, int nready);
+
+template <typename T, bool TRAIN, bool STAGED, int FUSE>
+__global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out,
+                                                            StepFuse fz) {
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
   // per-sample activations (dynamic).  Being distinct objects, accesses to the
   // activations are provably disjoint from the in-flight DMA, so the compiler's
@@ -328,8 +403,24 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (FUSE && (int)blockIdx.x >= a.grid) {
+    // update workgroup: lenet_update's roles on waves 0-7; the others end here (a
+    // barrier waits only for the waves that have not ended).  More, smaller update
+    // workgroups: the update phase is bound by per-CU load issue (UPD_NTH = NT was
+    // ~0.5 us slower per step).
+    if (tid >= UPD_NTH) return;
+    update_role<T, FUSE == 2, true, UPD_NTH>(fz.u, fz.u.vslab, fz.u.B, fz.loss_parts, fz.nparts, fz.loss_acc,
+                                             fz.px, fz.timeout_ticks, blockIdx.x - a.grid, fz.nupd, tid,
+                                             reinterpret_cast<float4*>(dsm),
+                                             reinterpret_cast<float*>(dsm + (UPD_NTH / UP_NT) * UP_S * UP_C * 16),
+                                             fz.bar, a.grid);
+    return;
+  }
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
-  const int G = gridDim.x, g = blockIdx.x;
+  const int G = FUSE ? a.grid : (int)gridDim.x, g = blockIdx.x;
+  // fused-step timeline (diagnostics): wall-clock start / signal of training workgroup g
+  // at udbg[(nupd + g) * 8 + 0 / 1], next to the update workgroups' stamps
+  if (FUSE && fz.u.dbg && tid == 0) fz.u.dbg[(fz.nupd + g) * 8] = __builtin_amdgcn_s_memrealtime();
   const float inv_std = 1.f / a.std_;
   const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
@@ -338,7 +429,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
   auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
-  if (a.dbg && tid == 0) DBGS[12] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && tid == 0) {
+    DBGS[12] = __builtin_amdgcn_s_memtime();
+    DBGS[22] = __builtin_amdgcn_s_memrealtime();  // wall clock (100 MHz), comparable across kernels
+  }
   // ---------------- once per workgroup: weight images, offset tables, fp32 params -> LDS
   // sample pipeline registers (non-staged batches): this sample's 4 pixels per
   // thread and label, the row indices of the next 64 samples (lane s) and their labels
@@ -625,7 +719,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
         P2[oc * 16 + w] = hv;
         I2[oc * 16 + w] = (uint8_t)bi;
-        if (TRAIN) vs[V_P2 + oc * 16 + w] = f16v<T>(hv);  // fc1 input, exactly as the forward used it
+        if (TRAIN) st_c<FUSE != 0>(vs + V_P2 + oc * 16 + w, f16v<T>(hv));  // fc1 input, exactly as the forward used it
       }
     }
     __syncthreads();
@@ -666,7 +760,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (o < 50) {
           const float h = fmaxf(c[0] + PAR[P_F1B + o], 0.f) * D1S[o];
           Hs[o] = h;
-          if (TRAIN) vs[V_H + o] = h;
+          if (TRAIN) st_c<FUSE != 0>(vs + V_H + o, h);
         }
       }
     }
@@ -731,7 +825,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           float mine = 0.f;
 #pragma unroll
           for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
-          vs[V_DLOG + lane] = mine;
+          st_c<FUSE != 0>(vs + V_DLOG + lane, mine);
         }
         // dZ1[o] = gate(o) * sum_c dl[c] * W2[c][o]   (lane o; every lane has all dl[c])
         const int o = min(lane, 49);
@@ -743,7 +837,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
         const float dz = (lane < 50 && Hs[o] > 0.f) ? (dh0 + dh1) * D1S[o] : 0.f;
         DZ1B[lane] = h16<T>(dz);
-        if (lane < 50) vs[V_DZ1 + lane] = dz;
+        if (lane < 50) st_c<FUSE != 0>(vs + V_DZ1 + lane, dz);
       }
     }
     if (!TRAIN) return;
@@ -934,7 +1028,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   if (TRAIN) {
     // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a
     // chunk ([chunk][WG][64]) so lenet_update reads each chunk contiguously
-    auto out = [&](int e) -> float& { return a.slab[((int64_t)(e >> 6) * G + g) * 64 + (e & 63)]; };
+    auto out_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
     // conv1: combine the four step-slices of each tile (fixed order)
     __syncthreads();
     // partial of wave w at part(w): RED for waves 0-7, the dead DC2H image for 8-15
@@ -949,8 +1043,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       for (int q = 0; q < 8; ++q) v += part(nt + 2 * q)[oc * 16 + col];
       const int k = nt * 16 + col;
       if (oc < 10) {
-        if (k < 25) out(O_C1W + oc * 25 + k) = v;
-        else if (k == 25) out(O_C1B + oc) = v;
+        if (k < 25) st_c<FUSE != 0>(out_at(O_C1W + oc * 25 + k), v);
+        else if (k == 25) st_c<FUSE != 0>(out_at(O_C1B + oc), v);
       }
     }
     // conv2
@@ -963,19 +1057,37 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         for (int r = 0; r < 4; ++r) {
           const int oc = mt * 16 + 4 * (lane >> 4) + r;
           if (oc < 20) {
-            if (k < 250) out(O_C2W + oc * 250 + k) = acc_c2[mt][jj][r];
-            else if (k == 250) out(O_C2B + oc) = acc_c2[mt][jj][r];
+            if (k < 250) st_c<FUSE != 0>(out_at(O_C2W + oc * 250 + k), acc_c2[mt][jj][r]);
+            else if (k == 250) st_c<FUSE != 0>(out_at(O_C2B + oc), acc_c2[mt][jj][r]);
           }
         }
       }
   }
   if (tid == 0) {
-    a.loss_acc[2 * g] = loss_sum;
-    a.loss_acc[2 * g + 1] = correct;
+    st_c<FUSE != 0>(a.loss_acc + 2 * g, loss_sum);
+    st_c<FUSE != 0>(a.loss_acc + 2 * g + 1, correct);
   }
   if (a.dbg) {
+    if (tid == 0) DBGS[23] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (tid < DBG_W) a.dbg[g * DBG_W + tid] = DBGS[tid];
+  }
+  if (FUSE) {
+    // every wave's (device-coherent, st_c) slab / vector / loss stores are complete
+    // (vmcnt), then the signal: no L2 write-back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == 0) {
+      int old = 0;
+      if (lane == 0) {
+        if (fz.u.dbg) fz.u.dbg[(fz.nupd + g) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        old = __hip_atomic_fetch_add(fz.bar + BAR_CNT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (__shfl(old, 0) == a.grid - 1) {  // the last training workgroup: re-arm, raise the go flags
+        if (lane == 0) sys_store(fz.bar + BAR_CNT, 0);
+        for (int b = lane; b < fz.nupd; b += 64) sys_store(fz.bar + BAR_GO + 32 * b, 1);
+      }
+    }
   }
 }
 
@@ -1046,7 +1158,6 @@ __global__ void lenet_pack_kernel(const float* __restrict__ params, unsigned sho
 //
 // Reductions run in a fixed order everywhere: bitwise reproducible.
 // ---------------------------------------------------------------------------
-constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
 constexpr int CNQ = CNP / 4;                        // conv float4 columns (1320)
 constexpr int NB_CONV = (CNQ + UP_C - 1) / UP_C;    // 83
 constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
@@ -1056,7 +1167,13 @@ constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
 __host__ __device__ constexpr int fc_waves_per_tile(int B) {
   return B <= 128 ? 1 : (B <= 256 ? 2 : (B <= 512 ? 4 : 8));
 }
-__host__ __device__ constexpr int fc_blocks(int B) { return FC_TILES / (8 / fc_waves_per_tile(B)); }
+// Update workgroups of NTH threads (UP_NT for lenet_update, NT in the fused step):
+// an FC workgroup holds NTH/64/wpt tiles, a CONV workgroup NTH/UP_NT 64-parameter blocks.
+__host__ __device__ constexpr int fc_blocks(int B, int nth = UP_NT) {
+  return (FC_TILES + nth / 64 / fc_waves_per_tile(B) - 1) / (nth / 64 / fc_waves_per_tile(B));
+}
+__host__ __device__ constexpr int conv_blocks(int nth = UP_NT) { return (NB_CONV + nth / UP_NT - 1) / (nth / UP_NT); }
+__host__ __device__ constexpr int update_blocks(int B, int nth = UP_NT) { return fc_blocks(B, nth) + conv_blocks(nth); }
 constexpr int NB_FC = FC_TILES;                     // FC blocks at most (one tile each)
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
@@ -1204,50 +1321,75 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t 
   }
 }
 
-template <typename T, bool EXCH>
-__global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
-                                                             int B, float* loss_parts, int nparts,
-                                                             float* loss_acc, comm::IpcPeers px,
-                                                             uint64_t timeout_ticks) {
-  __shared__ float4 part[UP_S][UP_C];
-  __shared__ float part2[4][UP_C * 4];
-
+// Update workgroup blk of nblk (NTH threads).  part: float4[NTH/UP_NT][UP_S][UP_C],
+// part2: float[NTH/UP_NT][4][UP_C*4] in LDS.  ready (fused step only): the BAR_* words;
+// wait for this workgroup's go flag -- the nready training workgroups' slabs are
+// complete -- before reading them.
+template <typename T, bool EXCH, bool FUSED, int NTH>
+__device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
+                            int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
+                            int nblk, int tid, float4* part_, float* part2_, const int* ready, int nready) {
+  static_assert(NTH % UP_NT == 0, "whole conv halves");
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
-  const int tid = threadIdx.x, blk = blockIdx.x;
   // exchange tag of this call (uniform load; written back after the block's last poll)
   const uint32_t xt = EXCH ? (uint32_t)(px.counters[blk] + 1) : 0u;
   bool timed_out = false;
 #define USTAMP(k) \
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
+  // fused step: wait for the training workgroups (bounded: a timeout raises bar[2])
+  auto wait_ready = [&]() {
+    if (!ready) return;
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int* go = const_cast<int*>(ready) + BAR_GO + 32 * blk;
+      while (sys_load(go) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+          atomicOr(const_cast<int*>(ready) + BAR_ERR, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      sys_store(go, 0);  // re-arm for the next launch
+    }
+    // no acquire fence: the training outputs are read with device-coherent loads (ld_c)
+    __syncthreads();
+    USTAMP(5);
+  };
 
-  const int nb_fc = fc_blocks(B);
+  const int nb_fc = fc_blocks(B, NTH);
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
-    // they are dispatched first)
-    const int cblk = blk - nb_fc;
-    const int cl = tid & (UP_C - 1), sl = tid / UP_C;
-    // wave 0 owns params cblk*64 + tid (16 float4 columns): prefetch p / m now
-    const int pi = cblk * (UP_C * 4) + tid;
+    // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
+    const int half = tid / UP_NT, ht = tid % UP_NT;
+    const int cblk = blk - nb_fc, pb = cblk * (NTH / UP_NT) + half;
+    const bool live_pb = pb < NB_CONV;
+    const int pbc = min(pb, NB_CONV - 1);  // a dead half reads a valid chunk, stores nothing
+    float4 (*part)[UP_C] = reinterpret_cast<float4 (*)[UP_C]>(part_ + half * UP_S * UP_C);
+    float (*part2)[UP_C * 4] = reinterpret_cast<float (*)[UP_C * 4]>(part2_ + half * 4 * UP_C * 4);
+    const int cl = ht & (UP_C - 1), sl = ht / UP_C;
+    // the half's first wave owns params pbc*64 + ht (16 float4 columns): prefetch p / m now
+    const int pi = pbc * (UP_C * 4) + ht;
     float p0 = 0.f, m0 = 0.f;
     int d0 = -1, d1 = -1;
-    if (a.apply_sgd && tid < 64) {
+    if (a.apply_sgd && ht < 64) {
       p0 = a.params[min(pi, NP - 1)];
       m0 = a.momentum[min(pi, NP - 1)];
       image_slots(pi, d0, d1);
     }
+    wait_ready();
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     // Loads are unconditional from a clamped address and masked afterwards: a
     // per-element "load or zero" select makes hipcc branch around every load
     // and wait vmcnt(0) each time (dependent round trips instead of one).
     // chunk blk of the slab is [WG][16 float4]: contiguous for this block
-    const float4* sp = reinterpret_cast<const float4*>(a.slab) + (int64_t)cblk * a.grid * UP_C + cl;
+    const float4* sp = reinterpret_cast<const float4*>(a.slab) + (int64_t)pbc * a.grid * UP_C + cl;
     for (int g0 = sl; g0 < a.grid; g0 += UP_S * UP_MAXL) {
       float4 v[UP_MAXL];
 #pragma unroll
-      for (int u = 0; u < UP_MAXL; ++u) v[u] = sp[(int64_t)min(g0 + u * UP_S, a.grid - 1) * UP_C];
+      for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(g0 + u * UP_S, a.grid - 1) * UP_C);
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u)
         if (g0 + u * UP_S < a.grid) add4(acc, v[u]);
@@ -1264,8 +1406,8 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
     }
     __syncthreads();
     USTAMP(3);
-    if (tid < 64 && pi < CNP) {
-      float g[1] = {(part2[0][tid] + part2[1][tid]) + (part2[2][tid] + part2[3][tid])};
+    if (ht < 64 && live_pb && pi < CNP) {
+      float g[1] = {(part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])};
       if (EXCH) {
         const int idx[1] = {pi};
         const bool live[1] = {true};
@@ -1274,12 +1416,12 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
     USTAMP(4);
-    if (cblk == 0 && loss_parts && tid < 64) {
+    if (pb == 0 && loss_parts && tid < 64) {
       // loss / accuracy partials: lane-strided sums, then a fixed butterfly
       float s0 = 0.f, s1 = 0.f;
       for (int q = tid; q < nparts; q += 64) {
-        s0 += loss_parts[2 * q];
-        s1 += loss_parts[2 * q + 1];
+        s0 += ld_c<FUSED>(loss_parts + 2 * q);
+        s1 += ld_c<FUSED>(loss_parts + 2 * q + 1);
       }
       s0 = wave_sum(s0);
       s1 = wave_sum(s1);
@@ -1292,7 +1434,9 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
     // ---------------- role FC: 16x16 tiles of [dW | db], K split over wpt waves per tile
     const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
     const int wpt = fc_waves_per_tile(B);
-    const int tile = blk * (UP_NT / 64 / wpt) + wave / wpt, sub = wave % wpt;
+    const int tile_w = blk * (NTH / 64 / wpt) + wave / wpt, sub = wave % wpt;
+    const bool live_tile = tile_w < FC_TILES;     // the last workgroup may hold dead waves:
+    const int tile = min(tile_w, FC_TILES - 1);   // they compute a valid tile, store nothing
     const bool fc1 = tile < FC1_TILES;
     const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
     const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
@@ -1305,7 +1449,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int oo = mt * 16 + 4 * kq + r;
-      pidx[r] = (oo < rows && i <= cols)
+      pidx[r] = (live_tile && oo < rows && i <= cols)
                     ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
                            : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
                     : -1;
@@ -1322,6 +1466,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       image_slots(max(pidx[r], 0), fd[r], d1);
       if (pidx[r] < 0) fd[r] = -1;
     }
+    wait_ready();
     // this wave's samples [k0, k1): a multiple-of-4 share of the batch
     const int kw = ((B + wpt - 1) / wpt + 3) & ~3;
     const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
@@ -1333,8 +1478,8 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
         const bool ok = s < k1;
         // unconditional loads from clamped addresses, masked after (see role CONV)
         const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
-        const float ra = rowc[a_off + min(o, rows - 1)];
-        const float rb = rowc[b_off + min(i, cols - 1)];
+        const float ra = ld_c<FUSED>(rowc + a_off + min(o, rows - 1));
+        const float rb = ld_c<FUSED>(rowc + b_off + min(i, cols - 1));
         av[u] = (ok && o < rows) ? ra : 0.f;
         bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
       }
@@ -1345,7 +1490,12 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       return c;
     };
     f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (k0 < k1) {
+    if (FUSED) {  // k1 - k0 <= 64
+      float a0[16], b0[16];
+      load(k0, a0, b0);
+      USTAMP(1);
+      c = mfma16(c, a0, b0);
+    } else if (k0 < k1) {
       float a0[16], b0[16], a1[16], b1[16];
       load(k0, a0, b0);
       for (int s0 = k0; s0 < k1; s0 += 128) {
@@ -1370,7 +1520,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
     asm volatile("" ::"v"(pp[0]), "v"(pp[1]), "v"(pp[2]), "v"(pp[3]), "v"(pm[0]), "v"(pm[1]), "v"(pm[2]),
                  "v"(pm[3]));
     // fixed-order combine of the tile's wpt partials (reuses the CONV role's LDS)
-    float* pfc = reinterpret_cast<float*>(&part[0][0]);
+    float* pfc = reinterpret_cast<float*>(part_);
     if (wpt > 1) {  // uniform
 #pragma unroll
       for (int r = 0; r < 4; ++r) pfc[wave * 256 + r * 64 + lane] = c[r];
@@ -1415,7 +1565,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       __syncthreads();
       if (tid == 0) {
         const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
-        if (t == (int)gridDim.x - 1) {
+        if (t == nblk - 1) {
           a.ticket[0] = 0;
           if (a.step) a.step[0] += 1;
         }
@@ -1428,6 +1578,17 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
       if (a.rng_offset) a.rng_offset[0] += 1;
     }
   }
+}
+
+template <typename T, bool EXCH>
+__global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
+                                                             int B, float* loss_parts, int nparts,
+                                                             float* loss_acc, comm::IpcPeers px,
+                                                             uint64_t timeout_ticks) {
+  __shared__ float4 part[UP_S][UP_C];
+  __shared__ float part2[4][UP_C * 4];
+  update_role<T, EXCH, false, UP_NT>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
+                       threadIdx.x, &part[0][0], &part2[0][0], nullptr, 0);
 }
 
 // SGD from an already-reduced gradient (DDP: after the all-reduce).
@@ -1474,15 +1635,15 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     if (a.xstage) {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true>,
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 0>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true>), dim3(a.grid), dim3(NT), lds, s, a, 0,
-                         (float*)nullptr);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 0>), dim3(a.grid), dim3(NT), lds, s, a, 0,
+                         (float*)nullptr, StepFuse{});
     } else {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, false>,
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, false, 0>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false>), dim3(a.grid), dim3(NT), lds, s, a, 0,
-                         (float*)nullptr);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false, 0>), dim3(a.grid), dim3(NT), lds, s, a, 0,
+                         (float*)nullptr, StepFuse{});
     }
   });
   return hipGetLastError();
@@ -1497,7 +1658,7 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     return hipGetLastError();
   }
   if (!a.vslab || a.B <= 0) return hipErrorInvalidValue;
-  const int nblocks = fc_blocks(a.B) + NB_CONV;
+  const int nblocks = update_blocks(a.B);
   comm::IpcPeers px{};
   if (a.exch_id >= 0) {
     // fused data-parallel exchange: the buffer must hold this kernel's word layout
@@ -1520,6 +1681,47 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
 }
 
 int64_t lenet_exch_words() { return EXCH_WORDS; }
+
+int lenet_fused_max_batch() { return FUSED_MAXB; }
+int lenet_step_bar_ints() { return BAR_INTS; }
+
+hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, float* loss_parts, int nparts,
+                             float* loss_acc, int* bar, hipStream_t s) {
+  // the fused step: staged batch (one sample per training workgroup), SGD applied,
+  // every slab produced by this launch (u describes t's outputs)
+  if (t.B <= 0 || t.B > FUSED_MAXB || t.grid != t.B || !t.xstage || !t.lstage || !bar) return hipErrorInvalidValue;
+  static_assert(NB_UPDATE <= 256, "one go flag per update workgroup");
+  if (!u.apply_sgd || u.grad_in || !u.vslab || u.B != t.B || u.grid != t.grid || u.slab != t.slab ||
+      u.vslab != t.vslab || u.exch_timeout_s <= 0.0)
+    return hipErrorInvalidValue;
+  StepFuse fz{};
+  fz.u = u; fz.loss_parts = loss_parts; fz.nparts = nparts; fz.loss_acc = loss_acc; fz.bar = bar;
+  fz.nupd = update_blocks(u.B, UPD_NTH);
+  fz.timeout_ticks = (uint64_t)(u.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  const bool exch = u.exch_id >= 0;
+  if (exch) {
+    const hipError_t e = comm::ipc_peers(u.exch_id, &fz.px);
+    if (e != hipSuccess) return e;
+    if (fz.px.cap < EXCH_WORDS) return hipErrorInvalidValue;
+  }
+  const size_t lds = (size_t)(S_TOTAL - S_X);
+  static_assert((UPD_NTH / UP_NT) * (UP_S * UP_C * 16 + 4 * UP_C * 4 * 4) <= S_TOTAL - S_X, "update role LDS");
+  const dim3 grid(t.grid + fz.nupd);
+  CSED_DISPATCH_MFMA(t.mfma_dtype, {
+    if (exch) {
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 2>), grid, dim3(NT), lds, s, t, 0,
+                         (float*)nullptr, fz);
+    } else {
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 1>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 1>), grid, dim3(NT), lds, s, t, 0,
+                         (float*)nullptr, fz);
+    }
+  });
+  return hipGetLastError();
+}
 
 int lenet_stage_max_batch() { return STAGE_MAXB; }
 
@@ -1551,10 +1753,10 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
-    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false>,
+    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false, 0>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false>), dim3(a.grid), dim3(NT), lds, s, a,
-                       logp_out ? 1 : 0, logp_out);
+    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false, 0>), dim3(a.grid), dim3(NT), lds, s, a,
+                       logp_out ? 1 : 0, logp_out, StepFuse{});
   });
   return hipGetLastError();
 }
