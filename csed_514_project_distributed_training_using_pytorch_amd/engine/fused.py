@@ -58,6 +58,14 @@ def fused_max_batch() -> int:
     return int(torch.ops.csed.lenet_layout()[6])
 
 
+def one_kernel_mode() -> str:
+    """CSED_ONE_KERNEL_STEP: "auto" (default), "0" or "1" (see FusedLeNetTrainer)."""
+    mode = os.environ.get("CSED_ONE_KERNEL_STEP", "auto").strip().lower()
+    if mode not in ("auto", "0", "1"):
+        raise ValueError(f"CSED_ONE_KERNEL_STEP={mode!r}: expected auto, 0 or 1")
+    return mode
+
+
 def exch_words() -> int:
     """8-byte words per sender of lenet_update's fused exchange buffer."""
     return int(torch.ops.csed.lenet_layout()[5])
@@ -124,10 +132,13 @@ class FusedLeNetTrainer:
         self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
         # one-kernel step (csed::lenet_step): training workgroups + trailing update
         # workgroups that wait on a device counter, instead of two launches.  bar:
-        # its synchronisation words ([2] != 0: a timed-out wait); CSED_ONE_KERNEL_STEP=0
-        # keeps two kernels.
-        self.one_kernel = (self.staged and self.B <= fused_max_batch()
-                           and os.environ.get("CSED_ONE_KERNEL_STEP", "1") != "0")
+        # its synchronisation words ([2] != 0: a timed-out wait).  CSED_ONE_KERNEL_STEP:
+        # "auto" (default) = one kernel on a single rank, two kernels with the fused
+        # exchange (in the one-kernel form its exchange role spills registers and it is
+        # unmeasured over xGMI), "1" = always, "0" = never.
+        ok_mode = one_kernel_mode()
+        self.one_kernel = (self.staged and self.B <= fused_max_batch() and ok_mode != "0"
+                           and (ok_mode == "1" or not (self.comm and self.world > 1)))
         self.bar = torch.zeros(int(torch.ops.csed.lenet_layout()[7]), dtype=torch.int32, device=dev)
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}

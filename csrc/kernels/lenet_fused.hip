@@ -587,6 +587,24 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // stage out of the sample loop, where they sit in ~100 long-lived registers
   // (scratch spills at 256 VGPRs) and run as one serial VALU block in front of
   // the first sample instead of inside the stages' latency bubbles.
+  // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a chunk
+  // ([chunk][WG][64]) so lenet_update reads each chunk contiguously
+  auto slab_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
+  // conv2 weight / bias gradient of this workgroup (C rows oc, column k = wave*16 + l16)
+  auto store_c2 = [&]() {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int k = wave * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oc = mt * 16 + 4 * (lane >> 4) + r;
+        if (oc < 20) {
+          if (k < 250) st_c<FUSE != 0>(slab_at(O_C2W + oc * 250 + k), acc_c2[mt][0][r]);
+          else if (k == 250) st_c<FUSE != 0>(slab_at(O_C2B + oc), acc_c2[mt][0][r]);
+        }
+      }
+    }
+  };
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
@@ -918,6 +936,14 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
+    if (TRAIN && STAGED) {
+      // final (one sample): the write latency of these stores hides under the dgrad
+      store_c2();
+      if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
+        if (tid >= 256 && tid - 256 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 256] = px_next;
+        if (tid == 256) a.lstage[g] = lab_next;
+      }
+    }
     STAMP(9);
     if (wave < 8) {
       // dP1[px][ic] = sum_{tap, oc} DC2H[px + shift(tap)][oc] * W2D[ic][tap*24 + oc]:
@@ -1020,15 +1046,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   }
 
   if (a.dbg && tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
-  if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
-    if (tid >= 256 && tid - 256 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 256] = px_next;
-    if (tid == 256) a.lstage[g] = lab_next;
-  }
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
-    // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a
-    // chunk ([chunk][WG][64]) so lenet_update reads each chunk contiguously
-    auto out_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
     // conv1: combine the four step-slices of each tile (fixed order)
     __syncthreads();
     // partial of wave w at part(w): RED for waves 0-7, the dead DC2H image for 8-15
@@ -1043,25 +1062,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       for (int q = 0; q < 8; ++q) v += part(nt + 2 * q)[oc * 16 + col];
       const int k = nt * 16 + col;
       if (oc < 10) {
-        if (k < 25) st_c<FUSE != 0>(out_at(O_C1W + oc * 25 + k), v);
-        else if (k == 25) st_c<FUSE != 0>(out_at(O_C1B + oc), v);
+        if (k < 25) st_c<FUSE != 0>(slab_at(O_C1W + oc * 25 + k), v);
+        else if (k == 25) st_c<FUSE != 0>(slab_at(O_C1B + oc), v);
       }
     }
-    // conv2
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int jj = 0; jj < 1; ++jj) {
-        const int k = wave * 16 + l16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int oc = mt * 16 + 4 * (lane >> 4) + r;
-          if (oc < 20) {
-            if (k < 250) st_c<FUSE != 0>(out_at(O_C2W + oc * 250 + k), acc_c2[mt][jj][r]);
-            else if (k == 250) st_c<FUSE != 0>(out_at(O_C2B + oc), acc_c2[mt][jj][r]);
-          }
-        }
-      }
+    if (!STAGED) store_c2();  // staged: stored right after conv2 wgrad
   }
   if (tid == 0) {
     st_c<FUSE != 0>(a.loss_acc + 2 * g, loss_sum);
@@ -1082,6 +1087,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       if (lane == 0) {
         if (fz.u.dbg) fz.u.dbg[(fz.nupd + g) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
         old = __hip_atomic_fetch_add(fz.bar + BAR_CNT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (fz.u.dbg) fz.u.dbg[(fz.nupd + g) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
       }
       if (__shfl(old, 0) == a.grid - 1) {  // the last training workgroup: re-arm, raise the go flags
         if (lane == 0) sys_store(fz.bar + BAR_CNT, 0);

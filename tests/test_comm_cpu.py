@@ -52,3 +52,17 @@ def test_exchange_buffer_layout():
     fc_tiles = 4 * 21 + 4  # fc1: 4 x 21 tiles of [dW1 | db1], fc2: 4 tiles of [dW2 | db2]
     assert words == conv_pad + fc_tiles * 256 == 27840
     assert words % 4 == 0  # the IPC buffers are allocated in multiples of 4 words
+
+
+def test_one_kernel_step_mode_validation(monkeypatch):
+    """CSED_ONE_KERNEL_STEP accepts auto / 0 / 1 only (engine/fused.py)."""
+    from csed_514_project_distributed_training_using_pytorch_amd.engine import fused
+
+    monkeypatch.delenv("CSED_ONE_KERNEL_STEP", raising=False)
+    assert fused.one_kernel_mode() == "auto"
+    for v in ("0", "1", " AUTO "):
+        monkeypatch.setenv("CSED_ONE_KERNEL_STEP", v)
+        assert fused.one_kernel_mode() == v.strip().lower()
+    monkeypatch.setenv("CSED_ONE_KERNEL_STEP", "sometimes")
+    with pytest.raises(ValueError):
+        fused.one_kernel_mode()

@@ -81,10 +81,13 @@ def _worker(rank, world, port, q):
 
         data = synthetic_mnist(2048, seed=3)
 
-        def train(mode):
+        def train(mode, key=None, one_kernel="auto"):
             # ipc: reduce-only update -> one-shot IPC all-reduce kernel -> SGD kernel;
-            # fused: lenet_update exchanges with the peer itself (one kernel)
+            # fused: lenet_update exchanges with the peer itself (one kernel), with
+            # one_kernel="1" inside the one-kernel step (csed::lenet_step)
+            key = key or mode
             os.environ["CSED_ALLREDUCE"] = mode
+            os.environ["CSED_ONE_KERNEL_STEP"] = one_kernel
             torch.manual_seed(1)
             eng = FusedLeNetTrainer(Net().to(dev), data, lr=0.05, global_batch=64, ctx=ctx)
             smp = ShardSampler(2048, world, rank, shuffle=True, seed=42)
@@ -96,16 +99,20 @@ def _worker(rank, world, port, q):
             p = eng.flat.data.cpu()
             other = p.clone()
             dist.broadcast(other, src=0)
-            res[f"kind_{mode}"] = eng.allreduce_kind
-            res[f"params_equal_{mode}"] = torch.equal(p, other)
-            res[f"engine_errors_{mode}"] = eng.comm_errors()
-            res[f"finite_{mode}"] = bool(torch.isfinite(p).all())
+            res[f"kind_{key}"] = eng.allreduce_kind
+            res[f"step_{key}"] = eng.step_kind
+            res[f"params_equal_{key}"] = torch.equal(p, other)
+            res[f"engine_errors_{key}"] = eng.comm_errors()
+            res[f"finite_{key}"] = bool(torch.isfinite(p).all())
             return p
 
         p_ipc = train("ipc")
         p_fused = train("fused")
-        # both sum the same rank-local gradients in rank order: bitwise-identical training
+        p_fused1 = train("fused", "fused1k", "1")
+        os.environ.pop("CSED_ONE_KERNEL_STEP")
+        # all sum the same rank-local gradients in rank order: bitwise-identical training
         res["fused_equals_ipc"] = torch.equal(p_ipc, p_fused)
+        res["fused1k_equals_ipc"] = torch.equal(p_ipc, p_fused1)
         q.put((rank, res))
         dist.destroy_process_group()
     except Exception as e:  # report, do not hang the parent
@@ -132,8 +139,9 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         assert "exception" not in res, res
         assert res["errors"] == 0, res  # first: a timed-out wait explains any mismatch below
         assert res["enabled"] and res["eager"] and res["graph"], res
-        for mode, kind in (("ipc", "ipc-oneshot"), ("fused", "fused-ipc")):
+        for mode, kind in (("ipc", "ipc-oneshot"), ("fused", "fused-ipc"), ("fused1k", "fused-ipc")):
             assert res[f"kind_{mode}"] == kind, res
             assert res[f"params_equal_{mode}"] and res[f"finite_{mode}"], res
             assert res[f"engine_errors_{mode}"] == 0, res
-        assert res["fused_equals_ipc"], res
+        assert res["step_fused"] == "two kernels" and res["step_fused1k"].startswith("one kernel"), res
+        assert res["fused_equals_ipc"] and res["fused1k_equals_ipc"], res

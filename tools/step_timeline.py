@@ -61,6 +61,10 @@ def main():
                     "update WG loads done": [r[1] - t0 for r in up],
                     "update WG finish": [max(r[3], r[4]) - t0 for r in up]}
             if name == "one kernel":
+                nupd = len(up)
+                tr = ud[nupd:nupd + B]
+                vals["train WG signal"] = [r[1] - t0 for r in tr]
+                vals["train WG counted"] = [r[2] - t0 for r in tr]
                 vals["update WG go seen"] = [r[5] - t0 for r in up]
             for k, v in vals.items():
                 rows.setdefault(k, ([], []))
