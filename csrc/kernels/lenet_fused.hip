@@ -276,6 +276,30 @@ __device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned sh
 // no code of the multi-sample pixel pipeline: its branches would merge register
 // state into the staged path and make hipcc wait for loads (and so for the LDS
 // DMA) that the staged path never issued.
+// conv1's per-thread address tables (thread tt: X offsets of its tiles 0..2, then P1H
+// offsets), a compile-time constant: the staged path loads its 16-byte row at kernel entry
+// instead of computing 2 x 1024 rows in the preamble (~200 VALU per wave on the SIMDs the
+// preamble's other waves are using).
+struct C1Tab {
+  unsigned short v[NT][8];
+};
+constexpr C1Tab make_c1tab() {
+  C1Tab t{};
+  for (int tt = 0; tt < NT; ++tt) {
+    const int tw = tt >> 6, tl16 = tt & 15, tkq = (tt & 63) >> 4;
+    for (int it = 0; it < 3; ++it) {
+      const int mt = (tw + it * NW) < 35 ? tw + it * NW : 35;
+      const int m = mt * 16 + tl16;
+      const int p = m >> 2, q = m & 3;
+      t.v[tt][it] = (unsigned short)((2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1));
+      const int w = mt * 4 + tkq;  // pooled position py*12 + px
+      t.v[tt][4 + it] = (unsigned short)((w / 12) * P1H_RP + (w % 12) * LD_P1H);
+    }
+  }
+  return t;
+}
+__constant__ C1Tab kC1Tab = make_c1tab();
+
 // One-kernel training step (FUSE > 0): workgroups [0, a.grid) train as below, then
 // signal a device counter; workgroups [a.grid, a.grid + nupd) run lenet_update's roles
 // (update_role) once every training workgroup has signalled.  The update workgroups
@@ -418,6 +442,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   }
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
   const int G = FUSE ? a.grid : (int)gridDim.x, g = blockIdx.x;
+  // staged: this thread's conv1 address row, first in the vector memory queue
+  const uint4 c1row = STAGED ? reinterpret_cast<const uint4*>(&kC1Tab)[tid] : make_uint4(0, 0, 0, 0);
   // fused-step timeline (diagnostics): wall-clock start / signal of training workgroup g
   // at udbg[(nupd + g) * 8 + 0 / 1], next to the update workgroups' stamps
   if (FUSE && fz.u.dbg && tid == 0) fz.u.dbg[(fz.nupd + g) * 8] = __builtin_amdgcn_s_memrealtime();
@@ -548,8 +574,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
                  "v"(lab0), "v"(kg));
   } else {
     // waves 8-15 (otherwise idle here): conv1's address tables of all 1024 threads
-    conv1_tables(tid - 512);
-    conv1_tables(tid);
+    // (non-staged; the staged path reads kC1Tab)
+    if (!STAGED) {
+      conv1_tables(tid - 512);
+      conv1_tables(tid);
+    }
     if (tid - 512 < 16) CONSTB[tid - 512] = tid - 512 < 8 ? (unsigned short)0 : h16<T>(1.f);
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
@@ -657,8 +686,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
       // 36 tiles over 16 waves: at most 3 per wave
       uint32_t rv[3][8];
-      const u16x4 xo = C1T[tid];  // per-thread tables (preamble, waves 8-15)
-      const u16x4 ho = C1H[tid];
+      // per-thread tables (kC1Tab row / preamble, waves 8-15)
+      const u16x4 xo = STAGED ? __builtin_bit_cast(u16x4, make_uint2(c1row.x, c1row.y)) : C1T[tid];
+      const u16x4 ho = STAGED ? __builtin_bit_cast(u16x4, make_uint2(c1row.z, c1row.w)) : C1H[tid];
 #pragma unroll
       for (int it = 0; it < 3; ++it) {
         const int pb = xo[it];
