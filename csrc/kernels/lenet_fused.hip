@@ -421,7 +421,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
-  float* LOGIT = Fs + F_LOGIT;
   float* PAR = Fs + F_PAR;
   float* RED = Fs + F_RED;
 
@@ -819,32 +818,39 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     STAMP(4);
     if (wave == 0) {
       const int t = STAGED ? LABEL[0] : t_lab;
-      // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12, two FMA chains),
-      // then a fixed-order 2-step butterfly inside each aligned 4-lane group
-      float zp0 = 0.f, zp1 = 0.f;
-      if (lane < 40) {
-        const int c = lane >> 2, q = lane & 3;
-        const float* wr = PAR + P_F2W + c * 50;
+      // Every LDS operand first (none depends on the logits): this lane's fc2 row slice
+      // for the logits and its fc2 column for dZ1, so the stage has one LDS round trip
+      // in front and none inside its dependency chain.
+      const int o = min(lane, 49);
+      float w2c[10];
 #pragma unroll
-        for (int u = 0; u < 13; ++u) {
-          const int o = q * 13 + u;
-          if (o < 50) {
-            if (u & 1) zp1 = fmaf(wr[o], Hs[o], zp1);
-            else zp0 = fmaf(wr[o], Hs[o], zp0);
-          }
-        }
+      for (int c = 0; c < 10; ++c) w2c[c] = PAR[P_F2W + c * 50 + o];
+      const float ho = Hs[o], d1 = D1S[o];
+      // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12, two FMA chains; lanes
+      // 40-63 duplicate logit 9), branch-free (o >= 50 multiplies a zero weight)
+      const int c4 = min(lane >> 2, 9), q = lane & 3;
+      const float* wr = PAR + P_F2W + c4 * 50;
+      float zp0 = 0.f, zp1 = 0.f;
+#pragma unroll
+      for (int u = 0; u < 13; ++u) {
+        const int oo = q * 13 + u, oc = min(oo, 49);
+        const float w = oo < 50 ? wr[oc] : 0.f;
+        if (u & 1) zp1 = fmaf(w, Hs[oc], zp1);
+        else zp0 = fmaf(w, Hs[oc], zp0);
       }
+      // fixed-order butterfly inside each aligned 4-lane group on DPP (no LDS)
       float zp = zp0 + zp1;
-      zp += __shfl_xor(zp, 1, 64);
-      zp += __shfl_xor(zp, 2, 64);
-      if (lane < 40 && (lane & 3) == 0) LOGIT[lane >> 2] = zp + PAR[P_F2B + (lane >> 2)];
-      __builtin_amdgcn_wave_barrier();
-      // every lane reads all 10 logits (same-wave LDS round trip, no barrier) and
-      // does the softmax locally: no cross-lane reductions.  The 10 exponentials
-      // serve the log-sum-exp and the softmax gradient alike.
+      zp += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, zp), 0xB1, 0xf, 0xf,
+                                                                   false));  // quad_perm 1,0,3,2
+      zp += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, zp), 0x4E, 0xf, 0xf,
+                                                                   false));  // quad_perm 2,3,0,1
+      // the 10 logits as wave-uniform values (lane 4c holds logit c): the softmax runs
+      // once per wave on scalars, no LDS round trip, no cross-lane reduction
       float lg[10];
 #pragma unroll
-      for (int c = 0; c < 10; ++c) lg[c] = LOGIT[c];
+      for (int c = 0; c < 10; ++c)
+        lg[c] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, zp), 4 * c)) +
+                PAR[P_F2B + c];
       float mx = lg[0];
       int amax = 0;
 #pragma unroll
@@ -862,7 +868,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         loss_sum += lse - lt;
         correct += (amax == t) ? 1.f : 0.f;
       }
-      if (write_logp && lane < 10) logp_out[(int64_t)b * 10 + lane] = LOGIT[lane] - lse;
+      if (write_logp && lane < 10) {
+        float mine = 0.f;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) mine = lane == c ? lg[c] : mine;
+        logp_out[(int64_t)b * 10 + lane] = mine - lse;
+      }
       if (TRAIN) {
         // dlogits = softmax - onehot, scaled by 1 / global batch
         const float gs = a.grad_scale * (1.f / se);
@@ -876,14 +887,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           st_c<FUSE != 0>(vs + V_DLOG + lane, mine);
         }
         // dZ1[o] = gate(o) * sum_c dl[c] * W2[c][o]   (lane o; every lane has all dl[c])
-        const int o = min(lane, 49);
         float dh0 = 0.f, dh1 = 0.f;
 #pragma unroll
         for (int c = 0; c < 10; ++c) {
-          if (c & 1) dh1 = fmaf(dl[c], PAR[P_F2W + c * 50 + o], dh1);
-          else dh0 = fmaf(dl[c], PAR[P_F2W + c * 50 + o], dh0);
+          if (c & 1) dh1 = fmaf(dl[c], w2c[c], dh1);
+          else dh0 = fmaf(dl[c], w2c[c], dh0);
         }
-        const float dz = (lane < 50 && Hs[o] > 0.f) ? (dh0 + dh1) * D1S[o] : 0.f;
+        const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
         DZ1B[lane] = h16<T>(dz);
         if (lane < 50) st_c<FUSE != 0>(vs + V_DZ1 + lane, dz);
       }
