@@ -46,6 +46,9 @@
 // Flat parameter order (= Net.state_dict() order, 21,840 floats):
 //   conv1.w 0, conv1.b 250, conv2.w 260, conv2.b 5260, fc1.w 5280,
 //   fc1.b 21280, fc2.w 21330, fc2.b 21830.
+#include <algorithm>
+#include <cstdlib>
+
 #include "comm/ipc_allreduce.h"
 #include "common.h"
 #include "dispatch.h"
@@ -362,6 +365,7 @@ struct StepFuse {
   uint64_t timeout_ticks;
   int* bar;  // BAR_INTS synchronisation words (BAR_ERR != 0: a wait timed out)
   int nupd;  // update workgroups
+  int fc_tpb;  // FC tiles per update workgroup
 };
 
 // FUSED_MAXB: the fused step's batch limit -- one 64-sample chunk per fc wave, so the
@@ -372,7 +376,8 @@ constexpr int UPD_NTH = 512;  // threads of a fused-step update role (UP_NT or N
 template <typename T, bool EXCH, bool FUSED, int NTH>
 __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
                             int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
-                            int nblk, int tid, float4* part, float* part2, const int* ready, int nready);
+                            int nblk, int tid, float4* part, float* part2, const int* ready, int nready,
+                            int fc_tpb = 0);
 
 template <typename T, bool TRAIN, bool STAGED, int FUSE>
 __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out,
@@ -436,7 +441,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
                                              fz.px, fz.timeout_ticks, blockIdx.x - a.grid, fz.nupd, tid,
                                              reinterpret_cast<float4*>(dsm),
                                              reinterpret_cast<float*>(dsm + (UPD_NTH / UP_NT) * UP_S * UP_C * 16),
-                                             fz.bar, a.grid);
+                                             fz.bar, a.grid, fz.fc_tpb);
     return;
   }
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
@@ -1213,13 +1218,21 @@ constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
 __host__ __device__ constexpr int fc_waves_per_tile(int B) {
   return B <= 128 ? 1 : (B <= 256 ? 2 : (B <= 512 ? 4 : 8));
 }
-// Update workgroups of NTH threads (UP_NT for lenet_update, NT in the fused step):
-// an FC workgroup holds NTH/64/wpt tiles, a CONV workgroup NTH/UP_NT 64-parameter blocks.
-__host__ __device__ constexpr int fc_blocks(int B, int nth = UP_NT) {
-  return (FC_TILES + nth / 64 / fc_waves_per_tile(B) - 1) / (nth / 64 / fc_waves_per_tile(B));
+// Update workgroups of NTH threads (UP_NT for lenet_update and the fused step, or NT):
+// a CONV workgroup holds NTH/UP_NT 64-parameter blocks, an FC workgroup NTH/64/wpt tiles
+// -- or FC_TPW_FUSED in the fused step, whose FC phase is bound by per-CU load / store
+// issue (32 loads and ~12 stores per tile wave) and which has idle CUs to spread it on.
+constexpr int FC_TPW_FUSED = 1;
+__host__ __device__ constexpr int fc_tiles_per_block(int B, int nth, bool fused) {
+  return fused ? FC_TPW_FUSED : nth / 64 / fc_waves_per_tile(B);
+}
+__host__ __device__ constexpr int fc_blocks(int B, int nth = UP_NT, bool fused = false) {
+  return (FC_TILES + fc_tiles_per_block(B, nth, fused) - 1) / fc_tiles_per_block(B, nth, fused);
 }
 __host__ __device__ constexpr int conv_blocks(int nth = UP_NT) { return (NB_CONV + nth / UP_NT - 1) / (nth / UP_NT); }
-__host__ __device__ constexpr int update_blocks(int B, int nth = UP_NT) { return fc_blocks(B, nth) + conv_blocks(nth); }
+__host__ __device__ constexpr int update_blocks(int B, int nth = UP_NT, bool fused = false) {
+  return fc_blocks(B, nth, fused) + conv_blocks(nth);
+}
 constexpr int NB_FC = FC_TILES;                     // FC blocks at most (one tile each)
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
@@ -1374,7 +1387,8 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t 
 template <typename T, bool EXCH, bool FUSED, int NTH>
 __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
                             int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
-                            int nblk, int tid, float4* part_, float* part2_, const int* ready, int nready) {
+                            int nblk, int tid, float4* part_, float* part2_, const int* ready, int nready,
+                            int fc_tpb) {
   static_assert(NTH % UP_NT == 0, "whole conv halves");
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
@@ -1405,7 +1419,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     USTAMP(5);
   };
 
-  const int nb_fc = fc_blocks(B, NTH);
+  // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (fused step)
+  const int nb_fc = fc_tpb > 0 ? (FC_TILES + fc_tpb - 1) / fc_tpb : fc_blocks(B, NTH, FUSED);
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
@@ -1480,8 +1495,10 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // ---------------- role FC: 16x16 tiles of [dW | db], K split over wpt waves per tile
     const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
     const int wpt = fc_waves_per_tile(B);
-    const int tile_w = blk * (NTH / 64 / wpt) + wave / wpt, sub = wave % wpt;
-    const bool live_tile = tile_w < FC_TILES;     // the last workgroup may hold dead waves:
+    const int tpb = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B, NTH, FUSED);
+    const bool live_wave = wave / wpt < tpb;      // (uniform) waves past the block's tiles idle
+    const int tile_w = blk * tpb + wave / wpt, sub = wave % wpt;
+    const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
     const int tile = min(tile_w, FC_TILES - 1);   // they compute a valid tile, store nothing
     const bool fc1 = tile < FC1_TILES;
     const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
@@ -1537,10 +1554,12 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     };
     f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
     if (FUSED) {  // k1 - k0 <= 64
-      float a0[16], b0[16];
-      load(k0, a0, b0);
-      USTAMP(1);
-      c = mfma16(c, a0, b0);
+      if (live_wave) {
+        float a0[16], b0[16];
+        load(k0, a0, b0);
+        USTAMP(1);
+        c = mfma16(c, a0, b0);
+      }
     } else if (k0 < k1) {
       float a0[16], b0[16], a1[16], b1[16];
       load(k0, a0, b0);
@@ -1742,7 +1761,10 @@ hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, 
     return hipErrorInvalidValue;
   StepFuse fz{};
   fz.u = u; fz.loss_parts = loss_parts; fz.nparts = nparts; fz.loss_acc = loss_acc; fz.bar = bar;
-  fz.nupd = update_blocks(u.B, UPD_NTH);
+  // FC tiles per workgroup: FC_TPW_FUSED, or CSED_FC_TPB (1..8) for experiments
+  fz.fc_tpb = FC_TPW_FUSED;
+  if (const char* e = std::getenv("CSED_FC_TPB")) fz.fc_tpb = std::max(1, std::min(8, std::atoi(e)));
+  fz.nupd = (FC_TILES + fz.fc_tpb - 1) / fz.fc_tpb + conv_blocks(UPD_NTH);
   fz.timeout_ticks = (uint64_t)(u.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
   const bool exch = u.exch_id >= 0;
   if (exch) {

@@ -61,6 +61,10 @@ def main():
                     "update WG loads done": [r[1] - t0 for r in up],
                     "update WG finish": [max(r[3], r[4]) - t0 for r in up]}
             if name == "one kernel":
+                nfc = int(os.environ.get("CSED_FC_TPB_COUNT", "88"))  # FC workgroups come first
+                for role, rr in (("FC", up[:nfc]), ("CONV", up[nfc:])):
+                    for si, nm in ((5, "go"), (1, "loads"), (2, "s2"), (3, "s3"), (4, "s4")):
+                        vals[f"{role} {nm}"] = [r[si] - t0 for r in rr]
                 nupd = len(up)
                 tr = ud[nupd:nupd + B]
                 vals["train WG signal"] = [r[1] - t0 for r in tr]
