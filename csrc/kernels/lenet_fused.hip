@@ -1219,12 +1219,12 @@ __host__ __device__ constexpr int fc_waves_per_tile(int B) {
   return B <= 128 ? 1 : (B <= 256 ? 2 : (B <= 512 ? 4 : 8));
 }
 // Update workgroups of NTH threads (UP_NT for lenet_update and the fused step, or NT):
-// a CONV workgroup holds NTH/UP_NT 64-parameter blocks, an FC workgroup NTH/64/wpt tiles
-// -- or FC_TPW_FUSED in the fused step, whose FC phase is bound by per-CU load / store
-// issue (32 loads and ~12 stores per tile wave) and which has idle CUs to spread it on.
-constexpr int FC_TPW_FUSED = 1;
+// a CONV workgroup holds NTH/UP_NT 64-parameter blocks; an FC workgroup NTH/64/wpt tiles
+// when the batch splits K over waves, else ONE tile: the FC phase is bound by per-CU load /
+// store issue (32 loads and ~12 stores per tile wave), so 88 workgroups of one tile beat
+// 11 of eight (fused step: 16.86 -> 16.38 us/step).
 __host__ __device__ constexpr int fc_tiles_per_block(int B, int nth, bool fused) {
-  return fused ? FC_TPW_FUSED : nth / 64 / fc_waves_per_tile(B);
+  return fc_waves_per_tile(B) == 1 ? 1 : nth / 64 / fc_waves_per_tile(B);
 }
 __host__ __device__ constexpr int fc_blocks(int B, int nth = UP_NT, bool fused = false) {
   return (FC_TILES + fc_tiles_per_block(B, nth, fused) - 1) / fc_tiles_per_block(B, nth, fused);
@@ -1761,8 +1761,8 @@ hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, 
     return hipErrorInvalidValue;
   StepFuse fz{};
   fz.u = u; fz.loss_parts = loss_parts; fz.nparts = nparts; fz.loss_acc = loss_acc; fz.bar = bar;
-  // FC tiles per workgroup: FC_TPW_FUSED, or CSED_FC_TPB (1..8) for experiments
-  fz.fc_tpb = FC_TPW_FUSED;
+  // FC tiles per workgroup: as lenet_update, or CSED_FC_TPB (1..8) for experiments
+  fz.fc_tpb = fc_tiles_per_block(u.B, UPD_NTH, true);
   if (const char* e = std::getenv("CSED_FC_TPB")) fz.fc_tpb = std::max(1, std::min(8, std::atoi(e)));
   fz.nupd = (FC_TILES + fz.fc_tpb - 1) / fz.fc_tpb + conv_blocks(UPD_NTH);
   fz.timeout_ticks = (uint64_t)(u.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
