@@ -13,7 +13,8 @@ from pathlib import Path
 
 import torch
 
-_SO = Path(__file__).resolve().parent.parent / "_C.so"
+# CSED_NATIVE_SO: load another build of the extension (same-box A/B timing of two builds)
+_SO = Path(os.environ.get("CSED_NATIVE_SO") or Path(__file__).resolve().parent.parent / "_C.so")
 _lock = threading.Lock()
 _loaded = False
 _error: Exception | None = None

@@ -324,6 +324,18 @@ __device__ __forceinline__ void st_c(float* p, float v) {
   else *p = v;
 }
 template <bool C>
+__device__ __forceinline__ void st4_c(float* p, float4 v) {
+  if (C) {
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    __hip_atomic_store(q, ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, ((uint64_t)__float_as_uint(v.w) << 32) | __float_as_uint(v.z), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+template <bool C>
 __device__ __forceinline__ float ld_c(const float* p) {
   if (C) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return *p;
@@ -623,8 +635,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a chunk
   // ([chunk][WG][64]) so lenet_update reads each chunk contiguously
   auto slab_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
-  // conv2 weight / bias gradient of this workgroup (C rows oc, column k = wave*16 + l16)
-  auto store_c2 = [&]() {
+  // The conv2 part of the workgroup's slab row (e = 260 .. 5279) goes out as float4 runs
+  // from an LDS copy in the dead fc1 image (F1 is last read in stage 5): 2 wide stores per
+  // lane instead of 8 scalar ones of 64 lanes (per-CU store issue is what those cost).
+  float* SLF = reinterpret_cast<float*>(wsm + S_F1);  // indexed by e
+  static_assert(O_C2B + 20 <= (S_X - S_F1) / 4 && O_C2W % 4 == 0 && (O_C2B + 20) % 4 == 0, "conv2 row staging");
+  auto stage_c2 = [&]() {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int k = wave * 16 + l16;
@@ -632,11 +648,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       for (int r = 0; r < 4; ++r) {
         const int oc = mt * 16 + 4 * (lane >> 4) + r;
         if (oc < 20) {
-          if (k < 250) st_c<FUSE != 0>(slab_at(O_C2W + oc * 250 + k), acc_c2[mt][0][r]);
-          else if (k == 250) st_c<FUSE != 0>(slab_at(O_C2B + oc), acc_c2[mt][0][r]);
+          if (k < 250) SLF[O_C2W + oc * 250 + k] = acc_c2[mt][0][r];
+          else if (k == 250) SLF[O_C2B + oc] = acc_c2[mt][0][r];
         }
       }
     }
+  };
+  auto store_c2 = [&](int t0, int nt) {  // after a barrier that follows stage_c2
+    for (int i = O_C2W / 4 + t0; i < (O_C2B + 20) / 4; i += nt)
+      st4_c<FUSE != 0>(slab_at(4 * i), reinterpret_cast<const float4*>(SLF)[i]);
   };
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = g + s * G;
@@ -982,8 +1002,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       }
     }
     if (TRAIN && STAGED) {
-      // final (one sample): the write latency of these stores hides under the dgrad
-      store_c2();
+      stage_c2();  // final (one sample); stored by idle threads at stage 7
+      // the write latency of these stores hides under the dgrad
       if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
         if (tid >= 256 && tid - 256 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 256] = px_next;
         if (tid == 256) a.lstage[g] = lab_next;
@@ -1049,6 +1069,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
     __syncthreads();
     STAMP(7);
+    if (TRAIN && STAGED && tid >= 256) store_c2(tid - 256, NT - 256);  // write latency hides under stage 8
     if (tid < 256) {  // tile 8: fixed-order sum of the 8 shares, then the pool1/relu backward
       const int rr = tid >> 4, ci = tid & 15;
       if (ci < 10) {
@@ -1093,14 +1114,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   if (a.dbg && tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
-    // conv1: combine the four step-slices of each tile (fixed order)
     __syncthreads();
-    // partial of wave w at part(w): RED for waves 0-7, the dead DC2H image for 8-15
+    // conv1: the four step-slices of each tile; partial of wave w at part(w): RED for
+    // waves 0-7, the dead DC2H image for 8-15
     auto part = [&](int w) { return w < 8 ? RED + w * 256 : reinterpret_cast<float*>(DC2H) + (w - 8) * 256; };
 #pragma unroll
     for (int r = 0; r < 4; ++r) part(wave)[(4 * (lane >> 4) + r) * 16 + l16] = acc_c1[r];
+    if (!STAGED) stage_c2();  // (staged: stored at stage 7)
     __syncthreads();
-    if (tid < 512) {
+    if (tid < 512) {  // conv1 combine (fixed order)
       const int nt = tid >> 8, oc = (tid >> 4) & 15, col = tid & 15;
       float v = 0.f;
 #pragma unroll
@@ -1110,8 +1132,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (k < 25) st_c<FUSE != 0>(slab_at(O_C1W + oc * 25 + k), v);
         else if (k == 25) st_c<FUSE != 0>(slab_at(O_C1B + oc), v);
       }
+    } else if (!STAGED) {
+      store_c2(tid - 512, NT - 512);
     }
-    if (!STAGED) store_c2();  // staged: stored right after conv2 wgrad
   }
   if (tid == 0) {
     st_c<FUSE != 0>(a.loss_acc + 2 * g, loss_sum);
