@@ -1328,6 +1328,33 @@ __device__ __forceinline__ void finish_param(const LenetUpdateArgs& a, int i, fl
   write_slots<T>(a.wimg, d0, d1, p);
 }
 
+// finish_param for 4 consecutive fc1 weights i .. i+3 (16-byte aligned; their weight-image
+// slots d0 .. d0+3 are consecutive and 8-byte aligned): the same arithmetic per element,
+// one wide store per array instead of four
+template <typename T>
+__device__ __forceinline__ void finish_param4(const LenetUpdateArgs& a, int i, float4 gsum, bool first, float4 p4,
+                                              float4 m4, int d0) {
+  float gv[4] = {gsum.x, gsum.y, gsum.z, gsum.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w}, mv[4] = {m4.x, m4.y, m4.z, m4.w};
+  if (!a.apply_sgd || a.grad_out) *reinterpret_cast<float4*>(a.grad_out + i) = gsum;
+  if (!a.apply_sgd) return;
+  u16x4 h;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float gj = gv[j] + a.weight_decay * pv[j];
+    float d = gj;
+    if (a.mom != 0.f) {
+      const float bj = first ? gj : fmaf(a.mom, mv[j], (1.f - a.dampening) * gj);
+      mv[j] = bj;
+      d = a.nesterov ? fmaf(a.mom, bj, gj) : bj;
+    }
+    pv[j] = fmaf(-a.lr, d, pv[j]);
+    h[j] = h16<T>(pv[j]);
+  }
+  if (a.mom != 0.f) *reinterpret_cast<float4*>(a.momentum + i) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+  *reinterpret_cast<float4*>(a.params + i) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  *reinterpret_cast<u16x4*>(a.wimg + d0) = h;
+}
+
 // ---------------------------------------------------------------------------
 // Data-parallel exchange fused into lenet_update (EXCH = true).
 //
@@ -1532,6 +1559,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // column i), their p / m
     int pidx[4];
     float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
+    // fc1 weight tiles (wave-uniform) finish in row layout: lane = (row, 4 columns), one
+    // float4 per array (finish_param4); the others per element in the MFMA layout
+    const bool vec = live_tile && fc1 && nt < 20;
+    const int vrow = mt * 16 + (lane >> 2), vcol = nt * 16 + 4 * (lane & 3);
+    const int vidx = O_F1W + min(vrow, 49) * 320 + vcol;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int oo = mt * 16 + 4 * kq + r;
@@ -1539,10 +1571,16 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
                     ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
                            : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
                     : -1;
-      if (a.apply_sgd && sub == 0) {
+      if (a.apply_sgd && sub == 0 && !vec) {
         pp[r] = a.params[max(pidx[r], 0)];
         pm[r] = a.momentum[max(pidx[r], 0)];
       }
+    }
+    if (a.apply_sgd && sub == 0 && vec) {
+      const float4 p4 = *reinterpret_cast<const float4*>(a.params + vidx);
+      const float4 m4 = *reinterpret_cast<const float4*>(a.momentum + vidx);
+      pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
+      pm[0] = m4.x; pm[1] = m4.y; pm[2] = m4.z; pm[3] = m4.w;
     }
     // fc destinations in the weight images (no table lookups for fc)
     int fd[4];
@@ -1633,9 +1671,21 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         }
         ll_allreduce<4>(px, xt, idx, live, g, timeout_ticks, timed_out);
       }
+      if (vec) {
+        // MFMA layout (row 4kq + r, column l16) -> row layout through this wave's LDS slot
+        float* tr = pfc + wave * 256;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
+        for (int r = 0; r < 4; ++r) tr[(4 * kq + r) * 16 + l16] = g[r];
+        __builtin_amdgcn_wave_barrier();
+        const float4 gv = *reinterpret_cast<const float4*>(tr + (lane >> 2) * 16 + 4 * (lane & 3));
+        if (vrow < 50)
+          finish_param4<T>(a, vidx, gv, first, make_float4(pp[0], pp[1], pp[2], pp[3]),
+                           make_float4(pm[0], pm[1], pm[2], pm[3]), I_F1 + vrow * LD_F1 + vcol);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
+      }
       USTAMP(4);
     }
   }
