@@ -1621,7 +1621,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         USTAMP(1);
         c = mfma16(c, a0, b0);
       }
-    } else if (k0 < k1) {
+    } else if (live_wave && k0 < k1) {
       float a0[16], b0[16], a1[16], b1[16];
       load(k0, a0, b0);
       for (int s0 = k0; s0 < k1; s0 += 128) {
@@ -1653,7 +1653,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       __syncthreads();
     }
     USTAMP(3);
-    if (sub == 0) {
+    if (sub == 0 && live_wave) {  // (idle waves: no exchange polls, no stores)
       float g[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
