@@ -131,14 +131,13 @@ class FusedLeNetTrainer:
         self.xstage = torch.zeros((self.B, 784), dtype=torch.uint8, device=dev) if self.staged else None
         self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
         # one-kernel step (csed::lenet_step): training workgroups + trailing update
-        # workgroups that wait on a device counter, instead of two launches.  bar:
-        # its synchronisation words ([2] != 0: a timed-out wait).  CSED_ONE_KERNEL_STEP:
-        # "auto" (default) = one kernel on a single rank, two kernels with the fused
-        # exchange (in the one-kernel form its exchange role spills registers and it is
-        # unmeasured over xGMI), "1" = always, "0" = never.
+        # workgroups that wait on device flags, instead of two launches.
+        # CSED_ONE_KERNEL_STEP: "1" = use it, "0" / "auto" (default) = two kernels.  After
+        # the update-kernel changes (one fc tile per workgroup, idle waves skipped) the two
+        # graph-replayed launches beat it by ~0.2 us at batch 64 (profiles/one_kernel_step_r1.md):
+        # a kernel boundary inside a graph costs about what the in-kernel hand-off does.
         ok_mode = one_kernel_mode()
-        self.one_kernel = (self.staged and self.B <= fused_max_batch() and ok_mode != "0"
-                           and (ok_mode == "1" or not (self.comm and self.world > 1)))
+        self.one_kernel = self.staged and self.B <= fused_max_batch() and ok_mode == "1"
         self.bar = torch.zeros(int(torch.ops.csed.lenet_layout()[7]), dtype=torch.int32, device=dev)
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}

@@ -216,7 +216,7 @@ def test_one_kernel_step_matches_two_kernels(B, dampening):
     for one in (True, False):
         torch.manual_seed(3)
         eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B, dampening=dampening)
-        assert eng.one_kernel
+        assert eng.staged and not eng.one_kernel  # eligible; two kernels by default
         eng.one_kernel = one
         assert eng.step_kind.startswith("one kernel") == one
         eng.set_epoch_order(torch.randperm(len(data), generator=torch.Generator().manual_seed(5)))

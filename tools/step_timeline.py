@@ -25,7 +25,6 @@ def main():
     dev = torch.device("cuda")
     eng = FusedLeNetTrainer(Net().to(dev), synthetic_mnist(B * 400, seed=1), global_batch=B)
     eng.set_epoch_order(torch.randperm(B * 400))
-    assert eng.one_kernel
     ops = torch.ops.csed
     dbg = torch.zeros(B * 32, dtype=torch.long, device=dev)
     udbg = torch.zeros(8 * 256, dtype=torch.long, device=dev)
