@@ -43,14 +43,13 @@ def _ddp_worker(rank, world, port, q, bucket_mb):
     destroy()
 
 
-@pytest.mark.parametrize("bucket_mb", [25.0, 0.02])
-def test_ddp_matches_single_process_full_batch(bucket_mb):
+@pytest.mark.parametrize("world,bucket_mb", [(2, 25.0), (2, 0.02), (4, 0.02)])
+def test_ddp_matches_single_process_full_batch(world, bucket_mb):
     import torch.nn.functional as F
 
     from csed_514_project_distributed_training_using_pytorch_amd.models import Net
     from csed_514_project_distributed_training_using_pytorch_amd.optim import FusedSGD
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -63,19 +62,20 @@ def test_ddp_matches_single_process_full_batch(bucket_mb):
         assert p.exitcode == 0
     # replicas start identical (rank 0 broadcast) and stay bitwise identical
     res = [(r, torch.from_numpy(a), torch.from_numpy(b), c) for r, a, b, c in res]
-    assert torch.equal(res[0][1], res[1][1])
-    assert torch.equal(res[0][2], res[1][2])
+    for r in res[1:]:
+        assert torch.equal(res[0][1], r[1])
+        assert torch.equal(res[0][2], r[2])
     if bucket_mb < 1:
         assert len(res[0][3]) >= 2  # several buckets -> overlap with backward
-    # reference: one process, full batch of 16, same init
+    # reference: one process, full batch of 8 * world, same init
     net = Net().eval()
     torch.manual_seed(100)
     ref = Net().eval()
     opt = FusedSGD(ref.parameters(), lr=0.05, momentum=0.5)
     opt.flat.data.copy_(res[0][1])
     g = torch.Generator().manual_seed(7)
-    x = torch.randn(16, 1, 28, 28, generator=g)
-    t = torch.randint(0, 10, (16,), generator=g)
+    x = torch.randn(8 * world, 1, 28, 28, generator=g)
+    t = torch.randint(0, 10, (8 * world,), generator=g)
     for _ in range(3):
         opt.zero_grad()
         F.nll_loss(ref(x), t).backward()
