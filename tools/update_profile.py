@@ -29,8 +29,9 @@ def timeit(fn, n=200, reps=5):
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     dev = torch.device("cuda")
-    eng = FusedLeNetTrainer(Net().to(dev), synthetic_mnist(4096, seed=1), global_batch=B)
-    eng.set_epoch_order(torch.randperm(4096))
+    n = max(4096, B)
+    eng = FusedLeNetTrainer(Net().to(dev), synthetic_mnist(n, seed=1), global_batch=B)
+    eng.set_epoch_order(torch.randperm(n))
     ops = torch.ops.csed
     g = torch.empty(21840, device=dev)
 
