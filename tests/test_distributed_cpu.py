@@ -43,7 +43,7 @@ def _ddp_worker(rank, world, port, q, bucket_mb):
     destroy()
 
 
-@pytest.mark.parametrize("world,bucket_mb", [(2, 25.0), (2, 0.02), (4, 0.02)])
+@pytest.mark.parametrize("world,bucket_mb", [(2, 25.0), (2, 0.02), (4, 0.02), (8, 0.02)])
 def test_ddp_matches_single_process_full_batch(world, bucket_mb):
     import torch.nn.functional as F
 
