@@ -42,6 +42,20 @@ from ..parallel.ipc import allreduce_mode, make_allreduce, open_exchange, wait_t
 from ..utils.flat import FlatParams
 
 
+def _clear_hip_error() -> None:
+    """Reset this thread's sticky HIP error after a failed stream capture.  Our ops report
+    ``hipGetLastError()`` after each launch, so an invalidated capture would otherwise
+    surface as a failure of the next (eager) launch."""
+    import ctypes
+
+    try:  # the HIP runtime this process already loaded (via torch), never a second copy
+        with open("/proc/self/maps") as f:
+            paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+        for path in paths:
+            ctypes.CDLL(path).hipGetLastError()
+    except OSError:
+        pass
+
 
 def layout() -> tuple[int, int, int, int]:
     """Buffer sizes of the fused kernels, from the extension (csrc/kernels/lenet_fused.hip):
@@ -236,6 +250,7 @@ class FusedLeNetTrainer:
             g = self._capture(nsteps)
         except Exception as e:  # same code on every rank: every rank lands here
             print(f"[csed] step-graph capture failed while timing ({e!r})", file=sys.stderr)
+            _clear_hip_error()
             g = None
         us = float("inf")
         if g is not None:
@@ -404,12 +419,17 @@ class FusedLeNetTrainer:
         key = (nsteps, self.perm.data_ptr(), self.B)
         if key in self._graphs:
             return self._graphs[key]
+        if self.allreduce_kind == "rccl" and dist.is_initialized() and dist.get_backend() == "gloo":
+            # the process group's all-reduce runs on the host (gloo): nothing to capture
+            self.capture_comm_ok = False
+            return None
         try:
             g = self._capture(nsteps)
             self.capture_comm_ok = True
         except Exception as e:  # RCCL capture unsupported -> eager fallback
             print(f"[csed] HIP graph capture failed ({e!r}); running steps eagerly", file=sys.stderr)
             self.capture_comm_ok = False
+            _clear_hip_error()
             torch.cuda.synchronize(self.device)
             return None
         self._graphs[key] = g
