@@ -102,3 +102,4 @@ def test_graft_smoke_entry():
     r = _run(["-c", "import __graft_entry__ as g; g.smoke()"])
     assert r.returncode == 0, r.stderr[-3000:]
     assert "smoke ok" in r.stdout
+
