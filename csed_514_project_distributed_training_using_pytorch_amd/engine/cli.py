@@ -25,9 +25,9 @@ import torch
 from .. import ops
 from ..data import DeviceLoader, get_mnist
 from ..models import Net
-from ..parallel.comm import barrier, destroy, init_distributed
+from ..parallel.comm import barrier, destroy, init_distributed, replica_checksum
 from ..parallel.sampler import ShardSampler
-from ..utils import checkpoint, metrics, plot
+from ..utils import checkpoint, metrics, plot, prof
 
 
 def _dtype(name: str) -> torch.dtype:
@@ -195,6 +195,21 @@ def single_main(argv=None) -> int:
 
 
 # ========================================================================== dist
+def _check_replicas(args, ctx, net, epoch: int) -> None:
+    """--check-replicas E: every E epochs, all ranks must hold bitwise-identical parameters
+    (the reference's DDP guarantees it; a divergence means a broken exchange)."""
+    if not args.check_replicas or not ctx.is_distributed or (epoch + 1) % args.check_replicas:
+        return
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+    ok, lo, hi = replica_checksum(ctx, flat)
+    if not ok:
+        raise SystemExit(f"replica check failed after epoch {epoch}: parameter hashes differ across ranks "
+                         f"(min {lo}, max {hi})")
+    if ctx.is_main:
+        print(f"[csed] replica check after epoch {epoch}: parameters bitwise identical on {ctx.world_size} ranks "
+              f"(hash {lo})", flush=True)
+
+
 def dist_main(argv=None) -> int:
     t0 = time.time()  # ref: taken before rendezvous (src/train_dist.py:119)
     ap = argparse.ArgumentParser(description="data-parallel MNIST trainer (ref src/train_dist.py)")
@@ -210,7 +225,12 @@ def dist_main(argv=None) -> int:
     ap.add_argument("--backend", default=None, help="nccl (RCCL) | gloo (default: nccl on GPU)")
     ap.add_argument("--master-addr", default=None)
     ap.add_argument("--master-port", type=int, default=None)
-    ap.add_argument("--bucket-mb", type=float, default=25.0, help="gradient bucket cap (modular engine)")
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="gradient bucket cap of the modular engine's DDP reducer (default 25, one bucket); "
+                         "rejected with --engine fused, whose exchange is fused into its update kernel")
+    ap.add_argument("--check-replicas", type=int, default=0, metavar="E",
+                    help="every E epochs, compare a bitwise hash of the parameters across ranks "
+                         "(all-reduce MIN/MAX) and abort on divergence (0 = off)")
     ap.add_argument("--progress", action="store_true", help="tqdm bars (syncs every step, like the reference)")
     ap.add_argument("--reference-metrics", action="store_true",
                     help="reproduce the reference's metric quirks (loss/bs sums, mean-of-batch-means val)")
@@ -230,6 +250,10 @@ def dist_main(argv=None) -> int:
     if args.batch_size % ctx.world_size:
         raise SystemExit(f"global batch {args.batch_size} must be divisible by world size {ctx.world_size}")
     per_rank = args.batch_size // ctx.world_size
+    use_fused = dev.type == "cuda" and args.engine == "fused"
+    if use_fused and args.bucket_mb is not None:
+        raise SystemExit("--bucket-mb applies to --engine modular only: the fused engine's gradient exchange "
+                         "runs inside its update kernel (one 87 KB exchange per step, no buckets)")
     train, test_set = _load_data(args, dev)
     if train.synthetic and ctx.is_main:
         print("[csed] MNIST files not found: using synthetic 1x28x28 data of the same shape")
@@ -237,8 +261,8 @@ def dist_main(argv=None) -> int:
     test_loader = DeviceLoader(test_set, args.test_batch_size, shuffle=True, device=dev)
     net = Net().to(dev)
     hist = metrics.LossHistory()
-    hist.test_counter = [i * len(sampler) for i in range(args.epochs)]
-    use_fused = dev.type == "cuda" and args.engine == "fused"
+    # ref train_dist.py:89,153: counters in units of the whole training set (len(dataset))
+    hist.test_counter = [i * len(train) for i in range(args.epochs)]
     bar = None
     if args.progress and ctx.is_main:
         try:
@@ -251,42 +275,56 @@ def dist_main(argv=None) -> int:
 
         eng = FusedLeNetTrainer(net, train, lr=args.lr, momentum=args.momentum, global_batch=args.batch_size,
                                 ctx=ctx, compute_dtype=_dtype(args.dtype), seed=args.seed)
+        sampler.set_epoch(0)
+        order = sampler.indices()
         for i in range(args.epochs):
-            sampler.set_epoch(i)
-            eng.set_epoch_order(sampler.indices())
-            steps = eng.steps_per_epoch()
-            if bar is not None:
-                it = bar(range(steps))
-                for s in it:
-                    if s < eng.full_steps():
-                        eng.run_steps(1)
-                    else:
-                        eng.last_partial_step()
-                    lsum, _ = eng.take_loss()
-                    it.set_description(f"training batch_loss={lsum / per_rank:.4f}")
-                    hist.train_losses.append(lsum / per_rank)
-                    hist.train_counter.append(s * 64 + i * len(sampler))
-                epoch_loss_sum = sum(hist.train_losses[-steps:]) * per_rank
-            else:
-                eng.run_steps(eng.full_steps())
-                eng.last_partial_step()
-                epoch_loss_sum, _ = eng.take_loss()
-            vloss_sum, correct = eng.evaluate(test_set)
+            eng.set_epoch_order(order)
+            steps, full, rem = eng.steps_per_epoch(), eng.full_steps(), eng.tail_size()
+            with prof.range(f"train_epoch{i}"):
+                if bar is not None:
+                    it = bar(range(steps))
+                    for s in it:
+                        if s < full:
+                            eng.run_steps(1)
+                        else:
+                            eng.last_partial_step()
+                        lsum, _ = eng.take_loss()
+                        bl = lsum / (per_rank if s < full else rem)  # ref: mean over data.shape[0]
+                        it.set_description(f"training batch_loss={bl:.4f}")
+                        hist.train_losses.append(bl)
+                        hist.train_counter.append(s * 64 + i * len(train))
+                    full_sum = sum(hist.train_losses[-steps:][:full]) * per_rank
+                    tail_sum = hist.train_losses[-1] * rem if rem else 0.0
+                else:
+                    eng.run_steps(full)
+                    if i + 1 < args.epochs:  # next epoch's order on the host while the graphs run
+                        sampler.set_epoch(i + 1)
+                        order = sampler.indices()
+                    full_sum, _ = eng.take_loss()
+                    eng.last_partial_step()
+                    tail_sum, _ = eng.take_loss()
+            if bar is not None and i + 1 < args.epochs:
+                sampler.set_epoch(i + 1)
+                order = sampler.indices()
+            with prof.range(f"eval_epoch{i}"):
+                vloss_sum, correct = eng.evaluate(test_set)
             n_test = len(test_set)
             if args.reference_metrics:
                 # ref: sum over batches of (mean batch loss / batch size) (train_dist.py:86)
-                train_loss = epoch_loss_sum / per_rank / per_rank
+                train_loss = full_sum / per_rank / per_rank + (tail_sum / rem / rem if rem else 0.0)
                 val_loss = vloss_sum / args.test_batch_size / n_test  # mean of batch means / dataset size
             else:
-                train_loss = epoch_loss_sum / len(sampler)
+                train_loss = (full_sum + tail_sum) / len(sampler)
                 val_loss = vloss_sum / n_test
             hist.test_losses.append(val_loss)
             acc = 100.0 * correct / n_test
             print(metrics.dist_epoch_line(i, train_loss, val_loss, acc, time.time() - t0), flush=True)
+            _check_replicas(args, ctx, net, i)
     else:
         from .modular import ModularTrainer
 
-        tr = ModularTrainer(net, lr=args.lr, momentum=args.momentum, ctx=ctx, loss="ce", bucket_cap_mb=args.bucket_mb)
+        tr = ModularTrainer(net, lr=args.lr, momentum=args.momentum, ctx=ctx, loss="ce",
+                            bucket_cap_mb=25.0 if args.bucket_mb is None else args.bucket_mb)
         loader = DeviceLoader(train, per_rank, sampler=sampler, device=dev,
                               dtype=ops.compute_dtype() if dev.type == "cuda" else torch.float32)
         for i in range(args.epochs):
@@ -300,7 +338,7 @@ def dist_main(argv=None) -> int:
                     it.set_description(f"training batch_loss={loss.item():.4f}")
             ls = torch.stack(losses).double()
             hist.train_losses.extend(ls.tolist())
-            hist.train_counter.extend(b * 64 + i * len(sampler) for b in range(len(losses)))
+            hist.train_counter.extend(b * 64 + i * len(train) for b in range(len(losses)))
             total, correct, batch_means = tr.evaluate(test_loader)
             n_test = len(test_set)
             if args.reference_metrics:
@@ -312,6 +350,7 @@ def dist_main(argv=None) -> int:
             hist.test_losses.append(val_loss)
             acc = 100.0 * correct.item() / n_test
             print(metrics.dist_epoch_line(i, train_loss, val_loss, acc, time.time() - t0), flush=True)
+            _check_replicas(args, ctx, net, i)
 
     barrier(ctx)
     if ctx.is_main:

@@ -155,6 +155,8 @@ class FusedLeNetTrainer:
         self.bar = torch.zeros(int(torch.ops.csed.lenet_layout()[7]), dtype=torch.int32, device=dev)
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._eval_cache: dict[int, tuple] = {}
+        self._order_host: torch.Tensor | None = None
         self.capture_comm_ok: bool | None = None
         # gradient all-reduce.  Fallback step (3 kernels): the one-shot IPC kernel
         # (csrc/comm) when every rank passes its self-test, else RCCL (parallel/ipc.py).
@@ -272,6 +274,21 @@ class FusedLeNetTrainer:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def close(self) -> None:
+        """Release the graphs and the IPC buffers (collective on every rank: a barrier runs
+        first so that no peer is still pushing into this rank's buffers)."""
+        self._graphs.clear()
+        if (self.exch is not None or self.allreduce is not None) and dist.is_initialized():
+            torch.cuda.synchronize(self.device)
+            if self.ctx.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+        for comm in (self.exch, self.allreduce):
+            if comm is not None:
+                comm.close()
+        self.exch = self.allreduce = None
+
     def comm_errors(self) -> int:
         """Nonzero if an IPC exchange ever timed out waiting for a peer (synchronous)."""
         e = self.exch.error() if self.exch is not None else 0
@@ -287,10 +304,20 @@ class FusedLeNetTrainer:
         torch.ops.csed.lenet_pack(self.flat.data, self.wimg, self.mfma)
 
     def set_epoch_order(self, order: torch.Tensor) -> None:
-        """This rank's sample order for the epoch (int64 indices into the train set)."""
-        order = order.to(self.device, torch.long).contiguous()
+        """This rank's sample order for the epoch (int64 indices into the train set).
+
+        A host order is uploaded asynchronously from pinned memory (the host never waits for
+        the device here), so the next epoch's permutation can be prepared while the current
+        epoch's graphs still run."""
         if order.numel() < self.B:
             raise ValueError("epoch order shorter than one batch")
+        if order.device.type == "cpu":
+            host = order.to(torch.long).contiguous().pin_memory()
+            self._order_host = host  # alive until the copy below has run
+            order = torch.empty(host.shape, dtype=torch.long, device=self.device)
+            order.copy_(host, non_blocking=True)
+        else:
+            order = order.to(self.device, torch.long).contiguous()
         if self._graphs and order.numel() != self.perm.numel():
             self._graphs.clear()  # captured pointers refer to the old buffer
         if order.numel() == self.perm.numel():
@@ -307,6 +334,11 @@ class FusedLeNetTrainer:
                                        self.B, self.xstage, self.lstage)
 
 
+
+    @property
+    def kernel_names(self) -> str:
+        """The HIP kernels of one training step (reports)."""
+        return "lenet_train + lenet_update"
 
     @property
     def step_kind(self) -> str:
@@ -377,16 +409,28 @@ class FusedLeNetTrainer:
         """One full-batch training step at the device cursor (eager launches)."""
         self._launch_step(self.B, self.grid, 1.0 / self.global_batch, self.cursor, self.perm)
 
-    def last_partial_step(self) -> None:
-        """The epoch's final short batch (ref DataLoader drop_last=False semantics)."""
-        rem = self.perm.numel() - self.full_steps() * self.B
-        if rem <= 0:
-            return
-        tail = self.perm[self.full_steps() * self.B:].contiguous()
+    def tail_size(self) -> int:
+        """Per-rank samples of the epoch's short last batch (0 if the epoch divides evenly)."""
+        return self.perm.numel() - self.full_steps() * self.B
+
+    def _tail_step(self) -> None:
+        rem = self.tail_size()
+        tail = self.perm[self.full_steps() * self.B:]  # a view: stable pointer for graph replay
         gb = rem * self.world  # every rank has the same remainder (sampler pads to a multiple)
         self._launch_step(rem, min(rem, self.grid), 1.0 / gb, None, tail)
         # the tail step does not use the cursor; keep it consistent for the next epoch
         self.cursor.add_(1)
+
+    def last_partial_step(self, use_graph: bool = True) -> None:
+        """The epoch's final short batch (ref DataLoader drop_last=False semantics); replayed
+        from its own captured graph like the full steps."""
+        if self.tail_size() <= 0:
+            return
+        g = self.graph(1, tail=True) if use_graph and self.capture_comm_ok is not False else None
+        if g is not None:
+            g.replay()
+        else:
+            self._tail_step()
 
     # --------------------------------------------------------- graph capture
     def _state(self) -> list[torch.Tensor]:
@@ -394,7 +438,8 @@ class FusedLeNetTrainer:
         return [self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor, self.rng_offset,
                 self.loss_acc] + ([self.xstage, self.lstage] if self.staged else [])
 
-    def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
+    def _capture(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph:
+        step = self._tail_step if tail else self.step
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
         # snapshot the state the capture warm-up will advance; the side stream must
@@ -403,7 +448,7 @@ class FusedLeNetTrainer:
         saved = [t.clone() for t in state]
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            self.step()  # warm-up on the capture stream (lazy RCCL init etc.)
+            step()  # warm-up on the capture stream (lazy RCCL init etc.)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         for t, v in zip(state, saved):
@@ -411,12 +456,13 @@ class FusedLeNetTrainer:
         torch.cuda.synchronize(self.device)
         with torch.cuda.graph(g, stream=s):
             for _ in range(nsteps):
-                self.step()
+                step()
         torch.cuda.synchronize(self.device)
         return g
 
-    def graph(self, nsteps: int) -> torch.cuda.CUDAGraph | None:
-        key = (nsteps, self.perm.data_ptr(), self.B)
+    def graph(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph | None:
+        """The captured graph of ``nsteps`` full steps (or of the epoch's tail step), cached."""
+        key = (nsteps, self.perm.data_ptr(), self.perm.numel(), self.B, tail)
         if key in self._graphs:
             return self._graphs[key]
         if self.allreduce_kind == "rccl" and dist.is_initialized() and dist.get_backend() == "gloo":
@@ -424,7 +470,7 @@ class FusedLeNetTrainer:
             self.capture_comm_ok = False
             return None
         try:
-            g = self._capture(nsteps)
+            g = self._capture(nsteps, tail)
             self.capture_comm_ok = True
         except Exception as e:  # RCCL capture unsupported -> eager fallback
             print(f"[csed] HIP graph capture failed ({e!r}); running steps eagerly", file=sys.stderr)
@@ -435,10 +481,28 @@ class FusedLeNetTrainer:
         self._graphs[key] = g
         return g
 
-    def prepare(self, steps_per_graph: int = 16) -> None:
-        """Capture the step graphs up front (capture is never inside a timed region)."""
-        if self.graph(max(1, steps_per_graph)) is not None:
-            self.graph(1)
+    @staticmethod
+    def graph_plan(k: int, steps_per_graph: int) -> list[int]:
+        """Graph sizes that run k steps: whole graphs of min(spg, k) steps, then one graph for
+        the remainder (never a run of 1-step replays)."""
+        if k <= 0:
+            return []
+        spg = max(1, min(steps_per_graph, k))
+        full, rem = divmod(k, spg)
+        return [spg] * full + ([rem] if rem else [])
+
+    def prepare(self, steps_per_graph: int = 16, ks: tuple[int, ...] = (), tail: bool = True) -> None:
+        """Capture up front (capture is never inside a timed region) every graph that
+        ``run_steps(k, steps_per_graph)`` for k in ``ks`` (default: one epoch) and the
+        epoch's tail step will replay."""
+        sizes = set()
+        for k in (ks or (self.full_steps(),)):
+            sizes.update(self.graph_plan(k, steps_per_graph))
+        for n in sorted(sizes, reverse=True):
+            if self.graph(n) is None:
+                return
+        if tail and self.tail_size() > 0:
+            self.graph(1, tail=True)
 
     def run_steps(self, k: int, steps_per_graph: int = 16, use_graph: bool = True) -> None:
         """Advance k full-batch steps from the current cursor."""
@@ -448,22 +512,13 @@ class FusedLeNetTrainer:
             for _ in range(k):
                 self.step()
             return
-        spg = max(1, steps_per_graph)
-        full, rem = divmod(k, spg)
-        g = self.graph(spg) if full else None
-        if g is None and full:
-            for _ in range(k):
-                self.step()
-            return
-        for _ in range(full):
-            g.replay()
-        if rem:
-            g1 = self.graph(1)
-            for _ in range(rem):
-                if g1 is not None:
-                    g1.replay()
-                else:
+        for n in self.graph_plan(k, steps_per_graph):
+            g = self.graph(n)
+            if g is None:
+                for _ in range(n):
                     self.step()
+            else:
+                g.replay()
 
     def train_epoch(self, order: torch.Tensor, steps_per_graph: int = 16, use_graph: bool = True) -> None:
         self.set_epoch_order(order)
@@ -477,12 +532,22 @@ class FusedLeNetTrainer:
         self.loss_acc.zero_()
         return v[0], v[1]
 
+    def _device_data(self, data: MNISTData) -> tuple[MNISTData, torch.Tensor]:
+        """(``data`` on this engine's device, arange(len)), uploaded once per dataset object:
+        evaluation runs every epoch and its 10k test images must not be re-copied each time."""
+        hit = self._eval_cache.get(id(data))
+        if hit is None or hit[0] is not data:
+            dev = data if data.images.device == self.device else data.to(self.device)
+            hit = (data, dev, torch.arange(len(data), device=self.device))
+            self._eval_cache = {id(data): hit}
+        return hit[1], hit[2]
+
     @torch.no_grad()
     def evaluate(self, test: MNISTData, order: torch.Tensor | None = None) -> tuple[float, int]:
         """Forward-only pass over ``test``: (summed NLL, correct).  No dropout."""
-        test = test.to(self.device)
+        test, ar = self._device_data(test)
         n = len(test)
-        order = torch.arange(n, device=self.device) if order is None else order.to(self.device)
+        order = ar if order is None else order.to(self.device)
         nparts = min(n, 256)
         torch.ops.csed.lenet_eval(test.images, test.labels, order, n, self.wimg, self.flat.data, MNIST_MEAN,
                                   MNIST_STD, self.eval_parts, None, self.mfma)
@@ -491,10 +556,10 @@ class FusedLeNetTrainer:
 
     @torch.no_grad()
     def eval_logp(self, test: MNISTData) -> torch.Tensor:
-        test = test.to(self.device)
+        test, ar = self._device_data(test)
         n = len(test)
         out = torch.empty(n, 10, device=self.device)
-        torch.ops.csed.lenet_eval(test.images, test.labels, torch.arange(n, device=self.device), n, self.wimg,
+        torch.ops.csed.lenet_eval(test.images, test.labels, ar, n, self.wimg,
                                   self.flat.data, MNIST_MEAN, MNIST_STD, self.eval_parts, out, self.mfma)
         return out
 

@@ -122,3 +122,21 @@ def all_reduce_max(ctx: DistContext, value: float) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def replica_checksum(ctx: DistContext, t: torch.Tensor) -> tuple[bool, int, int]:
+    """Bitwise replica check: a position-weighted int64 hash of ``t``'s bit
+    pattern, reduced with MIN and MAX over the ranks.  Equal on every rank iff (up to hash
+    collisions) every replica holds the same bytes.  Returns (equal, min, max); collective."""
+    flat = t.detach().reshape(-1)
+    bits = flat.view(torch.int32) if flat.dtype == torch.float32 else flat.float().view(torch.int32)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) * 2 + 1
+    h = (bits.to(torch.int64) * w).sum()  # int64 arithmetic wraps: deterministic
+    if not ctx.is_distributed:
+        v = int(h.item())
+        return True, v, v
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    lo, hi = h.to(dev).clone(), h.to(dev).clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(lo.item() == hi.item()), int(lo.item()), int(hi.item())

@@ -102,6 +102,14 @@ class IpcAllReduce:
     def error(self, reset: bool = False) -> int:
         return int(torch.ops.csed.ipc_error(self.id, reset))
 
+    def close(self) -> None:
+        """Unmap the peers and free this rank's buffers (call after a process-group barrier,
+        so that no peer is still pushing into them).  Idempotent."""
+        if self.id >= 0:
+            with torch.cuda.device(self.ctx.device):
+                torch.ops.csed.ipc_destroy(self.id)
+            self.id = -1
+
     def self_test(self, rounds: int = 4) -> bool:
         """Exact sums of integer-valued data over several rounds (both slot parities),
         no timeout, and bitwise agreement with the process group's all-reduce.

@@ -17,6 +17,9 @@ int ipc_handle_bytes();
 hipError_t ipc_open(int id, const void* handles, int world, int rank);
 // out = sum over ranks of in (n floats, n % 4 == 0); in == out is allowed.
 hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double timeout_s, hipStream_t s);
+// Unmap the peers, free the buffers and retire the id (after a process-group barrier:
+// no peer may still be pushing into this rank's buffer).
+hipError_t ipc_destroy(int id);
 // Error word: nonzero if a wait ever timed out (synchronous read).
 hipError_t ipc_error(int id, int* err_out, bool reset);
 

@@ -213,6 +213,27 @@ hipError_t ipc_peers(int id, IpcPeers* out) {
   return hipSuccess;
 }
 
+hipError_t ipc_destroy(int id) {
+  IpcComm* c = get(id);
+  if (!c) return hipErrorInvalidValue;
+  // every queued kernel that reads or writes the mappings must be done first; the caller
+  // runs a process-group barrier before this, so no peer is still pushing into `buf`
+  hipError_t e = hipDeviceSynchronize();
+  for (int r = 0; r < c->world; ++r)
+    if (r != c->rank && c->peers.base[r]) {
+      const hipError_t e2 = hipIpcCloseMemHandle(c->peers.base[r]);
+      if (e == hipSuccess) e = e2;
+    }
+  for (void* p : {(void*)c->buf, (void*)c->counters, (void*)c->err})
+    if (p) {
+      const hipError_t e2 = hipFree(p);
+      if (e == hipSuccess) e = e2;
+    }
+  registry()[id] = nullptr;
+  delete c;
+  return e;
+}
+
 hipError_t ipc_error(int id, int* err_out, bool reset) {
   IpcComm* c = get(id);
   if (!c) return hipErrorInvalidValue;

@@ -1722,11 +1722,11 @@ template <typename T, bool EXCH>
 __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
                                                              int B, float* loss_parts, int nparts,
                                                              float* loss_acc, comm::IpcPeers px,
-                                                             uint64_t timeout_ticks) {
+                                                             uint64_t timeout_ticks, int fc_tpb) {
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
   update_role<T, EXCH, false, UP_NT>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
-                       threadIdx.x, &part[0][0], &part2[0][0], nullptr, 0);
+                       threadIdx.x, &part[0][0], &part2[0][0], nullptr, 0, fc_tpb);
 }
 
 // SGD from an already-reduced gradient (DDP: after the all-reduce).
@@ -1796,24 +1796,28 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     return hipGetLastError();
   }
   if (!a.vslab || a.B <= 0) return hipErrorInvalidValue;
-  const int nblocks = update_blocks(a.B);
   comm::IpcPeers px{};
   if (a.exch_id >= 0) {
-    // fused data-parallel exchange: the buffer must hold this kernel's word layout
+    // fused data-parallel exchange: the buffer must hold this kernel's word layout.  The
+    // exchange tag is a per-workgroup call counter, so the workgroup -> exchange-word map
+    // must not depend on the batch: one FC tile per workgroup (NB_UPDATE workgroups) for
+    // every B, the full steps' and the epoch tail's alike (a batch-dependent layout let
+    // the counters of different words drift apart between steps of different batch sizes).
     static_assert(NB_UPDATE <= comm::kIpcMaxBlocks, "one exchange counter per update workgroup");
     const hipError_t e = comm::ipc_peers(a.exch_id, &px);
     if (e != hipSuccess) return e;
     if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
     CSED_DISPATCH_MFMA(a.mfma_dtype, {
-      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
-                         a.B, loss_parts, nparts, loss_acc, px, ticks);
+      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+                         a.B, loss_parts, nparts, loss_acc, px, ticks, 1);
     });
     return hipGetLastError();
   }
+  const int nblocks = update_blocks(a.B);
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
-                       a.B, loss_parts, nparts, loss_acc, px, (uint64_t)0);
+                       a.B, loss_parts, nparts, loss_acc, px, (uint64_t)0, 0);
   });
   return hipGetLastError();
 }
@@ -1836,10 +1840,11 @@ hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, 
   fz.u = u; fz.loss_parts = loss_parts; fz.nparts = nparts; fz.loss_acc = loss_acc; fz.bar = bar;
   // FC tiles per workgroup: as lenet_update, or CSED_FC_TPB (1..8) for experiments
   fz.fc_tpb = fc_tiles_per_block(u.B, UPD_NTH, true);
+  const bool exch = u.exch_id >= 0;
   if (const char* e = std::getenv("CSED_FC_TPB")) fz.fc_tpb = std::max(1, std::min(8, std::atoi(e)));
+  if (exch) fz.fc_tpb = 1;  // the exchange's fixed workgroup -> word map (see launch_lenet_update)
   fz.nupd = (FC_TILES + fz.fc_tpb - 1) / fz.fc_tpb + conv_blocks(UPD_NTH);
   fz.timeout_ticks = (uint64_t)(u.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
-  const bool exch = u.exch_id >= 0;
   if (exch) {
     const hipError_t e = comm::ipc_peers(u.exch_id, &fz.px);
     if (e != hipSuccess) return e;

@@ -116,11 +116,13 @@ def test_distributed_cli_cpu_two_ranks(tmp_path):
     r = _run([sys.executable, "-m", "csed_514_project_distributed_training_using_pytorch_amd.parallel.launch",
               "--nproc", "2", "--timeout", "240", "src/train_dist.py", "--device", "cpu", "--synthetic",
               "--epochs", "2", "--train-size", "512", "--test-size", "200", "--engine", "modular",
-              "--out-dir", str(tmp_path), "--bucket-mb", "0.02"])
+              "--out-dir", str(tmp_path), "--bucket-mb", "0.02", "--check-replicas", "1"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("Epoch=")]
     assert len(lines) == 4  # 2 epochs x 2 ranks print (every VM printed in the reference)
     assert "time_elapsed=" in lines[0]
+    # the per-epoch cross-rank parameter hash ran and found identical replicas
+    assert r.stdout.count("parameters bitwise identical on 2 ranks") == 2
     sd = torch.load(tmp_path / "model.pt", weights_only=True)
     assert "conv1.weight" in sd and not any(k.startswith("module.") for k in sd)
 
@@ -137,3 +139,30 @@ def test_p2p_smoke_two_ranks():
     assert p0.returncode == 0 and p1.returncode == 0
     assert "Rank  0  has data  tensor(1.)" in o0
     assert "Rank  1  has data  tensor(1.)" in o1
+
+
+def test_bench_self_spawns_ranks_cpu():
+    """bench.py --gpus N without a torchrun environment starts N ranks itself (one per GPU;
+    here gloo on the CPU) and rank 0 prints exactly one JSON line whose n_gpus is the
+    process group's size."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--device", "cpu",
+                        "--steps", "3", "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(js) == 1, r.stdout
+    import json
+
+    rec = json.loads(js[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["process_group"] == {"backend": "gloo", "ranks": 2}
+    assert rec["config"]["parallelism"] == "dp2" and rec["steps"] == 3 and rec["value"] > 0
+    assert rec["time_elapsed_s"] > 0
+
+
+def test_bench_rejects_world_size_mismatch_cpu():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup",
+                        "0"], cwd=ROOT, capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+

@@ -160,23 +160,27 @@ def test_fused_eval_matches_reference():
 
 
 def test_fused_training_converges_with_dropout_and_graphs():
-    train = synthetic_mnist(4096, seed=3)
+    """Three epochs over 12,800 samples of the (deliberately hard) synthetic set with dropout
+    and graph replay: the test NLL must fall well below chance and accuracy must rise far
+    above 10 % (the CPU reference reaches 86 % after a full 60k epoch)."""
+    n = 12800
+    train = synthetic_mnist(n, seed=3)
     test = synthetic_mnist(1000, seed=4, train=False)
     torch.manual_seed(1)
     net = Net()
     eng = FusedLeNetTrainer(net.to(DEV), train, lr=0.02, momentum=0.5, global_batch=64)
     l0, _ = eng.evaluate(test)
-    for epoch in range(2):
+    for epoch in range(3):
         g = torch.Generator()
         g.manual_seed(epoch)
-        eng.train_epoch(torch.randperm(4096, generator=g), steps_per_graph=8)
+        eng.train_epoch(torch.randperm(n, generator=g), steps_per_graph=8)
     torch.cuda.synchronize()
     l1, c1 = eng.evaluate(test)
     assert math.isfinite(l1)
     assert l1 < 0.5 * l0, (l0, l1)
-    assert c1 > 700
+    assert c1 > 600, c1
     assert eng.capture_comm_ok is True
-    assert eng.step_count.item() == 2 * 64
+    assert eng.step_count.item() == 3 * (n // 64)
 
 
 @pytest.mark.parametrize("B", [64, 24])
@@ -234,3 +238,40 @@ def test_one_kernel_step_matches_two_kernels(B, dampening):
         else:
             assert a == b
     assert finals[0][3] == 4 and finals[0][4] == 4
+
+
+@pytest.mark.parametrize("dtype,band", [(torch.bfloat16, 0.05), (torch.float16, 0.03)])
+def test_fused_trajectory_matches_cpu_reference(dtype, band):
+    """50 SGD steps with dropout off: the fused GPU engine vs the reference recipe on the CPU
+    (stock fp32 ``Net`` + ``torch.optim.SGD``, ref src/train.py:69-85), same initial weights,
+    same batches in the same order.  The per-step training losses must track each other
+    within the dtype's band over the whole trajectory, and so must the final weights."""
+    n, B, steps = 64 * 50, 64, 50
+    data = synthetic_mnist(n, seed=17)
+    order = torch.randperm(n, generator=torch.Generator().manual_seed(3))
+    torch.manual_seed(1)
+    ref = Net()
+    net = Net()
+    net.load_state_dict(ref.state_dict())
+    eng = FusedLeNetTrainer(net.to(DEV), data, lr=0.02, momentum=0.5, global_batch=B, compute_dtype=dtype,
+                            drop_p=0.0)
+    eng.set_epoch_order(order)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.02, momentum=0.5)
+    ref.eval()  # no dropout (Net has no other train/eval difference)
+    x_all = ((data.images.float() / 255.0 - MNIST_MEAN) / MNIST_STD).unsqueeze(1)
+    gpu_l, cpu_l = [], []
+    for s in range(steps):
+        eng.step()
+        lsum, _ = eng.take_loss()
+        gpu_l.append(lsum / B)
+        idx = order[s * B:(s + 1) * B]
+        opt.zero_grad()
+        loss = F.nll_loss(ref(x_all[idx]), data.labels[idx])
+        loss.backward()
+        opt.step()
+        cpu_l.append(loss.item())
+    gl, cl = torch.tensor(gpu_l), torch.tensor(cpu_l)
+    assert cl[-10:].mean() < 0.9 * cl[:5].mean()  # the reference itself learned something
+    assert ((gl - cl).abs() / cl).max() < band, list(zip(gpu_l, cpu_l))
+    for (name, p_ref), p in zip(ref.named_parameters(), net.parameters()):
+        assert _rel(p.detach().cpu(), p_ref.detach()) < band, name
