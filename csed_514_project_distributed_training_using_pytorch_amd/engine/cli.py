@@ -31,7 +31,7 @@ from ..utils import checkpoint, metrics, plot, prof
 
 
 def _dtype(name: str) -> torch.dtype:
-    return {"bf16": torch.bfloat16, "fp16": torch.float16}[name]
+    return {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[name]
 
 
 def _common_flags(ap: argparse.ArgumentParser) -> None:
@@ -41,7 +41,9 @@ def _common_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--test-size", type=int, default=None, help="synthetic test set size (default 10000)")
     ap.add_argument("--device", default=None, help="cuda | cpu (default: cuda if available)")
     ap.add_argument("--engine", choices=["fused", "modular"], default="fused")
-    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16", help="GPU compute dtype (fp32 masters)")
+    ap.add_argument("--dtype", choices=["bf16", "fp16", "fp32"], default="bf16",
+                    help="GPU compute dtype: bf16 / fp16 MFMA operands with fp32 masters, or exact fp32 "
+                         "(v_mfma_f32_16x16x4_f32, the reference's precision)")
     ap.add_argument("--no-plot", action="store_true")
     ap.add_argument("--out-dir", default=".", help="where images/, results/ and model.pt are written")
 

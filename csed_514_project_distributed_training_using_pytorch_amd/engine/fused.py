@@ -106,6 +106,8 @@ class FusedLeNetTrainer:
         self.global_batch = int(global_batch)
         self.B = self.global_batch // self.world
         self.grid = int(grid) if grid else min(self.B, 256)
+        if compute_dtype not in _native.MFMA_CODE:
+            raise ValueError(f"compute dtype {compute_dtype}: expected bfloat16, float16 or float32")
         self.lr, self.momentum, self.dampening = float(lr), float(momentum), float(dampening)
         self.weight_decay, self.nesterov = float(weight_decay), bool(nesterov)
         self.mfma = _native.MFMA_CODE[compute_dtype]
@@ -141,7 +143,9 @@ class FusedLeNetTrainer:
         self.perm = torch.arange(self.B, dtype=torch.long, device=dev)
         # batch staging (per-rank batch <= stage_max): lenet_update gathers the next step's
         # pixels + labels one step ahead, so lenet_train starts with no dependent index chain
-        self.staged = self.B <= stage_max and self.grid == self.B
+        # (the exact-fp32 kernel, lenet_fused_f32.hip, gathers its samples itself)
+        self.fp32 = compute_dtype == torch.float32
+        self.staged = self.B <= stage_max and self.grid == self.B and not self.fp32
         self.xstage = torch.zeros((self.B, 784), dtype=torch.uint8, device=dev) if self.staged else None
         self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
         # one-kernel step (csed::lenet_step): training workgroups + trailing update
@@ -338,7 +342,7 @@ class FusedLeNetTrainer:
     @property
     def kernel_names(self) -> str:
         """The HIP kernels of one training step (reports)."""
-        return "lenet_train + lenet_update"
+        return "lenet_train_f32 + lenet_update" if self.fp32 else "lenet_train + lenet_update"
 
     @property
     def step_kind(self) -> str:

@@ -20,7 +20,8 @@ _loaded = False
 _error: Exception | None = None
 
 BF16, F16, F32 = 1, 2, 0
-MFMA_CODE = {torch.bfloat16: BF16, torch.float16: F16}
+# compute dtype -> kernel code: 16-bit MFMA operands, or exact fp32 (v_mfma_f32_16x16x4_f32)
+MFMA_CODE = {torch.bfloat16: BF16, torch.float16: F16, torch.float32: F32}
 
 
 def so_path() -> Path:

@@ -46,6 +46,13 @@ int mcode(int64_t mfma_dtype) {
   return (int)mfma_dtype;
 }
 
+// fused LeNet kernels: bf16 / fp16 MFMA, or exact fp32 (0: v_mfma_f32_16x16x4_f32)
+int lcode(int64_t mfma_dtype) {
+  TORCH_CHECK(mfma_dtype == csed::kBF16 || mfma_dtype == csed::kF16 || mfma_dtype == csed::kF32,
+              "csed: fused LeNet dtype must be fp32 (0), bf16 (1) or fp16 (2)");
+  return (int)mfma_dtype;
+}
+
 void dev(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), "csed: ", name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), "csed: ", name, " must be contiguous");
@@ -296,7 +303,7 @@ void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
   TORCH_CHECK(params.scalar_type() == at::kFloat && params.numel() >= csed::lenet_param_count());
   TORCH_CHECK(wimg.numel() >= csed::lenet_wimg_elems() && wimg.element_size() == 2);
   const c10::DeviceGuard gd(params.device());
-  CHECK_HIP(csed::launch_lenet_pack(params.data_ptr<float>(), (uint16_t*)wimg.data_ptr(), mcode(mfma_dtype),
+  CHECK_HIP(csed::launch_lenet_pack(params.data_ptr<float>(), (uint16_t*)wimg.data_ptr(), lcode(mfma_dtype),
                                     cur_stream(params)));
 }
 
@@ -323,7 +330,10 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   a.wimg = (const uint16_t*)wimg.data_ptr(); a.params = params.data_ptr<float>(); a.slab = slab.data_ptr<float>();
   a.vslab = vslab.data_ptr<float>(); a.loss_acc = loss_parts.data_ptr<float>(); a.grad_scale = (float)grad_scale; a.mean = (float)mean;
   a.std_ = (float)std_; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.rng_offset = optpt<int64_t>(rng_offset);
-  a.grid = (int)grid; a.mfma_dtype = mcode(mfma_dtype);
+  a.grid = (int)grid; a.mfma_dtype = lcode(mfma_dtype);
+  if (a.mfma_dtype == csed::kF32)
+    TORCH_CHECK(grid <= 256 && !xstage.has_value() && !dbg.has_value(),
+                "lenet_train fp32: grid <= 256, no batch staging, no stage stamps");
   if (dbg.has_value()) {
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 32 * grid, "dbg: int64 [grid*32]");
     a.dbg = (uint64_t*)dbg->data_ptr<int64_t>();
@@ -405,7 +415,7 @@ csed::LenetUpdateArgs update_args(const Tensor& slab, int64_t grid, const Tensor
   a.lr = (float)lr; a.mom = (float)mom; a.dampening = (float)dampening; a.weight_decay = (float)weight_decay;
   a.nesterov = nesterov ? 1 : 0; a.step = step.data_ptr<int64_t>(); a.ticket = ticket.data_ptr<int>();
   a.cursor = optpt<int64_t>(cursor); a.rng_offset = optpt<int64_t>(rng_offset);
-  a.apply_sgd = apply_sgd ? 1 : 0; a.mfma_dtype = mcode(mfma_dtype);
+  a.apply_sgd = apply_sgd ? 1 : 0; a.mfma_dtype = lcode(mfma_dtype);
   if (dbg.has_value()) {
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 256, "lenet_update: dbg must be int64[>=2048]");
     a.dbg = (uint64_t*)dbg->data_ptr();
@@ -441,6 +451,7 @@ void lenet_step(const Tensor& images, const Tensor& labels, const Tensor& perm, 
                 Tensor& loss_acc, Tensor& bar, const optional<Tensor>& dbg, const optional<Tensor>& udbg,
                 int64_t exch_id, double exch_timeout_s) {
   dev(bar, "bar");
+  TORCH_CHECK(mfma_dtype != csed::kF32, "lenet_step: the one-kernel step has no fp32 form");
   TORCH_CHECK(bar.scalar_type() == at::kInt && bar.numel() >= csed::lenet_step_bar_ints(),
               "lenet_step: bar must be int32[", csed::lenet_step_bar_ints(), "]");
   const c10::DeviceGuard gd(images.device());
@@ -465,7 +476,7 @@ void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order,
   CHECK_HIP(csed::launch_lenet_eval(images.data_ptr<uint8_t>(), labels.data_ptr<int64_t>(), order.data_ptr<int64_t>(),
                                     n, (const uint16_t*)wimg.data_ptr(), params.data_ptr<float>(), (float)mean,
                                     (float)std_, out_parts.data_ptr<float>(), optpt<float>(logp_out),
-                                    mcode(mfma_dtype), cur_stream(images)));
+                                    lcode(mfma_dtype), cur_stream(images)));
 }
 
 }  // namespace

@@ -26,6 +26,15 @@
     default: return hipErrorInvalidValue;                    \
   }
 
+// lenet_update / SGD: the 16-bit weight-image dtypes, or fp32 (no images).
+#define CSED_DISPATCH_UPDATE(code, ...)                      \
+  switch (code) {                                            \
+    CSED_CASE(::csed::kBF16, __bf16, __VA_ARGS__)            \
+    CSED_CASE(::csed::kF16, _Float16, __VA_ARGS__)           \
+    CSED_CASE(::csed::kF32, float, __VA_ARGS__)              \
+    default: return hipErrorInvalidValue;                    \
+  }
+
 namespace csed {
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 }  // namespace csed

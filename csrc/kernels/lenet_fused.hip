@@ -48,6 +48,7 @@
 //   fc1.b 21280, fc2.w 21330, fc2.b 21830.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "comm/ipc_allreduce.h"
 #include "common.h"
@@ -1191,11 +1192,15 @@ __device__ __forceinline__ void image_slots(int i, int& d0, int& d1) {
   }
 }
 
+// (T = float: the fp32 path, lenet_fused_f32.hip, reads the fp32 master parameters and
+// keeps no weight images)
 template <typename T>
 __device__ __forceinline__ void write_slots(unsigned short* wimg, int d0, int d1, float v) {
-  const unsigned short h = h16<T>(v);
-  if (d0 >= 0) wimg[d0] = h;
-  if (d1 >= 0) wimg[d1] = h;
+  if constexpr (!std::is_same<T, float>::value) {
+    const unsigned short h = h16<T>(v);
+    if (d0 >= 0) wimg[d0] = h;
+    if (d1 >= 0) wimg[d1] = h;
+  }
 }
 
 template <typename T>
@@ -1348,11 +1353,11 @@ __device__ __forceinline__ void finish_param4(const LenetUpdateArgs& a, int i, f
       d = a.nesterov ? fmaf(a.mom, bj, gj) : bj;
     }
     pv[j] = fmaf(-a.lr, d, pv[j]);
-    h[j] = h16<T>(pv[j]);
+    if constexpr (!std::is_same<T, float>::value) h[j] = h16<T>(pv[j]);
   }
   if (a.mom != 0.f) *reinterpret_cast<float4*>(a.momentum + i) = make_float4(mv[0], mv[1], mv[2], mv[3]);
   *reinterpret_cast<float4*>(a.params + i) = make_float4(pv[0], pv[1], pv[2], pv[3]);
-  *reinterpret_cast<u16x4*>(a.wimg + d0) = h;
+  if constexpr (!std::is_same<T, float>::value) *reinterpret_cast<u16x4*>(a.wimg + d0) = h;
 }
 
 // ---------------------------------------------------------------------------
@@ -1767,6 +1772,7 @@ int64_t lenet_conv_param_count() { return CNP_PAD; }
 int64_t lenet_vec_len() { return VEC; }
 
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
+  if (a.mfma_dtype == kF32) return launch_lenet_train_f32(a, 0, nullptr, true, s);  // lenet_fused_f32.hip
   if (a.B <= 0 || a.grid <= 0 || a.grid > a.B) return hipErrorInvalidValue;
   // a staged batch has one sample per workgroup (the STAGED instantiation relies on it)
   if (a.xstage && (a.grid != a.B || !a.lstage)) return hipErrorInvalidValue;
@@ -1790,7 +1796,7 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
                                hipStream_t s) {
   if (a.apply_sgd && a.grad_in) {
-    CSED_DISPATCH_MFMA(a.mfma_dtype, {
+    CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       hipLaunchKernelGGL(lenet_sgd_kernel<scalar_t>, dim3(cdiv(NP, 256)), dim3(256), 0, s, a);
     });
     return hipGetLastError();
@@ -1808,14 +1814,14 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     if (e != hipSuccess) return e;
     if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
-    CSED_DISPATCH_MFMA(a.mfma_dtype, {
+    CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
                          a.B, loss_parts, nparts, loss_acc, px, ticks, 1);
     });
     return hipGetLastError();
   }
   const int nblocks = update_blocks(a.B);
-  CSED_DISPATCH_MFMA(a.mfma_dtype, {
+  CSED_DISPATCH_UPDATE(a.mfma_dtype, {
     hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
                        a.B, loss_parts, nparts, loss_acc, px, (uint64_t)0, 0);
   });
@@ -1878,6 +1884,7 @@ hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hi
 }
 
 hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype, hipStream_t s) {
+  if (mfma_dtype == kF32) return hipSuccess;  // the fp32 kernels read the master parameters
   CSED_DISPATCH_MFMA(mfma_dtype, {
     hipLaunchKernelGGL(lenet_pack_kernel<scalar_t>, dim3(cdiv(NP, 256)), dim3(256), 0, s, params,
                        (unsigned short*)wimg);
@@ -1897,6 +1904,7 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   a.B = (int)n; a.wimg = wimg; a.params = params; a.slab = nullptr; a.loss_acc = out;
   a.grad_scale = 0.f; a.mean = mean; a.std_ = std_; a.drop_p = 0.f; a.seed = 0; a.rng_offset = nullptr;
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
+  if (mfma_dtype == kF32) return launch_lenet_train_f32(a, logp_out ? 1 : 0, logp_out, false, s);
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
     hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false, 0>,

@@ -1,0 +1,541 @@
+// Fused LeNet (ref src/model.py:4-22) training step in exact fp32, for gfx950.
+//
+// The reference trains in fp32 everywhere (ref src/model.py defaults, CPU torch).  This is
+// the like-for-like path: every operand and every product is fp32, matrix work runs on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation: the same arithmetic as an
+// fmaf chain), so gradients agree with the CPU reference to fp32 rounding instead of a
+// 16-bit band.  It writes exactly the outputs of the 16-bit kernel (lenet_fused.hip): the
+// per-workgroup conv slab, the per-sample fc vector slab and the loss partials, so the same
+// lenet_update kernel reduces them (its fp32 instantiation reads no weight images: this
+// kernel reads the fp32 master parameters directly).
+//
+// Work per sample (one 1024-thread workgroup = 16 waves owns samples g, g+G, ...):
+//
+//   conv1 fwd   MFMA  [576 px x 28] . [28 x 16]   36 tiles x 7 K-steps, pool-fused pixel order
+//   conv2 fwd   MFMA  [64 px x 252] . [252 x 32]  8 tiles x 63 K-steps, K split over 2 waves
+//   fc1 fwd     VALU  16,000 MACs: 16 segments of 20 inputs per lane, fixed-order combine
+//   fc2 + log_softmax + NLL + dlogits + dZ1: one wave (as the 16-bit kernel)
+//   fc1 dX      VALU  16,000 MACs: 3 output ranges per input, fixed-order combine
+//   conv2 wgrad MFMA  [32 oc x 64 px] . [64 x 256] (col 250 = ones: bias grad), 16 tiles x 16
+//   conv2 dgrad MFMA  [144 px x 500] . [500 x 16] 9 tiles x 125 K-steps, K = (oc, tap) with
+//                     lane group q owning oc = 4j + q, so every address is a lane constant
+//                     plus an immediate; units of 25 K-steps split over the 16 waves
+//   conv1 wgrad VALU  only the pool1 argmax pixels carry gradient: 10 x 25 x 144 MACs
+//                     (a quarter of the dense 576-pixel GEMM, which would need 288 MFMAs)
+//
+// MFMA f32 16x16x4 operand layout: lane l holds A[row l&15][k 4*ks + (l>>4)] and
+// B[k 4*ks + (l>>4)][col l&15]; accumulator register j holds C[4*(l>>4) + j][l&15].  Padding
+// rows / columns of A / B only feed discarded outputs; K padding reads exact zeros.
+#include "common.h"
+#include "dispatch.h"
+
+namespace csed {
+namespace lenet32 {
+
+constexpr int NT = 1024, NW = 16;
+constexpr int NP = 21840;
+constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O_F1B = 21280,
+              O_F2W = 21330, O_F2B = 21830;
+constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;  // = lenet_fused.hip
+constexpr int LW1 = 321;  // fc1 weight row stride (odd: the fc1-forward lanes walk rows)
+constexpr int LW2 = 260;  // conv2 weight row stride (== 4 mod 64: conflict-free B fragments)
+
+// LDS carve, floats (every region 16-byte aligned)
+constexpr int F_W1 = 0;                       // fc1.w  [50][LW1]
+constexpr int F_W2 = F_W1 + 16052;            // conv2.w [20][LW2], cols 250..259 zero
+constexpr int F_W1B = F_W2 + 20 * LW2;        // conv1 B operand [16 n][28 k], zero padded
+constexpr int F_PAR = F_W1B + 448;            // c1b 0, c2b 10, f1b 30, f2b 80, f2w 90 (500)
+constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
+constexpr int F_X = F_PAR + 592;              // normalised pixels [784] (+ pad)
+constexpr int F_P1 = F_X + 788;               // pool1 output [10][144]
+constexpr int F_P2 = F_P1 + 1444;             // pool2 output = fc1 input [20][16]
+constexpr int F_DY2 = F_P2 + 320;             // dL/dconv2 [20][64], zero word at 1280
+constexpr int F_G1 = F_DY2 + 1284;            // gated dL/dP1 [10][144]
+constexpr int F_ONES = F_G1 + 1440;           // 96 ones (conv2 wgrad bias column)
+constexpr int F_ZEROS = F_ONES + 96;          // 96 zeros (its padding columns)
+constexpr int F_SM = F_ZEROS + 96;            // D2S 0, D1S 32, H 96, DZ1 160, label 224
+constexpr int F_RED = F_SM + 256;             // reduction scratch [8192]
+constexpr int F_END = F_RED + 8192;
+constexpr int B_I1 = F_END * 4;               // u8  [1440] pool1 argmax
+constexpr int B_I2 = B_I1 + 1440;             // u8  [320]  pool2 argmax
+constexpr int B_XPOS = B_I2 + 320;            // u16 [1440] X offset of the pool1 argmax pixel
+constexpr int B_K2 = B_XPOS + 2880;           // u16 [256]  conv2 fwd: k -> P1 offset
+constexpr int LDS_BYTES = B_K2 + 512;
+static_assert(LDS_BYTES <= 160 * 1024, "lds");
+static_assert(F_W2 % 4 == 0 && F_W1B % 4 == 0 && F_PAR % 4 == 0 && F_X % 4 == 0 && F_P1 % 4 == 0 &&
+                  F_P2 % 4 == 0 && F_DY2 % 4 == 0 && F_G1 % 4 == 0 && F_ONES % 4 == 0 && F_SM % 4 == 0 &&
+                  F_RED % 4 == 0,
+              "align");
+constexpr int S_D2S = 0, S_D1S = 32, S_H = 96, S_DZ1 = 160, S_LAB = 224;
+
+// An index the compiler cannot relate across loop iterations: the per-sample body takes its
+// lane indices through it, so hipcc does not hoist every lane-dependent LDS address of every
+// stage out of the sample loop (long-lived registers, scratch spills).
+__device__ __forceinline__ int opaque(int x) {
+  asm("" : "+v"(x));
+  return x;
+}
+
+__device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// conv2 dgrad work units: (tile t < 9, oc block j < 5) of 25 K-steps, tile-major; wave w owns
+// units [unit_lo(w), unit_lo(w + 1)): at most 3 units spanning at most 2 tiles
+__host__ __device__ constexpr int unit_lo(int w) { return (w * 45) / NW; }
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* L = reinterpret_cast<float*>(smem);
+  float* W1 = L + F_W1;
+  float* W2 = L + F_W2;
+  float* W1B = L + F_W1B;
+  float* PAR = L + F_PAR;
+  float* X = L + F_X;
+  float* P1 = L + F_P1;
+  float* P2 = L + F_P2;
+  float* DY2 = L + F_DY2;
+  float* G1 = L + F_G1;
+  float* SM = L + F_SM;
+  float* RED = L + F_RED;
+  uint8_t* I1 = smem + B_I1;
+  uint8_t* I2 = smem + B_I2;
+  unsigned short* XPOS = reinterpret_cast<unsigned short*>(smem + B_XPOS);
+  unsigned short* K2 = reinterpret_cast<unsigned short*>(smem + B_K2);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kq = lane >> 4;
+  const int G = gridDim.x, g = blockIdx.x;
+  const float inv_std = 1.f / a.std_;
+  const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
+  const int nsamp = g < a.B ? (a.B - g + G - 1) / G : 0;
+  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
+  auto row_of = [&](int s) { return a.perm[min(pbase + (int64_t)min(s, max(nsamp - 1, 0)) * G, a.perm_len - 1)]; };
+
+  // ---------------- once per workgroup: fp32 parameters -> LDS, constant tables
+  {
+    const float4* f1 = reinterpret_cast<const float4*>(a.params + O_F1W);  // 4000 float4
+    for (int q = tid; q < 4000; q += NT) {
+      const float4 v = f1[q];
+      const int e = 4 * q, o = e / 320, i = e - o * 320;  // 320 % 4 == 0: no row crossing
+      float* d = W1 + o * LW1 + i;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    for (int q = tid; q < 20 * LW2; q += NT) {
+      const int oc = q / LW2, k = q - oc * LW2;
+      W2[q] = k < 250 ? a.params[O_C2W + oc * 250 + k] : 0.f;
+    }
+    if (tid < 448) {
+      const int n = tid / 28, k = tid - n * 28;
+      W1B[tid] = (n < 10 && k < 25) ? a.params[O_C1W + n * 25 + k] : 0.f;
+    }
+    if (tid < 590) {
+      const int q = tid;
+      const int src = q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30
+                                                                : q < 90 ? O_F2B + q - 80 : O_F2W + q - 90;
+      PAR[q] = a.params[src];
+    }
+    if (tid < 96) {
+      L[F_ONES + tid] = 1.f;
+      L[F_ZEROS + tid] = 0.f;
+    }
+    if (tid < 4) X[784 + tid] = 0.f;
+    if (tid == 0) DY2[1280] = 0.f;
+    if (tid < 256) {  // conv2 fwd A offsets: k = ic*25 + kh*5 + kw -> ic*144 + kh*12 + kw (K pad -> k 249)
+      const int k = min(tid, 249), ic = k / 25, r = k - 25 * ic;
+      K2[tid] = (unsigned short)(ic * 144 + (r / 5) * 12 + (r % 5));
+    }
+  }
+  // conv1 A offsets of this lane's 7 K-steps (tap k = 4*ks + kq, K pad clamped to tap 24)
+  int c1k[7];
+#pragma unroll
+  for (int ks = 0; ks < 7; ++ks) {
+    const int k = min(4 * ks + kq, 24);
+    c1k[ks] = (k / 5) * 28 + (k % 5);
+  }
+
+  // gradient accumulators over this workgroup's samples
+  f32x4 acc_c2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};  // conv2 wgrad, N tile = wave
+  float acc_c1 = 0.f;                                                      // conv1 wgrad (tid < 260)
+  float loss_sum = 0.f, correct = 0.f;
+
+  // sample pipeline: pixels (4 per thread) and label of sample s, row of sample s+1
+  uint32_t px = 0;
+  int lab = 0;
+  int64_t rown = 0;
+  if (nsamp > 0) {
+    const int64_t r0 = row_of(0);
+    px = reinterpret_cast<const uint32_t*>(a.images + r0 * 784)[min(tid, 195)];
+    lab = (int)a.labels[r0];
+    rown = row_of(1);
+  }
+
+  for (int s = 0; s < nsamp; ++s) {
+    const int tid = opaque(threadIdx.x), lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
+    const int b = g + s * G;
+    float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
+    __syncthreads();  // previous sample's readers done (first pass: the preamble's writes)
+    // ---------------- stage 0: pixels, dropout masks; the next sample's loads
+    if (tid < 196) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        X[4 * tid + j] = ((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std;
+    }
+    if (tid == 0) reinterpret_cast<int*>(SM)[S_LAB] = lab;
+    if (tid < 70) {
+      float sc = 1.f;
+      if (TRAIN) {  // the 16-bit kernel's Philox stream: identical masks for a given step
+        const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)a.B + b) * 70ull + tid;
+        sc = dropout_keep(a.seed, rng_off, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
+      }
+      if (tid < 20) SM[S_D2S + tid] = sc;
+      else SM[S_D1S + tid - 20] = sc;
+    }
+    if (s + 1 < nsamp) {
+      px = reinterpret_cast<const uint32_t*>(a.images + rown * 784)[min(tid, 195)];
+      lab = (int)a.labels[rown];
+      rown = row_of(s + 2);
+    }
+    __syncthreads();
+
+    // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, XPOS
+    {
+      float bv[7];
+#pragma unroll
+      for (int ks = 0; ks < 7; ++ks) bv[ks] = W1B[l16 * 28 + 4 * ks + kq];
+      const float cb = PAR[P_C1B + min(l16, 9)];
+#pragma unroll
+      for (int it = 0; it < 3; ++it) {
+        const int mt = wave + it * NW;
+        if (mt < 36) {
+          const int m = mt * 16 + l16, p = m >> 2, q = m & 3;
+          const int base = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
+          float av[7];
+#pragma unroll
+          for (int ks = 0; ks < 7; ++ks) av[ks] = X[base + c1k[ks]];
+          f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 7; ++ks) c = mma(av[ks], bv[ks], c);
+          if (l16 < 10) {
+            float best = c[0];
+            int bi = 0;
+#pragma unroll
+            for (int r = 1; r < 4; ++r)
+              if (c[r] > best) { best = c[r]; bi = r; }
+            const int w = mt * 4 + kq, py = w / 12, pxw = w - 12 * py;  // pooled position
+            P1[l16 * 144 + w] = fmaxf(best + cb, 0.f);
+            I1[l16 * 144 + w] = (uint8_t)bi;
+            XPOS[l16 * 144 + w] = (unsigned short)((2 * py + (bi >> 1)) * 28 + 2 * pxw + (bi & 1));
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
+    {
+      const int tile = wave & 7, half = wave >> 3;  // K-steps [0, 32) / [32, 63)
+      const int mt = tile & 3, nt = tile >> 2;
+      const int m = mt * 16 + l16, w = m >> 2, q = m & 3;
+      const int abase = (2 * (w >> 2) + (q >> 1)) * 12 + 2 * (w & 3) + (q & 1);
+      const float* wrow = W2 + min(nt * 16 + l16, 19) * LW2;  // rows >= 20 feed discarded columns
+      f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int ks0 = half * 32, nks = half ? 31 : 32;
+#pragma unroll 8
+      for (int u = 0; u < nks; ++u) {
+        const int k = 4 * (ks0 + u) + kq;
+        c = mma(P1[abase + K2[k]], wrow[k], c);
+      }
+      if (half) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) RED[tile * 256 + r * 64 + lane] = c[r];
+      }
+      __syncthreads();
+      if (!half) {
+        const int oc = nt * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] += RED[tile * 256 + r * 64 + lane];
+        if (oc < 20) {
+          float best = c[0];
+          int bi = 0;
+#pragma unroll
+          for (int r = 1; r < 4; ++r)
+            if (c[r] > best) { best = c[r]; bi = r; }
+          const int wp = mt * 4 + kq;
+          const float v = fmaxf(best + PAR[P_C2B + oc], 0.f) * SM[S_D2S + oc];
+          P2[oc * 16 + wp] = v;
+          I2[oc * 16 + wp] = (uint8_t)bi;
+          if (TRAIN) vs[V_P2 + oc * 16 + wp] = v;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage 3: fc1 + bias + relu + dropout -> H (VALU, fixed-order combine)
+    {
+      const int o = min(lane, 49), i0 = wave * 20;
+      const float* wr = W1 + o * LW1 + i0;
+      float z0 = 0.f, z1 = 0.f;
+#pragma unroll
+      for (int u = 0; u < 20; u += 2) {
+        z0 = fmaf(wr[u], P2[i0 + u], z0);
+        z1 = fmaf(wr[u + 1], P2[i0 + u + 1], z1);
+      }
+      RED[wave * 64 + lane] = z0 + z1;
+      __syncthreads();
+      if (tid < 50) {
+        float z = 0.f;
+#pragma unroll
+        for (int sg = 0; sg < NW; ++sg) z += RED[sg * 64 + tid];
+        const float h = fmaxf(z + PAR[P_F1B + tid], 0.f) * SM[S_D1S + tid];
+        SM[S_H + tid] = h;
+        if (TRAIN) vs[V_H + tid] = h;
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage 4: fc2, log_softmax, NLL, dlogits, dZ1 (wave 0)
+    if (wave == 0) {
+      const int t = reinterpret_cast<const int*>(SM)[S_LAB];
+      const float* Hs = SM + S_H;
+      const int o = min(lane, 49);
+      float w2c[10];
+#pragma unroll
+      for (int c = 0; c < 10; ++c) w2c[c] = PAR[P_F2W + c * 50 + o];
+      const float ho = Hs[o], d1 = SM[S_D1S + o];
+      // 4 lanes per logit (lanes 4c..4c+3 cover o = 13q .. 13q+12), fixed-order DPP butterfly
+      const int c4 = min(lane >> 2, 9), q = lane & 3;
+      const float* wr = PAR + P_F2W + c4 * 50;
+      float zp0 = 0.f, zp1 = 0.f;
+#pragma unroll
+      for (int u = 0; u < 13; ++u) {
+        const int oo = q * 13 + u, oc = min(oo, 49);
+        const float wv = oo < 50 ? wr[oc] : 0.f;
+        if (u & 1) zp1 = fmaf(wv, Hs[oc], zp1);
+        else zp0 = fmaf(wv, Hs[oc], zp0);
+      }
+      float zp = zp0 + zp1;
+      zp += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, zp), 0xB1, 0xf, 0xf,
+                                                                   false));
+      zp += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, zp), 0x4E, 0xf, 0xf,
+                                                                   false));
+      float lg[10];
+#pragma unroll
+      for (int c = 0; c < 10; ++c)
+        lg[c] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, zp), 4 * c)) +
+                PAR[P_F2B + c];
+      float mx = lg[0];
+      int amax = 0;
+#pragma unroll
+      for (int c = 1; c < 10; ++c)
+        if (lg[c] > mx) { mx = lg[c]; amax = c; }
+      float ex[10], se = 0.f, lt = 0.f;
+#pragma unroll
+      for (int c = 0; c < 10; ++c) {
+        ex[c] = __expf(lg[c] - mx);
+        se += ex[c];
+        lt = c == t ? lg[c] : lt;
+      }
+      const float lse = mx + __logf(se);
+      if (lane == 0) {
+        loss_sum += lse - lt;
+        correct += (amax == t) ? 1.f : 0.f;
+      }
+      if (write_logp && lane < 10) {
+        float mine = 0.f;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) mine = lane == c ? lg[c] : mine;
+        logp_out[(int64_t)b * 10 + lane] = mine - lse;
+      }
+      if (TRAIN) {
+        const float gs = a.grad_scale * (1.f / se);
+        float dl[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
+        if (lane < 16) {
+          float mine = 0.f;
+#pragma unroll
+          for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
+          vs[V_DLOG + lane] = mine;
+        }
+        float dh0 = 0.f, dh1 = 0.f;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+          if (c & 1) dh1 = fmaf(dl[c], w2c[c], dh1);
+          else dh0 = fmaf(dl[c], w2c[c], dh0);
+        }
+        const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
+        SM[S_DZ1 + lane] = dz;
+        if (lane < 50) vs[V_DZ1 + lane] = dz;
+      }
+    }
+    if (!TRAIN) continue;
+    __syncthreads();
+
+    // ---------------- stage 5: dP2 = dZ1 . W1 (VALU), pool2 / relu / Dropout2d backward -> DY2
+    {
+      if (tid < 960) {
+        const int i = tid % 320, part = tid / 320, o0 = 17 * part, o1 = min(o0 + 17, 50);
+        float d0 = 0.f, d1 = 0.f;
+        for (int o = o0; o < o1; o += 2) {
+          d0 = fmaf(SM[S_DZ1 + o], W1[o * LW1 + i], d0);
+          if (o + 1 < o1) d1 = fmaf(SM[S_DZ1 + o + 1], W1[(o + 1) * LW1 + i], d1);
+        }
+        RED[part * 320 + i] = d0 + d1;
+      }
+      __syncthreads();
+      if (tid < 320) {
+        const int oc = tid >> 4, w = tid & 15;
+        const float dp = (RED[tid] + RED[320 + tid]) + RED[640 + tid];
+        const float gv = P2[tid] > 0.f ? dp * SM[S_D2S + oc] : 0.f;
+        const int bi = I2[tid], oy0 = 2 * (w >> 2), ox0 = 2 * (w & 3);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) DY2[oc * 64 + (oy0 + (q >> 1)) * 8 + ox0 + (q & 1)] = q == bi ? gv : 0.f;
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers; conv2 dgrad units
+    {
+      // wgrad: N tile = wave (k = wave*16 + l16 = ic*25 + kh*5 + kw, 250 = ones, > 250 zeros),
+      // M tiles oc 0-15 / 16-31, K = the 64 output pixels (pixel 4*ks + kq: row ks>>1,
+      // column 4*(ks&1) + kq -> P1 offset (ks>>1)*12 + 4*(ks&1) + kq from the tap's base)
+      const int k = wave * 16 + l16;
+      const float* bsrc;
+      if (k < 250) {
+        const int ic = k / 25, r = k - 25 * ic;
+        bsrc = P1 + ic * 144 + (r / 5) * 12 + (r % 5) + kq;
+      } else {
+        bsrc = L + (k == 250 ? F_ONES : F_ZEROS) + kq;
+      }
+      const float* arow0 = DY2 + l16 * 64 + kq;
+      const float* arow1 = DY2 + min(16 + l16, 19) * 64 + kq;  // rows >= 20: discarded outputs
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        const float bv = bsrc[(ks >> 1) * 12 + 4 * (ks & 1)];
+        acc_c2[0] = mma(arow0[4 * ks], bv, acc_c2[0]);
+        acc_c2[1] = mma(arow1[4 * ks], bv, acc_c2[1]);
+      }
+    }
+    {
+      // dgrad: dP1[ic][y*12 + x] = sum_{oc, kh, kw} DY2[oc][(y-kh)*8 + x-kw] W2[oc][ic][kh][kw];
+      // unit (tile t, j): rows p = 16t + l16, oc = 4j + kq, the 25 taps
+      const int u0 = unit_lo(wave), u1 = unit_lo(wave + 1), t0 = u0 / 5;
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      const float* bcol = W2 + kq * LW2 + min(l16, 9) * 25;  // columns >= 10: discarded outputs
+      for (int u = u0; u < u1; ++u) {  // wave-uniform
+        const int t = u / 5, j = u - 5 * t;
+        const int p = t * 16 + l16, y = p / 12, x = p - 12 * (p / 12);
+        const float* arow = DY2 + (4 * j + kq) * 64 + y * 8 + x;  // minus kh*8 + kw per tap
+        const float* brow = bcol + 4 * j * LW2;
+        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh) {
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) {
+            const bool ok = (unsigned)(y - kh) < 8u && (unsigned)(x - kw) < 8u;
+            const float av = ok ? arow[-(kh * 8 + kw)] : 0.f;
+            c = mma(av, brow[kh * 5 + kw], c);
+          }
+        }
+        if (t == t0) acc0 += c;
+        else acc1 += c;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        RED[(wave * 2) * 256 + r * 64 + lane] = acc0[r];
+        RED[(wave * 2 + 1) * 256 + r * 64 + lane] = acc1[r];
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage 7: dgrad combine (fixed wave order), relu / pool1 gate -> G1
+    for (int idx = tid; idx < 1440; idx += NT) {
+      const int ic = idx / 144, p = idx - 144 * ic, t = p >> 4, row = p & 15;
+      const int e = (row & 3) * 64 + (row >> 2) * 16 + ic;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int lo = unit_lo(w), hi = unit_lo(w + 1), tw = lo / 5;
+        if (tw == t && lo < hi) v += RED[(w * 2) * 256 + e];
+        else if (tw + 1 == t && (hi - 1) / 5 == t) v += RED[(w * 2 + 1) * 256 + e];
+      }
+      G1[idx] = P1[idx] > 0.f ? v : 0.f;
+    }
+    __syncthreads();
+
+    // ---------------- stage 8: conv1 wgrad over the argmax pixels (VALU) + bias
+    {
+      if (tid < 1000) {
+        const int j = tid % 250, part = tid / 250, oc = j / 25, tap = j - 25 * oc;
+        const int koff = (tap / 5) * 28 + (tap % 5);
+        const float* gr = G1 + oc * 144 + 36 * part;
+        const unsigned short* xr = XPOS + oc * 144 + 36 * part;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll 6
+        for (int p = 0; p < 36; p += 2) {
+          s0 = fmaf(gr[p], X[xr[p] + koff], s0);
+          s1 = fmaf(gr[p + 1], X[xr[p + 1] + koff], s1);
+        }
+        RED[part * 256 + j] = s0 + s1;
+      }
+      __syncthreads();
+      if (tid < 250) {
+        acc_c1 += (RED[tid] + RED[256 + tid]) + (RED[512 + tid] + RED[768 + tid]);
+      } else if (tid >= 256 && tid < 266) {  // conv1.b: sum over the 144 gated pooled pixels
+        const float* gr = G1 + (tid - 256) * 144;
+        float s0 = 0.f, s1 = 0.f;
+        for (int p = 0; p < 144; p += 2) {
+          s0 += gr[p];
+          s1 += gr[p + 1];
+        }
+        acc_c1 += s0 + s1;
+      }
+    }
+  }
+
+  // ---------------- epilogue: this workgroup's partial conv gradient + loss
+  if (TRAIN) {
+    auto slab_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
+    if (tid < 250) *slab_at(O_C1W + tid) = acc_c1;
+    else if (tid >= 256 && tid < 266) *slab_at(O_C1B + tid - 256) = acc_c1;
+    const int k = wave * 16 + l16;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oc = mt * 16 + 4 * kq + r;
+        if (oc < 20) {
+          if (k < 250) *slab_at(O_C2W + oc * 250 + k) = acc_c2[mt][r];
+          else if (k == 250) *slab_at(O_C2B + oc) = acc_c2[mt][r];
+        }
+      }
+  }
+  if (tid == 0) {
+    a.loss_acc[2 * g] = loss_sum;
+    a.loss_acc[2 * g + 1] = correct;
+  }
+}
+
+}  // namespace lenet32
+
+hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float* logp_out, bool train,
+                                  hipStream_t s) {
+  using namespace lenet32;
+  if (a.B <= 0 || a.grid <= 0 || a.grid > a.B || a.grid > 256 || a.xstage) return hipErrorInvalidValue;
+  if (train) {
+    hipFuncSetAttribute((const void*)lenet_train_f32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        LDS_BYTES);
+    hipLaunchKernelGGL(lenet_train_f32_kernel<true>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, 0, (float*)nullptr);
+  } else {
+    hipFuncSetAttribute((const void*)lenet_train_f32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        LDS_BYTES);
+    hipLaunchKernelGGL(lenet_train_f32_kernel<false>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, write_logp,
+                       logp_out);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace csed

@@ -152,7 +152,11 @@ struct LenetTrainArgs {
   int64_t* lstage;           // its labels [B]
   int stage_next;            // with xstage: also stage step cursor+1 (perm / cursor are read for it)
 };
+// mfma_dtype == kF32 selects the exact-fp32 kernel (lenet_fused_f32.hip: no weight images,
+// no batch staging, v_mfma_f32_16x16x4_f32).
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s);
+hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float* logp_out, bool train,
+                                  hipStream_t s);
 // Batch staging: pixels + labels of one step, gathered through the epoch permutation.
 struct LenetStageArgs {
   const uint8_t* images; const int64_t* labels; const int64_t* perm; int64_t perm_len;
