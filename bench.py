@@ -289,6 +289,10 @@ def main(argv=None) -> int:
             extra["allreduce_select_us"] = _ipc.LAST_TIMING
         if eng.path_timing_us:
             extra["step_path_select_us"] = eng.path_timing_us
+        if eng.exchange_note:
+            extra["exchange"] = eng.exchange_note
+        if _ipc.LAST_NOTE:
+            extra["allreduce_note"] = _ipc.LAST_NOTE
 
     value = args.steps * args.global_batch / elapsed
     base = BASELINE_EPOCH_S.get(n)

@@ -166,6 +166,7 @@ class FusedLeNetTrainer:
         # (csrc/comm) when every rank passes its self-test, else RCCL (parallel/ipc.py).
         # Preferred: the exchange fused into lenet_update (1 kernel), see module docstring.
         self.exch = None
+        self.exchange_note: str | None = None  # why the data-parallel step runs as it does (reports)
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
         multi = self.comm and self.world > 1
@@ -195,16 +196,25 @@ class FusedLeNetTrainer:
             if not ok:
                 why = "self-test mismatch or timeout on some rank"
         if not ok:
+            if ex is not None:
+                try:
+                    ex.close()  # collective: every rank opened it (a failed rank's buffer too)
+                except Exception:
+                    pass
             self.exch = None
+            self.exchange_note = f"fused exchange off: {why}; fallback {self.allreduce_kind}"
             if required:
                 raise RuntimeError(f"CSED_ALLREDUCE=fused but the fused exchange is unusable ({why})")
             return
+        self.exchange_note = "fused exchange on (self-test passed)"
         if not required and self.ctx.backend == "nccl":
             t_fused = self._time_steps()
             saved, self.exch = self.exch, None
             t_fallback = self._time_steps()
             # a path whose graph could not be captured times as inf; ties keep the fused path
             self.exch = saved if t_fused <= t_fallback else None
+            if self.exch is None:
+                self.exchange_note = "fused exchange off: slower than the fallback step"
             fin = lambda t: round(t, 2) if t != float("inf") else None  # noqa: E731
             self.path_timing_us = {"fused_step_us": fin(t_fused), "fallback_step_us": fin(t_fallback),
                                    "fallback": "ipc-oneshot" if self.allreduce is not None else "rccl"}

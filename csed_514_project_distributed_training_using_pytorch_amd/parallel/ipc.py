@@ -35,6 +35,8 @@ from .comm import DistContext
 
 # latencies measured by the last auto selection (us per call, max over ranks), for reports
 LAST_TIMING: dict | None = None
+# why the last make_allreduce() fell back to the process group, for reports
+LAST_NOTE: str | None = None
 
 
 def _gather_handles(ctx: DistContext, h: torch.Tensor) -> torch.Tensor:
@@ -142,6 +144,36 @@ class IpcAllReduce:
         return ok
 
 
+# Ranks that may share one GPU and still run the spin-waiting exchange kernels.  Every rank's
+# kernel must be resident at once (each waits for its peers' pushes): measured on one MI355X,
+# 2 processes sharing the GPU run both paths (tests/test_comm_gpu.py), 4 did not (the
+# self-test timed out: the GPU does not keep four processes' spinning kernels co-resident,
+# profiles/dp_exchange_r1.md).  Beyond the limit the process group's all-reduce is used.
+MAX_RANKS_PER_GPU = 2
+
+
+def _device_key(ctx: DistContext) -> int:
+    import hashlib
+    import socket
+
+    props = torch.cuda.get_device_properties(ctx.device)
+    ident = getattr(props, "uuid", None)
+    ident = str(ident) if ident is not None else f"{props.name}:{ctx.device.index}"
+    digest = hashlib.sha1(f"{socket.gethostname()}|{ident}".encode()).digest()
+    return int.from_bytes(digest[:7], "little")
+
+
+def ranks_per_gpu(ctx: DistContext) -> int:
+    """Largest number of ranks of the process group that drive the same physical GPU
+    (collective).  One process per GPU gives 1."""
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    mine = torch.tensor([_device_key(ctx)], dtype=torch.int64, device=dev)
+    keys = [torch.empty_like(mine) for _ in range(ctx.world_size)]
+    dist.all_gather(keys, mine)
+    vals = [int(k.item()) for k in keys]
+    return max(vals.count(v) for v in vals)
+
+
 def wait_timeout_s() -> float:
     """Wall-clock bound of every peer wait inside the exchange kernels (``CSED_IPC_TIMEOUT_S``,
     default 2 s): on expiry a kernel raises the comm error word and finishes instead of
@@ -184,6 +216,9 @@ def open_exchange(ctx: DistContext, words: int) -> tuple[IpcAllReduce | None, st
     self-tests it with that kernel.  Collective."""
     if not ctx.is_distributed or ctx.device.type != "cuda":
         return None, "not distributed on a GPU"
+    shared = ranks_per_gpu(ctx)
+    if shared > MAX_RANKS_PER_GPU:
+        return None, f"{shared} ranks share one GPU (spin-waiting exchange needs <= {MAX_RANKS_PER_GPU})"
     return _open(ctx, (words + 3) // 4 * 4, blocks=1)
 
 
@@ -193,8 +228,15 @@ def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
     Every rank runs the same sequence of collectives whatever fails locally:
     create -> vote -> all-gather handles -> open -> vote -> self-test -> vote.
     """
+    global LAST_NOTE
     mode = allreduce_mode()
     if mode == "rccl" or not ctx.is_distributed or ctx.device.type != "cuda":
+        return None
+    shared = ranks_per_gpu(ctx)
+    if shared > MAX_RANKS_PER_GPU:
+        LAST_NOTE = f"ipc all-reduce off: {shared} ranks share one GPU (needs <= {MAX_RANKS_PER_GPU})"
+        if mode == "ipc":
+            raise RuntimeError(f"CSED_ALLREDUCE=ipc but {LAST_NOTE}")
         return None
     ar, why = _open(ctx, n, blocks=32)
     ok = ar is not None
@@ -204,6 +246,7 @@ def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
     if not ok:
         if mode == "ipc":
             raise RuntimeError(f"CSED_ALLREDUCE=ipc but the IPC all-reduce is unusable ({why or 'a peer failed'})")
+        LAST_NOTE = f"ipc all-reduce off: {why or 'a peer failed'}"
         return None
     if mode == "auto" and ctx.backend == "nccl":
         # keep whichever is faster on this machine (slowest rank decides, all ranks agree)

@@ -145,3 +145,131 @@ def test_ipc_allreduce_two_ranks_one_gpu():
             assert res[f"engine_errors_{mode}"] == 0, res
         assert res["step_fused"] == "two kernels" and res["step_fused1k"].startswith("one kernel"), res
         assert res["fused_equals_ipc"] and res["fused1k_equals_ipc"], res
+
+
+def _tail_worker(rank, world, port, q):
+    """Fused exchange with a per-rank batch whose FC work splits K over waves (B = 256) and an
+    epoch tail in another split bucket (B = 100): two epochs of graph-replayed steps + tails.
+    The exchange tags are per-workgroup call counters, so the workgroup -> exchange-word map
+    must not depend on the batch (counters drifting between full and tail steps
+    made ranks add a peer's stale gradient, or time out)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CSED_IPC_TIMEOUT_S="30")
+        import torch.distributed as dist
+
+        from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+        from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
+        from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import DistContext
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        ctx = DistContext(rank, world, 0, dev, "gloo")
+        n = 2 * (2 * 256 + 100)  # per rank: 2 full steps of 256 + a tail of 100
+        data = synthetic_mnist(n, seed=5)
+        res = {}
+        finals = {}
+        # reference: the process group's all-reduce (gloo here: host sum, eager steps), bitwise
+        # the same rank-ordered sum as the fused exchange
+        for mode in ("fused", "rccl"):
+            os.environ["CSED_ALLREDUCE"] = mode
+            torch.manual_seed(1)
+            eng = FusedLeNetTrainer(Net().to(dev), data, lr=0.05, global_batch=512, ctx=ctx)
+            smp = ShardSampler(n, world, rank, shuffle=True, seed=42)
+            for epoch in range(2):
+                smp.set_epoch(epoch)
+                eng.train_epoch(smp.indices(), steps_per_graph=2)
+            torch.cuda.synchronize(dev)
+            p = eng.flat.data.cpu()
+            other = p.clone()
+            dist.broadcast(other, src=0)
+            res[f"kind_{mode}"] = eng.allreduce_kind
+            res[f"equal_{mode}"] = torch.equal(p, other)
+            res[f"errors_{mode}"] = eng.comm_errors()
+            res[f"tail_{mode}"] = eng.tail_size()
+            finals[mode] = p
+            eng.close()
+        res["fused_equals_pg"] = torch.equal(finals["fused"], finals["rccl"])
+        q.put((rank, res))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, {"exception": repr(e)}))
+
+
+def test_fused_exchange_large_batch_with_tail_two_ranks():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(2):
+        r, res = q.get(timeout=300)
+        results[r] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        res = results[r]
+        assert "exception" not in res, res
+        assert res["errors_fused"] == 0 and res["errors_rccl"] == 0, res
+        assert res["kind_fused"] == "fused-ipc" and res["kind_rccl"] == "rccl", res
+        assert res["tail_fused"] == 100, res
+        assert res["equal_fused"] and res["equal_rccl"] and res["fused_equals_pg"], res
+
+
+def _rccl_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CSED_ALLREDUCE="rccl")
+        import torch.distributed as dist
+
+        from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+        from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
+        from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import init_distributed
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
+
+        ctx = init_distributed(rank=rank, world_size=world, local_rank=rank, backend="nccl", device="cuda")
+        data = synthetic_mnist(2048, seed=3)
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(ctx.device), data, lr=0.05, global_batch=64, ctx=ctx)
+        smp = ShardSampler(2048, world, rank, shuffle=True, seed=42)
+        smp.set_epoch(0)
+        eng.set_epoch_order(smp.indices())
+        eng.run_steps(12, steps_per_graph=4)
+        torch.cuda.synchronize(ctx.device)
+        p = eng.flat.data.clone()
+        other = p.clone()
+        dist.broadcast(other, src=0)
+        q.put((rank, {"kind": eng.allreduce_kind, "captured": eng.capture_comm_ok, "equal": torch.equal(p, other),
+                      "finite": bool(torch.isfinite(p).all())}))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, {"exception": repr(e)}))
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (one rank per GPU on RCCL)")
+def test_rccl_fallback_captured_two_gpus():
+    """CSED_ALLREDUCE=rccl on a 2-rank RCCL process group, one rank per GPU: the step
+    (reduce-only update -> RCCL all-reduce -> SGD kernel) is captured in a HIP graph and
+    both replicas end bitwise identical."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        res = results[r]
+        assert "exception" not in res, res
+        assert res["kind"] == "rccl" and res["captured"] is True, res
+        assert res["equal"] and res["finite"], res
