@@ -9,7 +9,9 @@ Compute precision on the GPU: activations are stored in the compute dtype
 (bf16 by default, fp16 optional), matrix-shaped work runs on
 ``v_mfma_f32_16x16x32_{bf16,f16}`` with fp32 accumulation, weights stay fp32
 masters (the kernels convert while staging them into LDS), and weight
-gradients are produced in fp32.
+gradients are produced in fp32.  ``set_compute_dtype(torch.float32)`` is the
+reference's precision: fp32 activations and operands, each 16x16x32 K-slice
+as eight exact ``v_mfma_f32_16x16x4_f32`` (common.h ``Mfma<float>``).
 
 Reference parity map (ref = /root/reference):
   conv2d / conv2d_pool_relu   <- nn.Conv2d, F.max_pool2d, F.relu      src/model.py:9-10,16-17
@@ -31,8 +33,8 @@ _compute_dtype = torch.bfloat16
 
 def set_compute_dtype(dtype: torch.dtype) -> None:
     global _compute_dtype
-    if dtype not in (torch.bfloat16, torch.float16):
-        raise ValueError("compute dtype must be torch.bfloat16 or torch.float16")
+    if dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        raise ValueError("compute dtype must be torch.bfloat16, torch.float16 or torch.float32")
     _compute_dtype = dtype
 
 
@@ -49,6 +51,9 @@ def _ops():
 
 
 def _act_dtype(x: torch.Tensor) -> torch.dtype:
+    """Activation storage dtype: the compute dtype (fp32 activations on the exact-fp32 path)."""
+    if _compute_dtype == torch.float32:
+        return torch.float32
     return x.dtype if x.dtype in (torch.bfloat16, torch.float16) else _compute_dtype
 
 

@@ -40,9 +40,10 @@ int dcode(const Tensor& t) {
   return -1;
 }
 
+// matrix ops (conv / gemm): bf16 / fp16 MFMA operands, or exact fp32 (v_mfma_f32_16x16x4_f32)
 int mcode(int64_t mfma_dtype) {
-  TORCH_CHECK(mfma_dtype == csed::kBF16 || mfma_dtype == csed::kF16,
-              "csed: MFMA dtype must be bf16 (1) or fp16 (2)");
+  TORCH_CHECK(mfma_dtype == csed::kBF16 || mfma_dtype == csed::kF16 || mfma_dtype == csed::kF32,
+              "csed: compute dtype must be fp32 (0), bf16 (1) or fp16 (2)");
   return (int)mfma_dtype;
 }
 

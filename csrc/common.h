@@ -34,6 +34,33 @@ template <> struct Mfma<_Float16> {
   }
 };
 
+// Exact fp32 on the matrix cores: one 16x16x32 K-slice of the 16-bit layout (lane group q
+// holds k = 8q .. 8q+7) as eight v_mfma_f32_16x16x4_f32, MFMA i taking element i of every
+// lane (its K index 8q + i): the K order inside the slice is permuted identically for A and
+// B, so the sum is the slice's exact fp32 dot product; callers keep the 16-bit fragment
+// addressing and just stage fp32 values.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+template <> struct Mfma<float> {
+  typedef f32x8 frag;
+  __device__ static inline f32x4 mma(frag a, frag b, f32x4 c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[i], c, 0, 0, 0);
+    return c;
+  }
+};
+
+// LDS storage of MFMA operands: raw 16-bit for bf16 / fp16, fp32 as is.
+template <typename T> struct Stor {
+  typedef unsigned short S;
+  typedef u16x8 V8;
+  __device__ static inline S of(float f);
+};
+template <> struct Stor<float> {
+  typedef float S;
+  typedef f32x8 V8;
+  __device__ static inline S of(float f) { return f; }
+};
+
 template <typename T> __device__ __forceinline__ float to_f32(T x) { return (float)x; }
 template <> __device__ __forceinline__ float to_f32<uint8_t>(uint8_t x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
@@ -46,6 +73,7 @@ template <typename T> __device__ __forceinline__ unsigned short bits_of(T v) {
 template <typename T> __device__ __forceinline__ T of_bits(unsigned short b) {
   return __builtin_bit_cast(T, b);
 }
+template <typename T> __device__ inline typename Stor<T>::S Stor<T>::of(float f) { return bits_of<T>((T)f); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

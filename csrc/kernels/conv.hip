@@ -63,10 +63,11 @@ template <typename T>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   typedef typename Mfma<T>::frag frag;
+  typedef typename Stor<T>::S S;
   const int LDW = g.Kp + 8;                         // 16-B aligned row pad
-  unsigned short* Ws = (unsigned short*)smem;       // [Cop][LDW]
+  S* Ws = (S*)smem;                                 // [Cop][LDW]
   int* koff = (int*)(Ws + g.Cop * LDW);             // [Kp]
-  unsigned short* patch = (unsigned short*)(koff + g.Kp);  // [Ci][PR][PW]
+  S* patch = (S*)(koff + g.Kp);                     // [Ci][PR][PW]
 
   const int n = blockIdx.x / g.bands, band = blockIdx.x % g.bands;
   const int oh0 = band * g.TR;
@@ -82,7 +83,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
       const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
       v = weff(a.w, a.mode, g.Ci, g.Co, g.KH, g.KW, oc, ic, r / g.KW, r % g.KW);
     }
-    Ws[oc * LDW + k] = bits_of<T>((T)v);
+    Ws[oc * LDW + k] = Stor<T>::of(v);
   }
   for (int k = tid; k < g.Kp; k += 256) {
     int o = 0;
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
     const int ih = oh0 - g.pad + pr, iw = pc - g.pad;
     float v = 0.f;
     if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) v = ldf(a.x, a.x_dtype, xbase + ((int64_t)ic * g.H + ih) * g.W + iw);
-    patch[i] = bits_of<T>((T)v);
+    patch[i] = Stor<T>::of(v);
   }
   __syncthreads();
 
@@ -133,9 +134,9 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
         const int4 o1 = *reinterpret_cast<const int4*>(koff + kb + 4);
         const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
         frag fa;
-        u16x8 raw;
+        typename Stor<T>::V8 raw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[j] = valid ? patch[pb + oo[j]] : (unsigned short)0;
+        for (int j = 0; j < 8; ++j) raw[j] = valid ? patch[pb + oo[j]] : (S)0;
         fa = __builtin_bit_cast(frag, raw);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -200,11 +201,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
                                                          float* __restrict__ slab, WgradGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   typedef typename Mfma<T>::frag frag;
+  typedef typename Stor<T>::S S;
   const int LDY = g.npp + 8;
-  unsigned short* dys = (unsigned short*)smem;              // [Cop][LDY]
+  S* dys = (S*)smem;                                        // [Cop][LDY]
   int* koff = (int*)(dys + g.Cop * LDY);                    // [Kc]
   int* pbase = koff + g.Kc;                                 // [npp]
-  unsigned short* patch = (unsigned short*)(pbase + g.npp); // [Ci][PR][PW] (+1 slot holding 1.0)
+  S* patch = (S*)(pbase + g.npp);                           // [Ci][PR][PW] (+1 slot holding 1.0)
   const int pe = g.Ci * g.PR * g.PW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
@@ -242,13 +244,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
         const int ih = pr - g.pad, iw = pc - g.pad;
         v = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? ldf(x, xdt, xb + ((int64_t)ic * g.H + ih) * g.W + iw) : 0.f;
       }
-      patch[i] = bits_of<T>((T)v);
+      patch[i] = Stor<T>::of(v);
     }
     const int64_t yb = (int64_t)n * g.Co * g.npix;
     for (int i = tid; i < g.Cop * g.npp; i += 256) {
       const int oc = i / g.npp, p = i % g.npp;
       const float v = (oc < g.Co && p < g.npix) ? ldf(dy, dydt, yb + (int64_t)oc * g.npix + p) : 0.f;
-      dys[oc * LDY + p] = bits_of<T>((T)v);
+      dys[oc * LDY + p] = Stor<T>::of(v);
     }
     __syncthreads();
     if (my_nt0 >= NT) continue;
@@ -267,7 +269,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
         if (jj > 0 && NT < 4) break;
         if (nt >= NT) break;
         const int ko = koff[nt * 16 + (lane & 15)];
-        u16x8 raw;
+        typename Stor<T>::V8 raw;
 #pragma unroll
         for (int j = 0; j < 8; ++j) raw[j] = patch[bb[j] * (ko != pe) + ko];
         const frag fb = __builtin_bit_cast(frag, raw);
@@ -362,9 +364,10 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   int bands = (g.OH + tr - 1) / tr;
   tr = (g.OH + bands - 1) / bands;
   if (a.pool_k == 2 && (tr & 1)) tr += 1;
+  const size_t es = a.mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
   auto lds_bytes = [&](int trr) {
     const int pr = trr + g.KH - 1;
-    return (size_t)g.Cop * (g.Kp + 8) * 2 + (size_t)g.Kp * 4 + (size_t)g.Ci * pr * g.PW * 2 + 16;
+    return (size_t)g.Cop * (g.Kp + 8) * es + (size_t)g.Kp * 4 + (size_t)g.Ci * pr * g.PW * es + 16;
   };
   while (tr > (a.pool_k == 2 ? 2 : 1) && lds_bytes(tr) > 96 * 1024) tr -= (a.pool_k == 2 ? 2 : 1);
   if (lds_bytes(tr) > 160 * 1024) return hipErrorInvalidConfiguration;
@@ -373,7 +376,7 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   g.bands = (g.OH + tr - 1) / tr;
   const size_t lds = lds_bytes(tr);
   dim3 grid(a.N * g.bands);
-  CSED_DISPATCH_MFMA(a.mfma_dtype, {
+  CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_fwd_kernel<scalar_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(conv_fwd_kernel<scalar_t>, grid, dim3(256), lds, s, a, g);
@@ -411,12 +414,13 @@ hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int d
   WgradGeo g = wgrad_geo(N, IC, H, W, OC, KH, KW, pad);
   if (g.OH <= 0 || g.OW <= 0) return hipErrorInvalidValue;
   if (g.Cop > 64 || (g.Kc / 16) > 32) return hipErrorInvalidConfiguration;  // accumulator budget
-  const size_t lds_main = (size_t)g.Cop * (g.npp + 8) * 2 + (size_t)g.Kc * 4 + (size_t)g.npp * 4 +
-                          ((size_t)g.Ci * g.PR * g.PW + 1) * 2 + 16;
+  const size_t es = mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
+  const size_t lds_main = (size_t)g.Cop * (g.npp + 8) * es + (size_t)g.Kc * 4 + (size_t)g.npp * 4 +
+                          ((size_t)g.Ci * g.PR * g.PW + 1) * es + 16;
   const size_t lds_red = (size_t)4 * 4 * 16 * 16 * 4;
   const size_t lds = std::max(lds_main, lds_red);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  CSED_DISPATCH_MFMA(mfma_dtype, {
+  CSED_DISPATCH_COMPUTE(mfma_dtype, {
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_wgrad_kernel<scalar_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(conv_wgrad_kernel<scalar_t>, dim3(g.nblocks), dim3(256), lds, s, x, x_dtype, dy,

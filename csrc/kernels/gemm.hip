@@ -51,6 +51,7 @@ struct Raw {
 
 template <typename T>
 __device__ __forceinline__ bool packed(int dt) {
+  if constexpr (__is_same(T, float)) return false;  // fp32 compute: fp32 operands load as is
   constexpr int code = __is_same(T, __bf16) ? kBF16 : kF16;
   return dt == code;
 }
@@ -102,12 +103,16 @@ __device__ __forceinline__ void load_raw(Raw& raw, const void* X, int dt, int mo
     }
     f[j] = (gr < R && gk < K) ? ld_any(X, dt, (int64_t)gr * s_r + (int64_t)gk * s_k) : 0.f;
   }
-  if (pk) {
-    u16x8 v;
+  if constexpr (!__is_same(T, float)) {
+    if (pk) {
+      u16x8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = bits_of<T>((T)f[j]);
-    raw.r[0] = __builtin_bit_cast(float4, v);
-  } else {
+      for (int j = 0; j < 8; ++j) v[j] = bits_of<T>((T)f[j]);
+      raw.r[0] = __builtin_bit_cast(float4, v);
+      return;
+    }
+  }
+  {
     raw.r[0] = make_float4(f[0], f[1], f[2], f[3]);
     raw.r[1] = make_float4(f[4], f[5], f[6], f[7]);
   }
@@ -115,20 +120,22 @@ __device__ __forceinline__ void load_raw(Raw& raw, const void* X, int dt, int mo
 
 template <typename T>
 __device__ __forceinline__ float raw_at(const Raw& raw, bool pk, int j) {
-  if (pk) return (float)of_bits<T>(__builtin_bit_cast(u16x8, raw.r[0])[j]);
+  if constexpr (!__is_same(T, float))
+    if (pk) return (float)of_bits<T>(__builtin_bit_cast(u16x8, raw.r[0])[j]);
   const float4 q = raw.r[j >> 2];
   return (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
 }
 
 // Convert (+ gate, + ones row) and write the thread's 8 values into the LDS image.
 template <typename T>
-__device__ __forceinline__ void store_tile(unsigned short* lds, const Raw& raw, int dt, int mode, const Raw* graw,
-                                           int gdt, float gs, int r0, int ones_row, int k0, int K) {
+__device__ __forceinline__ void store_tile(typename Stor<T>::S* lds, const Raw& raw, int dt, int mode,
+                                           const Raw* graw, int gdt, float gs, int r0, int ones_row, int k0, int K) {
+  typedef typename Stor<T>::V8 V8;
   const int t = threadIdx.x;
   const bool pk = packed<T>(dt);
-  u16x8 v;
+  V8 v;
   if (pk && !graw && ones_row < 0) {
-    v = __builtin_bit_cast(u16x8, raw.r[0]);
+    if constexpr (!__is_same(T, float)) v = __builtin_bit_cast(u16x8, raw.r[0]);
   } else {
     const bool gpk = graw ? packed<T>(gdt) : false;
 #pragma unroll
@@ -140,7 +147,7 @@ __device__ __forceinline__ void store_tile(unsigned short* lds, const Raw& raw, 
         const int gk = k0 + (mode == kRContig ? (t >> 3) : (t & 3) * 8 + j);
         if (gr == ones_row && gk < K) f = 1.f;
       }
-      v[j] = bits_of<T>((T)f);
+      v[j] = Stor<T>::of(f);
     }
   }
   if (mode == kRContig) {
@@ -148,7 +155,7 @@ __device__ __forceinline__ void store_tile(unsigned short* lds, const Raw& raw, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) lds[(rq + j) * LDK + k] = v[j];
   } else {
-    *reinterpret_cast<u16x8*>(lds + (t >> 2) * LDK + (t & 3) * 8) = v;
+    *reinterpret_cast<V8*>(lds + (t >> 2) * LDK + (t & 3) * 8) = v;
   }
 }
 
@@ -174,8 +181,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float 
 
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][BN * LDK];
+  __shared__ __attribute__((aligned(32))) typename Stor<T>::S As[2][BM * LDK];
+  __shared__ __attribute__((aligned(32))) typename Stor<T>::S Bs[2][BN * LDK];
   typedef typename Mfma<T>::frag frag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -312,7 +319,7 @@ hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
   const int splits = a.ws ? gemm_splits(a) : 1;
   const int Np = a.N + (a.rowsum ? 1 : 0);
   dim3 grid(cdiv(Np, BN), cdiv(a.M, BM), splits);
-  CSED_DISPATCH_MFMA(a.mfma_dtype, {
+  CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
     hipLaunchKernelGGL(gemm_kernel<scalar_t>, grid, dim3(256), 0, s, a);
     if (splits > 1)
       hipLaunchKernelGGL(gemm_splitk_reduce<scalar_t>, dim3(cdiv((int64_t)a.M * Np, 256)), dim3(256), 0, s, a,
