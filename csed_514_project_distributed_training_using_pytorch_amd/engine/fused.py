@@ -62,7 +62,7 @@ def layout() -> tuple[int, int, int, int]:
     16-bit weight-image elements (I_END), conv slab row per workgroup (CNP_PAD: conv1.w/b +
     conv2.w/b = 5280 floats in 64-float chunks), per-sample fc vector length (VEC) and the
     largest per-rank batch that uses batch staging (STAGE_MAXB)."""
-    wimg, conv, vec, nparams, stage_max, _exch, _fmax, _bar = (int(v) for v in torch.ops.csed.lenet_layout())
+    wimg, conv, vec, nparams, stage_max, *_ = (int(v) for v in torch.ops.csed.lenet_layout())
     assert nparams == N_PARAMS
     return wimg, conv, vec, stage_max
 
@@ -80,6 +80,11 @@ def one_kernel_mode() -> str:
     return mode
 
 
+def split_factor() -> int:
+    """Workgroups per sample of the split step (csed::lenet_train KS)."""
+    return int(torch.ops.csed.lenet_layout()[8])
+
+
 def exch_words() -> int:
     """8-byte words per sender of lenet_update's fused exchange buffer."""
     return int(torch.ops.csed.lenet_layout()[5])
@@ -90,7 +95,8 @@ class FusedLeNetTrainer:
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
                  global_batch: int = 64, ctx: DistContext | None = None,
                  compute_dtype: torch.dtype = torch.bfloat16, drop_p: float = 0.5, seed: int = 1,
-                 grid: int | None = None, broadcast_init: bool = True, comm: bool | None = None):
+                 grid: int | None = None, broadcast_init: bool = True, comm: bool | None = None,
+                 split: bool | None = None):
         _native.require()
         self.ctx = ctx or DistContext(device=next(model.parameters()).device)
         self.device = self.ctx.device
@@ -146,15 +152,27 @@ class FusedLeNetTrainer:
         # (the exact-fp32 kernel, lenet_fused_f32.hip, gathers its samples itself)
         self.fp32 = compute_dtype == torch.float32
         self.staged = self.B <= stage_max and self.grid == self.B and not self.fp32
-        self.xstage = torch.zeros((self.B, 784), dtype=torch.uint8, device=dev) if self.staged else None
-        self.lstage = torch.zeros(self.B, dtype=torch.long, device=dev) if self.staged else None
+        # split step (lenet_fused.hip KS > 1): split_k workgroups per sample share the backward
+        # conv stages; used whenever the whole grid fits one wave of the GPU (split_k * B <= 256
+        # CUs).  CSED_SPLIT=0 keeps one workgroup per sample.
+        ok_mode = one_kernel_mode()
+        split_k = split_factor()
+        auto = os.environ.get("CSED_SPLIT", "auto").strip().lower() != "0"
+        self.split = (self.staged and grid is None and split_k * self.B <= 256 and ok_mode != "1"
+                      and (auto if split is None else bool(split)))
+        if self.split:
+            self.grid = split_k * self.B
+            self.slab = torch.empty((self._max_grid(), conv_params), dtype=torch.float32, device=dev)
+            self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
+        # one staging row per workgroup (split step: row r holds sample r % B)
+        self.xstage = torch.zeros((self.grid, 784), dtype=torch.uint8, device=dev) if self.staged else None
+        self.lstage = torch.zeros(self.grid, dtype=torch.long, device=dev) if self.staged else None
         # one-kernel step (csed::lenet_step): training workgroups + trailing update
         # workgroups that wait on device flags, instead of two launches.
         # CSED_ONE_KERNEL_STEP: "1" = use it, "0" / "auto" (default) = two kernels.  After
         # the update-kernel changes (one fc tile per workgroup, idle waves skipped) the two
         # graph-replayed launches beat it by ~0.2 us at batch 64 (profiles/one_kernel_step_r1.md):
         # a kernel boundary inside a graph costs about what the in-kernel hand-off does.
-        ok_mode = one_kernel_mode()
         self.one_kernel = self.staged and self.B <= fused_max_batch() and ok_mode == "1"
         self.bar = torch.zeros(int(torch.ops.csed.lenet_layout()[7]), dtype=torch.int32, device=dev)
         self.repack()
@@ -413,7 +431,8 @@ class FusedLeNetTrainer:
         ops.lenet_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B, self.ctx.rank,
                         self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts, 1.0 / self.global_batch,
                         MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg,
-                        self.xstage if grid == self.B else None, self.lstage if grid == self.B else None, False)
+                        self.xstage if self.staged and grid == self.grid else None,
+                        self.lstage if self.staged and grid == self.grid else None, False)
         ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
                          self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma)
@@ -537,7 +556,7 @@ class FusedLeNetTrainer:
     def train_epoch(self, order: torch.Tensor, steps_per_graph: int = 16, use_graph: bool = True) -> None:
         self.set_epoch_order(order)
         self.run_steps(self.full_steps(), steps_per_graph, use_graph)
-        self.last_partial_step()
+        self.last_partial_step(use_graph)
 
     # ---------------------------------------------------------------- metrics
     def take_loss(self) -> tuple[float, float]:

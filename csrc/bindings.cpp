@@ -296,7 +296,7 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 std::vector<int64_t> lenet_layout() {
   return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
           csed::lenet_param_count(), csed::lenet_stage_max_batch(), csed::lenet_exch_words(),
-          csed::lenet_fused_max_batch(), csed::lenet_step_bar_ints()};
+          csed::lenet_fused_max_batch(), csed::lenet_step_bar_ints(), csed::lenet_split_k()};
 }
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
@@ -319,7 +319,8 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   dev(slab, "slab"); dev(vslab, "vslab"); dev(loss_parts, "loss_parts");
   TORCH_CHECK(images.scalar_type() == at::kByte && images.numel() == images.size(0) * 784, "images: uint8 [N,28,28]");
   TORCH_CHECK(labels.scalar_type() == at::kLong && perm.scalar_type() == at::kLong);
-  TORCH_CHECK(grid >= 1 && grid <= B && grid <= 1024, "lenet_train: 1 <= grid <= B");
+  TORCH_CHECK(grid >= 1 && (grid <= B || (xstage.has_value() && grid == csed::lenet_split_k() * B)) && grid <= 1024,
+              "lenet_train: 1 <= grid <= B (or split_k * B for a staged batch)");
   TORCH_CHECK(slab.numel() >= grid * csed::lenet_conv_param_count() && loss_parts.numel() >= 2 * grid,
               "lenet_train: slab [grid, 5280] / loss_parts [grid, 2] too small");
   TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_train: vslab [B, 464] too small");
@@ -341,13 +342,14 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   }
   TORCH_CHECK(xstage.has_value() == lstage.has_value(), "lenet_train: xstage and lstage go together");
   if (xstage.has_value()) {
-    TORCH_CHECK(xstage->scalar_type() == at::kByte && xstage->numel() >= B * 784 && lstage->scalar_type() == at::kLong &&
-                    lstage->numel() >= B && xstage->is_contiguous() && lstage->is_contiguous(),
-                "lenet_train: staged batch must be uint8 [B, 784] + int64 [B]");
+    TORCH_CHECK(xstage->scalar_type() == at::kByte && xstage->numel() >= grid * 784 && lstage->scalar_type() == at::kLong &&
+                    lstage->numel() >= grid && xstage->is_contiguous() && lstage->is_contiguous(),
+                "lenet_train: staged batch must be uint8 [grid, 784] + int64 [grid] (one row per workgroup)");
     a.xstage = xstage->data_ptr<uint8_t>();
     a.lstage = lstage->data_ptr<int64_t>();
     if (stage_next) {
-      TORCH_CHECK(cursor.has_value() && grid == B, "lenet_train: stage_next needs the cursor and grid == B");
+      TORCH_CHECK(cursor.has_value() && (grid == B || grid == csed::lenet_split_k() * B),
+                  "lenet_train: stage_next needs the cursor and one staging row per workgroup");
       a.stage_next = 1;
     }
   }
@@ -383,6 +385,10 @@ csed::LenetStageArgs stage_args(const Tensor& images, const Tensor& labels, cons
   st.images = images.data_ptr<uint8_t>(); st.labels = labels.data_ptr<int64_t>();
   st.perm = perm.data_ptr<int64_t>(); st.perm_len = perm.numel(); st.B = (int)B;
   st.xstage = xstage.data_ptr<uint8_t>(); st.lstage = lstage.data_ptr<int64_t>();
+  // one staging row per workgroup: B, or split_k * B for the split step (row r = sample r % B)
+  st.rows = (int)lstage.numel();
+  TORCH_CHECK(st.rows >= B && st.rows <= csed::lenet_stage_max_batch() && xstage.numel() >= (int64_t)st.rows * 784,
+              "staging: lstage rows must be B..", csed::lenet_stage_max_batch(), " with xstage [rows, 784]");
   return st;
 }
 

@@ -53,13 +53,12 @@
 #include "comm/ipc_allreduce.h"
 #include "common.h"
 #include "dispatch.h"
+#include "kernels/lenet_layout.h"
 
 namespace csed {
 
 namespace lenet {
-constexpr int NP = 21840;
-constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O_F1B = 21280,
-              O_F2W = 21330, O_F2B = 21830;
+// (flat parameter order, slab and vector-slab layouts: kernels/lenet_layout.h)
 // 16-bit weight images.  Each operand keeps only its live rows plus ONE zero
 // row; fragment reads of padding rows are clamped onto that zero row.
 constexpr int C2_ICP = 16;  // conv2 fwd HWC: 10 input channels padded to 2 groups of 8
@@ -139,11 +138,6 @@ constexpr int I_F1 = I_W2D + DG_CH * 16 * 8;         // 19440
 constexpr int I_END = I_W2C + ((I_F1 + (R_F1 + 1) * LD_F1 - I_W2C + 4095) / 4096) * 4096;  // 33280
 constexpr int LD_DC2 = 72, LD_DC1 = 592;
 constexpr int NT = 1024, NW = 16;  // 16 waves, 4 per SIMD
-// conv partial-gradient slab: params [0, CNP) = conv1.w, conv1.b, conv2.w, conv2.b
-constexpr int CNP = O_F1W;
-constexpr int CNP_PAD = (CNP + 63) / 64 * 64;  // slab row: 83 chunks of 64 floats (see lenet_update)
-// per-sample vector slab (fp32): fc1 input P2 | dL/dz1 | fc1 output H | dL/dlogits
-constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;
 
 // LDS carve (bytes); every region 16-B aligned
 constexpr int S_W2C = 0;                              // u16 21*424  conv2 B operand [oc][tap*16+ic]
@@ -200,6 +194,12 @@ typedef __attribute__((address_space(1))) void glb_void;
 // in every build); the slots are copied out at the end.  Only for profiling builds
 // of the step; read the shares, not the absolute time.
 constexpr int DBG_W = 32;  // stamp slots per workgroup (a.dbg: int64 [grid][32])
+// split-step diagnostics: lane 0 of wave w records s_memtime into slot i (reuses the preamble's
+// wave-arrival slots 24-31)
+#define WSTAMP(w, i)                                                          \
+  do {                                                                        \
+    if (a.dbg && wave == (w) && lane == 0) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #define STAMP(i)                                                              \
   do {                                                                        \
     if (a.dbg && tid == 0 && s == (nsamp > 1 ? 1 : 0)) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
@@ -392,9 +392,17 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
                             int nblk, int tid, float4* part, float* part2, const int* ready, int nready,
                             int fc_tpb = 0);
 
-template <typename T, bool TRAIN, bool STAGED, int FUSE>
+// KS > 1 (split step, staged batches only): KS workgroups per sample.  Workgroup g is part
+// g / B of sample g % B (the parts of a sample share an XCD when B % 8 == 0: same L2 for
+// its pixels and weights).  Every part runs the forward and the loss (they are the
+// sample's dependency chain either way); the backward conv stages are divided: part j
+// owns conv2 wgrad columns [64j, 64j+64) and dgrad tiles {j, j+4, j+8}, and its conv1
+// wgrad covers the conv1 pixels of those tiles.  Part 0 alone writes the fc vector slab and
+// the loss partials.  The backward conv stages are a third of the per-sample chain.
+template <typename T, bool TRAIN, bool STAGED, int FUSE, int KS = 1>
 __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out,
                                                             StepFuse fz) {
+  static_assert(KS == 1 || (KS == SPLIT_K && STAGED && FUSE == 0 && TRAIN), "split step: staged training only");
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
   // per-sample activations (dynamic).  Being distinct objects, accesses to the
   // activations are provably disjoint from the in-flight DMA, so the compiler's
@@ -459,6 +467,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   }
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
   const int G = FUSE ? a.grid : (int)gridDim.x, g = blockIdx.x;
+  // this workgroup's (first) sample and, in the split step, which part of it
+  const int b0 = KS > 1 ? g % a.B : g, part = KS > 1 ? g / a.B : 0;
+  const bool own_vec = part == 0;  // writes the sample's fc vectors and loss
+  const int R2 = min(G, a.B);      // rows of the slab's conv2 chunks
   // staged: this thread's conv1 address row, first in the vector memory queue
   const uint4 c1row = STAGED ? reinterpret_cast<const uint4*>(&kC1Tab)[tid] : make_uint4(0, 0, 0, 0);
   // fused-step timeline (diagnostics): wall-clock start / signal of training workgroup g
@@ -469,7 +481,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
-  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
+  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + b0;
   auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
   if (a.dbg && tid == 0) {
@@ -541,7 +553,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     kg = t < 64 ? (int)kC2Order.fwd[min(4 * tks + tq, 49)] : (int)kDgOrder.fwd[min(4 * tks + tq, 74)];
     // the next step's row (batch staging); an opaque lane offset keeps it a VGPR (a
     // uniform load is moved to an SGPR right away, i.e. waited for here)
-    if (stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
+    if (KS == 1 && stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
     if (a.dbg && t == 0) DBGS[10 + 5] = __builtin_amdgcn_s_memtime();
   }
   lds_barrier();
@@ -597,6 +609,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       conv1_tables(tid);
     }
     if (tid - 512 < 16) CONSTB[tid - 512] = tid - 512 < 8 ? (unsigned short)0 : h16<T>(1.f);
+    // split step: waves 12-15 own every global store of the backward stages (next-step staging,
+    // conv2 slab) and sit out conv1 wgrad, so no wave that computes later waits for a store
+    // (hipcc's vmcnt(0) waits count stores too)
+    if (KS > 1 && stage_next && wave >= 12) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
@@ -635,7 +651,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // the first sample instead of inside the stages' latency bubbles.
   // slab layout: 64-float chunks of the conv gradient, workgroup-major inside a chunk
   // ([chunk][WG][64]) so lenet_update reads each chunk contiguously
-  auto slab_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
+  // (kernels/lenet_layout.h: conv1 rows per workgroup, conv2 rows per sample)
+  auto slab_at = [&](int e) { return a.slab + slab_off(slab_slot(e), e < O_C2W ? g : b0, G, R2); };
   // The conv2 part of the workgroup's slab row (e = 260 .. 5279) goes out as float4 runs
   // from an LDS copy in the dead fc1 image (F1 is last read in stage 5): 2 wide stores per
   // lane instead of 8 scalar ones of 64 lanes (per-CU store issue is what those cost).
@@ -660,7 +677,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       st4_c<FUSE != 0>(slab_at(4 * i), reinterpret_cast<const float4*>(SLF)[i]);
   };
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
-    const int b = g + s * G;
+    const int b = b0 + s * G;
+    const bool wvec = TRAIN && own_vec;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
     if (a.dbg && lane == 0 && s == 0 && wave < 8) DBGS[24 + wave] = __builtin_amdgcn_s_memtime();
     lds_barrier();  // previous sample's readers are done (first pass: preamble LDS writes)
@@ -792,15 +810,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
         P2[oc * 16 + w] = hv;
         I2[oc * 16 + w] = (uint8_t)bi;
-        if (TRAIN) st_c<FUSE != 0>(vs + V_P2 + oc * 16 + w, f16v<T>(hv));  // fc1 input, exactly as the forward used it
+        if (wvec) st_c<FUSE != 0>(vs + V_P2 + oc * 16 + w, f16v<T>(hv));  // fc1 input, exactly as the forward used it
       }
     }
     __syncthreads();
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3)
     STAMP(3);
-    if (stage_next && wave >= 4 && wave < 8) {  // waves 4-7: they hold nrow
-      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid - 256, 195)];
+    if (stage_next && (KS > 1 ? wave >= 12 : (wave >= 4 && wave < 8))) {  // the waves holding nrow
+      px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid & 255, 195)];
       lab_next = a.labels[nrow];
     }
     if (wave >= 8) {
@@ -810,6 +828,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       constexpr int NZ = (S_DC1 - S_DC2H) / 16;
       uint4* z = reinterpret_cast<uint4*>(DC2H);
       for (int i = tid - 512; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
+
       for (int m = tid - 512; m < 784; m += 512) {
         const unsigned short v = Xs[m];
 #pragma unroll
@@ -833,7 +852,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (o < 50) {
           const float h = fmaxf(c[0] + PAR[P_F1B + o], 0.f) * D1S[o];
           Hs[o] = h;
-          if (TRAIN) st_c<FUSE != 0>(vs + V_H + o, h);
+          if (wvec) st_c<FUSE != 0>(vs + V_H + o, h);
         }
       }
     }
@@ -842,6 +861,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 4: fc2 + log_softmax + NLL, then dlogits and the fc1
     // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
     STAMP(4);
+    if (KS > 1 && wave > 0) {
+      // split step, idle waves: this part's dgrad writes only its tiles' pool windows into
+      // dL/dconv1 and conv1 wgrad reads whole K-steps of it, so the rest must be zero
+      constexpr int NZ1 = (S_COFF - S_DC1) / 16;
+      uint4* z1 = reinterpret_cast<uint4*>(DC1);
+      for (int i = tid - 64; i < NZ1; i += NT - 64) z1[i] = make_uint4(0, 0, 0, 0);
+    }
     if (wave == 0) {
       const int t = STAGED ? LABEL[0] : t_lab;
       // Every LDS operand first (none depends on the logits): this lane's fc2 row slice
@@ -906,7 +932,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         float dl[10];
 #pragma unroll
         for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
-        if (lane < 16) {
+        if (wvec && lane < 16) {
           float mine = 0.f;
 #pragma unroll
           for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
@@ -921,7 +947,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
         const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
         DZ1B[lane] = h16<T>(dz);
-        if (lane < 50) st_c<FUSE != 0>(vs + V_DZ1 + lane, dz);
+        if (wvec && lane < 50) st_c<FUSE != 0>(vs + V_DZ1 + lane, dz);
       }
     }
     if (!TRAIN) return;
@@ -971,128 +997,247 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
     __syncthreads();
 
-    // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers, and
-    // conv2 dgrad -> dP1 -> relu/pool1 backward -> dC1
-    STAMP(6);
-    {
-      const unsigned short one = h16<T>(1.f);
-      // 16 waves x 16 columns cover the 251 B columns (k = wave*16 + l16) in one pass
-      frag fa[2][2];
-      u16x8 raw[2][1];
+    if constexpr (KS > 1) {
+      // ---------------- stage 6 (split step): this part's conv2 wgrad N-tile on waves 12-15,
+      // its dgrad tiles on waves 0-11 (each tile's 19 K-steps split over 4 or 6 waves)
+      STAMP(6);
+      if (wave >= 12) {
+        // waves 12-15 are the youngest on their SIMDs: raised priority for this short chain,
+        // which the dgrad waves beside it would otherwise starve of issue slots
+        __builtin_amdgcn_s_setprio(2);
+        const int k = (4 * part + (wave - 12)) * 16 + l16;  // B column: ic*25 + tap, 250 = bias
+        const int kc = min(k, 249), ic = kc / 25, r = kc - 25 * ic;
+        // B fragment of K-step ps, lane group kq: output row 4*ps + kq, pixels 0..7 of it:
+        // P1 row (4*ps + kq + kh), columns kw .. kw+7 -> two runs of 8 at immediate offsets
+        const unsigned short* pb = P1 + ic * 144 + (r / 5) * 12 + (r % 5) + kq * 12;
+        uint32_t rv0[8], rv1[8];
+        rv0[0] = lds_u16<0>(pb); rv0[1] = lds_u16<1>(pb); rv0[2] = lds_u16<2>(pb); rv0[3] = lds_u16<3>(pb);
+        rv0[4] = lds_u16<4>(pb); rv0[5] = lds_u16<5>(pb); rv0[6] = lds_u16<6>(pb); rv0[7] = lds_u16<7>(pb);
+        rv1[0] = lds_u16<48>(pb); rv1[1] = lds_u16<49>(pb); rv1[2] = lds_u16<50>(pb); rv1[3] = lds_u16<51>(pb);
+        rv1[4] = lds_u16<52>(pb); rv1[5] = lds_u16<53>(pb); rv1[6] = lds_u16<54>(pb); rv1[7] = lds_u16<55>(pb);
+        const frag f00 = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + kb);
+        const frag f10 = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + kb);
+        const frag f01 = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + 32 + kb);
+        const frag f11 = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + 32 + kb);
+        lds_wait8(rv0);
+        lds_wait8(rv1);
+        const unsigned short cst = k == 250 ? h16<T>(1.f) : (unsigned short)0;
+        u16x8 b0v, b1v;
 #pragma unroll
-      for (int ps = 0; ps < 2; ++ps) {
-        fa[ps][0] = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + ps * 32 + kb);
-        fa[ps][1] = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + ps * 32 + kb);
-        const int ohr = ((ps * 32 + kb) >> 3) * 12;
+        for (int jj = 0; jj < 8; ++jj) {
+          b0v[jj] = k < 250 ? (unsigned short)rv0[jj] : cst;
+          b1v[jj] = k < 250 ? (unsigned short)rv1[jj] : cst;
+        }
+        acc_c2[0][0] = Mfma<T>::mma(f00, __builtin_bit_cast(frag, b0v), acc_c2[0][0]);
+        acc_c2[1][0] = Mfma<T>::mma(f10, __builtin_bit_cast(frag, b0v), acc_c2[1][0]);
+        acc_c2[0][0] = Mfma<T>::mma(f01, __builtin_bit_cast(frag, b1v), acc_c2[0][0]);
+        acc_c2[1][0] = Mfma<T>::mma(f11, __builtin_bit_cast(frag, b1v), acc_c2[1][0]);
+        WSTAMP(12, 26);
+        // this part's conv2 wgrad columns, straight from the accumulators (one slab row per
+        // sample; their write latency hides under the dgrad of waves 0-11)
+        const bool kw = k < 250, kbias = k == 250;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[ps][0][j] = P1[opaque(kwb[0] + ohr + j)];
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int oc = mt * 16 + 4 * kq + rr;
+            const int slot = kw ? S_C2 + oc * 250 + k : S_C2 + 5000 + oc;
+            if (oc < 20 && (kw || kbias))
+              a.slab[((slot >> 6) * R2 + C1_CH * (G - R2) + b0) * 64 + (slot & 63)] = acc_c2[mt][0][rr];
+          }
+        if (stage_next) {  // this workgroup's sample of step cursor+1 (its own staging row g)
+          if (tid - 768 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 768] = px_next;
+          if (tid == 768) a.lstage[g] = lab_next;
+        }
+        __builtin_amdgcn_s_setprio(0);
       }
+      STAMP(9);
+      // dgrad partials go to conv1's per-thread address tables, unused by the staged path (not to
+      // a dead weight image: LDS traffic to the LDS-DMA target makes hipcc wait vmcnt(0), i.e.
+      // for this step's global stores)
+      float* SCR = reinterpret_cast<float*>(C1T);
+      static_assert(3 * 4 * 256 * 4 <= S_XC - S_C1T && 2 * 6 * 256 * 4 <= S_XC - S_C1T, "dgrad partials");
+      const int T3 = part == 0 ? 3 : 2;  // dgrad tiles part, part + 4 (, part + 8)
+      const int P = T3 == 3 ? 4 : 6;     // K parts per tile
+      if (wave < 12) {
+        const int ts = wave % T3, pp = wave / T3;
+        const int mw = (part + 4 * ts) * 16 + l16;
+        const int ks0 = pp * DG_KS / P, ks1 = (pp + 1) * DG_KS / P;  // at most 5 K-steps
+        const unsigned short* aw = DC2H + (mw / 12) * DC2H_RP + (mw % 12) * DG_OCP;
+        const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
+        const unsigned short* wz = W2d + ((DG_CH - 1) * 16 + l16) * 8;  // the zero chunk
+        int off[5];
 #pragma unroll
-      for (int jj = 0; jj < 1; ++jj) {
-        const int k = wave * 16 + l16;
-        const unsigned short cst = k == 250 ? one : (unsigned short)0;  // bias column / padding
+        for (int u = 0; u < 5; ++u) off[u] = DOFF[kq * 24 + min(ks0 + u, DG_KS - 1)];
+        // every fragment read in flight before the first MFMA (one LDS round trip, not five)
+        frag fa[5], fb[5];
 #pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
-          u16x8 rv = raw[ps][jj];
+        for (int u = 0; u < 5; ++u) {
+          const int ks = ks0 + u;
+          fa[u] = *reinterpret_cast<const frag*>(aw + off[u]);
+          fb[u] = *reinterpret_cast<const frag*>(ks < ks1 ? wrow + ks * 512 : wz);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c;  // two accumulator chains
 #pragma unroll
-          for (int j = 0; j < 8; ++j) rv[j] = k < 250 ? rv[j] : cst;
-          const frag fb = __builtin_bit_cast(frag, rv);
-          acc_c2[0][jj] = Mfma<T>::mma(fa[ps][0], fb, acc_c2[0][jj]);
-          acc_c2[1][jj] = Mfma<T>::mma(fa[ps][1], fb, acc_c2[1][jj]);
+        for (int u = 0; u < 5; ++u) {
+          if (u & 1) c1 = Mfma<T>::mma(fa[u], fb[u], c1);
+          else c = Mfma<T>::mma(fa[u], fb[u], c);
+        }
+        c += c1;
+        WSTAMP(0, 24);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) SCR[(ts * P + pp) * 256 + r * 64 + lane] = c[r];
+        WSTAMP(0, 25);
+        WSTAMP(4, 28);
+        WSTAMP(11, 29);
+      }
+      WSTAMP(12, 27);
+      __syncthreads();
+      STAMP(7);
+      if (tid < T3 * 256) {
+        // dgrad: fixed-order sum of the K parts, then the relu / pool1 backward into DC1
+        const int ts = tid >> 8, idx = tid & 255, row = idx >> 4, ci = idx & 15;
+        if (ci < 10) {
+          const int e = (row & 3) * 64 + (row >> 2) * 16 + ci;
+          float pv[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) pv[q] = SCR[(ts * P + q) * 256 + e];  // (q >= P: in bounds, unused)
+          float v = 0.f;
+#pragma unroll
+          for (int q = 0; q < 6; ++q) v += q < P ? pv[q] : 0.f;
+          dgrad_out<T>(DC1, P1, I1, ci, (part + 4 * ts) * 16 + row, v);
         }
       }
-    }
-    if (TRAIN && STAGED) {
-      stage_c2();  // final (one sample); stored by idle threads at stage 7
-      // the write latency of these stores hides under the dgrad
-      if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
-        if (tid >= 256 && tid - 256 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 256] = px_next;
-        if (tid == 256) a.lstage[g] = lab_next;
-      }
-    }
-    STAMP(9);
-    if (wave < 8) {
-      // dP1[px][ic] = sum_{tap, oc} DC2H[px + shift(tap)][oc] * W2D[ic][tap*24 + oc]:
-      // tile `wave` = pixels 16*wave .. +15, all 19 K-steps (tile 8 is split over waves
-      // 8-15 below, so each SIMD carries ~43 of the 171 MFMAs)
-      const s16x8 dof0 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24);
-      const s16x8 dof1 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 8);
-      const s16x8 dof2 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 16);
-      // B fragment of K-step ks: chunk 4*ks + kq, row l16 (ic)
-      const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
-      const int mw = wave * 16 + l16;
-      const unsigned short* aw = DC2H + (mw / 12) * DC2H_RP + (mw % 12) * DG_OCP;
-      // the pool1/ReLU gate of this lane's 4 outputs does not depend on the MFMAs:
-      // read it first so its LDS latency hides under the K loop
-      const int ci = min(l16, 9);
-      unsigned short gp[4];
-      uint8_t gi[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int pi = ci * 144 + wave * 16 + 4 * kq + r;
-        gp[r] = P1[pi];
-        gi[r] = I1[pi];
-      }
-      // two accumulator chains (even / odd K-steps) halve the dependent-MFMA latency
-      f32x4 cw0 = f32x4{0.f, 0.f, 0.f, 0.f}, cw1 = cw0;
-#pragma unroll
-      for (int ks = 0; ks < DG_KS; ++ks) {
-        const int off = ks < 8 ? dof0[ks] : (ks < 16 ? dof1[ks - 8] : dof2[ks - 16]);
-        const frag fa = *reinterpret_cast<const frag*>(aw + off);
-        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 512);
-        if (ks & 1) cw1 = Mfma<T>::mma(fa, fb, cw1);
-        else cw0 = Mfma<T>::mma(fa, fb, cw0);
-      }
-      if (l16 < 10) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int mm = wave * 16 + 4 * kq + r;
-          const float v = f16v<T>(gp[r]) > 0.f ? cw0[r] + cw1[r] : 0.f;
-          dgrad_store<T>(DC1, l16, mm, v, gi[r]);
-        }
-      }
+      WSTAMP(0, 30);
+      WSTAMP(12, 31);
+      __syncthreads();
     } else {
-      // tile 8 (pixels 128..143), K-steps ks = (wave - 8) + 8j: a split-K share
-      const int w8 = wave - 8, m8 = 128 + l16;
-      const unsigned short* a8 = DC2H + (m8 / 12) * DC2H_RP + (m8 % 12) * DG_OCP;
-      const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
-      f32x4 c8 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int ks = w8 + 8 * j;  // the third share only for w8 < 3 (others read the zero chunk)
-        const int off = DOFF[kq * 24 + min(ks, DG_KS - 1)];
-        const frag fa = *reinterpret_cast<const frag*>(a8 + off);
-        const frag fb = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 512 : W2d + ((DG_CH - 1) * 16 + l16) * 8);
-        c8 = Mfma<T>::mma(fa, fb, c8);
+    // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers, and
+      // conv2 dgrad -> dP1 -> relu/pool1 backward -> dC1
+      STAMP(6);
+      {
+        const unsigned short one = h16<T>(1.f);
+        // 16 waves x 16 columns cover the 251 B columns (k = wave*16 + l16) in one pass
+        frag fa[2][2];
+        u16x8 raw[2][1];
+  #pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+          fa[ps][0] = *reinterpret_cast<const frag*>(DC2 + l16 * LD_DC2 + ps * 32 + kb);
+          fa[ps][1] = *reinterpret_cast<const frag*>(DC2 + (16 + l16) * LD_DC2 + ps * 32 + kb);
+          const int ohr = ((ps * 32 + kb) >> 3) * 12;
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) raw[ps][0][j] = P1[opaque(kwb[0] + ohr + j)];
+        }
+  #pragma unroll
+        for (int jj = 0; jj < 1; ++jj) {
+          const int k = wave * 16 + l16;
+          const unsigned short cst = k == 250 ? one : (unsigned short)0;  // bias column / padding
+  #pragma unroll
+          for (int ps = 0; ps < 2; ++ps) {
+            u16x8 rv = raw[ps][jj];
+  #pragma unroll
+            for (int j = 0; j < 8; ++j) rv[j] = k < 250 ? rv[j] : cst;
+            const frag fb = __builtin_bit_cast(frag, rv);
+            acc_c2[0][jj] = Mfma<T>::mma(fa[ps][0], fb, acc_c2[0][jj]);
+            acc_c2[1][jj] = Mfma<T>::mma(fa[ps][1], fb, acc_c2[1][jj]);
+          }
+        }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) RED[w8 * 256 + (4 * kq + r) * 16 + l16] = c8[r];
-    }
-    __syncthreads();
-    STAMP(7);
-    if (TRAIN && STAGED && tid >= 256) store_c2(tid - 256, NT - 256);  // write latency hides under stage 8
-    if (tid < 256) {  // tile 8: fixed-order sum of the 8 shares, then the pool1/relu backward
-      const int rr = tid >> 4, ci = tid & 15;
-      if (ci < 10) {
-        float v = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v += RED[q * 256 + rr * 16 + ci];
-        dgrad_out<T>(DC1, P1, I1, ci, 128 + rr, v);
+      if (TRAIN && STAGED) {
+        stage_c2();  // final (one sample); stored by idle threads at stage 7
+        // the write latency of these stores hides under the dgrad
+        if (stage_next) {  // this workgroup's sample of step cursor+1 (it read slot g at its start)
+          if (tid >= 256 && tid - 256 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 256] = px_next;
+          if (tid == 256) a.lstage[g] = lab_next;
+        }
       }
+      STAMP(9);
+      if (wave < 8) {
+        // dP1[px][ic] = sum_{tap, oc} DC2H[px + shift(tap)][oc] * W2D[ic][tap*24 + oc]:
+        // tile `wave` = pixels 16*wave .. +15, all 19 K-steps (tile 8 is split over waves
+        // 8-15 below, so each SIMD carries ~43 of the 171 MFMAs)
+        const s16x8 dof0 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24);
+        const s16x8 dof1 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 8);
+        const s16x8 dof2 = *reinterpret_cast<const s16x8*>(DOFF + kq * 24 + 16);
+        // B fragment of K-step ks: chunk 4*ks + kq, row l16 (ic)
+        const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
+        const int mw = wave * 16 + l16;
+        const unsigned short* aw = DC2H + (mw / 12) * DC2H_RP + (mw % 12) * DG_OCP;
+        // the pool1/ReLU gate of this lane's 4 outputs does not depend on the MFMAs:
+        // read it first so its LDS latency hides under the K loop
+        const int ci = min(l16, 9);
+        unsigned short gp[4];
+        uint8_t gi[4];
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int pi = ci * 144 + wave * 16 + 4 * kq + r;
+          gp[r] = P1[pi];
+          gi[r] = I1[pi];
+        }
+        // two accumulator chains (even / odd K-steps) halve the dependent-MFMA latency
+        f32x4 cw0 = f32x4{0.f, 0.f, 0.f, 0.f}, cw1 = cw0;
+  #pragma unroll
+        for (int ks = 0; ks < DG_KS; ++ks) {
+          const int off = ks < 8 ? dof0[ks] : (ks < 16 ? dof1[ks - 8] : dof2[ks - 16]);
+          const frag fa = *reinterpret_cast<const frag*>(aw + off);
+          const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 512);
+          if (ks & 1) cw1 = Mfma<T>::mma(fa, fb, cw1);
+          else cw0 = Mfma<T>::mma(fa, fb, cw0);
+        }
+        if (l16 < 10) {
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int mm = wave * 16 + 4 * kq + r;
+            const float v = f16v<T>(gp[r]) > 0.f ? cw0[r] + cw1[r] : 0.f;
+            dgrad_store<T>(DC1, l16, mm, v, gi[r]);
+          }
+        }
+      } else {
+        // tile 8 (pixels 128..143), K-steps ks = (wave - 8) + 8j: a split-K share
+        const int w8 = wave - 8, m8 = 128 + l16;
+        const unsigned short* a8 = DC2H + (m8 / 12) * DC2H_RP + (m8 % 12) * DG_OCP;
+        const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
+        f32x4 c8 = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int ks = w8 + 8 * j;  // the third share only for w8 < 3 (others read the zero chunk)
+          const int off = DOFF[kq * 24 + min(ks, DG_KS - 1)];
+          const frag fa = *reinterpret_cast<const frag*>(a8 + off);
+          const frag fb = *reinterpret_cast<const frag*>(ks < DG_KS ? wrow + ks * 512 : W2d + ((DG_CH - 1) * 16 + l16) * 8);
+          c8 = Mfma<T>::mma(fa, fb, c8);
+        }
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) RED[w8 * 256 + (4 * kq + r) * 16 + l16] = c8[r];
+      }
+      __syncthreads();
+      STAMP(7);
+      if (TRAIN && STAGED && tid >= 256) store_c2(tid - 256, NT - 256);  // write latency hides under stage 8
+      if (tid < 256) {  // tile 8: fixed-order sum of the 8 shares, then the pool1/relu backward
+        const int rr = tid >> 4, ci = tid & 15;
+        if (ci < 10) {
+          float v = 0.f;
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) v += RED[q * 256 + rr * 16 + ci];
+          dgrad_out<T>(DC1, P1, I1, ci, 128 + rr, v);
+        }
+      }
+      __syncthreads();
+  
     }
-    __syncthreads();
 
     // ---------------- stage 8: conv1 wgrad (+bias column 25), accumulate in registers
-    // (tile wave&1, K-steps ps = (wave>>1) + 8i: 18 steps over 8 wave pairs)
+    // (tile wave&1, K-steps ps = (wave>>1) + 8i: 18 steps over 8 wave pairs; split step: over
+    // the 6 pairs of waves 0-11, waves 12-15 only store)
     STAMP(8);
-    {
+    if (KS == 1 || wave < 12) {
       // B fragment = X[base + 0..7] (one output row run of 8 pixels), two aligned b64
       // reads from the shifted copy; columns past the 25 taps read a constant run instead
       // (ones for the bias column 25, zeros beyond), so nothing is masked per element
       frag fa[3], fbv[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        const int ps = min((wave >> 1) + 8 * i, 17);
+        const int ps = min((wave >> 1) + (KS > 1 ? 6 : 8) * i, 17);
         const int p0 = ps * 32 + kb;
         fa[i] = *reinterpret_cast<const frag*>(DC1 + l16 * LD_DC1 + p0);
         const int oh = p0 / 24, ow0 = p0 - oh * 24;
@@ -1100,9 +1245,22 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         const uint2 lo = reinterpret_cast<const uint2*>(src)[0], hi = reinterpret_cast<const uint2*>(src)[1];
         fbv[i] = __builtin_bit_cast(frag, uint4{lo.x, lo.y, hi.x, hi.y});
       }
+      // split step: only the K-steps (32 conv1 pixels each) under this part's dgrad tiles
+      // carry gradient (the rest of DC1 is zero)
+      uint32_t need = (1u << 18) - 1;
+      if (KS > 1) {
+        need = 0;
+        for (int ts = 0; ts < (part == 0 ? 3 : 2); ++ts) {
+          const int t = part + 4 * ts, py0 = (16 * t) / 12, py1 = (16 * t + 15) / 12;
+          const int ps0 = (48 * py0) / 32, ps1 = (48 * (py1 + 1) - 1) / 32;
+          need |= ((2u << ps1) - 1) & ~((1u << ps0) - 1);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 3; ++i)
-        if ((wave >> 1) + 8 * i < 18) acc_c1 = Mfma<T>::mma(fa[i], fbv[i], acc_c1);
+        if ((KS == 1 || wave < 12) && (wave >> 1) + (KS > 1 ? 6 : 8) * i < 18 &&
+            ((need >> ((wave >> 1) + (KS > 1 ? 6 : 8) * i)) & 1u))
+          acc_c1 = Mfma<T>::mma(fa[i], fbv[i], acc_c1);
     }
     STAMP(14);
   };
@@ -1137,9 +1295,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       store_c2(tid - 512, NT - 512);
     }
   }
-  if (tid == 0) {
-    st_c<FUSE != 0>(a.loss_acc + 2 * g, loss_sum);
-    st_c<FUSE != 0>(a.loss_acc + 2 * g + 1, correct);
+  if (tid == 0) {  // (split step: part 0 reports the sample)
+    st_c<FUSE != 0>(a.loss_acc + 2 * g, own_vec ? loss_sum : 0.f);
+    st_c<FUSE != 0>(a.loss_acc + 2 * g + 1, own_vec ? correct : 0.f);
   }
   if (a.dbg) {
     if (tid == 0) DBGS[23] = __builtin_amdgcn_s_memrealtime();
@@ -1237,8 +1395,8 @@ __global__ void lenet_pack_kernel(const float* __restrict__ params, unsigned sho
 //
 // Reductions run in a fixed order everywhere: bitwise reproducible.
 // ---------------------------------------------------------------------------
-constexpr int CNQ = CNP / 4;                        // conv float4 columns (1320)
-constexpr int NB_CONV = (CNQ + UP_C - 1) / UP_C;    // 83
+constexpr int NB_CONV = N_CHUNKS;                   // 84: one 64-slot slab chunk per block half
+static_assert(UP_C * 4 == 64, "a CONV block half reduces one 64-slot slab chunk");
 constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
 // FC role: wpt waves per tile (K split over them), 8 / wpt tiles per block.  A
 // small batch uses one wave per tile (no combine, no barrier: the tile's K is one
@@ -1281,15 +1439,16 @@ constexpr int IMG_U4 = 784 / 16;  // 49 16-byte chunks per image
 
 __device__ __forceinline__ void gather_batch(const LenetStageArgs& st, int64_t step, int64_t* rows_sh) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  for (int b = tid; b < st.B; b += nt) {
-    const int64_t row = st.perm[min(step * st.B + b, st.perm_len - 1)];
+  const int nrows = st.rows > 0 ? st.rows : st.B;  // staging row r holds sample r % B (split step)
+  for (int b = tid; b < nrows; b += nt) {
+    const int64_t row = st.perm[min(step * st.B + b % st.B, st.perm_len - 1)];
     rows_sh[b] = row;
     st.lstage[b] = st.labels[row];
   }
   __syncthreads();
   const uint4* __restrict__ src = reinterpret_cast<const uint4*>(st.images);
   uint4* __restrict__ dst = reinterpret_cast<uint4*>(st.xstage);
-  const int total = st.B * IMG_U4;
+  const int total = nrows * IMG_U4;
   constexpr int U = 8;
   for (int i0 = tid; i0 < total; i0 += nt * U) {
     uint4 v[U];
@@ -1486,29 +1645,32 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     float4 (*part)[UP_C] = reinterpret_cast<float4 (*)[UP_C]>(part_ + half * UP_S * UP_C);
     float (*part2)[UP_C * 4] = reinterpret_cast<float (*)[UP_C * 4]>(part2_ + half * 4 * UP_C * 4);
     const int cl = ht & (UP_C - 1), sl = ht / UP_C;
-    // the half's first wave owns params pbc*64 + ht (16 float4 columns): prefetch p / m now
-    const int pi = pbc * (UP_C * 4) + ht;
+    // the half's first wave owns slab slots pbc*64 + ht (16 float4 columns) = parameter pi
+    // (-1: padding slot): prefetch p / m now
+    const int pi = slot_param(pbc * (UP_C * 4) + min(ht, 63));
     float p0 = 0.f, m0 = 0.f;
     int d0 = -1, d1 = -1;
     if (a.apply_sgd && ht < 64) {
-      p0 = a.params[min(pi, NP - 1)];
-      m0 = a.momentum[min(pi, NP - 1)];
-      image_slots(pi, d0, d1);
+      p0 = a.params[max(pi, 0)];
+      m0 = a.momentum[max(pi, 0)];
+      image_slots(max(pi, 0), d0, d1);
     }
     wait_ready();
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     // Loads are unconditional from a clamped address and masked afterwards: a
     // per-element "load or zero" select makes hipcc branch around every load
     // and wait vmcnt(0) each time (dependent round trips instead of one).
-    // chunk blk of the slab is [WG][16 float4]: contiguous for this block
-    const float4* sp = reinterpret_cast<const float4*>(a.slab) + (int64_t)pbc * a.grid * UP_C + cl;
-    for (int g0 = sl; g0 < a.grid; g0 += UP_S * UP_MAXL) {
+    // chunk pbc of the slab is [row][16 float4]: contiguous for this block; conv1 chunks have a
+    // row per workgroup, conv2 chunks a row per sample (kernels/lenet_layout.h)
+    const int rows = pbc < C1_CH ? a.grid : min(a.grid, B);
+    const float4* sp = reinterpret_cast<const float4*>(a.slab + slab_off(pbc * 64, 0, a.grid, min(a.grid, B))) + cl;
+    for (int g0 = sl; g0 < rows; g0 += UP_S * UP_MAXL) {
       float4 v[UP_MAXL];
 #pragma unroll
-      for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(g0 + u * UP_S, a.grid - 1) * UP_C);
+      for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(g0 + u * UP_S, rows - 1) * UP_C);
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u)
-        if (g0 + u * UP_S < a.grid) add4(acc, v[u]);
+        if (g0 + u * UP_S < rows) add4(acc, v[u]);
     }
     USTAMP(1);
     part[sl][cl] = acc;
@@ -1522,7 +1684,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     }
     __syncthreads();
     USTAMP(3);
-    if (ht < 64 && live_pb && pi < CNP) {
+    if (ht < 64 && live_pb && pi >= 0) {
       float g[1] = {(part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])};
       if (EXCH) {
         const int idx[1] = {pi};
@@ -1773,12 +1935,19 @@ int64_t lenet_vec_len() { return VEC; }
 
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   if (a.mfma_dtype == kF32) return launch_lenet_train_f32(a, 0, nullptr, true, s);  // lenet_fused_f32.hip
-  if (a.B <= 0 || a.grid <= 0 || a.grid > a.B) return hipErrorInvalidValue;
+  // split step: a staged batch with SPLIT_K workgroups (parts) per sample, one staging row each
+  const bool split = a.xstage && a.lstage && a.grid == SPLIT_K * a.B && a.grid <= 256;
+  if (a.B <= 0 || a.grid <= 0 || (a.grid > a.B && !split)) return hipErrorInvalidValue;
   // a staged batch has one sample per workgroup (the STAGED instantiation relies on it)
-  if (a.xstage && (a.grid != a.B || !a.lstage)) return hipErrorInvalidValue;
+  if (a.xstage && ((a.grid != a.B && !split) || !a.lstage)) return hipErrorInvalidValue;
   const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
-    if (a.xstage) {
+    if (split) {
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 0, SPLIT_K>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 0, SPLIT_K>), dim3(a.grid), dim3(NT), lds, s,
+                         a, 0, (float*)nullptr, StepFuse{});
+    } else if (a.xstage) {
       hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 0>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 0>), dim3(a.grid), dim3(NT), lds, s, a, 0,
@@ -1876,9 +2045,10 @@ hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, 
 }
 
 int lenet_stage_max_batch() { return STAGE_MAXB; }
+int lenet_split_k() { return SPLIT_K; }
 
 hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hipStream_t s) {
-  if (a.B <= 0 || a.B > STAGE_MAXB || !a.xstage || !a.lstage) return hipErrorInvalidValue;
+  if (a.B <= 0 || a.B > STAGE_MAXB || a.rows > STAGE_MAXB || !a.xstage || !a.lstage) return hipErrorInvalidValue;
   hipLaunchKernelGGL(lenet_stage_kernel, dim3(1), dim3(512), 0, s, a, cursor);
   return hipGetLastError();
 }

@@ -28,15 +28,13 @@
 // rows / columns of A / B only feed discarded outputs; K padding reads exact zeros.
 #include "common.h"
 #include "dispatch.h"
+#include "kernels/lenet_layout.h"
 
 namespace csed {
 namespace lenet32 {
 
+using namespace csed::lenet;  // parameter order, slab and vector-slab layouts (lenet_layout.h)
 constexpr int NT = 1024, NW = 16;
-constexpr int NP = 21840;
-constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O_F1B = 21280,
-              O_F2W = 21330, O_F2B = 21830;
-constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;  // = lenet_fused.hip
 constexpr int LW1 = 321;  // fc1 weight row stride (odd: the fc1-forward lanes walk rows)
 constexpr int LW2 = 260;  // conv2 weight row stride (== 4 mod 64: conflict-free B fragments)
 
@@ -498,7 +496,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
 
   // ---------------- epilogue: this workgroup's partial conv gradient + loss
   if (TRAIN) {
-    auto slab_at = [&](int e) { return a.slab + ((int64_t)(e >> 6) * G + g) * 64 + (e & 63); };
+    auto slab_at = [&](int e) { return a.slab + slab_off(slab_slot(e), g, G, G); };  // grid <= B: R2 = G
     if (tid < 250) *slab_at(O_C1W + tid) = acc_c1;
     else if (tid >= 256 && tid < 266) *slab_at(O_C1B + tid - 256) = acc_c1;
     const int k = wave * 16 + l16;

@@ -1,0 +1,46 @@
+// Layout contract shared by the fused LeNet kernels (lenet_fused.hip: 16-bit train, update,
+// eval; lenet_fused_f32.hip: exact-fp32 train, eval) -- the flat parameter order, the
+// per-workgroup conv-gradient slab and the per-sample fc vector slab.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace csed {
+namespace lenet {
+
+// Flat parameter order (= Net.state_dict() order, 21,840 floats, ref src/model.py:9-13)
+constexpr int NP = 21840;
+constexpr int O_C1W = 0, O_C1B = 250, O_C2W = 260, O_C2B = 5260, O_F1W = 5280, O_F1B = 21280,
+              O_F2W = 21330, O_F2B = 21830;
+constexpr int CNP = O_F1W;  // conv parameters (conv1.w, conv1.b, conv2.w, conv2.b)
+
+// Conv-gradient slab: 64-float chunks, row-major inside a chunk ([chunk][row][64]) so that
+// lenet_update reads each chunk contiguously.  conv1's 260 parameters fill chunks 0-4 (slab
+// slots 0..319, 60 padding) with ONE ROW PER WORKGROUP; conv2's 5,020 fill chunks 5-83 (slots
+// 320..5375) with ONE ROW PER SAMPLE: in the split step (several workgroups per sample) the
+// workgroups of a sample own disjoint conv2 columns but each holds a partial conv1 sum.
+constexpr int C1_CH = 5;
+constexpr int S_C2 = C1_CH * 64;                                 // slab slot of conv2.w[0]
+constexpr int CNP_PAD = S_C2 + ((CNP - O_C2W) + 63) / 64 * 64;   // 5376 slots = 84 chunks
+constexpr int N_CHUNKS = CNP_PAD / 64;
+__host__ __device__ constexpr int slab_slot(int p) { return p < O_C2W ? p : p - O_C2W + S_C2; }
+// parameter of a slab slot, -1 for padding
+__host__ __device__ constexpr int slot_param(int s) {
+  return s < O_C2W ? s : (s < S_C2 ? -1 : (s - S_C2 + O_C2W < CNP ? s - S_C2 + O_C2W : -1));
+}
+// rows of a chunk: G (workgroups) for conv1 chunks, R2 = min(G, B) for conv2 chunks
+// (32-bit arithmetic: at most 84 chunks x 256 rows x 64 slots)
+__host__ __device__ inline int slab_off(int s, int row, int G, int R2) {
+  const int c = s >> 6;
+  const int r = c < C1_CH ? c * G + row : C1_CH * (G - R2) + c * R2 + row;
+  return r * 64 + (s & 63);
+}
+
+// per-sample vector slab (fp32): fc1 input P2 | dL/dz1 | fc1 output H | dL/dlogits
+constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;
+
+// Split step: workgroups per sample (the backward conv stages are divided among them)
+constexpr int SPLIT_K = 4;
+
+}  // namespace lenet
+}  // namespace csed

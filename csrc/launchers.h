@@ -162,7 +162,9 @@ struct LenetStageArgs {
   const uint8_t* images; const int64_t* labels; const int64_t* perm; int64_t perm_len;
   int B;                     // <= lenet_stage_max_batch()
   uint8_t* xstage; int64_t* lstage;
+  int rows;                  // staging rows (0 = B); row r holds sample r % B (split step: SPLIT_K * B)
 };
+int lenet_split_k();         // workgroups per sample of the split step (grid = split_k * B)
 int lenet_stage_max_batch();
 // Gather the batch of step cursor[0] (no counter change).
 hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hipStream_t s);

@@ -41,16 +41,17 @@ def test_no_ipc_without_distributed_gpu(monkeypatch):
 
 def test_exchange_buffer_layout():
     """lenet_update's exchange words: conv params 0..5279 map to themselves, each of the
-    88 fc tiles owns 256 words after the 64-aligned conv block (csrc/kernels/lenet_fused.hip)."""
+    88 fc tiles owns 256 words after the conv slab row (csrc/kernels/lenet_layout.h: conv1's
+    260 slots padded to 5 chunks, conv2's 5020 to 79: 84 chunks of 64 = 5376)."""
     from csed_514_project_distributed_training_using_pytorch_amd.ops import _native
 
     if not _native.load(build_if_missing=False):
         pytest.skip("native extension not built")
     layout = [int(v) for v in torch.ops.csed.lenet_layout()]
     conv_pad, nparams, words = layout[1], layout[3], layout[5]
-    assert nparams == 21840 and conv_pad == 5312
+    assert nparams == 21840 and conv_pad == 5376 and layout[8] == 4  # split step: 4 workgroups / sample
     fc_tiles = 4 * 21 + 4  # fc1: 4 x 21 tiles of [dW1 | db1], fc2: 4 tiles of [dW2 | db2]
-    assert words == conv_pad + fc_tiles * 256 == 27840
+    assert words == conv_pad + fc_tiles * 256 == 27904
     assert words % 4 == 0  # the IPC buffers are allocated in multiples of 4 words
 
 

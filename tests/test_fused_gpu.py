@@ -24,7 +24,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("dt,tol", [(torch.bfloat16, 6e-2), (torch.float16, 2.5e-2)])
-@pytest.mark.parametrize("B,grid", [(64, 64), (64, 16), (8, 8), (100, 7)])
+@pytest.mark.parametrize("B,grid", [(64, 64), (64, 16), (8, 8), (100, 7), (64, None), (8, None)])
 def test_fused_gradient_matches_reference(dt, tol, B, grid):
     data = synthetic_mnist(256, seed=11)
     torch.manual_seed(1)
@@ -192,7 +192,7 @@ def test_batch_staging_is_bitwise_transparent(B):
     finals = []
     for staged in (True, False):
         torch.manual_seed(1)
-        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B, split=False)
         assert eng.staged
         eng.staged = staged
         g = torch.Generator().manual_seed(7)
@@ -219,7 +219,8 @@ def test_one_kernel_step_matches_two_kernels(B, dampening):
     finals = []
     for one in (True, False):
         torch.manual_seed(3)
-        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B, dampening=dampening)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B, dampening=dampening,
+                                split=False)
         assert eng.staged and not eng.one_kernel  # eligible; two kernels by default
         eng.one_kernel = one
         assert eng.step_kind.startswith("one kernel") == one
@@ -275,3 +276,50 @@ def test_fused_trajectory_matches_cpu_reference(dtype, band):
     assert ((gl - cl).abs() / cl).max() < band, list(zip(gpu_l, cpu_l))
     for (name, p_ref), p in zip(ref.named_parameters(), net.parameters()):
         assert _rel(p.detach().cpu(), p_ref.detach()) < band, name
+
+
+@pytest.mark.parametrize("B", [64, 8, 24])
+def test_split_step_matches_one_workgroup_per_sample(B):
+    """The split step (4 workgroups per sample dividing the backward conv stages) computes the
+    same gradient as one workgroup per sample, up to summation order (dgrad K parts, conv1
+    wgrad partials summed by lenet_update); loss and accuracy are identical."""
+    data = synthetic_mnist(256, seed=23)
+    order = torch.randperm(256, generator=torch.Generator().manual_seed(1))[:B]
+    res = []
+    for split in (True, False):
+        torch.manual_seed(3)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, global_batch=B, drop_p=0.0, split=split)
+        assert eng.split == split and eng.grid == (4 * B if split else B)
+        eng.set_epoch_order(order)
+        g = eng.gradient()
+        torch.cuda.synchronize()
+        res.append((g, eng.loss_acc.clone()))
+    (gs, ls), (g1, l1) = res
+    assert torch.equal(ls, l1)
+    net = Net()
+    off = 0
+    for name, p in net.named_parameters():
+        n = p.numel()
+        rel = _rel(gs[off:off + n], g1[off:off + n])
+        assert rel < 2e-2, f"{name}: split vs one-workgroup relative L2 error {rel:.3e}"
+        if name.startswith("fc"):
+            assert torch.equal(gs[off:off + n], g1[off:off + n]), name  # fc grads: same kernel path
+        off += n
+
+
+def test_split_step_trains_and_replays_bitwise():
+    """Graph-replayed split steps across an epoch boundary (with the tail step) equal the same
+    steps launched eagerly, bit for bit; staging rows stay per workgroup."""
+    data = synthetic_mnist(64 * 5 + 17, seed=5)
+    finals = []
+    for use_graph in (True, False):
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=64)
+        assert eng.split and eng.grid == 256 and eng.xstage.shape[0] == 256
+        g = torch.Generator().manual_seed(7)
+        for _ in range(2):
+            eng.train_epoch(torch.randperm(len(data), generator=g), steps_per_graph=2, use_graph=use_graph)
+        torch.cuda.synchronize()
+        finals.append((eng.flat.data.clone(), eng.loss_acc.clone()))
+    assert torch.equal(finals[0][0], finals[1][0]) and torch.equal(finals[0][1], finals[1][1])
+    assert torch.isfinite(finals[0][0]).all()

@@ -22,12 +22,13 @@ NAMES = ["preamble end->stage 0", "pixels+masks+prefetch", "conv1", "conv2", "fc
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-    grid = int(sys.argv[2]) if len(sys.argv) > 2 else B
+    grid = int(sys.argv[2]) if len(sys.argv) > 2 else None  # default: the engine's (split step: 4 * B)
     dev = torch.device("cuda")
     n = max(4096, 2 * B)
     data = synthetic_mnist(n, seed=1)
     torch.manual_seed(1)
     eng = FusedLeNetTrainer(Net().to(dev), data, global_batch=B, grid=grid)
+    grid = eng.grid
     eng.set_epoch_order(torch.randperm(n))
     dbg = torch.zeros(grid * 32, dtype=torch.long, device=dev)
     for _ in range(20):
