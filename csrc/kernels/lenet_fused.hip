@@ -815,26 +815,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
     __syncthreads();
 
-    // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3)
+    // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3; the idle waves
+    // zeroing / X copies moved to stage 4, where 15 waves are idle)
     STAMP(3);
     if (stage_next && (KS > 1 ? wave >= 12 : (wave >= 4 && wave < 8))) {  // the waves holding nrow
       px_next = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[min(tid & 255, 195)];
       lab_next = a.labels[nrow];
-    }
-    if (wave >= 8) {
-      // idle waves: zero the dgrad input image (its 4-pixel border and channels 20-23
-      // are the convolution's zero padding; stage 5 writes the interior), and make the
-      // shifted copies of X that conv1 wgrad reads as aligned runs (stage 8)
-      constexpr int NZ = (S_DC1 - S_DC2H) / 16;
-      uint4* z = reinterpret_cast<uint4*>(DC2H);
-      for (int i = tid - 512; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
-
-      for (int m = tid - 512; m < 784; m += 512) {
-        const unsigned short v = Xs[m];
-#pragma unroll
-        for (int k = 1; k < 4; ++k)
-          if (m - k >= 0) XC[(k - 1) * XC_LD + m - k] = v;
-      }
     }
     if (wave < 4) {
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
@@ -861,12 +847,26 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 4: fc2 + log_softmax + NLL, then dlogits and the fc1
     // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
     STAMP(4);
-    if (KS > 1 && wave > 0) {
-      // split step, idle waves: this part's dgrad writes only its tiles' pool windows into
-      // dL/dconv1 and conv1 wgrad reads whole K-steps of it, so the rest must be zero
-      constexpr int NZ1 = (S_COFF - S_DC1) / 16;
-      uint4* z1 = reinterpret_cast<uint4*>(DC1);
-      for (int i = tid - 64; i < NZ1; i += NT - 64) z1[i] = make_uint4(0, 0, 0, 0);
+    if (TRAIN && wave > 0) {
+      // waves 1-15 are idle here: zero the dgrad input image (its 4-pixel border and channels
+      // 20-23 are the convolution's zero padding; stage 5 writes the interior), make the
+      // shifted copies of X that conv1 wgrad reads as aligned runs (stage 8), and in the
+      // split step zero dL/dconv1 (this part's dgrad writes only its tiles' pool windows
+      // and conv1 wgrad reads whole K-steps of it)
+      constexpr int NZ = (S_DC1 - S_DC2H) / 16;
+      uint4* z = reinterpret_cast<uint4*>(DC2H);
+      for (int i = tid - 64; i < NZ; i += NT - 64) z[i] = make_uint4(0, 0, 0, 0);
+      for (int m = tid - 64; m < 784; m += NT - 64) {
+        const unsigned short v = Xs[m];
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+          if (m - k >= 0) XC[(k - 1) * XC_LD + m - k] = v;
+      }
+      if (KS > 1) {
+        constexpr int NZ1 = (S_COFF - S_DC1) / 16;
+        uint4* z1 = reinterpret_cast<uint4*>(DC1);
+        for (int i = tid - 64; i < NZ1; i += NT - 64) z1[i] = make_uint4(0, 0, 0, 0);
+      }
     }
     if (wave == 0) {
       const int t = STAGED ? LABEL[0] : t_lab;

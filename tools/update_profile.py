@@ -38,7 +38,7 @@ def main():
     def train():
         ops.lenet_train(eng.train_data.images, eng.train_data.labels, eng.perm, eng.cursor, B, 0, eng.wimg,
                         eng.flat.data, eng.slab, eng.vslab, eng.loss_parts, 1.0 / B, MNIST_MEAN, MNIST_STD, 0.5, 1,
-                        eng.rng_offset, eng.grid, eng.mfma)
+                        eng.rng_offset, eng.grid, eng.mfma, None, eng.xstage, eng.lstage, False)
 
     common = lambda: (eng.flat.data, eng.momentum_buf, eng.wimg, 0.01, 0.5, 0.0, 0.0, False, eng.step_count,
                       eng.ticket)
@@ -82,8 +82,8 @@ def main():
         torch.cuda.synchronize()
     st = dbg.view(256, 8).cpu().double()
     wpt = 1 if B <= 128 else (2 if B <= 256 else (4 if B <= 512 else 8))  # fc_waves_per_tile
-    nfc = 88 // (8 // wpt)  # blocks [0, nfc) FC role, then 83 CONV role blocks
-    nb = nfc + 83
+    nfc = 88 if wpt == 1 else 88 // (8 // wpt)  # blocks [0, nfc) FC role, then 84 CONV role blocks
+    nb = nfc + 84
     t0 = st[:nb, 0].min()
     rel = (st - t0) * 0.01  # us
     for role, sl, ks in [("CONV", slice(nfc, nb), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 3, 4])]:
