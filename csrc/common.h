@@ -86,6 +86,27 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Kernel-argument prefetch.  hipcc reads each argument with a scalar load placed near its
+// first use, behind its own wait.  A graph-replayed kernel's argument segment is cold in
+// the scalar cache (and in L2, behind the launch's cache invalidation), so every new
+// 64-byte line of it costs a serial memory round trip: four or five of them sat in front
+// of lenet_update's first data load.  Touching every line of the first BYTES bytes once
+// at kernel entry -- all loads in flight, one wait -- leaves one round trip; the argument
+// loads that follow hit the scalar cache.  (One dword at each line start: never past the
+// explicit arguments.)
+template <int BYTES>
+__device__ __forceinline__ void prefetch_kernargs() {
+  constexpr int L = (BYTES + 63) / 64;
+  static_assert(L >= 1 && L <= 12, "one to twelve argument lines");
+  typedef const __attribute__((address_space(4))) uint32_t* kptr;
+  const kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t v[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) v[i] = ka[16 * (i < L ? i : 0)];
+  asm volatile("" ::"s"(v[0]), "s"(v[1]), "s"(v[2]), "s"(v[3]), "s"(v[4]), "s"(v[5]), "s"(v[6]), "s"(v[7]),
+               "s"(v[8]), "s"(v[9]), "s"(v[10]), "s"(v[11]));
+}
+
 // ---------------------------------------------------------------------------
 // Counter-based RNG (Philox4x32-10).  Dropout masks are a pure function of
 // (seed, offset, element), so forward and backward regenerate the identical

@@ -220,6 +220,8 @@ __device__ __forceinline__ s16x4 lds_read_tr16(const unsigned short* p) {
 // An LDS index the compiler cannot relate to its neighbours: keeps a run of
 // 16-bit reads at a sliding (2-byte aligned) window as single ds_read_u16s
 // instead of one merged, misaligned ds_read_b128 (replayed at ~64 cycles).
+__device__ const int64_t kZeroWord = 0;
+
 __device__ __forceinline__ int opaque(int x) {
   asm("" : "+v"(x));
   return x;
@@ -403,6 +405,9 @@ template <typename T, bool TRAIN, bool STAGED, int FUSE, int KS = 1>
 __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out,
                                                             StepFuse fz) {
   static_assert(KS == 1 || (KS == SPLIT_K && STAGED && FUSE == 0 && TRAIN), "split step: staged training only");
+  // argument lines this instantiation reads (the fused-step block only with FUSE)
+  struct TrainKargs { LenetTrainArgs a; int write_logp; float* logp_out; };
+  prefetch_kernargs<FUSE ? (int)(sizeof(TrainKargs) + sizeof(StepFuse)) : (int)sizeof(TrainKargs)>();
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
   // per-sample activations (dynamic).  Being distinct objects, accesses to the
   // activations are provably disjoint from the in-flight DMA, so the compiler's
@@ -466,7 +471,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     return;
   }
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
-  const int G = FUSE ? a.grid : (int)gridDim.x, g = blockIdx.x;
+  // (a.grid, not gridDim.x: every launcher sets it, and it is in the prefetched argument lines)
+  const int G = a.grid, g = blockIdx.x;
   // this workgroup's (first) sample and, in the split step, which part of it
   const int b0 = KS > 1 ? g % a.B : g, part = KS > 1 ? g / a.B : 0;
   const bool own_vec = part == 0;  // writes the sample's fc vectors and loss
@@ -477,11 +483,22 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // at udbg[(nupd + g) * 8 + 0 / 1], next to the update workgroups' stamps
   if (FUSE && fz.u.dbg && tid == 0) fz.u.dbg[(fz.nupd + g) * 8] = __builtin_amdgcn_s_memrealtime();
   const float inv_std = 1.f / a.std_;
-  const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
+  // Device counters as per-lane loads: an opaque lane offset keeps them VGPRs (a uniform
+  // load is moved to an SGPR, i.e. waited for, right here at the kernel's top: two serial
+  // memory round trips in front of every wave).  rng_off: stage 0's dropout lanes only.
+  // (the raw counter: shifted at its use, rng_offset(0, .) = counter << 20, so no instruction
+  // here needs the loaded value)
+  // Unconditional (a branch around the load ends in a wait at its join), from a zero word
+  // when there is no counter.
+  const int64_t* rngp = (TRAIN && a.rng_offset) ? a.rng_offset : &kZeroWord;
+  // (a global-space load: a flat load would also count in lgkmcnt, and the next wait for the
+  // argument loads would wait for it)
+  typedef const __attribute__((address_space(1))) int64_t* gptr64;
+  const uint64_t rng_ctr = (uint64_t)((gptr64)rngp)[opaque(0)];
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
-  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + b0;
+  const int64_t pbase = (a.cursor ? a.cursor[opaque(0)] : 0) * (int64_t)a.B + b0;
   auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
   if (a.dbg && tid == 0) {
@@ -528,36 +545,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     C1T[tt] = xo;
     C1H[tt] = ho;
   };
-  uint32_t px0 = 0;
-  int lab0 = 0, kg = 0;
-  float pv[3] = {0.f, 0.f, 0.f};
-  uint4 w1 = make_uint4(0, 0, 0, 0);
-  if (wave >= 4 && wave < 8) {
-    const int t = tid - 256;
-    if (a.dbg && t == 0) DBGS[17] = __builtin_amdgcn_s_memtime();
-    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread)
-    auto par_index = [](int q) {
-      return q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30 : q < 90 ? O_F2B + q - 80
-                                                                                          : O_F2W + q - 90;
-    };
-#pragma unroll
-    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * 256, 589))];
-    w1 = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t & 63];
-    if (STAGED) {
-      px0 = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(t, 195)];
-      lab0 = (int)a.lstage[g];
-    }
-    // K-slice orders (constant memory) for the conv2 / dgrad A-offset tables
-    const int tq = t < 64 ? t >> 4 : (t - 64) / 24;
-    const int tks = t < 64 ? t & 15 : (t - 64) - 24 * tq;
-    kg = t < 64 ? (int)kC2Order.fwd[min(4 * tks + tq, 49)] : (int)kDgOrder.fwd[min(4 * tks + tq, 74)];
-    // the next step's row (batch staging); an opaque lane offset keeps it a VGPR (a
-    // uniform load is moved to an SGPR right away, i.e. waited for here)
-    if (KS == 1 && stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
-    if (a.dbg && t == 0) DBGS[10 + 5] = __builtin_amdgcn_s_memtime();
-  }
-  lds_barrier();
+  // Each role branch holds its own barrier (every wave meets exactly one): waves 4-7's
+  // loads are issued before it and consumed after it inside their branch, so no branch merge
+  // carries them as pending -- at a merge hipcc takes the union of the branches' in-flight
+  // loads, and a register reused after it then waits vmcnt(0), in waves 0-3 for the DMA.
   if (wave < 4) {
+    lds_barrier();  // waves 4-7's loads go first
     // W2C | W2D | F1 by LDS-DMA: each wave-instruction moves 1 KB to a wave-uniform
     // base + lane*16, so the image stays lane-linear
     constexpr int DMA_NT = 256;  // waves 0-3
@@ -570,6 +563,32 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     if (a.dbg && lane == 0) DBGS[(wave == 0 ? 10 : 17 + wave)] = __builtin_amdgcn_s_memtime();
   } else if (wave < 8) {
     const int t = tid - 256;
+    if (a.dbg && t == 0) DBGS[17] = __builtin_amdgcn_s_memtime();
+    // K-slice orders (constant memory) for the conv2 / dgrad A-offset tables; first, so the
+    // index math does not reuse a register of an in-flight load (a vmcnt(0) wait for all
+    // of them before this load was issued: one more serial round trip)
+    const int tq = t < 64 ? t >> 4 : (t - 64) / 24;
+    const int tks = t < 64 ? t & 15 : (t - 64) - 24 * tq;
+    const int kg = t < 64 ? (int)kC2Order.fwd[min(4 * tks + tq, 49)] : (int)kDgOrder.fwd[min(4 * tks + tq, 74)];
+    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread)
+    auto par_index = [](int q) {
+      return q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30 : q < 90 ? O_F2B + q - 80
+                                                                                          : O_F2W + q - 90;
+    };
+    float pv[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * 256, 589))];
+    const uint4 w1 = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t & 63];
+    uint32_t px0 = 0;
+    int lab0 = 0;
+    if (STAGED) {
+      px0 = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(t, 195)];
+      lab0 = (int)a.lstage[g];
+    }
+    // the next step's row (batch staging); an opaque lane offset keeps it a VGPR (a
+    // uniform load is moved to an SGPR right away, i.e. waited for here)
+    if (KS == 1 && stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
+    lds_barrier();
     if (t < 64) {
       // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
       // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
@@ -602,6 +621,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     asm volatile("" ::"v"(pv[0]), "v"(pv[1]), "v"(pv[2]), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(px0),
                  "v"(lab0), "v"(kg));
   } else {
+    lds_barrier();
     // waves 8-15 (otherwise idle here): conv1's address tables of all 1024 threads
     // (non-staged; the staged path reads kC1Tab)
     if (!STAGED) {
@@ -609,10 +629,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       conv1_tables(tid);
     }
     if (tid - 512 < 16) CONSTB[tid - 512] = tid - 512 < 8 ? (unsigned short)0 : h16<T>(1.f);
-    // split step: waves 12-15 own every global store of the backward stages (next-step staging,
-    // conv2 slab) and sit out conv1 wgrad, so no wave that computes later waits for a store
-    // (hipcc's vmcnt(0) waits count stores too)
-    if (KS > 1 && stage_next && wave >= 12) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
@@ -685,6 +701,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
     // then start the next sample's loads (consumed one sample later)
     STAMP(0);
+    // split step: the next step's row, for waves 12-15 (not in the preamble: a value loaded in
+    // one wave-role branch there made hipcc wait vmcnt(0) -- for the weight DMA -- at the end
+    // of the DMA branch of waves 0-3)
+    if (KS > 1 && stage_next && wave >= 12 && s == 0) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
     if (wave >= 8) {
       // idle waves: zero the HWC conv1 image.  conv1 writes channels 0-9 of each
       // position at stage 1; channels 10-15 meet zero conv2 weights in the K sum, so
@@ -708,7 +728,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         float sc = 1.f;
         if (TRAIN) {
           const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)a.B + b) * 70ull + tid;
-          sc = dropout_keep(a.seed, rng_off, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
+          sc = dropout_keep(a.seed, rng_ctr << 20, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
         }
         if (tid < 20) D2S[tid] = sc;
         else D1S[tid - 20] = sc;
@@ -1885,11 +1905,17 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   }
 }
 
+// lenet_update_kernel's arguments as laid out in its argument segment (then px)
+struct UpdateKargs {
+  LenetUpdateArgs a; const float* vslab; int B; float* loss_parts; int nparts; float* loss_acc;
+  uint64_t timeout_ticks; int fc_tpb;
+};
 template <typename T, bool EXCH>
 __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
                                                              int B, float* loss_parts, int nparts,
-                                                             float* loss_acc, comm::IpcPeers px,
-                                                             uint64_t timeout_ticks, int fc_tpb) {
+                                                             float* loss_acc, uint64_t timeout_ticks, int fc_tpb,
+                                                             comm::IpcPeers px) {
+  prefetch_kernargs<sizeof(UpdateKargs) + sizeof(comm::IpcPeers)>();  // (+ gridDim.x after px)
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
   update_role<T, EXCH, false, UP_NT>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
@@ -1985,14 +2011,14 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                         a.B, loss_parts, nparts, loss_acc, px, ticks, 1);
+                         a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
     });
     return hipGetLastError();
   }
   const int nblocks = update_blocks(a.B);
   CSED_DISPATCH_UPDATE(a.mfma_dtype, {
     hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
-                       a.B, loss_parts, nparts, loss_acc, px, (uint64_t)0, 0);
+                       a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 0, px);
   });
   return hipGetLastError();
 }

@@ -35,7 +35,7 @@ def main():
         eng.gradient(grid, dbg)
     torch.cuda.synchronize()
     st = dbg.view(grid, 32).cpu().double()
-    # Stamps (thread 0): 12 kernel start, 10 LDS-DMA issued, 15 small loads issued (wave 4),
+    # Stamps (thread 0): 12 kernel start, 10 LDS-DMA issued, 17 / 16 wave 4 start / small loads consumed,
     # 13 preamble end, 0..8 stage starts of the stamped sample (9 = dgrad inside stage 6),
     # 14 end of the stamped sample, 11 after all samples.  The stamped sample is sample 1
     # when a workgroup has several (steady state), else sample 0.
@@ -45,11 +45,10 @@ def main():
     tot = (st[:, 11] - st[:, 12]).median().item()
     per = (st[:, 14] - st[:, 0]).median().item()
     print(f"B={B} grid={grid}: median kernel {tot:.0f} cycles (s_memtime ticks), stamped sample {per:.0f}")
-    pre = [(st[:, 10] - st[:, 12]).median().item(), (st[:, 15] - st[:, 12]).median().item(),
-           (st[:, 13] - st[:, 12]).median().item()]
+    pre = [(st[:, 10] - st[:, 12]).median().item(), (st[:, 13] - st[:, 12]).median().item()]
     ld = [(st[:, 17] - st[:, 12]).median().item(), (st[:, 16] - st[:, 12]).median().item()]
     print(f"  preamble (from kernel start): DMA issued {pre[0]:.0f}, wave 4 starts {ld[0]:.0f}, small loads "
-          f"issued {pre[1]:.0f}, consumed {ld[1]:.0f}; wave 0 done {pre[2]:.0f}")
+          f"consumed {ld[1]:.0f}; wave 0 done {pre[1]:.0f}")
     dma = [(st[:, 17 + w] - st[:, 12]).median().item() for w in (1, 2, 3)]
     arr = [(st[:, 24 + w] - st[:, 12]).median().item() for w in range(8)]
     print(f"  DMA issued by waves 1-3: {dma}; waves 0-7 reach the first barrier: {arr}")

@@ -81,6 +81,16 @@ def main():
                          eng.grid, eng.loss_acc, eng.mfma, dbg)
         torch.cuda.synchronize()
     st = dbg.view(256, 8).cpu().double()
+    stamps(st, B, "after train")
+    for _ in range(3):  # the update again, with nothing in between (its inputs unchanged)
+        dbg.zero_()
+        ops.lenet_update(eng.slab, eng.grid, eng.vslab, B, None, None, *common(), None, None, True, eng.loss_parts,
+                         eng.grid, eng.loss_acc, eng.mfma, dbg)
+        torch.cuda.synchronize()
+    stamps(dbg.view(256, 8).cpu().double(), B, "after update")
+
+
+def stamps(st, B, what):
     wpt = 1 if B <= 128 else (2 if B <= 256 else (4 if B <= 512 else 8))  # fc_waves_per_tile
     nfc = 88 if wpt == 1 else 88 // (8 // wpt)  # blocks [0, nfc) FC role, then 84 CONV role blocks
     nb = nfc + 84
@@ -89,7 +99,7 @@ def main():
     for role, sl, ks in [("CONV", slice(nfc, nb), [0, 1, 2, 3, 4]), ("FC", slice(0, nfc), [0, 1, 2, 3, 4])]:
         r = rel[sl]
         desc = "  ".join(f"s{k} med {r[:, k].median().item():.2f} max {r[:, k].max().item():.2f}" for k in ks)
-        print(f"stamps {role}: {desc}")
+        print(f"stamps {what} {role}: {desc}")
 
 
 if __name__ == "__main__":
