@@ -1370,6 +1370,23 @@ __device__ __forceinline__ void image_slots(int i, int& d0, int& d1) {
   }
 }
 
+// image_slots without branches: both table loads unconditional (clamped indices), the
+// results selected -- so nothing waits for the tables until d0 / d1 are used (image_slots'
+// branch merge waits for them at once)
+__device__ __forceinline__ void image_slots_flat(int i, int& d0, int& d1) {
+  const int j = min(max(i - O_C2W, 0), O_C2B - O_C2W - 1);
+  const int oc = j / 250, k = j % 250;
+  const int ic = k / 25, r = k % 25, kh = r / 5, kw = r % 5;
+  const int c2 = kC2Order.inv[r * 2 + (ic >> 3)];
+  const int slice = kDgOrder.inv[((4 - kh) * 5 + (4 - kw)) * 3 + (oc >> 3)];
+  const int i1 = min(max(i, 0), O_C1B - 1), r1 = i1 % 25;
+  const int jf = min(max(i - O_F1W, 0), O_F1B - O_F1W - 1);
+  const bool is_c1 = i < O_C1B, is_c2 = i >= O_C2W && i < O_C2B, is_f1 = i >= O_F1W && i < O_F1B;
+  d0 = is_c1 ? I_W1C + (i1 / 25) * 32 + w1c_slot(r1 / 5, r1 % 5)
+             : is_c2 ? I_W2C + oc * LD_W2C + c2 * 8 + (ic & 7) : is_f1 ? I_F1 + (jf / 320) * LD_F1 + (jf % 320) : -1;
+  d1 = is_c2 ? I_W2D + (slice * 16 + ic) * 8 + (oc & 7) : -1;
+}
+
 // (T = float: the fp32 path, lenet_fused_f32.hip, reads the fp32 master parameters and
 // keeps no weight images)
 template <typename T>
@@ -1670,11 +1687,14 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     const int pi = slot_param(pbc * (UP_C * 4) + min(ht, 63));
     float p0 = 0.f, m0 = 0.f;
     int d0 = -1, d1 = -1;
-    if (a.apply_sgd && ht < 64) {
-      p0 = a.params[max(pi, 0)];
-      m0 = a.momentum[max(pi, 0)];
-      image_slots(max(pi, 0), d0, d1);
-    }
+    auto pm_loads = [&]() {
+      if (a.apply_sgd && ht < 64) {
+        p0 = a.params[max(pi, 0)];
+        m0 = a.momentum[max(pi, 0)];
+      }
+      image_slots_flat(max(pi, 0), d0, d1);  // (lanes without a parameter store nothing)
+    };
+    if (FUSED) pm_loads();  // the fused step: prefetched while the go flag is polled
     wait_ready();
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     // Loads are unconditional from a clamped address and masked afterwards: a
@@ -1684,7 +1704,20 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // row per workgroup, conv2 chunks a row per sample (kernels/lenet_layout.h)
     const int rows = pbc < C1_CH ? a.grid : min(a.grid, B);
     const float4* sp = reinterpret_cast<const float4*>(a.slab + slab_off(pbc * 64, 0, a.grid, min(a.grid, B))) + cl;
-    for (int g0 = sl; g0 < rows; g0 += UP_S * UP_MAXL) {
+    // The first UP_S * UP_MAXL = 256 rows (all of them: rows <= grid <= 256) in straight-line
+    // code, the p / m / weight-image-table loads issued right behind them: one memory round
+    // trip for the lot (image_slots' table loads used to be waited for before these loads).
+    {
+      float4 v[UP_MAXL];
+#pragma unroll
+      for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(sl + u * UP_S, rows - 1) * UP_C);
+      if (!FUSED) pm_loads();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < UP_MAXL; ++u)
+        if (sl + u * UP_S < rows) add4(acc, v[u]);
+    }
+    for (int g0 = sl + UP_S * UP_MAXL; g0 < rows; g0 += UP_S * UP_MAXL) {
       float4 v[UP_MAXL];
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(g0 + u * UP_S, rows - 1) * UP_C);
