@@ -1764,6 +1764,13 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   } else {
     // ---------------- role FC: 16x16 tiles of [dW | db], K split over wpt waves per tile
     const int wave = tid >> 6, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
+    // small batch (<= 32, the strong-scaled per-rank batch of 4-8 ranks), separate update
+    // kernel: the tile's wave issues only the K-steps the batch fills -- 2 * ceil(B / 4) loads
+    // and ceil(B / 4) MFMAs (rounded to 2 / 4 / 8) instead of a whole 64-sample chunk's 32
+    // loads and 16 MFMAs.  The K-steps dropped would add exact zeros: bitwise the same sums
+    // as the chunk path (and the one-kernel step).  Splitting K over waves instead (B = 32 /
+    // 64: 2 / 4 waves per tile + an LDS combine) was slower: +0.1 / +0.4 us per step.
+    const bool small = !FUSED && B <= 32;
     const int wpt = fc_waves_per_tile(B);
     const int tpb = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B, NTH, FUSED);
     const bool live_wave = wave / wpt < tpb;      // (uniform) waves past the block's tiles idle
@@ -1833,8 +1840,36 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       for (int u = 0; u < 16; ++u) c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], c, 0, 0, 0);
       return c;
     };
+    // the same for NC K-steps of 4 samples (NC = 2 or 4: the small-batch split)
+    auto load_n = [&](auto nc, int s0, float* av, float* bv) {
+      constexpr int NC = decltype(nc)::value;
+#pragma unroll
+      for (int u = 0; u < NC; ++u) {
+        const int s = s0 + 4 * u + kq;
+        const bool ok = s < k1;
+        const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
+        const float ra = ld_c<FUSED>(rowc + a_off + min(o, rows - 1));
+        const float rb = ld_c<FUSED>(rowc + b_off + min(i, cols - 1));
+        av[u] = (ok && o < rows) ? ra : 0.f;
+        bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
+      }
+    };
     f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (FUSED) {  // k1 - k0 <= 64
+    auto small_k = [&](auto nc) {
+      constexpr int NC = decltype(nc)::value;
+      float a0[NC], b0[NC];
+      load_n(nc, k0, a0, b0);
+      USTAMP(1);
+#pragma unroll
+      for (int u = 0; u < NC; ++u) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b0[u], c, 0, 0, 0);
+    };
+    if (small) {  // (wpt == 1: k0 = 0, k1 = B)
+      if (live_wave) {
+        if (B <= 8) small_k(std::integral_constant<int, 2>{});
+        else if (B <= 16) small_k(std::integral_constant<int, 4>{});
+        else small_k(std::integral_constant<int, 8>{});
+      }
+    } else if (FUSED) {  // k1 - k0 <= 64
       if (live_wave) {
         float a0[16], b0[16];
         load(k0, a0, b0);
