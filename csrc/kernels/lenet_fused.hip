@@ -498,7 +498,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
-  const int64_t pbase = (a.cursor ? a.cursor[opaque(0)] : 0) * (int64_t)a.B + b0;
+  // (staged: a deferred per-lane load, only the next-step row needs it; the multi-sample path
+  // reads every sample's row through it, as scalars)
+  const int64_t pbase = (a.cursor ? (STAGED ? a.cursor[opaque(0)] : a.cursor[0]) : 0) * (int64_t)a.B + b0;
   auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
   if (a.dbg && tid == 0) {

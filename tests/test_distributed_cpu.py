@@ -166,3 +166,40 @@ def test_bench_rejects_world_size_mismatch_cpu():
                         "0"], cwd=ROOT, capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
 
+
+
+def _replica_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel import destroy, init_distributed
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import replica_checksum
+
+    ctx = init_distributed(rank=rank, world_size=world, backend="gloo", device="cpu")
+    t = torch.linspace(-1, 1, 21840)
+    same = replica_checksum(ctx, t)[0]
+    u = t.clone()
+    if rank == 1:  # one ulp of one parameter on one replica
+        u[12345] = torch.nextafter(u[12345], torch.tensor(2.0))
+    diverged = replica_checksum(ctx, u)[0]
+    v = t.clone()
+    if rank == 1:  # two entries swapped: same multiset of bits, different positions
+        v[[10, 11]] = v[[11, 10]]
+    swapped = replica_checksum(ctx, v)[0]
+    q.put((rank, same, diverged, swapped))
+    destroy()
+
+
+def test_replica_checksum_detects_divergence():
+    """--check-replicas' collective: equal replicas pass; a one-ulp change or a
+    swap of two parameters on one rank is caught on every rank."""
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_replica_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same, diverged, swapped in res:
+        assert same and not diverged and not swapped, (rank, same, diverged, swapped)
