@@ -1824,17 +1824,24 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     const int kw = ((B + wpt - 1) / wpt + 3) & ~3;
     const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
     // K = samples; 16x16x4 f32 MFMA: lane holds A[o][s0 + 4u + kq] and B[s0 + 4u + kq][i]
+    // Loads and masking are separate phases: a chunk's 32 loads are all issued before any
+    // select consumes one (a select right behind its load pair let the scheduler wait on
+    // each pair in turn whenever it chose a low register budget).
     auto load = [&](int s0, float (&av)[16], float (&bv)[16]) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
-        const int s = s0 + 4 * u + kq;
-        const bool ok = s < k1;
         // unconditional loads from clamped addresses, masked after (see role CONV)
-        const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
-        const float ra = ld_c<FUSED>(rowc + a_off + min(o, rows - 1));
-        const float rb = ld_c<FUSED>(rowc + b_off + min(i, cols - 1));
-        av[u] = (ok && o < rows) ? ra : 0.f;
-        bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
+        const float* rowc = vslab + (int64_t)min(s0 + 4 * u + kq, B - 1) * VEC;
+        av[u] = ld_c<FUSED>(rowc + a_off + min(o, rows - 1));
+        bv[u] = ld_c<FUSED>(rowc + b_off + min(i, cols - 1));
+      }
+    };
+    auto mask = [&](int s0, float (&av)[16], float (&bv)[16]) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const bool ok = s0 + 4 * u + kq < k1;
+        av[u] = (ok && o < rows) ? av[u] : 0.f;
+        bv[u] = ok ? (i < cols ? bv[u] : (i == cols ? 1.f : 0.f)) : 0.f;
       }
     };
     auto mfma16 = [&](f32x4 c, const float (&av)[16], const float (&bv)[16]) {
@@ -1875,6 +1882,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       if (live_wave) {
         float a0[16], b0[16];
         load(k0, a0, b0);
+        mask(k0, a0, b0);
         USTAMP(1);
         c = mfma16(c, a0, b0);
       }
@@ -1888,10 +1896,12 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         // interleaves them and waits on each pair in turn)
         __builtin_amdgcn_sched_barrier(0);
         USTAMP(1);
+        mask(s0, a0, b0);
         c = mfma16(c, a0, b0);
         if (more) {
           if (s0 + 128 < k1) load(s0 + 128, a0, b0);
           __builtin_amdgcn_sched_barrier(0);
+          mask(s0 + 64, a1, b1);
           c = mfma16(c, a1, b1);
         }
       }
