@@ -67,22 +67,9 @@ def layout() -> tuple[int, int, int, int]:
     return wimg, conv, vec, stage_max
 
 
-def fused_max_batch() -> int:
-    """Largest per-rank batch of the one-kernel step (csed::lenet_step)."""
-    return int(torch.ops.csed.lenet_layout()[6])
-
-
-def one_kernel_mode() -> str:
-    """CSED_ONE_KERNEL_STEP: "auto" (default), "0" or "1" (see FusedLeNetTrainer)."""
-    mode = os.environ.get("CSED_ONE_KERNEL_STEP", "auto").strip().lower()
-    if mode not in ("auto", "0", "1"):
-        raise ValueError(f"CSED_ONE_KERNEL_STEP={mode!r}: expected auto, 0 or 1")
-    return mode
-
-
 def split_factor() -> int:
     """Workgroups per sample of the split step (csed::lenet_train KS)."""
-    return int(torch.ops.csed.lenet_layout()[8])
+    return int(torch.ops.csed.lenet_layout()[6])
 
 
 def exch_words() -> int:
@@ -155,10 +142,9 @@ class FusedLeNetTrainer:
         # split step (lenet_fused.hip KS > 1): split_k workgroups per sample share the backward
         # conv stages; used whenever the whole grid fits one wave of the GPU (split_k * B <= 256
         # CUs).  CSED_SPLIT=0 keeps one workgroup per sample.
-        ok_mode = one_kernel_mode()
         split_k = split_factor()
         auto = os.environ.get("CSED_SPLIT", "auto").strip().lower() != "0"
-        self.split = (self.staged and grid is None and split_k * self.B <= 256 and ok_mode != "1"
+        self.split = (self.staged and grid is None and split_k * self.B <= 256
                       and (auto if split is None else bool(split)))
         if self.split:
             self.grid = split_k * self.B
@@ -167,14 +153,6 @@ class FusedLeNetTrainer:
         # one staging row per workgroup (split step: row r holds sample r % B)
         self.xstage = torch.zeros((self.grid, 784), dtype=torch.uint8, device=dev) if self.staged else None
         self.lstage = torch.zeros(self.grid, dtype=torch.long, device=dev) if self.staged else None
-        # one-kernel step (csed::lenet_step): training workgroups + trailing update
-        # workgroups that wait on device flags, instead of two launches.
-        # CSED_ONE_KERNEL_STEP: "1" = use it, "0" / "auto" (default) = two kernels.  After
-        # the update-kernel changes (one fc tile per workgroup, idle waves skipped) the two
-        # graph-replayed launches beat it by ~0.2 us at batch 64 (profiles/one_kernel_step_r1.md):
-        # a kernel boundary inside a graph costs about what the in-kernel hand-off does.
-        self.one_kernel = self.staged and self.B <= fused_max_batch() and ok_mode == "1"
-        self.bar = torch.zeros(int(torch.ops.csed.lenet_layout()[7]), dtype=torch.int32, device=dev)
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._eval_cache: dict[int, tuple] = {}
@@ -324,7 +302,6 @@ class FusedLeNetTrainer:
     def comm_errors(self) -> int:
         """Nonzero if an IPC exchange ever timed out waiting for a peer (synchronous)."""
         e = self.exch.error() if self.exch is not None else 0
-        e |= int(self.bar[2].item())  # a one-kernel step's update workgroups timed out
         return e | (self.allreduce.error() if self.allreduce is not None else 0)
 
     def _max_grid(self) -> int:
@@ -375,8 +352,6 @@ class FusedLeNetTrainer:
     @property
     def step_kind(self) -> str:
         """How a full (staged) training step is launched."""
-        if self.one_kernel and (not self.comm or self.exch is not None):
-            return "one kernel (lenet_step)"
         return "two kernels" if (not self.comm or self.exch is not None) else "update split around an all-reduce"
 
     def steps_per_epoch(self) -> int:
@@ -391,14 +366,6 @@ class FusedLeNetTrainer:
         ops = torch.ops.csed
         # full steps read the staged batch and stage the next one; the epoch's short tail uses perm
         st = self.staged and cursor is not None
-        if st and self.one_kernel and (not self.comm or self.exch is not None):
-            ops.lenet_step(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
-                           self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
-                           self.drop_p, self.seed, self.rng_offset, self.mfma, self.xstage, self.lstage,
-                           self.momentum_buf, self.lr, self.momentum, self.dampening, self.weight_decay,
-                           self.nesterov, self.step_count, self.ticket, self.loss_acc, self.bar, None, None,
-                           self.exch.id if self.exch is not None else -1, self.exch_timeout_s)
-            return
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
                         self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
                         self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,
@@ -537,21 +504,24 @@ class FusedLeNetTrainer:
         if tail and self.tail_size() > 0:
             self.graph(1, tail=True)
 
-    def run_steps(self, k: int, steps_per_graph: int = 16, use_graph: bool = True) -> None:
-        """Advance k full-batch steps from the current cursor."""
+    def step_plan(self, k: int, steps_per_graph: int = 16, use_graph: bool = True) -> list:
+        """The launches that advance k full-batch steps from the current cursor, as a list of
+        callables (graph replays, or eager steps where no graph applies), resolved up front so
+        that a timed region holds nothing but the launches."""
         if k <= 0:
-            return
+            return []
         if not use_graph or self.capture_comm_ok is False:
-            for _ in range(k):
-                self.step()
-            return
+            return [self.step] * k
+        plan = []
         for n in self.graph_plan(k, steps_per_graph):
             g = self.graph(n)
-            if g is None:
-                for _ in range(n):
-                    self.step()
-            else:
-                g.replay()
+            plan += [self.step] * n if g is None else [g.replay]
+        return plan
+
+    def run_steps(self, k: int, steps_per_graph: int = 16, use_graph: bool = True) -> None:
+        """Advance k full-batch steps from the current cursor."""
+        for launch in self.step_plan(k, steps_per_graph, use_graph):
+            launch()
 
     def train_epoch(self, order: torch.Tensor, steps_per_graph: int = 16, use_graph: bool = True) -> None:
         self.set_epoch_order(order)

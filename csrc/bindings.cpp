@@ -292,11 +292,12 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 // ----------------------------------------------------------- fused lenet
 // Buffer sizes the fused LeNet kernels expect: [weight-image elements, conv
 // slab row (floats per workgroup), per-sample vector length, flat params,
-// largest per-rank batch the batch-staging path handles].
+// largest per-rank batch the batch-staging path handles, exchange words per sender,
+// workgroups per sample of the split step].
 std::vector<int64_t> lenet_layout() {
   return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
           csed::lenet_param_count(), csed::lenet_stage_max_batch(), csed::lenet_exch_words(),
-          csed::lenet_fused_max_batch(), csed::lenet_step_bar_ints(), csed::lenet_split_k()};
+          csed::lenet_split_k()};
 }
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
@@ -448,31 +449,6 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
                                       cur_stream(params)));
 }
 
-// One-kernel training step on a staged batch (csed::launch_lenet_step): lenet_train
-// with stage_next, then lenet_update with SGD, in one launch.
-void lenet_step(const Tensor& images, const Tensor& labels, const Tensor& perm, Tensor& cursor, int64_t B,
-                int64_t rank, Tensor& wimg, Tensor& params, Tensor& slab, Tensor& vslab, Tensor& loss_parts,
-                double grad_scale, double mean, double std_, double drop_p, int64_t seed, Tensor& rng_offset,
-                int64_t mfma_dtype, Tensor& xstage, Tensor& lstage, Tensor& momentum, double lr, double mom,
-                double dampening, double weight_decay, bool nesterov, Tensor& step, Tensor& ticket,
-                Tensor& loss_acc, Tensor& bar, const optional<Tensor>& dbg, const optional<Tensor>& udbg,
-                int64_t exch_id, double exch_timeout_s) {
-  dev(bar, "bar");
-  TORCH_CHECK(mfma_dtype != csed::kF32, "lenet_step: the one-kernel step has no fp32 form");
-  TORCH_CHECK(bar.scalar_type() == at::kInt && bar.numel() >= csed::lenet_step_bar_ints(),
-              "lenet_step: bar must be int32[", csed::lenet_step_bar_ints(), "]");
-  const c10::DeviceGuard gd(images.device());
-  const csed::LenetTrainArgs t = train_args(images, labels, perm, cursor, B, rank, wimg, params, slab, vslab,
-                                            loss_parts, grad_scale, mean, std_, drop_p, seed, rng_offset, B,
-                                            mfma_dtype, dbg, xstage, lstage, true);
-  const csed::LenetUpdateArgs u =
-      update_args(slab, B, vslab, B, c10::nullopt, c10::nullopt, params, momentum, wimg, lr, mom, dampening,
-                  weight_decay, nesterov, step, ticket, cursor, rng_offset, true, loss_parts, loss_acc, mfma_dtype,
-                  udbg, exch_id, exch_timeout_s);
-  CHECK_HIP(csed::launch_lenet_step(t, u, loss_parts.data_ptr<float>(), (int)B, loss_acc.data_ptr<float>(),
-                                    bar.data_ptr<int>(), cur_stream(images)));
-}
-
 void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order, int64_t n, const Tensor& wimg,
                 const Tensor& params, double mean, double std_, Tensor& out_parts, const optional<Tensor>& logp_out,
                 int64_t mfma_dtype) {
@@ -502,12 +478,6 @@ TORCH_LIBRARY(csed, m) {
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
         "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
         "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
-  m.def("lenet_step(Tensor images, Tensor labels, Tensor perm, Tensor(a!) cursor, int B, int rank, Tensor(b!) wimg, "
-        "Tensor(c!) params, Tensor(d!) slab, Tensor(e!) vslab, Tensor(f!) loss_parts, float grad_scale, float mean, "
-        "float std, float drop_p, int seed, Tensor(g!) rng_offset, int mfma_dtype, Tensor(h!) xstage, "
-        "Tensor(i!) lstage, Tensor(j!) momentum, float lr, float mom, float dampening, float weight_decay, "
-        "bool nesterov, Tensor(k!) step, Tensor(l!) ticket, Tensor(m!) loss_acc, Tensor(n!) bar, "
-        "Tensor(o!)? dbg=None, Tensor(p!)? udbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
         "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "
@@ -555,7 +525,6 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);
   m.impl("lenet_update", &lenet_update);
-  m.impl("lenet_step", &lenet_step);
   m.impl("lenet_stage", &lenet_stage);
   m.impl("lenet_eval", &lenet_eval);
 }

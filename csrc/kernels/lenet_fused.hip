@@ -306,93 +306,8 @@ constexpr C1Tab make_c1tab() {
 }
 __constant__ C1Tab kC1Tab = make_c1tab();
 
-// One-kernel training step (FUSE > 0): workgroups [0, a.grid) train as below, then
-// signal a device counter; workgroups [a.grid, a.grid + nupd) run lenet_update's roles
-// (update_role) once every training workgroup has signalled.  The update workgroups
-// come after the training ones in dispatch order and training never waits on them,
-// so the step cannot deadlock whatever the occupancy; they load their parameters and
-// momenta while training runs, and the kernel boundary between the two phases is
-// gone.  FUSE = 2 adds the in-kernel data-parallel exchange.
 // lenet_update workgroup shape (see the update kernel below)
 constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
-
-// Cross-XCD hand-off of the fused step without cache maintenance: the training
-// workgroups write their outputs with device-coherent stores (global_store sc1,
-// written through to memory) and the update workgroups read them with
-// device-coherent loads (sc1), so neither side needs an L2 write-back or
-// invalidate (buffer_wbl2 / buffer_inv walk the whole 4 MB L2 of the XCD).
-template <bool C>
-__device__ __forceinline__ void st_c(float* p, float v) {
-  if (C) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool C>
-__device__ __forceinline__ void st4_c(float* p, float4 v) {
-  if (C) {
-    uint64_t* q = reinterpret_cast<uint64_t*>(p);
-    __hip_atomic_store(q, ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, ((uint64_t)__float_as_uint(v.w) << 32) | __float_as_uint(v.z), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *reinterpret_cast<float4*>(p) = v;
-  }
-}
-template <bool C>
-__device__ __forceinline__ float ld_c(const float* p) {
-  if (C) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return *p;
-}
-template <bool C>
-__device__ __forceinline__ float4 ld4_c(const float4* p) {
-  if (C) {
-    uint64_t* q = reinterpret_cast<uint64_t*>(const_cast<float4*>(p));
-    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
-                       __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
-  }
-  return *p;
-}
-
-// Fused-step synchronisation words (int32, zero-initialised, one 128-byte line each
-// where polled).  The training workgroups count themselves in BAR_CNT; the last one
-// re-arms BAR_CNT and raises every update workgroup's own go flag (BAR_GO + 32*blk),
-// so each update workgroup polls a line of its own (94 pollers on one address queue
-// behind each other at the memory side: ~4 us); the update workgroup clears its flag
-// once seen.  Nothing is read back at the end of the launch (a re-arm that needs an
-// atomic's return value there costs ~1.5 us on the critical path).
-constexpr int BAR_CNT = 0, BAR_ERR = 2, BAR_GO = 32;
-constexpr int BAR_INTS = BAR_GO + 32 * 256;
-__device__ __forceinline__ int sys_load(const int* p) {
-  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void sys_store(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-struct StepFuse {
-  LenetUpdateArgs u;
-  float* loss_parts;
-  int nparts;
-  float* loss_acc;
-  comm::IpcPeers px;
-  uint64_t timeout_ticks;
-  int* bar;  // BAR_INTS synchronisation words (BAR_ERR != 0: a wait timed out)
-  int nupd;  // update workgroups
-  int fc_tpb;  // FC tiles per update workgroup
-};
-
-// FUSED_MAXB: the fused step's batch limit -- one 64-sample chunk per fc wave, so the
-// update role fits the training kernel's 128 VGPRs (no second load buffer).  With
-// FUSED, update_role also reads the training outputs with device-coherent loads.
-constexpr int FUSED_MAXB = 64;
-constexpr int UPD_NTH = 512;  // threads of a fused-step update role (UP_NT or NT)
-template <typename T, bool EXCH, bool FUSED, int NTH>
-__device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
-                            int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
-                            int nblk, int tid, float4* part, float* part2, const int* ready, int nready,
-                            int fc_tpb = 0);
 
 // KS > 1 (split step, staged batches only): KS workgroups per sample.  Workgroup g is part
 // g / B of sample g % B (the parts of a sample share an XCD when B % 8 == 0: same L2 for
@@ -401,13 +316,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
 // owns conv2 wgrad columns [64j, 64j+64) and dgrad tiles {j, j+4, j+8}, and its conv1
 // wgrad covers the conv1 pixels of those tiles.  Part 0 alone writes the fc vector slab and
 // the loss partials.  The backward conv stages are a third of the per-sample chain.
-template <typename T, bool TRAIN, bool STAGED, int FUSE, int KS = 1>
-__global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out,
-                                                            StepFuse fz) {
-  static_assert(KS == 1 || (KS == SPLIT_K && STAGED && FUSE == 0 && TRAIN), "split step: staged training only");
-  // argument lines this instantiation reads (the fused-step block only with FUSE)
+template <typename T, bool TRAIN, bool STAGED, int KS = 1>
+__global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
+  static_assert(KS == 1 || (KS == SPLIT_K && STAGED && TRAIN), "split step: staged training only");
   struct TrainKargs { LenetTrainArgs a; int write_logp; float* logp_out; };
-  prefetch_kernargs<FUSE ? (int)(sizeof(TrainKargs) + sizeof(StepFuse)) : (int)sizeof(TrainKargs)>();
+  prefetch_kernargs<(int)sizeof(TrainKargs)>();
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
   // per-sample activations (dynamic).  Being distinct objects, accesses to the
   // activations are provably disjoint from the in-flight DMA, so the compiler's
@@ -457,19 +370,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (FUSE && (int)blockIdx.x >= a.grid) {
-    // update workgroup: lenet_update's roles on waves 0-7; the others end here (a
-    // barrier waits only for the waves that have not ended).  More, smaller update
-    // workgroups: the update phase is bound by per-CU load issue (UPD_NTH = NT was
-    // ~0.5 us slower per step).
-    if (tid >= UPD_NTH) return;
-    update_role<T, FUSE == 2, true, UPD_NTH>(fz.u, fz.u.vslab, fz.u.B, fz.loss_parts, fz.nparts, fz.loss_acc,
-                                             fz.px, fz.timeout_ticks, blockIdx.x - a.grid, fz.nupd, tid,
-                                             reinterpret_cast<float4*>(dsm),
-                                             reinterpret_cast<float*>(dsm + (UPD_NTH / UP_NT) * UP_S * UP_C * 16),
-                                             fz.bar, a.grid, fz.fc_tpb);
-    return;
-  }
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
   // (a.grid, not gridDim.x: every launcher sets it, and it is in the prefetched argument lines)
   const int G = a.grid, g = blockIdx.x;
@@ -479,9 +379,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   const int R2 = min(G, a.B);      // rows of the slab's conv2 chunks
   // staged: this thread's conv1 address row, first in the vector memory queue
   const uint4 c1row = STAGED ? reinterpret_cast<const uint4*>(&kC1Tab)[tid] : make_uint4(0, 0, 0, 0);
-  // fused-step timeline (diagnostics): wall-clock start / signal of training workgroup g
-  // at udbg[(nupd + g) * 8 + 0 / 1], next to the update workgroups' stamps
-  if (FUSE && fz.u.dbg && tid == 0) fz.u.dbg[(fz.nupd + g) * 8] = __builtin_amdgcn_s_memrealtime();
   const float inv_std = 1.f / a.std_;
   // Device counters as per-lane loads: an opaque lane offset keeps them VGPRs (a uniform
   // load is moved to an SGPR, i.e. waited for, right here at the kernel's top: two serial
@@ -692,7 +589,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   };
   auto store_c2 = [&](int t0, int nt) {  // after a barrier that follows stage_c2
     for (int i = O_C2W / 4 + t0; i < (O_C2B + 20) / 4; i += nt)
-      st4_c<FUSE != 0>(slab_at(4 * i), reinterpret_cast<const float4*>(SLF)[i]);
+      *reinterpret_cast<float4*>(slab_at(4 * i)) = reinterpret_cast<const float4*>(SLF)[i];
   };
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = b0 + s * G;
@@ -832,7 +729,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
         P2[oc * 16 + w] = hv;
         I2[oc * 16 + w] = (uint8_t)bi;
-        if (wvec) st_c<FUSE != 0>(vs + V_P2 + oc * 16 + w, f16v<T>(hv));  // fc1 input, exactly as the forward used it
+        if (wvec) vs[V_P2 + oc * 16 + w] = f16v<T>(hv);  // fc1 input, exactly as the forward used it
       }
     }
     __syncthreads();
@@ -860,7 +757,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (o < 50) {
           const float h = fmaxf(c[0] + PAR[P_F1B + o], 0.f) * D1S[o];
           Hs[o] = h;
-          if (wvec) st_c<FUSE != 0>(vs + V_H + o, h);
+          if (wvec) vs[V_H + o] = h;
         }
       }
     }
@@ -958,7 +855,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           float mine = 0.f;
 #pragma unroll
           for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
-          st_c<FUSE != 0>(vs + V_DLOG + lane, mine);
+          vs[V_DLOG + lane] = mine;
         }
         // dZ1[o] = gate(o) * sum_c dl[c] * W2[c][o]   (lane o; every lane has all dl[c])
         float dh0 = 0.f, dh1 = 0.f;
@@ -969,7 +866,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
         const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
         DZ1B[lane] = h16<T>(dz);
-        if (wvec && lane < 50) st_c<FUSE != 0>(vs + V_DZ1 + lane, dz);
+        if (wvec && lane < 50) vs[V_DZ1 + lane] = dz;
       }
     }
     if (!TRAIN) return;
@@ -1310,39 +1207,21 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       for (int q = 0; q < 8; ++q) v += part(nt + 2 * q)[oc * 16 + col];
       const int k = nt * 16 + col;
       if (oc < 10) {
-        if (k < 25) st_c<FUSE != 0>(slab_at(O_C1W + oc * 25 + k), v);
-        else if (k == 25) st_c<FUSE != 0>(slab_at(O_C1B + oc), v);
+        if (k < 25) *slab_at(O_C1W + oc * 25 + k) = v;
+        else if (k == 25) *slab_at(O_C1B + oc) = v;
       }
     } else if (!STAGED) {
       store_c2(tid - 512, NT - 512);
     }
   }
   if (tid == 0) {  // (split step: part 0 reports the sample)
-    st_c<FUSE != 0>(a.loss_acc + 2 * g, own_vec ? loss_sum : 0.f);
-    st_c<FUSE != 0>(a.loss_acc + 2 * g + 1, own_vec ? correct : 0.f);
+    a.loss_acc[2 * g] = own_vec ? loss_sum : 0.f;
+    a.loss_acc[2 * g + 1] = own_vec ? correct : 0.f;
   }
   if (a.dbg) {
     if (tid == 0) DBGS[23] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (tid < DBG_W) a.dbg[g * DBG_W + tid] = DBGS[tid];
-  }
-  if (FUSE) {
-    // every wave's (device-coherent, st_c) slab / vector / loss stores are complete
-    // (vmcnt), then the signal: no L2 write-back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (wave == 0) {
-      int old = 0;
-      if (lane == 0) {
-        if (fz.u.dbg) fz.u.dbg[(fz.nupd + g) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-        old = __hip_atomic_fetch_add(fz.bar + BAR_CNT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (fz.u.dbg) fz.u.dbg[(fz.nupd + g) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-      }
-      if (__shfl(old, 0) == a.grid - 1) {  // the last training workgroup: re-arm, raise the go flags
-        if (lane == 0) sys_store(fz.bar + BAR_CNT, 0);
-        for (int b = lane; b < fz.nupd; b += 64) sys_store(fz.bar + BAR_GO + 32 * b, 1);
-      }
-    }
   }
 }
 
@@ -1443,21 +1322,17 @@ constexpr int FC1_TILES = 4 * 21, FC_TILES = FC1_TILES + 4;
 __host__ __device__ constexpr int fc_waves_per_tile(int B) {
   return B <= 128 ? 1 : (B <= 256 ? 2 : (B <= 512 ? 4 : 8));
 }
-// Update workgroups of NTH threads (UP_NT for lenet_update and the fused step, or NT):
-// a CONV workgroup holds NTH/UP_NT 64-parameter blocks; an FC workgroup NTH/64/wpt tiles
-// when the batch splits K over waves, else ONE tile: the FC phase is bound by per-CU load /
-// store issue (32 loads and ~12 stores per tile wave), so 88 workgroups of one tile beat
-// 11 of eight (fused step: 16.86 -> 16.38 us/step).
-__host__ __device__ constexpr int fc_tiles_per_block(int B, int nth, bool fused) {
-  return fc_waves_per_tile(B) == 1 ? 1 : nth / 64 / fc_waves_per_tile(B);
+// Update workgroups of UP_NT threads: a CONV workgroup holds one 64-parameter block; an FC
+// workgroup UP_NT/64/wpt tiles when the batch splits K over waves, else ONE tile: the FC
+// phase is bound by per-CU load / store issue (32 loads and ~12 stores per tile wave), so
+// 88 workgroups of one tile beat 11 of eight (16.86 -> 16.38 us/step, round 1).
+__host__ __device__ constexpr int fc_tiles_per_block(int B) {
+  return fc_waves_per_tile(B) == 1 ? 1 : UP_NT / 64 / fc_waves_per_tile(B);
 }
-__host__ __device__ constexpr int fc_blocks(int B, int nth = UP_NT, bool fused = false) {
-  return (FC_TILES + fc_tiles_per_block(B, nth, fused) - 1) / fc_tiles_per_block(B, nth, fused);
+__host__ __device__ constexpr int fc_blocks(int B) {
+  return (FC_TILES + fc_tiles_per_block(B) - 1) / fc_tiles_per_block(B);
 }
-__host__ __device__ constexpr int conv_blocks(int nth = UP_NT) { return (NB_CONV + nth / UP_NT - 1) / (nth / UP_NT); }
-__host__ __device__ constexpr int update_blocks(int B, int nth = UP_NT, bool fused = false) {
-  return fc_blocks(B, nth, fused) + conv_blocks(nth);
-}
+__host__ __device__ constexpr int update_blocks(int B) { return fc_blocks(B) + NB_CONV; }
 constexpr int NB_FC = FC_TILES;                     // FC blocks at most (one tile each)
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
@@ -1633,16 +1508,13 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t 
   }
 }
 
-// Update workgroup blk of nblk (NTH threads).  part: float4[NTH/UP_NT][UP_S][UP_C],
-// part2: float[NTH/UP_NT][4][UP_C*4] in LDS.  ready (fused step only): the BAR_* words;
-// wait for this workgroup's go flag -- the nready training workgroups' slabs are
-// complete -- before reading them.
-template <typename T, bool EXCH, bool FUSED, int NTH>
+// Update workgroup blk of nblk (UP_NT threads).  part: float4[UP_S][UP_C], part2:
+// float[4][UP_C*4] in LDS.
+template <typename T, bool EXCH>
 __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
                             int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
-                            int nblk, int tid, float4* part_, float* part2_, const int* ready, int nready,
-                            int fc_tpb) {
-  static_assert(NTH % UP_NT == 0, "whole conv halves");
+                            int nblk, int tid, float4* part_, float* part2_, int fc_tpb) {
+  constexpr int NTH = UP_NT;
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
@@ -1652,28 +1524,9 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
 #define USTAMP(k) \
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
-  // fused step: wait for the training workgroups (bounded: a timeout raises bar[2])
-  auto wait_ready = [&]() {
-    if (!ready) return;
-    if (tid == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int* go = const_cast<int*>(ready) + BAR_GO + 32 * blk;
-      while (sys_load(go) == 0) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-          atomicOr(const_cast<int*>(ready) + BAR_ERR, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      sys_store(go, 0);  // re-arm for the next launch
-    }
-    // no acquire fence: the training outputs are read with device-coherent loads (ld_c)
-    __syncthreads();
-    USTAMP(5);
-  };
 
-  // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (fused step)
-  const int nb_fc = fc_tpb > 0 ? (FC_TILES + fc_tpb - 1) / fc_tpb : fc_blocks(B, NTH, FUSED);
+  // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (the exchange's fixed map)
+  const int nb_fc = fc_tpb > 0 ? (FC_TILES + fc_tpb - 1) / fc_tpb : fc_blocks(B);
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
@@ -1696,8 +1549,6 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       }
       image_slots_flat(max(pi, 0), d0, d1);  // (lanes without a parameter store nothing)
     };
-    if (FUSED) pm_loads();  // the fused step: prefetched while the go flag is polled
-    wait_ready();
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     // Loads are unconditional from a clamped address and masked afterwards: a
     // per-element "load or zero" select makes hipcc branch around every load
@@ -1712,8 +1563,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     {
       float4 v[UP_MAXL];
 #pragma unroll
-      for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(sl + u * UP_S, rows - 1) * UP_C);
-      if (!FUSED) pm_loads();
+      for (int u = 0; u < UP_MAXL; ++u) v[u] = sp[(int64_t)min(sl + u * UP_S, rows - 1) * UP_C];
+      pm_loads();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u)
@@ -1722,7 +1573,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     for (int g0 = sl + UP_S * UP_MAXL; g0 < rows; g0 += UP_S * UP_MAXL) {
       float4 v[UP_MAXL];
 #pragma unroll
-      for (int u = 0; u < UP_MAXL; ++u) v[u] = ld4_c<FUSED>(sp + (int64_t)min(g0 + u * UP_S, rows - 1) * UP_C);
+      for (int u = 0; u < UP_MAXL; ++u) v[u] = sp[(int64_t)min(g0 + u * UP_S, rows - 1) * UP_C];
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u)
         if (g0 + u * UP_S < rows) add4(acc, v[u]);
@@ -1753,8 +1604,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       // loss / accuracy partials: lane-strided sums, then a fixed butterfly
       float s0 = 0.f, s1 = 0.f;
       for (int q = tid; q < nparts; q += 64) {
-        s0 += ld_c<FUSED>(loss_parts + 2 * q);
-        s1 += ld_c<FUSED>(loss_parts + 2 * q + 1);
+        s0 += loss_parts[2 * q];
+        s1 += loss_parts[2 * q + 1];
       }
       s0 = wave_sum(s0);
       s1 = wave_sum(s1);
@@ -1770,11 +1621,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // kernel: the tile's wave issues only the K-steps the batch fills -- 2 * ceil(B / 4) loads
     // and ceil(B / 4) MFMAs (rounded to 2 / 4 / 8) instead of a whole 64-sample chunk's 32
     // loads and 16 MFMAs.  The K-steps dropped would add exact zeros: bitwise the same sums
-    // as the chunk path (and the one-kernel step).  Splitting K over waves instead (B = 32 /
+    // as the chunk path.  Splitting K over waves instead (B = 32 /
     // 64: 2 / 4 waves per tile + an LDS combine) was slower: +0.1 / +0.4 us per step.
-    const bool small = !FUSED && B <= 32;
+    const bool small = B <= 32;
     const int wpt = fc_waves_per_tile(B);
-    const int tpb = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B, NTH, FUSED);
+    const int tpb = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
     const bool live_wave = wave / wpt < tpb;      // (uniform) waves past the block's tiles idle
     const int tile_w = blk * tpb + wave / wpt, sub = wave % wpt;
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
@@ -1819,7 +1670,6 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       image_slots(max(pidx[r], 0), fd[r], d1);
       if (pidx[r] < 0) fd[r] = -1;
     }
-    wait_ready();
     // this wave's samples [k0, k1): a multiple-of-4 share of the batch
     const int kw = ((B + wpt - 1) / wpt + 3) & ~3;
     const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
@@ -1832,8 +1682,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       for (int u = 0; u < 16; ++u) {
         // unconditional loads from clamped addresses, masked after (see role CONV)
         const float* rowc = vslab + (int64_t)min(s0 + 4 * u + kq, B - 1) * VEC;
-        av[u] = ld_c<FUSED>(rowc + a_off + min(o, rows - 1));
-        bv[u] = ld_c<FUSED>(rowc + b_off + min(i, cols - 1));
+        av[u] = rowc[a_off + min(o, rows - 1)];
+        bv[u] = rowc[b_off + min(i, cols - 1)];
       }
     };
     auto mask = [&](int s0, float (&av)[16], float (&bv)[16]) {
@@ -1857,8 +1707,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         const int s = s0 + 4 * u + kq;
         const bool ok = s < k1;
         const float* rowc = vslab + (int64_t)min(s, B - 1) * VEC;
-        const float ra = ld_c<FUSED>(rowc + a_off + min(o, rows - 1));
-        const float rb = ld_c<FUSED>(rowc + b_off + min(i, cols - 1));
+        const float ra = rowc[a_off + min(o, rows - 1)];
+        const float rb = rowc[b_off + min(i, cols - 1)];
         av[u] = (ok && o < rows) ? ra : 0.f;
         bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
       }
@@ -1877,14 +1727,6 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         if (B <= 8) small_k(std::integral_constant<int, 2>{});
         else if (B <= 16) small_k(std::integral_constant<int, 4>{});
         else small_k(std::integral_constant<int, 8>{});
-      }
-    } else if (FUSED) {  // k1 - k0 <= 64
-      if (live_wave) {
-        float a0[16], b0[16];
-        load(k0, a0, b0);
-        mask(k0, a0, b0);
-        USTAMP(1);
-        c = mfma16(c, a0, b0);
       }
     } else if (live_wave && k0 < k1) {
       float a0[16], b0[16], a1[16], b1[16];
@@ -1998,8 +1840,8 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   prefetch_kernargs<sizeof(UpdateKargs) + sizeof(comm::IpcPeers)>();  // (+ gridDim.x after px)
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
-  update_role<T, EXCH, false, UP_NT>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
-                       threadIdx.x, &part[0][0], &part2[0][0], nullptr, 0, fc_tpb);
+  update_role<T, EXCH>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
+                       threadIdx.x, &part[0][0], &part2[0][0], fc_tpb);
 }
 
 // SGD from an already-reduced gradient (DDP: after the all-reduce).
@@ -2049,20 +1891,20 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     if (split) {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 0, SPLIT_K>,
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, SPLIT_K>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 0, SPLIT_K>), dim3(a.grid), dim3(NT), lds, s,
-                         a, 0, (float*)nullptr, StepFuse{});
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, SPLIT_K>), dim3(a.grid), dim3(NT), lds, s,
+                         a, 0, (float*)nullptr);
     } else if (a.xstage) {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 0>,
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 0>), dim3(a.grid), dim3(NT), lds, s, a, 0,
-                         (float*)nullptr, StepFuse{});
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true>), dim3(a.grid), dim3(NT), lds, s, a, 0,
+                         (float*)nullptr);
     } else {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, false, 0>,
+      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false, 0>), dim3(a.grid), dim3(NT), lds, s, a, 0,
-                         (float*)nullptr, StepFuse{});
+      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false>), dim3(a.grid), dim3(NT), lds, s, a, 0,
+                         (float*)nullptr);
     }
   });
   return hipGetLastError();
@@ -2105,50 +1947,6 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
 
 int64_t lenet_exch_words() { return EXCH_WORDS; }
 
-int lenet_fused_max_batch() { return FUSED_MAXB; }
-int lenet_step_bar_ints() { return BAR_INTS; }
-
-hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, float* loss_parts, int nparts,
-                             float* loss_acc, int* bar, hipStream_t s) {
-  // the fused step: staged batch (one sample per training workgroup), SGD applied,
-  // every slab produced by this launch (u describes t's outputs)
-  if (t.B <= 0 || t.B > FUSED_MAXB || t.grid != t.B || !t.xstage || !t.lstage || !bar) return hipErrorInvalidValue;
-  static_assert(NB_UPDATE <= 256, "one go flag per update workgroup");
-  if (!u.apply_sgd || u.grad_in || !u.vslab || u.B != t.B || u.grid != t.grid || u.slab != t.slab ||
-      u.vslab != t.vslab || u.exch_timeout_s <= 0.0)
-    return hipErrorInvalidValue;
-  StepFuse fz{};
-  fz.u = u; fz.loss_parts = loss_parts; fz.nparts = nparts; fz.loss_acc = loss_acc; fz.bar = bar;
-  // FC tiles per workgroup: as lenet_update, or CSED_FC_TPB (1..8) for experiments
-  fz.fc_tpb = fc_tiles_per_block(u.B, UPD_NTH, true);
-  const bool exch = u.exch_id >= 0;
-  if (const char* e = std::getenv("CSED_FC_TPB")) fz.fc_tpb = std::max(1, std::min(8, std::atoi(e)));
-  if (exch) fz.fc_tpb = 1;  // the exchange's fixed workgroup -> word map (see launch_lenet_update)
-  fz.nupd = (FC_TILES + fz.fc_tpb - 1) / fz.fc_tpb + conv_blocks(UPD_NTH);
-  fz.timeout_ticks = (uint64_t)(u.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
-  if (exch) {
-    const hipError_t e = comm::ipc_peers(u.exch_id, &fz.px);
-    if (e != hipSuccess) return e;
-    if (fz.px.cap < EXCH_WORDS) return hipErrorInvalidValue;
-  }
-  const size_t lds = (size_t)(S_TOTAL - S_X);
-  static_assert((UPD_NTH / UP_NT) * (UP_S * UP_C * 16 + 4 * UP_C * 4 * 4) <= S_TOTAL - S_X, "update role LDS");
-  const dim3 grid(t.grid + fz.nupd);
-  CSED_DISPATCH_MFMA(t.mfma_dtype, {
-    if (exch) {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 2>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 2>), grid, dim3(NT), lds, s, t, 0,
-                         (float*)nullptr, fz);
-    } else {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, 1>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, 1>), grid, dim3(NT), lds, s, t, 0,
-                         (float*)nullptr, fz);
-    }
-  });
-  return hipGetLastError();
-}
 
 int lenet_stage_max_batch() { return STAGE_MAXB; }
 int lenet_split_k() { return SPLIT_K; }
@@ -2183,10 +1981,10 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   if (mfma_dtype == kF32) return launch_lenet_train_f32(a, logp_out ? 1 : 0, logp_out, false, s);
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
-    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false, 0>,
+    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false, 0>), dim3(a.grid), dim3(NT), lds, s, a,
-                       logp_out ? 1 : 0, logp_out, StepFuse{});
+    hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false>), dim3(a.grid), dim3(NT), lds, s, a,
+                       logp_out ? 1 : 0, logp_out);
   });
   return hipGetLastError();
 }

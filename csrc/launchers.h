@@ -194,13 +194,6 @@ struct LenetUpdateArgs {
   double exch_timeout_s;
 };
 int64_t lenet_exch_words();
-// One-kernel training step: lenet_train's workgroups, then lenet_update's roles in
-// trailing workgroups that wait on device flags (bar: int32[lenet_step_bar_ints()],
-// zero-initialised; bar[2] != 0 after a timed-out wait).  Staged batches with SGD only.
-int lenet_fused_max_batch();  // largest per-rank batch of launch_lenet_step
-int lenet_step_bar_ints();     // its synchronisation words (int32, zero-initialised)
-hipError_t launch_lenet_step(const LenetTrainArgs& t, const LenetUpdateArgs& u, float* loss_parts, int nparts,
-                             float* loss_acc, int* bar, hipStream_t s);
 // loss_parts [nparts, 2] are summed in a fixed order into loss_acc[2] (optional).
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
                                hipStream_t s);

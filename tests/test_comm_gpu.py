@@ -81,13 +81,11 @@ def _worker(rank, world, port, q):
 
         data = synthetic_mnist(2048, seed=3)
 
-        def train(mode, key=None, one_kernel="auto", split=False):
+        def train(mode, key=None, split=False):
             # ipc: reduce-only update -> one-shot IPC all-reduce kernel -> SGD kernel;
-            # fused: lenet_update exchanges with the peer itself (one kernel), with
-            # one_kernel="1" inside the one-kernel step (csed::lenet_step)
+            # fused: lenet_update exchanges with the peer itself (one kernel)
             key = key or mode
             os.environ["CSED_ALLREDUCE"] = mode
-            os.environ["CSED_ONE_KERNEL_STEP"] = one_kernel
             torch.manual_seed(1)
             eng = FusedLeNetTrainer(Net().to(dev), data, lr=0.05, global_batch=64, ctx=ctx, split=split)
             res[f"split_{key}"] = eng.split
@@ -109,15 +107,11 @@ def _worker(rank, world, port, q):
 
         p_ipc = train("ipc")
         p_fused = train("fused")
-        p_fused1 = train("fused", "fused1k", "1")
-        os.environ["CSED_ONE_KERNEL_STEP"] = "auto"
         # the split step (4 workgroups per sample) through both exchange paths
         p_ipc_s = train("ipc", "ipc_split", split=True)
         p_fused_s = train("fused", "fused_split", split=True)
-        os.environ.pop("CSED_ONE_KERNEL_STEP")
         # all sum the same rank-local gradients in rank order: bitwise-identical training
         res["fused_equals_ipc"] = torch.equal(p_ipc, p_fused)
-        res["fused1k_equals_ipc"] = torch.equal(p_ipc, p_fused1)
         res["split_fused_equals_ipc"] = torch.equal(p_ipc_s, p_fused_s)
         q.put((rank, res))
         dist.destroy_process_group()
@@ -145,13 +139,13 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         assert "exception" not in res, res
         assert res["errors"] == 0, res  # first: a timed-out wait explains any mismatch below
         assert res["enabled"] and res["eager"] and res["graph"], res
-        for mode, kind in (("ipc", "ipc-oneshot"), ("fused", "fused-ipc"), ("fused1k", "fused-ipc"),
-                           ("ipc_split", "ipc-oneshot"), ("fused_split", "fused-ipc")):
+        for mode, kind in (("ipc", "ipc-oneshot"), ("fused", "fused-ipc"), ("ipc_split", "ipc-oneshot"),
+                           ("fused_split", "fused-ipc")):
             assert res[f"kind_{mode}"] == kind, res
             assert res[f"params_equal_{mode}"] and res[f"finite_{mode}"], res
             assert res[f"engine_errors_{mode}"] == 0, res
-        assert res["step_fused"] == "two kernels" and res["step_fused1k"].startswith("one kernel"), res
-        assert res["fused_equals_ipc"] and res["fused1k_equals_ipc"] and res["split_fused_equals_ipc"], res
+        assert res["step_fused"] == "two kernels", res
+        assert res["fused_equals_ipc"] and res["split_fused_equals_ipc"], res
         assert res["split_fused_split"] and not res["split_fused"], res
 
 

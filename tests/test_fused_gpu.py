@@ -209,38 +209,6 @@ def test_batch_staging_is_bitwise_transparent(B):
     assert finals[0][2] == finals[1][2] == 4
 
 
-@pytest.mark.parametrize("B,dampening", [(64, 0.0), (8, 0.1), (40, 0.0)])
-def test_one_kernel_step_matches_two_kernels(B, dampening):
-    """csed::lenet_step (training workgroups + trailing update workgroups waiting on a
-    device counter) must give bitwise the parameters, momenta, loss totals and device
-    counters of the two-kernel step, eager and graph-replayed, and leave its counters
-    re-armed (bar == 0) with no timed-out wait."""
-    data = synthetic_mnist(B * 5, seed=11)
-    finals = []
-    for one in (True, False):
-        torch.manual_seed(3)
-        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B, dampening=dampening,
-                                split=False)
-        assert eng.staged and not eng.one_kernel  # eligible; two kernels by default
-        eng.one_kernel = one
-        assert eng.step_kind.startswith("one kernel") == one
-        eng.set_epoch_order(torch.randperm(len(data), generator=torch.Generator().manual_seed(5)))
-        eng.run_steps(2, use_graph=False)
-        eng.run_steps(2, steps_per_graph=2)
-        torch.cuda.synchronize()
-        assert eng.comm_errors() == 0
-        assert not eng.bar.any().item()  # re-armed counter and go flags, no timed-out wait
-        assert eng.ticket.item() == 0
-        finals.append((eng.flat.data.clone(), eng.momentum_buf.clone(), eng.loss_acc.clone(),
-                       eng.step_count.item(), eng.cursor.item(), eng.rng_offset.item(), eng.wimg.clone()))
-    for a, b in zip(finals[0], finals[1]):
-        if isinstance(a, torch.Tensor):
-            assert torch.equal(a, b)
-        else:
-            assert a == b
-    assert finals[0][3] == 4 and finals[0][4] == 4
-
-
 @pytest.mark.parametrize("dtype,band", [(torch.bfloat16, 0.05), (torch.float16, 0.03)])
 def test_fused_trajectory_matches_cpu_reference(dtype, band):
     """50 SGD steps with dropout off: the fused GPU engine vs the reference recipe on the CPU

@@ -1,5 +1,4 @@
-"""N eager full-batch steps of the fused engine (for kernel traces): python tools/step_loop.py [B] [N]
-(CSED_ONE_KERNEL_STEP=0 selects the two-kernel step)."""
+"""N eager full-batch steps of the fused engine (for kernel traces): python tools/step_loop.py [B] [N]"""
 import os
 import sys
 
