@@ -766,16 +766,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 4: fc2 + log_softmax + NLL, then dlogits and the fc1
     // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
     STAMP(4);
-    if (TRAIN && wave > 0) {
-      // waves 1-15 are idle here: zero the dgrad input image (its 4-pixel border and channels
-      // 20-23 are the convolution's zero padding; stage 5 writes the interior), make the
-      // shifted copies of X that conv1 wgrad reads as aligned runs (stage 8), and in the
-      // split step zero dL/dconv1 (this part's dgrad writes only its tiles' pool windows
-      // and conv1 wgrad reads whole K-steps of it)
+    if (TRAIN && (wave & 3) != 0) {
+      // The 12 waves on SIMDs 1-3 are idle here: zero the dgrad input image (its 4-pixel
+      // border and channels 20-23 are the convolution's zero padding; stage 5 writes the
+      // interior), make the shifted copies of X that conv1 wgrad reads as aligned runs
+      // (stage 8), and in the split step zero dL/dconv1 (this part's dgrad writes only its
+      // tiles' pool windows and conv1 wgrad reads whole K-steps of it).  SIMD 0 is left to
+      // wave 0's loss chain, the stage's critical path.
+      const int zt = (wave - 1 - (wave >> 2)) * 64 + lane;  // 0 .. 767 over the 12 waves
+      constexpr int ZN = 12 * 64;
       constexpr int NZ = (S_DC1 - S_DC2H) / 16;
       uint4* z = reinterpret_cast<uint4*>(DC2H);
-      for (int i = tid - 64; i < NZ; i += NT - 64) z[i] = make_uint4(0, 0, 0, 0);
-      for (int m = tid - 64; m < 784; m += NT - 64) {
+      for (int i = zt; i < NZ; i += ZN) z[i] = make_uint4(0, 0, 0, 0);
+      for (int m = zt; m < 784; m += ZN) {
         const unsigned short v = Xs[m];
 #pragma unroll
         for (int k = 1; k < 4; ++k)
@@ -784,10 +787,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       if (KS > 1) {
         constexpr int NZ1 = (S_COFF - S_DC1) / 16;
         uint4* z1 = reinterpret_cast<uint4*>(DC1);
-        for (int i = tid - 64; i < NZ1; i += NT - 64) z1[i] = make_uint4(0, 0, 0, 0);
+        for (int i = zt; i < NZ1; i += ZN) z1[i] = make_uint4(0, 0, 0, 0);
       }
     }
     if (wave == 0) {
+      __builtin_amdgcn_s_setprio(3);  // the stage's critical chain: first claim on SIMD 0
       const int t = STAGED ? LABEL[0] : t_lab;
       // Every LDS operand first (none depends on the logits): this lane's fc2 row slice
       // for the logits and its fc2 column for dZ1, so the stage has one LDS round trip
@@ -868,6 +872,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         DZ1B[lane] = h16<T>(dz);
         if (wvec && lane < 50) vs[V_DZ1 + lane] = dz;
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     if (!TRAIN) return;
     __syncthreads();
