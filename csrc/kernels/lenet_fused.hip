@@ -571,7 +571,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // The conv2 part of the workgroup's slab row (e = 260 .. 5279) goes out as float4 runs
   // from an LDS copy in the dead fc1 image (F1 is last read in stage 5): 2 wide stores per
   // lane instead of 8 scalar ones of 64 lanes (per-CU store issue is what those cost).
-  float* SLF = reinterpret_cast<float*>(wsm + S_F1);  // indexed by e
+  float* SLF = reinterpret_cast<float*>(wsm + S_F1);  // conv2 slot S_C2 + j at SLF[O_C2W + j]
   static_assert(O_C2B + 20 <= (S_X - S_F1) / 4 && O_C2W % 4 == 0 && (O_C2B + 20) % 4 == 0, "conv2 row staging");
   auto stage_c2 = [&]() {
 #pragma unroll
@@ -581,15 +581,16 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       for (int r = 0; r < 4; ++r) {
         const int oc = mt * 16 + 4 * (lane >> 4) + r;
         if (oc < 20) {
-          if (k < 250) SLF[O_C2W + oc * 250 + k] = acc_c2[mt][0][r];
-          else if (k == 250) SLF[O_C2B + oc] = acc_c2[mt][0][r];
+          if (k <= 250) SLF[O_C2W + k * 20 + oc] = acc_c2[mt][0][r];  // slot order (lenet_layout.h)
         }
       }
     }
   };
   auto store_c2 = [&](int t0, int nt) {  // after a barrier that follows stage_c2
+    // SLF[O_C2W + j] holds conv2 slab slot S_C2 + j (4 consecutive slots: one chunk row run)
     for (int i = O_C2W / 4 + t0; i < (O_C2B + 20) / 4; i += nt)
-      *reinterpret_cast<float4*>(slab_at(4 * i)) = reinterpret_cast<const float4*>(SLF)[i];
+      *reinterpret_cast<float4*>(a.slab + slab_off(S_C2 + 4 * i - O_C2W, b0, G, R2)) =
+          reinterpret_cast<const float4*>(SLF)[i];
   };
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = b0 + s * G;
@@ -958,17 +959,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         acc_c2[1][0] = Mfma<T>::mma(f11, __builtin_bit_cast(frag, b1v), acc_c2[1][0]);
         WSTAMP(12, 26);
         // this part's conv2 wgrad columns, straight from the accumulators (one slab row per
-        // sample; their write latency hides under the dgrad of waves 0-11)
-        const bool kw = k < 250, kbias = k == 250;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int oc = mt * 16 + 4 * kq + rr;
-            const int slot = kw ? S_C2 + oc * 250 + k : S_C2 + 5000 + oc;
-            if (oc < 20 && (kw || kbias))
-              a.slab[((slot >> 6) * R2 + C1_CH * (G - R2) + b0) * 64 + (slot & 63)] = acc_c2[mt][0][rr];
-          }
+        // sample; their write latency hides under the dgrad of waves 0-11).  The slab's conv2
+        // slots are column-major (S_C2 + k*20 + oc), so a lane's four channels 4kq .. 4kq+3 of
+        // column k are one aligned float4 run: one wide store per lane (and one more for
+        // channels 16-19 on lanes kq = 0) instead of eight scalar ones -- store issue was
+        // what these cost.
+        if (k <= 250) {
+          const int slot0 = S_C2 + k * 20 + 4 * kq;
+          float* row = a.slab + (C1_CH * (G - R2) + b0) * 64;  // + chunk * R2 * 64 + slot % 64
+          *reinterpret_cast<f32x4*>(row + (slot0 >> 6) * R2 * 64 + (slot0 & 63)) = acc_c2[0][0];
+          if (kq == 0)
+            *reinterpret_cast<f32x4*>(row + ((slot0 + 16) >> 6) * R2 * 64 + ((slot0 + 16) & 63)) = acc_c2[1][0];
+        }
         if (stage_next) {  // this workgroup's sample of step cursor+1 (its own staging row g)
           if (tid - 768 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 768] = px_next;
           if (tid == 768) a.lstage[g] = lab_next;

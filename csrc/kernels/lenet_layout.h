@@ -19,14 +19,25 @@ constexpr int CNP = O_F1W;  // conv parameters (conv1.w, conv1.b, conv2.w, conv2
 // slots 0..319, 60 padding) with ONE ROW PER WORKGROUP; conv2's 5,020 fill chunks 5-83 (slots
 // 320..5375) with ONE ROW PER SAMPLE: in the split step (several workgroups per sample) the
 // workgroups of a sample own disjoint conv2 columns but each holds a partial conv1 sum.
+// conv2's slots are column-major in the wgrad GEMM: weight (oc, k = ic*25 + tap) and bias
+// (oc, k = 250) at S_C2 + k*20 + oc, so the four output channels an MFMA lane holds for one
+// column are one aligned float4 (lenet_update maps slots back to parameters: slot_param).
 constexpr int C1_CH = 5;
-constexpr int S_C2 = C1_CH * 64;                                 // slab slot of conv2.w[0]
+constexpr int S_C2 = C1_CH * 64;                                 // slab slot of conv2 column 0
 constexpr int CNP_PAD = S_C2 + ((CNP - O_C2W) + 63) / 64 * 64;   // 5376 slots = 84 chunks
 constexpr int N_CHUNKS = CNP_PAD / 64;
-__host__ __device__ constexpr int slab_slot(int p) { return p < O_C2W ? p : p - O_C2W + S_C2; }
+__host__ __device__ constexpr int slab_slot(int p) {
+  return p < O_C2W ? p
+                   : (p < O_C2B ? S_C2 + ((p - O_C2W) % 250) * 20 + (p - O_C2W) / 250  // weight (oc, k)
+                                : S_C2 + 250 * 20 + (p - O_C2B));                    // bias oc: k = 250
+}
 // parameter of a slab slot, -1 for padding
 __host__ __device__ constexpr int slot_param(int s) {
-  return s < O_C2W ? s : (s < S_C2 ? -1 : (s - S_C2 + O_C2W < CNP ? s - S_C2 + O_C2W : -1));
+  return s < O_C2W ? s
+                   : (s < S_C2 ? -1
+                               : (s - S_C2 < 251 * 20 ? ((s - S_C2) / 20 < 250 ? O_C2W + ((s - S_C2) % 20) * 250 + (s - S_C2) / 20
+                                                                              : O_C2B + (s - S_C2) % 20)
+                                                      : -1));
 }
 // rows of a chunk: G (workgroups) for conv1 chunks, R2 = min(G, B) for conv2 chunks
 // (32-bit arithmetic: at most 84 chunks x 256 rows x 64 slots)
