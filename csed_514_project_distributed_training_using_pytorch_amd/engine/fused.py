@@ -77,6 +77,12 @@ def exch_words() -> int:
     return int(torch.ops.csed.lenet_layout()[5])
 
 
+def native_max_steps() -> int:
+    """Longest run of full steps launched by the native executor instead of a graph replay
+    (``CSED_NATIVE_STEPS``; 0 = always graphs).  See ``FusedLeNetTrainer.step_plan``."""
+    return int(os.environ.get("CSED_NATIVE_STEPS", "0"))
+
+
 class FusedLeNetTrainer:
     def __init__(self, model: Net, train: MNISTData, lr: float = 0.01, momentum: float = 0.5,
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
@@ -155,6 +161,8 @@ class FusedLeNetTrainer:
         self.lstage = torch.zeros(self.grid, dtype=torch.long, device=dev) if self.staged else None
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._stepper: tuple | None = None  # (key, csed.LenetStepper), see stepper()
+        self.native_max = native_max_steps()
         self._eval_cache: dict[int, tuple] = {}
         self._order_host: torch.Tensor | None = None
         self.capture_comm_ok: bool | None = None
@@ -288,6 +296,7 @@ class FusedLeNetTrainer:
         """Release the graphs and the IPC buffers (collective on every rank: a barrier runs
         first so that no peer is still pushing into this rank's buffers)."""
         self._graphs.clear()
+        self._stepper = None
         if (self.exch is not None or self.allreduce is not None) and dist.is_initialized():
             torch.cuda.synchronize(self.device)
             if self.ctx.backend == "nccl":
@@ -504,14 +513,43 @@ class FusedLeNetTrainer:
         if tail and self.tail_size() > 0:
             self.graph(1, tail=True)
 
+    def stepper(self):
+        """The native step executor (``csrc/bindings.cpp:LenetStepper``) for this engine's full
+        steps: both kernels' argument blocks built once, ``run(k)`` enqueues 2k launches from
+        C++.  None where a step is more than two launches (the all-reduce fallback)."""
+        if self.comm and self.exch is None:
+            return None
+        exch_id = -1 if self.exch is None else self.exch.id
+        key = (self.perm.data_ptr(), exch_id)
+        if self._stepper is None or self._stepper[0] != key:
+            st = torch.classes.csed.LenetStepper()
+            st.set_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B,
+                         self.ctx.rank, self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts,
+                         1.0 / self.global_batch, MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset,
+                         self.grid, self.mfma, self.xstage if self.staged else None,
+                         self.lstage if self.staged else None, self.staged)
+            st.set_update(self.slab, self.grid, self.vslab, self.B, self.flat.data, self.momentum_buf, self.wimg,
+                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
+                          self.step_count, self.ticket, self.cursor, self.rng_offset, self.loss_parts, self.grid,
+                          self.loss_acc, self.mfma, exch_id, self.exch_timeout_s if exch_id >= 0 else 2.0)
+            self._stepper = (key, st)
+        return self._stepper[1]
+
     def step_plan(self, k: int, steps_per_graph: int = 16, use_graph: bool = True) -> list:
         """The launches that advance k full-batch steps from the current cursor, as a list of
-        callables (graph replays, or eager steps where no graph applies), resolved up front so
-        that a timed region holds nothing but the launches."""
+        callables (graph replays, or native-executor runs where no graph applies), resolved up
+        front so that a timed region holds nothing but the launches.
+
+        Without graphs the native executor launches the steps from C++ (eager Python launches
+        only where a step is more than two kernels).  Runs of at most ``self.native_max`` steps
+        (``CSED_NATIVE_STEPS``, default 0) also take the executor instead of a graph replay:
+        measured, graphs win even at 20 steps -- a replay's ~10 us setup is paid back by shorter
+        gaps between its kernels (``profiles/bench_r2.md``, "Native step executor")."""
         if k <= 0:
             return []
-        if not use_graph or self.capture_comm_ok is False:
-            return [self.step] * k
+        if not use_graph or self.capture_comm_ok is False or k <= self.native_max:
+            st = self.stepper()
+            return [self.step] * k if st is None else [lambda: st.run(k)]
         plan = []
         for n in self.graph_plan(k, steps_per_graph):
             g = self.graph(n)
@@ -591,6 +629,7 @@ class FusedLeNetTrainer:
         g = sd["param_groups"][0]
         self.lr, self.momentum = float(g["lr"]), float(g["momentum"])
         self._graphs.clear()
+        self._stepper = None  # the executor's argument blocks hold lr / momentum
 
     def params_changed(self) -> None:
         """Call after writing the model parameters from outside (e.g. a checkpoint load)."""

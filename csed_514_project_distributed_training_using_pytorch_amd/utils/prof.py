@@ -61,15 +61,16 @@ class EventTimer:
         self._t0 = self._t1 = 0.0
 
     def start(self):
-        if self.cuda:
+        if self.cuda:  # both events made here: stop() inside a timed region only records
             self._s = torch.cuda.Event(enable_timing=True)
+            self._e = torch.cuda.Event(enable_timing=True)
+            self._e.record()  # creates the HIP event now; stop() records it again
             self._s.record()
         self._t0 = time.perf_counter()
         return self
 
     def stop(self):
         if self.cuda:
-            self._e = torch.cuda.Event(enable_timing=True)
             self._e.record()
         self._t1 = time.perf_counter()
         return self

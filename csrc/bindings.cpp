@@ -9,6 +9,7 @@
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
+#include <torch/custom_class.h>
 #include <torch/library.h>
 
 #include "launchers.h"
@@ -462,9 +463,66 @@ void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order,
                                     lcode(mfma_dtype), cur_stream(images)));
 }
 
+// Native step executor: the two launches of a full-batch training step (lenet_train +
+// single-kernel lenet_update: local SGD, or the fused exchange), argument blocks built and
+// checked once, then `run(k)` enqueues the 2k launches on the current stream from C++.  A
+// short run (the driver's 20-step window) pays no graph-launch setup and no Python per
+// launch; long runs use the captured graphs (engine/fused.py:step_plan picks).
+struct LenetStepper : torch::CustomClassHolder {
+  csed::LenetTrainArgs ta{};
+  csed::LenetUpdateArgs ua{};
+  float* loss_parts = nullptr;
+  float* loss_acc = nullptr;
+  int64_t nparts = 0;
+  int device = -1;
+  std::vector<Tensor> keep;  // every tensor the argument blocks point into stays alive
+
+  void set_train(Tensor images, Tensor labels, Tensor perm, Tensor cursor, int64_t B, int64_t rank, Tensor wimg,
+                 Tensor params, Tensor slab, Tensor vslab, Tensor loss_parts_t, double grad_scale, double mean,
+                 double std_, double drop_p, int64_t seed, Tensor rng_offset, int64_t grid, int64_t mfma_dtype,
+                 optional<Tensor> xstage, optional<Tensor> lstage, bool stage_next) {
+    ta = train_args(images, labels, perm, cursor, B, rank, wimg, params, slab, vslab, loss_parts_t, grad_scale,
+                    mean, std_, drop_p, seed, rng_offset, grid, mfma_dtype, c10::nullopt, xstage, lstage,
+                    stage_next);
+    device = images.device().index();
+    keep.insert(keep.end(), {images, labels, perm, cursor, wimg, params, slab, vslab, loss_parts_t, rng_offset});
+    if (xstage.has_value()) keep.insert(keep.end(), {*xstage, *lstage});
+  }
+
+  void set_update(Tensor slab, int64_t grid, Tensor vslab, int64_t B, Tensor params, Tensor momentum, Tensor wimg,
+                  double lr, double mom, double dampening, double weight_decay, bool nesterov, Tensor step,
+                  Tensor ticket, Tensor cursor, Tensor rng_offset, Tensor loss_parts_t, int64_t nparts_,
+                  Tensor loss_acc_t, int64_t mfma_dtype, int64_t exch_id, double exch_timeout_s) {
+    ua = update_args(slab, grid, vslab, B, c10::nullopt, c10::nullopt, params, momentum, wimg, lr, mom, dampening,
+                     weight_decay, nesterov, step, ticket, cursor, rng_offset, true, loss_parts_t, loss_acc_t,
+                     mfma_dtype, c10::nullopt, exch_id, exch_timeout_s);
+    loss_parts = loss_parts_t.data_ptr<float>();
+    loss_acc = loss_acc_t.data_ptr<float>();
+    nparts = nparts_;
+    keep.insert(keep.end(), {slab, vslab, params, momentum, wimg, step, ticket, cursor, rng_offset, loss_parts_t,
+                             loss_acc_t});
+  }
+
+  void run(int64_t k) {
+    TORCH_CHECK(device >= 0 && ua.params, "LenetStepper: set_train and set_update first");
+    TORCH_CHECK(ta.cursor && ua.cursor == ta.cursor, "LenetStepper: full steps advance one device cursor");
+    const c10::DeviceGuard gd(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+    const hipStream_t s = c10::hip::getCurrentHIPStream(device).stream();
+    for (int64_t i = 0; i < k; ++i) {
+      CHECK_HIP(csed::launch_lenet_train(ta, s));
+      CHECK_HIP(csed::launch_lenet_update(ua, loss_parts, (int)nparts, loss_acc, s));
+    }
+  }
+};
+
 }  // namespace
 
 TORCH_LIBRARY(csed, m) {
+  m.class_<LenetStepper>("LenetStepper")
+      .def(torch::init<>())
+      .def("set_train", &LenetStepper::set_train)
+      .def("set_update", &LenetStepper::set_update)
+      .def("run", &LenetStepper::run);
   m.def("lenet_layout() -> int[]", &lenet_layout);
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "

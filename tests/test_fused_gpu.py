@@ -291,3 +291,36 @@ def test_split_step_trains_and_replays_bitwise():
         finals.append((eng.flat.data.clone(), eng.loss_acc.clone()))
     assert torch.equal(finals[0][0], finals[1][0]) and torch.equal(finals[0][1], finals[1][1])
     assert torch.isfinite(finals[0][0]).all()
+
+
+@pytest.mark.parametrize("B", [64, 8])
+def test_native_stepper_matches_graphs_and_eager(B):
+    """The native step executor (csed.LenetStepper: argument blocks built once, 2k launches
+    from C++) runs exactly the steps that graph replay and per-step Python launches run,
+    across an epoch boundary and a tail step, bit for bit; it is rebuilt when the epoch
+    buffer changes."""
+    data = synthetic_mnist(B * 7 + 3, seed=9)
+    finals = []
+    for mode in ("native", "graph", "python"):
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=B)
+        eng.native_max = 64 if mode == "native" else 0
+        g = torch.Generator().manual_seed(7)
+        for _ in range(2):
+            eng.set_epoch_order(torch.randperm(len(data), generator=g))
+            if mode == "python":
+                for _ in range(eng.full_steps()):
+                    eng.step()
+            else:
+                plan = eng.step_plan(3, 2)
+                assert len(plan) == 1 if mode == "native" else len(plan) == 2
+                for launch in plan:
+                    launch()
+                eng.run_steps(eng.full_steps() - 3, 2, use_graph=mode == "graph")
+            eng.last_partial_step(use_graph=mode == "graph")
+        torch.cuda.synchronize()
+        finals.append((eng.flat.data.clone(), eng.momentum_buf.clone(), eng.loss_acc.clone(),
+                       eng.step_count.item()))
+    for other in finals[1:]:
+        assert torch.equal(finals[0][0], other[0]) and torch.equal(finals[0][1], other[1])
+        assert torch.equal(finals[0][2], other[2]) and finals[0][3] == other[3] == 2 * 8

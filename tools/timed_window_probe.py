@@ -16,17 +16,22 @@ from csed_514_project_distributed_training_using_pytorch_amd.models import Net  
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     dev = torch.device("cuda")
-    data = synthetic_mnist(8192, seed=1)
+    data = synthetic_mnist(64 * 256, seed=1)  # 256 steps at B = 64: every plan stays inside the order
     torch.manual_seed(1)
     eng = FusedLeNetTrainer(Net().to(dev), data, global_batch=B)
     eng.set_epoch_order(torch.randperm(len(data)))
-    plans = {"1": [1], "2": [2], "5": [5], "20": [20], "1+19": [1, 19], "2+18": [2, 18], "4+16": [4, 16]}
+    plans = {"1": [1], "2": [2], "5": [5], "20": [20], "1+19": [1, 19], "2+18": [2, 18], "4+16": [4, 16],
+             "200": [200]}
     for p in plans.values():
         for n in p:
             eng.graph(n)
     eng.step()
     res = {}
-    plans.update({"sleep+1": ["s", 1], "sleep+20": ["s", 20], "eager1": ["e"], "eager5": ["e"] * 5})
+    plans.update({"sleep+1": ["s", 1], "sleep+20": ["s", 20], "eager1": ["e"], "eager5": ["e"] * 5, "eager20": ["e"] * 20,
+                  "native1": [("n", 1)], "native5": [("n", 5)], "native20": [("n", 20)], "native200": [("n", 200)],
+                  "sleep+native20": ["s", ("n", 20)]})
+    st = eng.stepper()  # csed.LenetStepper: the native step executor
+    st.run(1)
     for name, p in plans.items():
         walls, evs = [], []
         for _ in range(30):
@@ -40,6 +45,8 @@ def main():
             for n in p:
                 if n == "e":
                     eng.step()
+                elif isinstance(n, tuple):
+                    st.run(n[1])
                 elif n != "s":
                     eng.graph(n).replay()
             b.record()
@@ -48,7 +55,7 @@ def main():
             evs.append(a.elapsed_time(b) * 1e3)
         walls.sort()
         evs.sort()
-        k = sum(1 if n == "e" else n for n in p if n != "s")
+        k = sum(1 if n == "e" else n[1] if isinstance(n, tuple) else n for n in p if n != "s")
         res[name] = (walls[15], evs[15])
         print(f"B={B} plan {name:5s}: wall {walls[15]:8.1f} us ({walls[15] / k:6.2f}/step)   "
               f"events {evs[15]:8.1f} us ({evs[15] / k:6.2f}/step)", flush=True)
