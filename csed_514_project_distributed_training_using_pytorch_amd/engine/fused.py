@@ -520,7 +520,7 @@ class FusedLeNetTrainer:
         if self.comm and self.exch is None:
             return None
         exch_id = -1 if self.exch is None else self.exch.id
-        key = (self.perm.data_ptr(), exch_id)
+        key = (self.perm.data_ptr(), exch_id, self.staged)
         if self._stepper is None or self._stepper[0] != key:
             st = torch.classes.csed.LenetStepper()
             st.set_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B,

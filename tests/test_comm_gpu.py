@@ -94,6 +94,10 @@ def _worker(rank, world, port, q):
             eng.set_epoch_order(smp.indices())
             eng.run_steps(12, steps_per_graph=4)
             eng.step()  # one eager step after the graph replays
+            # no-graph steps: the native executor (csed.LenetStepper) with the fused exchange;
+            # per-step launches on the ipc path (a step there is more than two launches)
+            eng.run_steps(3, use_graph=False)
+            res[f"native_{key}"] = eng.stepper() is not None
             torch.cuda.synchronize(dev)
             p = eng.flat.data.cpu()
             other = p.clone()
@@ -150,6 +154,7 @@ def test_ipc_allreduce_two_ranks_one_gpu():
             assert res[f"kind_{mode}"] == kind, (r, mode, mine)
             assert res[f"params_equal_{mode}"] and res[f"finite_{mode}"], (r, mode, mine)
         assert res["step_fused"] == "two kernels", res
+        assert res["native_fused"] and res["native_fused_split"] and not res["native_ipc"], res
         assert res["fused_equals_ipc"] and res["split_fused_equals_ipc"], res
         assert res["split_fused_split"] and not res["split_fused"], res
 
