@@ -475,7 +475,7 @@ struct LenetStepper : torch::CustomClassHolder {
   float* loss_acc = nullptr;
   int64_t nparts = 0;
   int device = -1;
-  std::vector<Tensor> keep;  // every tensor the argument blocks point into stays alive
+  std::vector<Tensor> keep_t, keep_u;  // every tensor the argument blocks point into stays alive
 
   void set_train(Tensor images, Tensor labels, Tensor perm, Tensor cursor, int64_t B, int64_t rank, Tensor wimg,
                  Tensor params, Tensor slab, Tensor vslab, Tensor loss_parts_t, double grad_scale, double mean,
@@ -485,8 +485,8 @@ struct LenetStepper : torch::CustomClassHolder {
                     mean, std_, drop_p, seed, rng_offset, grid, mfma_dtype, c10::nullopt, xstage, lstage,
                     stage_next);
     device = images.device().index();
-    keep.insert(keep.end(), {images, labels, perm, cursor, wimg, params, slab, vslab, loss_parts_t, rng_offset});
-    if (xstage.has_value()) keep.insert(keep.end(), {*xstage, *lstage});
+    keep_t = {images, labels, perm, cursor, wimg, params, slab, vslab, loss_parts_t, rng_offset};
+    if (xstage.has_value()) keep_t.insert(keep_t.end(), {*xstage, *lstage});
   }
 
   void set_update(Tensor slab, int64_t grid, Tensor vslab, int64_t B, Tensor params, Tensor momentum, Tensor wimg,
@@ -499,8 +499,7 @@ struct LenetStepper : torch::CustomClassHolder {
     loss_parts = loss_parts_t.data_ptr<float>();
     loss_acc = loss_acc_t.data_ptr<float>();
     nparts = nparts_;
-    keep.insert(keep.end(), {slab, vslab, params, momentum, wimg, step, ticket, cursor, rng_offset, loss_parts_t,
-                             loss_acc_t});
+    keep_u = {slab, vslab, params, momentum, wimg, step, ticket, cursor, rng_offset, loss_parts_t, loss_acc_t};
   }
 
   void run(int64_t k) {
