@@ -148,6 +148,16 @@ def main(argv=None) -> int:
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         return 2
     backend = None if args.backend == "auto" else args.backend
+    data_job = None
+    if args.device == "cuda":  # the data set builds (CPU threads) while the GPU context comes up
+        from concurrent.futures import ThreadPoolExecutor
+
+        from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+
+        pool = ThreadPoolExecutor(1)
+        data_job = pool.submit(lambda: (synthetic_mnist(60000, seed=0, train=True),
+                                        synthetic_mnist(10000, seed=0, train=False)))
+        pool.shutdown(wait=False)
     ctx = init_distributed(world_size=world, device=args.device, backend=backend)
     n = ctx.world_size
     if ctx.is_distributed and dist.get_world_size() != args.gpus:
@@ -160,15 +170,13 @@ def main(argv=None) -> int:
         time_elapsed, epoch0_s, epoch_s, val, loss_avg, comm_err, comm_retry = r["time_elapsed_s"], None, None, \
             None, None, 0, None
     else:
-        from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
         from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
         from csed_514_project_distributed_training_using_pytorch_amd.models import Net
         from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
 
         dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
         with prof.range("bench:data"):
-            train = synthetic_mnist(60000, seed=0, train=True)
-            test = synthetic_mnist(10000, seed=0, train=False)
+            train, test = data_job.result()
         use_graph = not args.no_graph
 
         def sync_barrier():
