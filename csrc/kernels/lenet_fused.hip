@@ -1341,6 +1341,23 @@ __host__ __device__ constexpr int fc_blocks(int B) {
 }
 __host__ __device__ constexpr int update_blocks(int B) { return fc_blocks(B) + NB_CONV; }
 constexpr int NB_FC = FC_TILES;                     // FC blocks at most (one tile each)
+// FC tile of workgroup b (one tile per workgroup): b = 8 * slot + xcd takes position
+// 11 * xcd + slot of the fc1 tiles in column-block-major order (q -> row block q % 4, column
+// block q / 4), then the 4 fc2 tiles.  A bijection on [0, 88): see the static_assert below.
+__host__ __device__ constexpr int fc_tile_of_block(int b) {
+  const int q = (FC_TILES / 8) * (b % 8) + b / 8;
+  return q < FC1_TILES ? (q % 4) * 21 + q / 4 : q;
+}
+__host__ __device__ constexpr bool fc_tile_map_is_bijective() {
+  bool seen[FC_TILES] = {};
+  for (int b = 0; b < FC_TILES; ++b) {
+    const int t = fc_tile_of_block(b);
+    if (t < 0 || t >= FC_TILES || seen[t]) return false;
+    seen[t] = true;
+  }
+  return true;
+}
+static_assert(FC_TILES % 8 == 0 && fc_tile_map_is_bijective(), "FC tile map");
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
@@ -1634,7 +1651,10 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     const int wpt = fc_waves_per_tile(B);
     const int tpb = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
     const bool live_wave = wave / wpt < tpb;      // (uniform) waves past the block's tiles idle
-    const int tile_w = blk * tpb + wave / wpt, sub = wave % wpt;
+    // one tile per workgroup: XCD-grouped tiles.  Workgroup b runs on XCD b % 8; the tiles
+    // in (fc1 column-block, row-block) order are dealt out 11 per XCD, so an XCD's tiles share
+    // their column blocks (B operand rows of the vector slab) and its L2 fetches each line once
+    const int tile_w = tpb == 1 ? fc_tile_of_block(blk) : blk * tpb + wave / wpt, sub = wave % wpt;
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
     const int tile = min(tile_w, FC_TILES - 1);   // they compute a valid tile, store nothing
     const bool fc1 = tile < FC1_TILES;
