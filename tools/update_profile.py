@@ -100,6 +100,17 @@ def stamps(st, B, what):
         r = rel[sl]
         desc = "  ".join(f"s{k} med {r[:, k].median().item():.2f} max {r[:, k].max().item():.2f}" for k in ks)
         print(f"stamps {what} {role}: {desc}")
+    # the slowest FC blocks (s4) and their tiles (lenet_fused.hip fc_tile_of_block: one tile
+    # per block at this batch)
+    if wpt == 1:
+        def tile_of(b):
+            q = 11 * (b % 8) + b // 8
+            return (q % 4) * 21 + q // 4 if q < 84 else q
+        fc = rel[:nfc, 4]
+        order = sorted(range(nfc), key=lambda b: -fc[b].item())[:10]
+        print(f"slowest FC blocks {what}: " + "  ".join(
+            f"b{b}/t{tile_of(b)}(mt{tile_of(b) // 21 if tile_of(b) < 84 else 'fc2'},nt{tile_of(b) % 21 if tile_of(b) < 84 else tile_of(b) - 84})"
+            f"={fc[b].item():.2f}/s1={rel[b, 1].item():.2f}" for b in order))
 
 
 if __name__ == "__main__":
