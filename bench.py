@@ -64,6 +64,10 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                     help="process group: auto = RCCL ('nccl') on GPUs; gloo lets ranks share one GPU "
                          "(rehearsal of the multi-rank path; the gradient exchange still runs on the GPU)")
+    ap.add_argument("--loopback-world", type=int, default=0, metavar="N",
+                    help="one GPU only: run lenet_update's fused exchange with N-1 virtual peers (slots of "
+                         "this rank's own buffer) -- the per-rank step of an N-GPU run minus the xGMI flight "
+                         "time; use with --global-batch 64/N")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: plumbing only (launch/rendezvous/JSON contract), stock PyTorch ops")
     return ap.parse_args(argv)
@@ -189,7 +193,7 @@ def main(argv=None) -> int:
             torch.manual_seed(1)
             net = Net().to(ctx.device)
             eng = FusedLeNetTrainer(net, train, lr=0.02, momentum=0.5, global_batch=args.global_batch, ctx=ctx,
-                                    compute_dtype=dt, grid=args.grid or None)
+                                    compute_dtype=dt, grid=args.grid or None, loopback_world=args.loopback_world)
             sampler = ShardSampler(len(train), ctx.world_size, ctx.rank, shuffle=True, seed=42)
             state = {"epoch": 0, "pos": 0}
             spg = args.steps_per_graph
@@ -298,10 +302,15 @@ def main(argv=None) -> int:
         loss_avg = r["loss_sum"] / max(1, args.steps * eng.B)
         engine_kernels = {"fused-ipc": " with in-kernel xGMI gradient exchange", "none": ""}.get(
             eng.allreduce_kind, " + gradient all-reduce")
+        if eng.loopback_world:
+            engine_kernels = f" with the in-kernel exchange looped back to {eng.loopback_world} virtual ranks"
+            extra_lb = {"loopback_world": eng.loopback_world}
+        else:
+            extra_lb = {}
         cfg_engine = f"fused HIP ({eng.kernel_names}{engine_kernels})"
         allreduce, step_kind = eng.allreduce_kind, eng.step_kind
         hip_graph = use_graph and bool(eng.capture_comm_ok)
-        extra = {"device_ms_per_step": round(r["dev_ms"] / args.steps, 5)}
+        extra = {"device_ms_per_step": round(r["dev_ms"] / args.steps, 5), **extra_lb}
         if _ipc.LAST_TIMING:
             extra["allreduce_select_us"] = _ipc.LAST_TIMING
         if eng.path_timing_us:

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import sys
 import time
 
 import torch
@@ -25,7 +26,7 @@ import torch
 from .. import ops
 from ..data import DeviceLoader, get_mnist
 from ..models import Net
-from ..parallel.comm import barrier, destroy, init_distributed, replica_checksum
+from ..parallel.comm import all_reduce_max, barrier, destroy, init_distributed, replica_checksum
 from ..parallel.sampler import ShardSampler
 from ..utils import checkpoint, metrics, plot, prof
 
@@ -279,8 +280,16 @@ def dist_main(argv=None) -> int:
                                 ctx=ctx, compute_dtype=_dtype(args.dtype), seed=args.seed)
         sampler.set_epoch(0)
         order = sampler.indices()
-        for i in range(args.epochs):
+        i = 0
+        while i < args.epochs:
+            # the IPC exchange paths raise a device error word when a peer wait times out (the
+            # kernel then finishes with an incomplete sum instead of hanging): snapshot the
+            # training state so the epoch can be re-run on the process group's all-reduce
+            ipc_live = ctx.is_distributed and (eng.exch is not None or eng.allreduce is not None)
+            snap = [t.clone() for t in eng._state()] if ipc_live else None
+            n_hist = (len(hist.train_losses), len(hist.train_counter))
             eng.set_epoch_order(order)
+            epoch_order = order
             steps, full, rem = eng.steps_per_epoch(), eng.full_steps(), eng.tail_size()
             with prof.range(f"train_epoch{i}"):
                 if bar is not None:
@@ -308,6 +317,20 @@ def dist_main(argv=None) -> int:
             if bar is not None and i + 1 < args.epochs:
                 sampler.set_epoch(i + 1)
                 order = sampler.indices()
+            if ipc_live and int(all_reduce_max(ctx, float(eng.comm_errors()))):
+                # some rank's peer wait timed out this epoch: its gradients are not the global
+                # sum.  Every rank restores the epoch-start state, releases the IPC buffers
+                # (collective) and re-runs the epoch on the process group's all-reduce (RCCL).
+                if ctx.is_main:
+                    print(f"[csed] epoch {i}: an IPC gradient exchange timed out waiting for a peer; "
+                          "re-running the epoch on the process-group all-reduce", file=sys.stderr, flush=True)
+                torch.cuda.synchronize(dev)
+                for t, v in zip(eng._state(), snap):
+                    t.copy_(v)
+                eng.close()
+                del hist.train_losses[n_hist[0]:], hist.train_counter[n_hist[1]:]
+                order = epoch_order
+                continue
             with prof.range(f"eval_epoch{i}"):
                 vloss_sum, correct = eng.evaluate(test_set)
             n_test = len(test_set)
@@ -322,6 +345,8 @@ def dist_main(argv=None) -> int:
             acc = 100.0 * correct / n_test
             print(metrics.dist_epoch_line(i, train_loss, val_loss, acc, time.time() - t0), flush=True)
             _check_replicas(args, ctx, net, i)
+            i += 1
+        eng.close()
     else:
         from .modular import ModularTrainer
 

@@ -38,7 +38,8 @@ from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
 from ..parallel.comm import DistContext
-from ..parallel.ipc import allreduce_mode, make_allreduce, open_exchange, wait_timeout_s
+from ..parallel.ipc import (allreduce_mode, make_allreduce, open_exchange, open_loopback_exchange,
+                            wait_timeout_s)
 from ..utils.flat import FlatParams
 
 
@@ -89,7 +90,7 @@ class FusedLeNetTrainer:
                  global_batch: int = 64, ctx: DistContext | None = None,
                  compute_dtype: torch.dtype = torch.bfloat16, drop_p: float = 0.5, seed: int = 1,
                  grid: int | None = None, broadcast_init: bool = True, comm: bool | None = None,
-                 split: bool | None = None):
+                 split: bool | None = None, loopback_world: int = 0):
         _native.require()
         self.ctx = ctx or DistContext(device=next(model.parameters()).device)
         self.device = self.ctx.device
@@ -178,9 +179,29 @@ class FusedLeNetTrainer:
         self.allreduce = make_allreduce(self.ctx, N_PARAMS) if multi and mode != "fused" else None
         if multi and mode in ("auto", "fused"):
             self._enable_exchange(required=(mode == "fused"))
+        # Loopback exchange (one GPU, no process group): lenet_update runs its full push + poll
+        # code for loopback_world - 1 virtual peers that are slots of this rank's own buffer
+        # (csrc/comm ipc_open_loopback).  Each peer returns this rank's own gradient, and the
+        # loss is scaled by 1 / (loopback_world * global batch), so the summed gradient is this
+        # rank's batch mean: the same training math as world 1, at the per-step kernel cost of a
+        # world-N exchange minus the xGMI flight time (the per-rank step of the driver's N-GPU
+        # run, measured on one GPU: bench.py --loopback-world N).
+        self.loopback_world = int(loopback_world) if loopback_world and int(loopback_world) > 1 else 0
+        if self.loopback_world:
+            if self.world > 1:
+                raise ValueError("loopback_world is a one-GPU measurement mode (world size 1)")
+            self.exch = open_loopback_exchange(self.device, exch_words(), self.loopback_world)
+            self.exchange_note = f"loopback exchange: {self.loopback_world} virtual ranks on one GPU"
+
+    @property
+    def grad_scale(self) -> float:
+        """Loss-gradient scale of a full step: 1 / (global batch) (x 1 / loopback_world)."""
+        return 1.0 / (self.global_batch * max(1, self.loopback_world))
 
     @property
     def allreduce_kind(self) -> str:
+        if self.loopback_world:
+            return f"fused-ipc-loopback{self.loopback_world}"
         if not self.comm:
             return "none"
         if self.exch is not None:
@@ -215,12 +236,23 @@ class FusedLeNetTrainer:
             t_fused = self._time_steps()
             saved, self.exch = self.exch, None
             t_fallback = self._time_steps()
+            # the same step with no exchange at all (each rank updates on its own gradient; the
+            # state is restored): fused - local = what the exchange costs per step
+            self.comm = False
+            t_local = self._time_steps()
+            self.comm = True
             # a path whose graph could not be captured times as inf; ties keep the fused path
             self.exch = saved if t_fused <= t_fallback else None
             if self.exch is None:
                 self.exchange_note = "fused exchange off: slower than the fallback step"
+                # every rank finished the timing above (device synchronize before the timing
+                # all-reduce), so no peer still pushes into these buffers: the close is safe
+                saved.close()
             fin = lambda t: round(t, 2) if t != float("inf") else None  # noqa: E731
             self.path_timing_us = {"fused_step_us": fin(t_fused), "fallback_step_us": fin(t_fallback),
+                                   "local_step_us": fin(t_local),
+                                   "exchange_us": fin(t_fused - t_local) if max(t_fused, t_local) != float("inf")
+                                   else None,
                                    "fallback": "ipc-oneshot" if self.allreduce is not None else "rccl"}
 
     def _vote(self, ok: bool) -> bool:
@@ -297,6 +329,10 @@ class FusedLeNetTrainer:
         first so that no peer is still pushing into this rank's buffers)."""
         self._graphs.clear()
         self._stepper = None
+        if self.loopback_world and self.exch is not None:  # local buffer, no peers
+            torch.cuda.synchronize(self.device)
+            self.exch.close()
+            self.exch = None
         if (self.exch is not None or self.allreduce is not None) and dist.is_initialized():
             torch.cuda.synchronize(self.device)
             if self.ctx.backend == "nccl":
@@ -416,7 +452,7 @@ class FusedLeNetTrainer:
 
     def step(self) -> None:
         """One full-batch training step at the device cursor (eager launches)."""
-        self._launch_step(self.B, self.grid, 1.0 / self.global_batch, self.cursor, self.perm)
+        self._launch_step(self.B, self.grid, self.grad_scale, self.cursor, self.perm)
 
     def tail_size(self) -> int:
         """Per-rank samples of the epoch's short last batch (0 if the epoch divides evenly)."""
@@ -425,7 +461,7 @@ class FusedLeNetTrainer:
     def _tail_step(self) -> None:
         rem = self.tail_size()
         tail = self.perm[self.full_steps() * self.B:]  # a view: stable pointer for graph replay
-        gb = rem * self.world  # every rank has the same remainder (sampler pads to a multiple)
+        gb = rem * self.world * max(1, self.loopback_world)  # (the sampler pads to a multiple: same on every rank)
         self._launch_step(rem, min(rem, self.grid), 1.0 / gb, None, tail)
         # the tail step does not use the cursor; keep it consistent for the next epoch
         self.cursor.add_(1)
@@ -525,7 +561,7 @@ class FusedLeNetTrainer:
             st = torch.classes.csed.LenetStepper()
             st.set_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B,
                          self.ctx.rank, self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts,
-                         1.0 / self.global_batch, MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset,
+                         self.grad_scale, MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset,
                          self.grid, self.mfma, self.xstage if self.staged else None,
                          self.lstage if self.staged else None, self.staged)
             st.set_update(self.slab, self.grid, self.vslab, self.B, self.flat.data, self.momentum_buf, self.wimg,

@@ -70,6 +70,7 @@ class IpcAllReduce:
         self.timeout_s = float(timeout_s if timeout_s is not None else wait_timeout_s())
         self.id = -1
         self.measured_us: dict | None = None
+        self.loopback_world = 0
         self._pad_in = self._pad_out = None
         if self.n_pad != self.n:
             self._pad_in = torch.zeros(self.n_pad, dtype=torch.float32, device=ctx.device)
@@ -88,6 +89,14 @@ class IpcAllReduce:
     def open(self, handles: torch.Tensor) -> None:
         with torch.cuda.device(self.ctx.device):
             torch.ops.csed.ipc_open(self.id, handles, self.ctx.rank)
+
+    def open_loopback(self, world: int) -> None:
+        """Map ``world`` virtual ranks onto this rank's own buffer (csrc/comm ipc_open_loopback):
+        every exchange returns world x the local value, through the kernels' full push + poll
+        code for world - 1 peers.  A one-GPU measurement of the world-N exchange's kernel side."""
+        with torch.cuda.device(self.ctx.device):
+            torch.ops.csed.ipc_open_loopback(self.id, int(world))
+        self.loopback_world = int(world)
 
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """out = sum over ranks of x (in place when ``out`` is None).  Graph-capturable."""
@@ -220,6 +229,16 @@ def open_exchange(ctx: DistContext, words: int) -> tuple[IpcAllReduce | None, st
     if shared > MAX_RANKS_PER_GPU:
         return None, f"{shared} ranks share one GPU (spin-waiting exchange needs <= {MAX_RANKS_PER_GPU})"
     return _open(ctx, (words + 3) // 4 * 4, blocks=1)
+
+
+def open_loopback_exchange(device: torch.device, words: int, world: int, blocks: int = 1) -> IpcAllReduce:
+    """An exchange buffer of ``words`` 8-byte words per sender with ``world`` virtual ranks on
+    ``device`` (see :meth:`IpcAllReduce.open_loopback`); ``blocks``: workgroups of its one-shot
+    all-reduce kernel.  Local: no process group."""
+    ar = IpcAllReduce(DistContext(device=device), (words + 3) // 4 * 4, blocks=blocks)
+    ar.create()
+    ar.open_loopback(world)
+    return ar
 
 
 def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:

@@ -474,6 +474,7 @@ struct LenetStepper : torch::CustomClassHolder {
   float* loss_parts = nullptr;
   float* loss_acc = nullptr;
   int64_t nparts = 0;
+  csed::comm::IpcPeers px{};  // the exchange buffer's device view (ua.exch_id >= 0)
   int device = -1;
   std::vector<Tensor> keep_t, keep_u;  // every tensor the argument blocks point into stays alive
 
@@ -499,6 +500,8 @@ struct LenetStepper : torch::CustomClassHolder {
     loss_parts = loss_parts_t.data_ptr<float>();
     loss_acc = loss_acc_t.data_ptr<float>();
     nparts = nparts_;
+    px = {};
+    if (exch_id >= 0) CHECK_HIP(csed::comm::ipc_peers((int)exch_id, &px));  // once, not per launch
     keep_u = {slab, vslab, params, momentum, wimg, step, ticket, cursor, rng_offset, loss_parts_t, loss_acc_t};
   }
 
@@ -509,7 +512,7 @@ struct LenetStepper : torch::CustomClassHolder {
     const hipStream_t s = c10::hip::getCurrentHIPStream(device).stream();
     for (int64_t i = 0; i < k; ++i) {
       CHECK_HIP(csed::launch_lenet_train(ta, s));
-      CHECK_HIP(csed::launch_lenet_update(ua, loss_parts, (int)nparts, loss_acc, s));
+      CHECK_HIP(csed::launch_lenet_update(ua, loss_parts, (int)nparts, loss_acc, s, ua.exch_id >= 0 ? &px : nullptr));
     }
   }
 };

@@ -15,6 +15,10 @@ hipError_t ipc_get_handle(int id, void* handle_out);
 int ipc_handle_bytes();
 // Map every peer's buffer; `handles` is [world][ipc_handle_bytes()] in rank order.
 hipError_t ipc_open(int id, const void* handles, int world, int rank);
+// Loopback: `world` virtual ranks on this device (this rank = 0), each peer a sender slot of
+// this rank's own buffer, so an exchange returns world x the local value.  Measures the
+// kernels' push + poll cost for N - 1 peers on one GPU.
+hipError_t ipc_open_loopback(int id, int world);
 // out = sum over ranks of in (n floats, n % 4 == 0); in == out is allowed.
 hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double timeout_s, hipStream_t s);
 // Unmap the peers, free the buffers and retire the id (after a process-group barrier:

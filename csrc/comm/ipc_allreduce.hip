@@ -43,6 +43,16 @@ __device__ __forceinline__ uint64_t ll_word(float v, uint32_t t) {
   return ((uint64_t)t << 32) | (uint64_t)__float_as_uint(v);
 }
 
+// One LL word into a peer's receive buffer: a relaxed system-scope store (global_store_dwordx2
+// sc0 sc1), i.e. written through to the buffer's memory.  A plain store into an IPC-imported
+// mapping may be held dirty in the WRITER's L2 (the importer's mapping need not carry the
+// owner's uncached attribute); the owner polls its buffer from another XCD or device and would
+// not see the word until that line happened to be evicted: the intermittent stall of two
+// ranks sharing one GPU (profiles/dp_exchange_r3.md).
+__device__ __forceinline__ void push_word(uint64_t* q, uint64_t w) {
+  __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(kThreads) ipc_allreduce_kernel(const float* __restrict__ in, float* out, int64_t n2,
                                                                  int64_t cap, int world, int rank, PeerBufs peers,
                                                                  int64_t* __restrict__ counters, int* err,
@@ -57,13 +67,16 @@ __global__ void __launch_bounds__(kThreads) ipc_allreduce_kernel(const float* __
   const int64_t slot = (int64_t)(t & 1) * kMaxRanks * cap;
   const float2* in2 = reinterpret_cast<const float2*>(in);
 
-  // 1. push: my words -> slot[rank] of every peer (posted 16-byte stores, N-1 links)
+  // 1. push: my words -> slot[rank] of every peer (posted write-through stores, N-1 links)
   for (int64_t i = lo + tid; i < hi; i += kThreads) {
     const float2 v = in2[i];
-    const u64x2 w = {ll_word(v.x, t), ll_word(v.y, t)};
 #pragma unroll
     for (int p = 0; p < kMaxRanks; ++p)
-      if (p < world && p != rank) reinterpret_cast<u64x2*>(peers.base[p] + slot + (int64_t)rank * cap)[i] = w;
+      if (p < world && p != rank) {
+        uint64_t* q = peers.base[p] + slot + (int64_t)rank * cap + 2 * i;
+        push_word(q, ll_word(v.x, t));
+        push_word(q + 1, ll_word(v.y, t));
+      }
   }
   // 2. reduce in rank order from my local receive buffer.  All senders' words of
   // an element pair are loaded together (unconditionally, from clamped rows) and
@@ -120,6 +133,7 @@ struct IpcComm {
   int* err = nullptr;
   PeerBufs peers{};
   int world = 0, rank = -1;
+  bool loopback = false;  // peers are slots of this rank's own buffer (ipc_open_loopback)
 };
 
 std::vector<IpcComm*>& registry() {
@@ -192,6 +206,23 @@ hipError_t ipc_open(int id, const void* handles, int world, int rank) {
   return hipSuccess;
 }
 
+hipError_t ipc_open_loopback(int id, int world) {
+  // Virtual peers on one device: sender slot p of this rank's own buffer stands in for
+  // peer p's receive buffer (base[p] = buf + p * cap, this rank is rank 0), so a push to
+  // peer p lands exactly where the poll for sender p reads.  Every exchange then returns
+  // world x the local value, and the kernels run their full push + poll code for N - 1
+  // peers: the kernel-side cost of a world-N exchange without a second GPU.
+  IpcComm* c = get(id);
+  if (!c || world < 1 || world > kMaxRanks) return hipErrorInvalidValue;
+  PeerBufs p{};
+  for (int r = 0; r < world; ++r) p.base[r] = c->buf + (int64_t)r * c->cap;
+  c->peers = p;
+  c->world = world;
+  c->rank = 0;
+  c->loopback = true;
+  return hipSuccess;
+}
+
 hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double timeout_s, hipStream_t s) {
   IpcComm* c = get(id);
   if (!c || c->world < 1 || n > c->cap || n % 4) return hipErrorInvalidValue;
@@ -219,7 +250,7 @@ hipError_t ipc_destroy(int id) {
   // every queued kernel that reads or writes the mappings must be done first; the caller
   // runs a process-group barrier before this, so no peer is still pushing into `buf`
   hipError_t e = hipDeviceSynchronize();
-  for (int r = 0; r < c->world; ++r)
+  for (int r = 0; r < c->world && !c->loopback; ++r)
     if (r != c->rank && c->peers.base[r]) {
       const hipError_t e2 = hipIpcCloseMemHandle(c->peers.base[r]);
       if (e == hipSuccess) e = e2;

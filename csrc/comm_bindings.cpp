@@ -26,6 +26,11 @@ int64_t ipc_create(int64_t n, int64_t blocks) {
   return id;
 }
 
+// `world` virtual ranks on this device (ipc_allreduce.h: the loopback measurement mode)
+void ipc_open_loopback(int64_t id, int64_t world) {
+  COMM_CHECK(csed::comm::ipc_open_loopback((int)id, (int)world));
+}
+
 Tensor ipc_handle(int64_t id) {
   Tensor h = at::empty({csed::comm::ipc_handle_bytes()}, at::kByte);
   COMM_CHECK(csed::comm::ipc_get_handle((int)id, h.data_ptr()));
@@ -65,6 +70,7 @@ TORCH_LIBRARY_FRAGMENT(csed, m) {
   m.def("ipc_create(int n, int blocks) -> int", &ipc_create);
   m.def("ipc_handle(int id) -> Tensor", &ipc_handle);
   m.def("ipc_open(int id, Tensor handles, int rank) -> ()", &ipc_open);
+  m.def("ipc_open_loopback(int id, int world) -> ()", &ipc_open_loopback);
   m.def("ipc_allreduce(int id, Tensor input, Tensor(a!) out, float timeout_s=2.0) -> ()", &ipc_allreduce);
   m.def("ipc_error(int id, bool reset=False) -> int", &ipc_error);
   m.def("ipc_destroy(int id) -> ()", &ipc_destroy);

@@ -107,6 +107,17 @@ __device__ __forceinline__ void prefetch_kernargs() {
                "s"(v[8]), "s"(v[9]), "s"(v[10]), "s"(v[11]));
 }
 
+// Raise a kernel's dynamic-LDS limit once per instantiation (host side).  The attribute
+// is a property of the function, not of a launch: setting it on every launch was host
+// work on every step of the native executor (csrc/bindings.cpp LenetStepper).
+template <auto KERNEL>
+inline void allow_dynamic_lds(size_t bytes) {
+  static size_t done = 0;  // one flag per kernel instantiation
+  if (done >= bytes) return;
+  hipFuncSetAttribute((const void*)KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  done = bytes;
+}
+
 // ---------------------------------------------------------------------------
 // Counter-based RNG (Philox4x32-10).  Dropout masks are a pure function of
 // (seed, offset, element), so forward and backward regenerate the identical

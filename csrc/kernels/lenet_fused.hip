@@ -1497,8 +1497,8 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t 
     if (p < px.world && p != px.rank) {
       uint64_t* dst = px.base[p] + slot + (int64_t)px.rank * px.cap;
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (live[k]) dst[idx[k]] = ll_word(v[k], t);
+      for (int k = 0; k < K; ++k)  // write-through (system scope): see comm::push_word
+        if (live[k]) __hip_atomic_store(dst + idx[k], ll_word(v[k], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   const uint64_t* mine = px.base[px.rank] + slot;
@@ -1918,18 +1918,15 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     if (split) {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true, SPLIT_K>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      allow_dynamic_lds<lenet_train_kernel<scalar_t, true, true, SPLIT_K>>(lds);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, SPLIT_K>), dim3(a.grid), dim3(NT), lds, s,
                          a, 0, (float*)nullptr);
     } else if (a.xstage) {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      allow_dynamic_lds<lenet_train_kernel<scalar_t, true, true>>(lds);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true>), dim3(a.grid), dim3(NT), lds, s, a, 0,
                          (float*)nullptr);
     } else {
-      hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, true, false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      allow_dynamic_lds<lenet_train_kernel<scalar_t, true, false>>(lds);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false>), dim3(a.grid), dim3(NT), lds, s, a, 0,
                          (float*)nullptr);
     }
@@ -1938,7 +1935,7 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
-                               hipStream_t s) {
+                               hipStream_t s, const comm::IpcPeers* px_cached) {
   if (a.apply_sgd && a.grad_in) {
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       hipLaunchKernelGGL(lenet_sgd_kernel<scalar_t>, dim3(cdiv(NP, 256)), dim3(256), 0, s, a);
@@ -1954,8 +1951,12 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     // every B, the full steps' and the epoch tail's alike (a batch-dependent layout let
     // the counters of different words drift apart between steps of different batch sizes).
     static_assert(NB_UPDATE <= comm::kIpcMaxBlocks, "one exchange counter per update workgroup");
-    const hipError_t e = comm::ipc_peers(a.exch_id, &px);
-    if (e != hipSuccess) return e;
+    if (px_cached) {  // resolved once by the caller (csrc/bindings.cpp LenetStepper)
+      px = *px_cached;
+    } else {
+      const hipError_t e = comm::ipc_peers(a.exch_id, &px);
+      if (e != hipSuccess) return e;
+    }
     if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
@@ -2008,8 +2009,7 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   if (mfma_dtype == kF32) return launch_lenet_train_f32(a, logp_out ? 1 : 0, logp_out, false, s);
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
-    hipFuncSetAttribute((const void*)lenet_train_kernel<scalar_t, false, false>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    allow_dynamic_lds<lenet_train_kernel<scalar_t, false, false>>(lds);
     hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false>), dim3(a.grid), dim3(NT), lds, s, a,
                        logp_out ? 1 : 0, logp_out);
   });

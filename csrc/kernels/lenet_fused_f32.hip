@@ -524,12 +524,10 @@ hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float
   using namespace lenet32;
   if (a.B <= 0 || a.grid <= 0 || a.grid > a.B || a.grid > 256 || a.xstage) return hipErrorInvalidValue;
   if (train) {
-    hipFuncSetAttribute((const void*)lenet_train_f32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        LDS_BYTES);
+    allow_dynamic_lds<lenet_train_f32_kernel<true>>(LDS_BYTES);
     hipLaunchKernelGGL(lenet_train_f32_kernel<true>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, 0, (float*)nullptr);
   } else {
-    hipFuncSetAttribute((const void*)lenet_train_f32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        LDS_BYTES);
+    allow_dynamic_lds<lenet_train_f32_kernel<false>>(LDS_BYTES);
     hipLaunchKernelGGL(lenet_train_f32_kernel<false>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, write_logp,
                        logp_out);
   }

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "comm/ipc_allreduce.h"
+
 namespace csed {
 
 // dtype codes shared with Python (see ops/_dtypes.py)
@@ -195,8 +197,10 @@ struct LenetUpdateArgs {
 };
 int64_t lenet_exch_words();
 // loss_parts [nparts, 2] are summed in a fixed order into loss_acc[2] (optional).
+// px: the exchange buffer's device view resolved once by the caller (csrc/bindings.cpp
+// LenetStepper), so a launch does no registry lookup; null: looked up from a.exch_id.
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
-                               hipStream_t s);
+                               hipStream_t s, const comm::IpcPeers* px = nullptr);
 hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype, hipStream_t s);
 // Forward-only evaluation: out_parts [min(n,256), 2] per-workgroup (loss sum, correct).
 hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,

@@ -111,12 +111,12 @@ def _worker(rank, world, port, q):
             return p
 
         # The one-shot IPC engine path (reduce-only update -> spinning all-reduce kernel -> SGD
-        # kernel) intermittently stalled its peer on this shared GPU until a 30 s wait expired
-        # (2 of the last 8 runs, parameters otherwise right): a co-residency effect of two ranks
-        # on one device.  It runs here only on request (CSED_TEST_SHARED_GPU_IPC=1); its
-        # all-reduce kernel itself is checked above (eager and graph-replayed), and the fused
-        # engine below is checked against the ranks' own sums.
-        ipc_engine = os.environ.get("CSED_TEST_SHARED_GPU_IPC", "0") == "1"
+        # kernel).  Until round 3 it intermittently stalled its peer here until a 30 s wait
+        # expired, parameters otherwise right: the pushes were plain stores into the importer's
+        # mapping of the peer buffer, which could sit dirty in the writer's L2 while the owner
+        # polled memory.  The pushes are write-through (system-scope) stores now
+        # (csrc/comm/ipc_allreduce.hip push_word); CSED_TEST_SHARED_GPU_IPC=0 skips the case.
+        ipc_engine = os.environ.get("CSED_TEST_SHARED_GPU_IPC", "1") == "1"
         p_ipc = train("ipc") if ipc_engine else None
         res["ipc_engine"] = ipc_engine
         p_fused = train("fused")
@@ -125,11 +125,9 @@ def _worker(rank, world, port, q):
         # fills a CU -- at batch 32 (2 x 128 of them) a rank spinning in its exchange could
         # hold the CUs its peer's training step waits for; one process per GPU has no such
         # contention)
-        # (the split step through the one-shot IPC path is not run here: on this shared GPU its
-        # spinning all-reduce kernel intermittently stalled the peer until a 30 s wait expired
-        # (3 of 5 runs, parameters still equal) -- a co-residency effect of two ranks on one
-        # device, not of the split step, which the fused path below covers)
-        train("fused", "fused_split", split=True, gb=16)
+        p_fs = train("fused", "fused_split", split=True, gb=16)
+        p_is = train("ipc", "ipc_split", split=True, gb=16) if ipc_engine else None
+        res["fused_split_equals_ipc_split"] = p_is is None or torch.equal(p_is, p_fs)
         # both sum the same rank-local gradients in rank order: bitwise-identical training
         res["fused_equals_ipc"] = p_ipc is None or torch.equal(p_ipc, p_fused)
         q.put((rank, res))
@@ -158,7 +156,7 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         assert "exception" not in res, res
         assert res["errors"] == 0, res  # first: a timed-out wait explains any mismatch below
         assert res["enabled"] and res["eager"] and res["graph"], res
-        modes = (("ipc", "ipc-oneshot"),) if res["ipc_engine"] else ()
+        modes = (("ipc", "ipc-oneshot"), ("ipc_split", "ipc-oneshot")) if res["ipc_engine"] else ()
         for mode, kind in modes + (("fused", "fused-ipc"), ("fused_split", "fused-ipc")):
             mine = {k: v for k, v in res.items() if k.endswith("_" + mode)}
             assert res[f"engine_errors_{mode}"] == 0, (r, mode, mine)  # first: explains a mismatch
@@ -167,7 +165,7 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         assert res["step_fused"] == "two kernels", res
         assert res["native_fused"] and res["native_fused_split"], res
         assert not res.get("native_ipc", False), res
-        assert res["fused_equals_ipc"], res
+        assert res["fused_equals_ipc"] and res["fused_split_equals_ipc_split"], res
         assert res["split_fused_split"] and not res["split_fused"], res
 
 

@@ -1,0 +1,97 @@
+"""The fused gradient exchange of lenet_update (csrc/kernels/lenet_fused.hip ll_allreduce) and
+the one-shot IPC all-reduce (csrc/comm/ipc_allreduce.hip) at world sizes 2 / 4 / 8 on ONE GPU:
+loopback mode (csrc/comm ipc_open_loopback) maps the N - 1 virtual peers onto sender slots of
+this rank's own receive buffer, so the kernels run their full push + poll code for N - 1 peers
+and every exchange returns N x the local value.  The reference's exchange is DDP's all-reduce
+of the 21,840-float gradient once per step (ref src/train_dist.py:63,83)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N_PARAMS = 21840
+
+
+def _engine(B, loopback_world=0, dtype=torch.bfloat16, n=2048, drop_p=0.5):
+    from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+    from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1)
+    return FusedLeNetTrainer(Net().to(dev), synthetic_mnist(n, seed=3), lr=0.05, momentum=0.5, global_batch=B,
+                             compute_dtype=dtype, drop_p=drop_p, loopback_world=loopback_world)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("B", [8, 64])
+def test_loopback_exchange_returns_world_copies(world, B):
+    """Integer-valued slabs through the reduce-only update with the exchange: the result is
+    exactly world x the local sum, for both slot parities (4 rounds), with no timed-out wait."""
+    eng = _engine(B, loopback_world=world)
+    ops = torch.ops.csed
+    gen = torch.Generator(device="cpu").manual_seed(5 + world + B)
+    common = (eng.flat.data, eng.momentum_buf, eng.wimg, eng.lr, eng.momentum, eng.dampening, eng.weight_decay,
+              eng.nesterov, eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
+    for _ in range(4):
+        eng.slab.copy_(torch.randint(-8, 9, eng.slab.shape, generator=gen, dtype=torch.float32))
+        eng.vslab.copy_(torch.randint(-4, 5, eng.vslab.shape, generator=gen, dtype=torch.float32))
+        local = torch.empty(N_PARAMS, device=eng.device)
+        fused = torch.empty_like(local)
+        ops.lenet_update(eng.slab, eng.grid, eng.vslab, eng.B, None, local, *common)
+        ops.lenet_update(eng.slab, eng.grid, eng.vslab, eng.B, None, fused, *common, None, eng.exch.id,
+                         eng.exch_timeout_s)
+        torch.cuda.synchronize()
+        assert torch.equal(fused, local * world)
+    assert eng.comm_errors() == 0
+    eng.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_oneshot_allreduce(world):
+    """The standalone one-shot IPC all-reduce kernel (32 blocks) in loopback: world x input."""
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ipc import open_loopback_exchange
+
+    dev = torch.device("cuda", 0)
+    ar = open_loopback_exchange(dev, N_PARAMS, world, blocks=32)
+    x = torch.remainder(torch.arange(N_PARAMS, device=dev, dtype=torch.float32) * 7, 61.0)
+    for r in range(4):
+        y = ar(x + r, torch.empty_like(x))
+        torch.cuda.synchronize()
+        assert torch.equal(y, (x + r) * world)
+    assert ar.error() == 0
+    ar.close()
+
+
+def test_loopback_training_is_local_training():
+    """At world 2 the loopback step scales the loss by 1/2 and sums two copies of the gradient:
+    power-of-two scaling commutes with bf16 rounding, so training is bitwise the world-1
+    training (graph replays + the native executor), and every exchange completed."""
+    finals = []
+    for world in (0, 2):
+        eng = _engine(16, loopback_world=world)
+        eng.set_epoch_order(torch.randperm(2048, generator=torch.Generator().manual_seed(0)))
+        eng.run_steps(8, steps_per_graph=4)
+        eng.run_steps(4, use_graph=False)
+        torch.cuda.synchronize()
+        assert eng.comm_errors() == 0
+        assert eng.allreduce_kind == ("none" if world == 0 else "fused-ipc-loopback2")
+        finals.append(eng.flat.data.clone())
+        eng.close()
+    assert torch.isfinite(finals[0]).all()
+    assert torch.equal(finals[0], finals[1])
+
+
+def test_loopback_world8_trains_close_to_local():
+    """World 8 sums eight copies in rank order (not exactly 8x in fp32): close to world 1."""
+    finals = []
+    for world in (0, 8):
+        eng = _engine(8, loopback_world=world)
+        eng.set_epoch_order(torch.randperm(2048, generator=torch.Generator().manual_seed(1)))
+        eng.run_steps(16, steps_per_graph=8)
+        torch.cuda.synchronize()
+        assert eng.comm_errors() == 0
+        finals.append(eng.flat.data.clone())
+        eng.close()
+    rel = (finals[1] - finals[0]).norm() / finals[0].norm()
+    assert rel < 1e-4, rel.item()
