@@ -73,6 +73,21 @@ def split_factor() -> int:
     return int(torch.ops.csed.lenet_layout()[6])
 
 
+def tile_samples() -> int:
+    """Samples per tile of the sample-tile training kernel (csrc/kernels/lenet_tile.hip)."""
+    return int(torch.ops.csed.lenet_layout()[7])
+
+
+def tile_min_batch() -> int:
+    """Smallest per-rank batch the auto mode runs on the sample-tile kernel."""
+    return int(torch.ops.csed.lenet_layout()[8])
+
+
+def tile_grid(B: int) -> int:
+    """Workgroups of the sample-tile kernel at per-rank batch B."""
+    return min(256, -(-B // tile_samples()))
+
+
 def exch_words() -> int:
     """8-byte words per sender of lenet_update's fused exchange buffer."""
     return int(torch.ops.csed.lenet_layout()[5])
@@ -164,6 +179,10 @@ class FusedLeNetTrainer:
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._stepper: tuple | None = None  # (key, csed.LenetStepper), see stepper()
         self.native_max = native_max_steps()
+        # which training kernel runs a step: 0 auto (the sample-tile kernel, csrc/kernels/
+        # lenet_tile.hip, for 16-bit unstaged per-rank batches >= tile_min_batch()), 1 the
+        # per-sample lenet_train, 2 the sample-tile kernel
+        self.train_kernel = 0
         self._eval_cache: dict[int, tuple] = {}
         self._order_host: torch.Tensor | None = None
         self.capture_comm_ok: bool | None = None
@@ -414,7 +433,7 @@ class FusedLeNetTrainer:
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
                         self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
                         self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,
-                        self.xstage if st else None, self.lstage if st else None, st)
+                        self.xstage if st else None, self.lstage if st else None, st, self.kernel_for(B, grid))
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
         if self.exch is not None:
@@ -433,6 +452,15 @@ class FusedLeNetTrainer:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
                              self.loss_parts, grid, self.loss_acc, self.mfma)
 
+    def kernel_for(self, B: int, grid: int) -> int:
+        """``train_kernel`` for a launch of per-rank batch B on ``grid`` workgroups: the tile kernel
+        only where its grid (min(256, ceil(B / tile_samples()))) is the launch's, else per-sample."""
+        if self.train_kernel == 0:
+            return 0 if (B < tile_min_batch() or grid == tile_grid(B)) else 1
+        if self.train_kernel == 2 and grid != tile_grid(B):
+            return 1
+        return self.train_kernel
+
     def gradient(self, grid: int | None = None, dbg: torch.Tensor | None = None) -> torch.Tensor:
         """Mean-loss gradient of the batch at the cursor, without updating anything
         (lenet_train + the reduce-only lenet_update).  Also accumulates the batch's
@@ -444,7 +472,8 @@ class FusedLeNetTrainer:
                         self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts, 1.0 / self.global_batch,
                         MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg,
                         self.xstage if self.staged and grid == self.grid else None,
-                        self.lstage if self.staged and grid == self.grid else None, False)
+                        self.lstage if self.staged and grid == self.grid else None, False,
+                        self.kernel_for(self.B, grid))
         ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
                          self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma)
@@ -563,7 +592,7 @@ class FusedLeNetTrainer:
                          self.ctx.rank, self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts,
                          self.grad_scale, MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset,
                          self.grid, self.mfma, self.xstage if self.staged else None,
-                         self.lstage if self.staged else None, self.staged)
+                         self.lstage if self.staged else None, self.staged, self.kernel_for(self.B, self.grid))
             st.set_update(self.slab, self.grid, self.vslab, self.B, self.flat.data, self.momentum_buf, self.wimg,
                           self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                           self.step_count, self.ticket, self.cursor, self.rng_offset, self.loss_parts, self.grid,

@@ -298,7 +298,7 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 std::vector<int64_t> lenet_layout() {
   return {csed::lenet_wimg_elems(), csed::lenet_conv_param_count(), csed::lenet_vec_len(),
           csed::lenet_param_count(), csed::lenet_stage_max_batch(), csed::lenet_exch_words(),
-          csed::lenet_split_k()};
+          csed::lenet_split_k(), csed::lenet_tile_samples(), csed::lenet_tile_min_batch()};
 }
 
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
@@ -316,13 +316,19 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
                                 double grad_scale, double mean, double std_, double drop_p, int64_t seed,
                                 const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
                                 const optional<Tensor>& dbg, const optional<Tensor>& xstage,
-                                const optional<Tensor>& lstage, bool stage_next) {
+                                const optional<Tensor>& lstage, bool stage_next, int64_t kernel = 0) {
   dev(images, "images"); dev(labels, "labels"); dev(perm, "perm"); dev(wimg, "wimg"); dev(params, "params");
   dev(slab, "slab"); dev(vslab, "vslab"); dev(loss_parts, "loss_parts");
   TORCH_CHECK(images.scalar_type() == at::kByte && images.numel() == images.size(0) * 784, "images: uint8 [N,28,28]");
   TORCH_CHECK(labels.scalar_type() == at::kLong && perm.scalar_type() == at::kLong);
   TORCH_CHECK(grid >= 1 && (grid <= B || (xstage.has_value() && grid == csed::lenet_split_k() * B)) && grid <= 1024,
               "lenet_train: 1 <= grid <= B (or split_k * B for a staged batch)");
+  TORCH_CHECK(kernel >= 0 && kernel <= 2, "lenet_train: kernel 0 (auto), 1 (per sample) or 2 (sample tiles)");
+  const bool tile = mfma_dtype != csed::kF32 && !xstage.has_value() &&
+                    (kernel == 2 || (kernel == 0 && B >= csed::kLenetTileMinB));
+  if (tile)
+    TORCH_CHECK(grid == csed::lenet_tile_grid((int)B) && !dbg.has_value(),
+                "lenet_train: the sample-tile kernel runs grid ", csed::lenet_tile_grid((int)B), " (no stage stamps)");
   TORCH_CHECK(slab.numel() >= grid * csed::lenet_conv_param_count() && loss_parts.numel() >= 2 * grid,
               "lenet_train: slab [grid, 5280] / loss_parts [grid, 2] too small");
   TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_train: vslab [B, 464] too small");
@@ -334,7 +340,7 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   a.wimg = (const uint16_t*)wimg.data_ptr(); a.params = params.data_ptr<float>(); a.slab = slab.data_ptr<float>();
   a.vslab = vslab.data_ptr<float>(); a.loss_acc = loss_parts.data_ptr<float>(); a.grad_scale = (float)grad_scale; a.mean = (float)mean;
   a.std_ = (float)std_; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.rng_offset = optpt<int64_t>(rng_offset);
-  a.grid = (int)grid; a.mfma_dtype = lcode(mfma_dtype);
+  a.grid = (int)grid; a.mfma_dtype = lcode(mfma_dtype); a.kernel = (int)kernel;
   if (a.mfma_dtype == csed::kF32)
     TORCH_CHECK(grid <= 256 && !xstage.has_value() && !dbg.has_value(),
                 "lenet_train fp32: grid <= 256, no batch staging, no stage stamps");
@@ -364,11 +370,11 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
                  double grad_scale, double mean, double std_, double drop_p, int64_t seed,
                  const optional<Tensor>& rng_offset, int64_t grid, int64_t mfma_dtype,
                  const optional<Tensor>& dbg, const optional<Tensor>& xstage, const optional<Tensor>& lstage,
-                 bool stage_next) {
+                 bool stage_next, int64_t kernel) {
   const c10::DeviceGuard gd(images.device());
   const csed::LenetTrainArgs a = train_args(images, labels, perm, cursor, B, rank, wimg, params, slab, vslab,
                                             loss_parts, grad_scale, mean, std_, drop_p, seed, rng_offset, grid,
-                                            mfma_dtype, dbg, xstage, lstage, stage_next);
+                                            mfma_dtype, dbg, xstage, lstage, stage_next, kernel);
   CHECK_HIP(csed::launch_lenet_train(a, cur_stream(images)));
 }
 
@@ -452,7 +458,9 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
 
 void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order, int64_t n, const Tensor& wimg,
                 const Tensor& params, double mean, double std_, Tensor& out_parts, const optional<Tensor>& logp_out,
-                int64_t mfma_dtype) {
+                int64_t mfma_dtype, int64_t kernel) {
+  TORCH_CHECK(kernel >= 0 && kernel <= 2, "lenet_eval: kernel 0 (auto), 1 (per sample) or 2 (sample tiles)");
+  TORCH_CHECK(kernel != 2 || out_parts.numel() >= 2 * csed::lenet_tile_grid((int)n), "lenet_eval: out_parts too small");
   dev(images, "images"); dev(labels, "labels"); dev(order, "order"); dev(out_parts, "out_parts");
   TORCH_CHECK(order.numel() >= n && out_parts.numel() >= 2 * std::min<int64_t>(n, 256));
   if (logp_out.has_value()) TORCH_CHECK(logp_out->numel() >= n * 10 && logp_out->scalar_type() == at::kFloat);
@@ -460,7 +468,7 @@ void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order,
   CHECK_HIP(csed::launch_lenet_eval(images.data_ptr<uint8_t>(), labels.data_ptr<int64_t>(), order.data_ptr<int64_t>(),
                                     n, (const uint16_t*)wimg.data_ptr(), params.data_ptr<float>(), (float)mean,
                                     (float)std_, out_parts.data_ptr<float>(), optpt<float>(logp_out),
-                                    lcode(mfma_dtype), cur_stream(images)));
+                                    lcode(mfma_dtype), cur_stream(images), (int)kernel));
 }
 
 // Native step executor: the two launches of a full-batch training step (lenet_train +
@@ -481,10 +489,10 @@ struct LenetStepper : torch::CustomClassHolder {
   void set_train(Tensor images, Tensor labels, Tensor perm, Tensor cursor, int64_t B, int64_t rank, Tensor wimg,
                  Tensor params, Tensor slab, Tensor vslab, Tensor loss_parts_t, double grad_scale, double mean,
                  double std_, double drop_p, int64_t seed, Tensor rng_offset, int64_t grid, int64_t mfma_dtype,
-                 optional<Tensor> xstage, optional<Tensor> lstage, bool stage_next) {
+                 optional<Tensor> xstage, optional<Tensor> lstage, bool stage_next, int64_t kernel) {
     ta = train_args(images, labels, perm, cursor, B, rank, wimg, params, slab, vslab, loss_parts_t, grad_scale,
                     mean, std_, drop_p, seed, rng_offset, grid, mfma_dtype, c10::nullopt, xstage, lstage,
-                    stage_next);
+                    stage_next, kernel);
     device = images.device().index();
     keep_t = {images, labels, perm, cursor, wimg, params, slab, vslab, loss_parts_t, rng_offset};
     if (xstage.has_value()) keep_t.insert(keep_t.end(), {*xstage, *lstage});
@@ -530,7 +538,7 @@ TORCH_LIBRARY(csed, m) {
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
         "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "
         "float drop_p, int seed, Tensor? rng_offset, int grid, int mfma_dtype, Tensor(c!)? dbg=None, "
-        "Tensor(e!)? xstage=None, Tensor(f!)? lstage=None, bool stage_next=False) -> ()");
+        "Tensor(e!)? xstage=None, Tensor(f!)? lstage=None, bool stage_next=False, int kernel=0) -> ()");
   m.def("lenet_stage(Tensor images, Tensor labels, Tensor perm, Tensor cursor, int B, Tensor(a!) xstage, "
         "Tensor(b!) lstage) -> ()");
   m.def("lenet_update(Tensor slab, int grid, Tensor vslab, int B, Tensor? grad_in, Tensor(a!)? grad_out, Tensor(b!) params, "
@@ -539,7 +547,7 @@ TORCH_LIBRARY(csed, m) {
         "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
         "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
-        "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype) -> ()");
+        "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype, int kernel=0) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "
         "Tensor(b!)? labels_out, Tensor? labels_src) -> ()");
   m.def("sgd_flat(Tensor(a!) p, Tensor g, Tensor(b!) buf, float lr, float momentum, float dampening, "

@@ -53,89 +53,14 @@
 #include "comm/ipc_allreduce.h"
 #include "common.h"
 #include "dispatch.h"
+#include "kernels/lenet_dev.h"
+#include "kernels/lenet_images.h"
 #include "kernels/lenet_layout.h"
 
 namespace csed {
 
 namespace lenet {
 // (flat parameter order, slab and vector-slab layouts: kernels/lenet_layout.h)
-// 16-bit weight images.  Each operand keeps only its live rows plus ONE zero
-// row; fragment reads of padding rows are clamped onto that zero row.
-constexpr int C2_ICP = 16;  // conv2 fwd HWC: 10 input channels padded to 2 groups of 8
-constexpr int LD_P1H = 24;  // P1H position stride (elements): 12 dwords, conflict-free b128 rows
-constexpr int C2_KS = 13;   // conv2 fwd K-steps: 25 taps x 16 channels = 400 -> 416
-constexpr int P1H_RP = 320; // P1H row pitch (elements): 12 positions x 24 + 32
-constexpr int DG_OCP = 24;  // dgrad HWC: 20 channels padded to 3 groups of 8
-constexpr int DG_KS = 19;   // dgrad K-steps: 25 taps x 24 channels = 600 -> 608
-// DC2H (zero-padded HWC dL/dconv2) row pitch in elements: 16 positions x 24 + 32.  With the
-// K-slice order below it makes the dgrad A reads (16 output pixels crossing a 12-wide row,
-// two K slices per ds_read_b128 lane group) nearly conflict-free: 30 modelled extra LDS
-// cycles per sample instead of 1200 (pitch 384, natural order).
-constexpr int DC2H_RP = 16 * 24 + 32;
-// dgrad K-slice order: K-step ks, lane group q reads slice DG_ORDER[4*ks + q] = tap*3 + ocg
-// (channels 8*ocg .. +7 of tap); slice 75 is padding (zero weights).  Found by local search
-// in tools/lds_bank_model.py (which parses this table).
-struct DgOrder {
-  uint8_t fwd[75], inv[75];
-};
-// conv2 forward K-slice order: K-step ks, lane group q reads slice C2_ORDER[4*ks + q] =
-// tap*2 + icg (channels 8*icg .. +7 of tap); with P1H_RP it makes the conv2 A reads
-// conflict-free (416 modelled extra cycles per sample before).  Slices 50, 51 are padding.
-struct C2Order {
-  uint8_t fwd[50], inv[50];
-};
-constexpr C2Order make_c2_order() {
-  C2Order o{{42, 2, 43, 41, 27, 37, 26, 31, 5, 1, 29, 19, 34, 24, 33, 18, 48, 13, 14, 16, 12, 10, 38, 28, 23,
-             3, 22, 32, 17, 47, 39, 49, 20, 30, 35, 15, 8, 6, 21, 46, 36, 11, 4, 0, 25, 45, 7, 9, 44, 40},
-            {}};
-  for (int i = 0; i < 50; ++i) o.inv[o.fwd[i]] = (uint8_t)i;
-  return o;
-}
-constexpr bool c2_order_is_permutation() {
-  const C2Order o = make_c2_order();
-  for (int c = 0; c < 50; ++c)
-    if (o.fwd[o.inv[c]] != c) return false;
-  return true;
-}
-static_assert(c2_order_is_permutation(), "C2_ORDER must be a permutation of the 50 K slices");
-__constant__ C2Order kC2Order = make_c2_order();
-constexpr DgOrder make_dg_order() {
-  DgOrder o{{10, 70, 33, 22, 35, 46, 63, 52, 49, 27, 66, 6, 7, 56, 11, 71, 64, 53, 47, 74, 36, 42, 51, 40, 16,
-             54, 68, 57, 65, 5, 24, 21, 45, 12, 67, 18, 55, 17, 50, 1, 28, 19, 9, 58, 60, 0, 20, 29, 59, 32,
-             13, 73, 38, 44, 61, 39, 8, 30, 41, 3, 14, 25, 69, 31, 23, 72, 4, 15, 62, 2, 26, 48, 43, 34, 37},
-            {}};
-  for (int i = 0; i < 75; ++i) o.inv[o.fwd[i]] = (uint8_t)i;
-  return o;
-}
-constexpr bool dg_order_is_permutation() {
-  const DgOrder o = make_dg_order();
-  for (int c = 0; c < 75; ++c)
-    if (o.fwd[o.inv[c]] != c) return false;
-  return true;
-}
-static_assert(dg_order_is_permutation(), "DG_ORDER must be a permutation of the 75 K slices");
-__constant__ DgOrder kDgOrder = make_dg_order();
-constexpr int LD_W2C = 432, LD_F1 = 328;   // row strides chosen bank-conflict-free (tools/lds_bank_model.py)
-constexpr int R_W2C = 20, R_F1 = 50;       // live rows; row R_* is the zero row
-// dgrad B operand, chunk-major: [DG_CH chunks of 8 K][16 rows (ic; 10..15 zero)][8]; chunk
-// DG_CH-1 is all zero.  Every 16-lane ds_read_b128 group then hits 16 distinct 16-byte slots
-// (row-major rows collide between the kq0 / kq1 halves of a group whatever the stride).
-constexpr int DG_CH = 4 * DG_KS + 1;
-constexpr int I_W1C = 0, I_W2C = 512;
-// conv1 K slot of tap (kh, kw): lane group q of the MFMA A fragment owns slots
-// 8q..8q+7; slots 8q+j (j < 5) are row q's taps, so every group reads its row as
-// base + 28q + {0..4} (immediate LDS offsets), and the five row-4 taps fill slots
-// 8q+5..8q+7 of groups 0 and 1 as base + 112 + e_q + {0,1,2} (e_0 = 0, e_1 = 2;
-// slot 7 of group 0 duplicates tap (4,2) with a zero weight; groups 2, 3 read
-// (4,0..2) with zero weights).
-constexpr int w1c_slot(int kh, int kw) {
-  return kh < 4 ? kh * 8 + kw : (kw < 2 ? 5 + kw : 8 + 5 + (kw - 2));
-}
-constexpr int W1_E1 = 2;  // row-4 column offset of lane group 1's extra slots
-constexpr int I_W2D = I_W2C + (R_W2C + 1) * LD_W2C;  // 9584
-constexpr int I_F1 = I_W2D + DG_CH * 16 * 8;         // 19440
-// padded so the LDS copy is whole 512-thread x 16-byte rounds
-constexpr int I_END = I_W2C + ((I_F1 + (R_F1 + 1) * LD_F1 - I_W2C + 4095) / 4096) * 4096;  // 33280
 constexpr int LD_DC2 = 72, LD_DC1 = 592;
 constexpr int NT = 1024, NW = 16;  // 16 waves, 4 per SIMD
 
@@ -181,12 +106,6 @@ static_assert(25 * DG_OCP <= DG_KS * 32, "dgrad K");
 
 using namespace lenet;
 
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) void glb_void;
 
 // Diagnostic stage stamps (a.dbg non-null): thread 0 of each workgroup records
 // s_memtime at each stage start of its first sample, into LDS (a global store
@@ -205,50 +124,8 @@ constexpr int DBG_W = 32;  // stamp slots per workgroup (a.dbg: int64 [grid][32]
     if (a.dbg && tid == 0 && s == (nsamp > 1 ? 1 : 0)) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-template <typename T>
-__device__ __forceinline__ unsigned short h16(float v) { return bits_of<T>((T)v); }
-template <typename T>
-__device__ __forceinline__ float f16v(unsigned short b) { return (float)of_bits<T>(b); }
-
-// ds_read_b64_tr_b16: lanes 4q+p of each 16-lane group address row q, columns
-// 4p..4p+3 of a 4x16 block; lane i of the group receives column i (row q in
-// element q).  EXEC must be all ones (the gather crosses lanes).
-__device__ __forceinline__ s16x4 lds_read_tr16(const unsigned short* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
-}
-
-// An LDS index the compiler cannot relate to its neighbours: keeps a run of
-// 16-bit reads at a sliding (2-byte aligned) window as single ds_read_u16s
-// instead of one merged, misaligned ds_read_b128 (replayed at ~64 cycles).
-__device__ const int64_t kZeroWord = 0;
-
-__device__ __forceinline__ int opaque(int x) {
-  asm("" : "+v"(x));
-  return x;
-}
-
-// Workgroup barrier for LDS traffic only: this wave's LDS operations complete,
-// then s_barrier; a compiler memory barrier too.  Unlike __syncthreads() it does
-// not wait for an in-flight LDS-DMA (the legaliser makes an LDS release fence
-// wait vmcnt(0) while one is outstanding), so stages that do not read the DMA'd
-// weights run under it.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// One ds_read_u16 at an immediate offset (OFF elements) from p.  Inline asm keeps
-// neighbouring 16-bit reads at a sliding, 2-byte-aligned window from being merged
-// into misaligned ds_read_b32/b64 (replayed at ~64 cycles); the compiler does not
-// track these reads, so their consumer must wait with lds_wait8 first.
-template <int OFF>
-__device__ __forceinline__ uint32_t lds_u16(const unsigned short* p) {
-  uint32_t v;
-  asm volatile("ds_read_u16 %0, %1 offset:%2" : "=v"(v) : "v"((uint32_t)reinterpret_cast<uintptr_t>(p)), "i"(OFF * 2));
-  return v;
-}
-// lgkmcnt(0), threading the eight values through the asm so no use is hoisted above it
-__device__ __forceinline__ void lds_wait8(uint32_t (&v)[8]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
-}
+// (h16 / f16v, lds_read_tr16, opaque, lds_barrier, lds_u16 / lds_wait8: kernels/lenet_dev.h)
+__device__ const int64_t kZeroWord = 0;  // a zero counter for loads that have no counter
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
@@ -1908,8 +1785,15 @@ int64_t lenet_param_count() { return NP; }
 int64_t lenet_conv_param_count() { return CNP_PAD; }
 int64_t lenet_vec_len() { return VEC; }
 
+// the sample-tile kernel (lenet_tile.hip) for this launch?  kernel: 0 auto, 1 no, 2 yes
+static bool use_tile(int kernel, int B, int mfma_dtype, bool staged) {
+  if (mfma_dtype == kF32 || staged || kernel == 1) return false;
+  return kernel == 2 || B >= kLenetTileMinB;
+}
+
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   if (a.mfma_dtype == kF32) return launch_lenet_train_f32(a, 0, nullptr, true, s);  // lenet_fused_f32.hip
+  if (use_tile(a.kernel, a.B, a.mfma_dtype, a.xstage != nullptr)) return launch_lenet_tile(a, 0, nullptr, true, s);
   // split step: a staged batch with SPLIT_K workgroups (parts) per sample, one staging row each
   const bool split = a.xstage && a.lstage && a.grid == SPLIT_K * a.B && a.grid <= 256;
   if (a.B <= 0 || a.grid <= 0 || (a.grid > a.B && !split)) return hipErrorInvalidValue;
@@ -1996,7 +1880,8 @@ hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype
 
 hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,
                              int64_t n, const uint16_t* wimg, const float* params, float mean,
-                             float std_, float* out, float* logp_out, int mfma_dtype, hipStream_t s) {
+                             float std_, float* out, float* logp_out, int mfma_dtype, hipStream_t s,
+                             int kernel) {
   // Evaluation reuses the training kernel's forward (TRAIN = false): every
   // workgroup walks samples g, g+G, ... and writes its [loss, correct] pair
   // into `out` (2*G floats); the caller reduces them in a fixed order.
@@ -2007,6 +1892,10 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   a.grad_scale = 0.f; a.mean = mean; a.std_ = std_; a.drop_p = 0.f; a.seed = 0; a.rng_offset = nullptr;
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
   if (mfma_dtype == kF32) return launch_lenet_train_f32(a, logp_out ? 1 : 0, logp_out, false, s);
+  if (use_tile(kernel, a.B, mfma_dtype, false)) {
+    a.grid = lenet_tile_grid(a.B);  // == min(n, 256) for every n the auto mode sends here
+    return launch_lenet_tile(a, logp_out ? 1 : 0, logp_out, false, s);
+  }
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
     allow_dynamic_lds<lenet_train_kernel<scalar_t, false, false>>(lds);

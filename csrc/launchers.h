@@ -153,10 +153,19 @@ struct LenetTrainArgs {
   uint8_t* xstage;           // optional staged batch [B, 784] (grid == B): sample b = workgroup b
   int64_t* lstage;           // its labels [B]
   int stage_next;            // with xstage: also stage step cursor+1 (perm / cursor are read for it)
+  int kernel;                // 0 auto, 1 per-sample lenet_train, 2 sample-tile kernel (lenet_tile.hip)
 };
 // mfma_dtype == kF32 selects the exact-fp32 kernel (lenet_fused_f32.hip: no weight images,
 // no batch staging, v_mfma_f32_16x16x4_f32).
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s);
+// Sample-tile training / evaluation kernel for large batches (lenet_tile.hip): tiles of
+// lenet_tile_samples() samples, grid lenet_tile_grid(B); same outputs as lenet_train.  The auto
+// mode picks it for 16-bit, unstaged batches of at least kLenetTileMinB samples.
+constexpr int kLenetTileMinB = 1024;
+int lenet_tile_samples();
+int lenet_tile_min_batch();
+int lenet_tile_grid(int B);
+hipError_t launch_lenet_tile(const LenetTrainArgs& a, int write_logp, float* logp_out, bool train, hipStream_t s);
 hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float* logp_out, bool train,
                                   hipStream_t s);
 // Batch staging: pixels + labels of one step, gathered through the epoch permutation.
@@ -205,6 +214,7 @@ hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype
 // Forward-only evaluation: out_parts [min(n,256), 2] per-workgroup (loss sum, correct).
 hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,
                              int64_t n, const uint16_t* wimg, const float* params, float mean,
-                             float std_, float* out_parts, float* logp_out, int mfma_dtype, hipStream_t s);
+                             float std_, float* out_parts, float* logp_out, int mfma_dtype, hipStream_t s,
+                             int kernel = 0);
 
 }  // namespace csed

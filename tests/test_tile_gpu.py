@@ -1,0 +1,131 @@
+"""Sample-tile training kernel for large per-rank batches (csrc/kernels/lenet_tile.hip) vs the
+per-sample lenet_train (csrc/kernels/lenet_fused.hip) and the fp32 CPU reference Net.
+
+The large-batch configuration of BASELINE.json (global batch 8192: 8192 samples per rank on one
+GPU, 1024 on each of 8) runs this kernel.  Its forward is bitwise lenet_train's (same weight
+images, same K orders and accumulation chains, same Philox dropout draws), so the loss, the
+accuracy and the fc gradients (formed by lenet_update from the per-sample vectors) must match
+bit for bit; the conv gradients sum in another order and must match to fp32 rounding of
+16-bit products.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNIST_MEAN, MNIST_STD
+from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer, tile_grid
+from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _rel(a, b):
+    return ((a.double().cpu() - b.double().cpu()).norm() / b.double().cpu().norm().clamp_min(1e-30)).item()
+
+
+def _grads(B, kernel, dt=torch.bfloat16, drop_p=0.5, n=None, seed=23, counter=3):
+    n = n or B + 100
+    data = synthetic_mnist(n, seed=seed)
+    torch.manual_seed(3)
+    grid = tile_grid(B) if kernel == 2 else min(B, 256)
+    eng = FusedLeNetTrainer(Net().to(DEV), data, global_batch=B, compute_dtype=dt, drop_p=drop_p, grid=grid)
+    eng.train_kernel = kernel
+    assert eng.kernel_for(B, grid) == kernel
+    eng.set_epoch_order(torch.randperm(n, generator=torch.Generator().manual_seed(1))[:B])
+    eng.rng_offset.fill_(counter)
+    g = eng.gradient()
+    torch.cuda.synchronize()
+    return g.cpu(), eng.loss_acc.cpu().clone(), eng.vslab[:B].cpu().clone()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B", [1024, 1001, 64, 7])
+def test_tile_matches_per_sample_kernel(B, dt):
+    gt, lt, vt = _grads(B, 2, dt)
+    gs, ls, vs = _grads(B, 1, dt)
+    # loss sum / correct count: the same per-sample values, summed over another number of
+    # workgroup partials
+    assert torch.allclose(lt, ls, rtol=1e-6, atol=0), (lt, ls)
+    assert torch.equal(vt, vs)                 # per-sample fc vectors: the forward is bitwise
+    off = 0
+    for name, p in Net().named_parameters():
+        n = p.numel()
+        a, b = gt[off:off + n], gs[off:off + n]
+        if name.startswith("fc"):
+            assert torch.equal(a, b), name
+        else:
+            rel = _rel(a, b)
+            assert rel < 1e-2, f"{name}: tile vs per-sample relative L2 {rel:.3e}"
+        off += n
+
+
+def test_tile_gradient_matches_cpu_reference():
+    """Dropout off: the tile kernel's gradient against the fp32 CPU Net (16-bit bands, as
+    test_fused_gpu.test_fused_gradient_matches_reference)."""
+    B = 1024
+    data = synthetic_mnist(2048, seed=11)
+    torch.manual_seed(1)
+    net, ref = Net(), Net()
+    ref.load_state_dict(net.state_dict())
+    eng = FusedLeNetTrainer(net.to(DEV), data, global_batch=B, drop_p=0.0)
+    assert eng.kernel_for(B, eng.grid) == 0 and eng.grid == tile_grid(B)  # auto -> tile kernel
+    order = torch.randperm(2048, generator=torch.Generator().manual_seed(0))[:B]
+    eng.set_epoch_order(order)
+    g = eng.gradient().cpu()
+    x = ((data.images[order].float() / 255.0 - MNIST_MEAN) / MNIST_STD).to(torch.bfloat16).float().view(-1, 1, 28, 28)
+    ref.eval()
+    out = ref(x)
+    loss = F.nll_loss(out, data.labels[order])
+    loss.backward()
+    lsum, _ = eng.loss_acc.tolist()
+    assert abs(lsum / B - loss.item()) < 0.05 * max(1.0, loss.item())
+    off = 0
+    for name, p in ref.named_parameters():
+        n = p.numel()
+        rel = _rel(g[off:off + n].view_as(p), p.grad)
+        assert rel < (6e-2 if name.startswith("fc") else 0.2), f"{name}: {rel:.3e}"
+        off += n
+
+
+def test_tile_eval_matches_per_sample_eval():
+    data = synthetic_mnist(3000, seed=9, train=False)
+    torch.manual_seed(2)
+    eng = FusedLeNetTrainer(Net().to(DEV), synthetic_mnist(64, seed=1), global_batch=64)
+    test, ar = eng._device_data(data)
+    ops = torch.ops.csed
+    res = []
+    for kernel in (2, 1):
+        out = torch.empty(3000, 10, device=DEV)
+        parts = torch.zeros(512, device=DEV)
+        ops.lenet_eval(test.images, test.labels, ar, 3000, eng.wimg, eng.flat.data, MNIST_MEAN, MNIST_STD, parts,
+                       out, eng.mfma, kernel)
+        torch.cuda.synchronize()
+        res.append((out.cpu(), parts[:512].view(256, 2).double().sum(0).cpu()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.allclose(res[0][1], res[1][1], rtol=1e-6)
+
+
+def test_tile_training_epoch_matches_per_sample_and_converges():
+    """Two epochs at per-rank batch 1024 (graph-replayed, with the epoch tail on the tile kernel
+    too): the tile-kernel and per-sample trainings stay within the 16-bit band of each other,
+    and the loss falls."""
+    n = 1024 * 5 + 300
+    train = synthetic_mnist(n, seed=3)
+    test = synthetic_mnist(1000, seed=4, train=False)
+    finals = []
+    for kernel in (0, 1):
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(DEV), train, lr=0.1, momentum=0.5, global_batch=1024)
+        eng.train_kernel = kernel
+        l0, _ = eng.evaluate(test)
+        g = torch.Generator().manual_seed(0)
+        for _ in range(2):
+            eng.train_epoch(torch.randperm(n, generator=g), steps_per_graph=2)
+        torch.cuda.synchronize()
+        l1, c1 = eng.evaluate(test)
+        assert l1 < 0.8 * l0, (kernel, l0, l1)
+        finals.append(eng.flat.data.cpu().clone())
+    assert torch.isfinite(finals[0]).all()
+    assert _rel(finals[0], finals[1]) < 3e-2

@@ -5,7 +5,7 @@
 T=${1:-r3x}
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out && \
-timeout -k 10 400 python -u -m pytest tests/test_exchange_loopback_gpu.py tests/test_comm_gpu.py -v --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 && \
+timeout -k 10 400 python -u -m pytest tests/test_exchange_loopback_gpu.py tests/test_comm_gpu.py tests/test_dropout_pin_gpu.py -v --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 ; [ $? -le 1 ] && \
 timeout -k 10 200 python -u tools/exchange_loopback.py 8 16 32 64 > gpurun_out/${T}_loopback.log 2>&1 && \
 timeout -k 10 200 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 tools/dp_step_bench.py --gloo --no-time-steps > gpurun_out/${T}_dp_order.log 2>&1 && \
 timeout -k 10 200 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 tools/dp_step_bench.py --gloo > gpurun_out/${T}_dp.log 2>&1 && \

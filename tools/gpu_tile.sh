@@ -1,0 +1,11 @@
+# Sample-tile kernel bring-up: its tests first (bounded), then the whole GPU suite, then the
+# large-batch benches (B = 8192 fp16 on one GPU, B = 1024 = the per-rank batch at 8 GPUs).
+#   gpurun --timeout 900 -- bash tools/gpu_tile.sh [tag]
+T=${1:-r3t}
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out && \
+timeout -k 10 300 python -u -m pytest tests/test_tile_gpu.py -v -x --timeout 120 --timeout-method thread > gpurun_out/${T}_tile_tests.log 2>&1 && \
+timeout -k 10 200 python bench.py --global-batch 8192 --dtype fp16 --steps 40 --warmup 5 > gpurun_out/${T}_bench_lb.log 2>&1 && \
+timeout -k 10 200 python bench.py --global-batch 1024 --dtype fp16 --steps 200 --warmup 20 --no-epoch > gpurun_out/${T}_bench_1024.log 2>&1 && \
+timeout -k 10 500 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1
+echo rc=$?

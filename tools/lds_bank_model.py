@@ -73,9 +73,9 @@ def lanes():
 
 
 def kernel_order(name):
-    """A K-slice order table of the kernel (kDgOrder / kC2Order in lenet_fused.hip)."""
+    """A K-slice order table of the kernel (kDgOrder / kC2Order in lenet_images.h)."""
     src = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "csrc", "kernels",
-                            "lenet_fused.hip")).read()
+                            "lenet_images.h")).read()
     body = re.search(name + r" o\{\{([0-9,\s]+)\}", src).group(1)
     return [int(v) for v in body.replace("\n", " ").split(",")]
 
