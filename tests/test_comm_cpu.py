@@ -50,7 +50,7 @@ def test_exchange_buffer_layout():
     layout = [int(v) for v in torch.ops.csed.lenet_layout()]
     conv_pad, nparams, words = layout[1], layout[3], layout[5]
     assert nparams == 21840 and conv_pad == 5376 and layout[6] == 4  # split step: 4 workgroups / sample
-    assert len(layout) == 7
+    assert len(layout) == 9 and layout[7] == 4 and layout[8] == 1024  # sample tiles of 4 from batch 1024
     fc_tiles = 4 * 21 + 4  # fc1: 4 x 21 tiles of [dW1 | db1], fc2: 4 tiles of [dW2 | db2]
     assert words == conv_pad + fc_tiles * 256 == 27904
     assert words % 4 == 0  # the IPC buffers are allocated in multiples of 4 words
