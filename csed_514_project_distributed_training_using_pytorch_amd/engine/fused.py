@@ -75,11 +75,13 @@ def split_factor() -> int:
 
 def tile_samples() -> int:
     """Samples per tile of the sample-tile training kernel (csrc/kernels/lenet_tile.hip)."""
+    _native.require()
     return int(torch.ops.csed.lenet_layout()[7])
 
 
 def tile_min_batch() -> int:
     """Smallest per-rank batch the auto mode runs on the sample-tile kernel."""
+    _native.require()
     return int(torch.ops.csed.lenet_layout()[8])
 
 

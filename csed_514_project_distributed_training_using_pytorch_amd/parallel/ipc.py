@@ -257,6 +257,14 @@ def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
         if mode == "ipc":
             raise RuntimeError(f"CSED_ALLREDUCE=ipc but {LAST_NOTE}")
         return None
+    if shared > 1 and mode != "ipc":
+        # Ranks sharing a GPU (a rehearsal setup, never a real node): the auto mode keeps the
+        # process group's all-reduce as the fallback.  Its spinning kernel depends on how the
+        # GPU interleaves the processes' queues: tools/dp_step_bench.py --gloo still records one
+        # 2 s timed-out wait per run on one shared MI355X (profiles/dp_exchange_r3.md), which the
+        # fused exchange (one waiting point per step, inside lenet_update) does not show.
+        LAST_NOTE = f"ipc all-reduce off: {shared} ranks share one GPU (auto mode; CSED_ALLREDUCE=ipc forces it)"
+        return None
     ar, why = _open(ctx, n, blocks=32)
     ok = ar is not None
     if ok:

@@ -342,8 +342,7 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   a.std_ = (float)std_; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.rng_offset = optpt<int64_t>(rng_offset);
   a.grid = (int)grid; a.mfma_dtype = lcode(mfma_dtype); a.kernel = (int)kernel;
   if (a.mfma_dtype == csed::kF32)
-    TORCH_CHECK(grid <= 256 && !xstage.has_value() && !dbg.has_value(),
-                "lenet_train fp32: grid <= 256, no batch staging, no stage stamps");
+    TORCH_CHECK(grid <= 256 && !xstage.has_value(), "lenet_train fp32: grid <= 256, no batch staging");
   if (dbg.has_value()) {
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 32 * grid, "dbg: int64 [grid*32]");
     a.dbg = (uint64_t*)dbg->data_ptr<int64_t>();

@@ -58,7 +58,8 @@ constexpr int B_I1 = F_END * 4;               // u8  [1440] pool1 argmax
 constexpr int B_I2 = B_I1 + 1440;             // u8  [320]  pool2 argmax
 constexpr int B_XPOS = B_I2 + 320;            // u16 [1440] X offset of the pool1 argmax pixel
 constexpr int B_K2 = B_XPOS + 2880;           // u16 [256]  conv2 fwd: k -> P1 offset
-constexpr int LDS_BYTES = B_K2 + 512;
+constexpr int B_DBG = B_K2 + 512;             // u64 [16]   stage stamps (a.dbg, diagnostics)
+constexpr int LDS_BYTES = B_DBG + 16 * 8;
 static_assert(LDS_BYTES <= 160 * 1024, "lds");
 static_assert(F_W2 % 4 == 0 && F_W1B % 4 == 0 && F_PAR % 4 == 0 && F_X % 4 == 0 && F_P1 % 4 == 0 &&
                   F_P2 % 4 == 0 && F_DY2 % 4 == 0 && F_G1 % 4 == 0 && F_ONES % 4 == 0 && F_SM % 4 == 0 &&
@@ -101,6 +102,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   uint8_t* I2 = smem + B_I2;
   unsigned short* XPOS = reinterpret_cast<unsigned short*>(smem + B_XPOS);
   unsigned short* K2 = reinterpret_cast<unsigned short*>(smem + B_K2);
+  uint64_t* DBGS = reinterpret_cast<uint64_t*>(smem + B_DBG);
+  // Diagnostic stamps (a.dbg non-null): thread 0 records s_memtime at kernel entry (0), after the
+  // preamble (1), at stage k's start of the first sample (2 + k, k = 0..8), at its end (11) and at
+  // the kernel's end (12); copied to a.dbg[g * 32 ...] at the end (tools/stage_profile_f32.py).
+#define STAMP32(i)                                                          \
+  do {                                                                      \
+    if (a.dbg && tid == 0 && s == 0) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  if (a.dbg && threadIdx.x == 0) DBGS[0] = __builtin_amdgcn_s_memtime();
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -170,11 +180,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     rown = row_of(1);
   }
 
+  if (a.dbg && threadIdx.x == 0) DBGS[1] = __builtin_amdgcn_s_memtime();
   for (int s = 0; s < nsamp; ++s) {
     const int tid = opaque(threadIdx.x), lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
     const int b = g + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
     __syncthreads();  // previous sample's readers done (first pass: the preamble's writes)
+    STAMP32(2);
     // ---------------- stage 0: pixels, dropout masks; the next sample's loads
     if (tid < 196) {
 #pragma unroll
@@ -199,6 +211,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, XPOS
+    STAMP32(3);
     {
       float bv[7];
 #pragma unroll
@@ -233,6 +246,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
+    STAMP32(4);
     {
       const int tile = wave & 7, half = wave >> 3;  // K-steps [0, 32) / [32, 63)
       const int mt = tile & 3, nt = tile >> 2;
@@ -272,6 +286,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H (VALU, fixed-order combine)
+    STAMP32(5);
     {
       const int o = min(lane, 49), i0 = wave * 20;
       const float* wr = W1 + o * LW1 + i0;
@@ -295,6 +310,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 4: fc2, log_softmax, NLL, dlogits, dZ1 (wave 0)
+    STAMP32(6);
     if (wave == 0) {
       const int t = reinterpret_cast<const int*>(SM)[S_LAB];
       const float* Hs = SM + S_H;
@@ -373,6 +389,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 5: dP2 = dZ1 . W1 (VALU), pool2 / relu / Dropout2d backward -> DY2
+    STAMP32(7);
     {
       if (tid < 960) {
         const int i = tid % 320, part = tid / 320, o0 = 17 * part, o1 = min(o0 + 17, 50);
@@ -396,6 +413,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers; conv2 dgrad units
+    STAMP32(8);
     {
       // wgrad: N tile = wave (k = wave*16 + l16 = ic*25 + kh*5 + kw, 250 = ones, > 250 zeros),
       // M tiles oc 0-15 / 16-31, K = the 64 output pixels (pixel 4*ks + kq: row ks>>1,
@@ -450,6 +468,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 7: dgrad combine (fixed wave order), relu / pool1 gate -> G1
+    STAMP32(9);
     for (int idx = tid; idx < 1440; idx += NT) {
       const int ic = idx / 144, p = idx - 144 * ic, t = p >> 4, row = p & 15;
       const int e = (row & 3) * 64 + (row >> 2) * 16 + ic;
@@ -465,6 +484,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 8: conv1 wgrad over the argmax pixels (VALU) + bias
+    STAMP32(10);
     {
       if (tid < 1000) {
         const int j = tid % 250, part = tid / 250, oc = j / 25, tap = j - 25 * oc;
@@ -492,6 +512,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         acc_c1 += s0 + s1;
       }
     }
+    STAMP32(11);
   }
 
   // ---------------- epilogue: this workgroup's partial conv gradient + loss
@@ -515,6 +536,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     a.loss_acc[2 * g] = loss_sum;
     a.loss_acc[2 * g + 1] = correct;
   }
+  if (a.dbg) {
+    if (tid == 0) DBGS[12] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (tid < 16) a.dbg[g * 32 + tid] = DBGS[tid];
+  }
+#undef STAMP32
 }
 
 }  // namespace lenet32

@@ -117,15 +117,16 @@ def test_tile_training_epoch_matches_per_sample_and_converges():
     finals = []
     for kernel in (0, 1):
         torch.manual_seed(1)
-        eng = FusedLeNetTrainer(Net().to(DEV), train, lr=0.1, momentum=0.5, global_batch=1024)
+        eng = FusedLeNetTrainer(Net().to(DEV), train, lr=0.5, momentum=0.5, global_batch=1024)
         eng.train_kernel = kernel
         l0, _ = eng.evaluate(test)
         g = torch.Generator().manual_seed(0)
-        for _ in range(2):
+        for _ in range(3):
             eng.train_epoch(torch.randperm(n, generator=g), steps_per_graph=2)
         torch.cuda.synchronize()
         l1, c1 = eng.evaluate(test)
-        assert l1 < 0.8 * l0, (kernel, l0, l1)
-        finals.append(eng.flat.data.cpu().clone())
-    assert torch.isfinite(finals[0]).all()
-    assert _rel(finals[0], finals[1]) < 3e-2
+        assert l1 < 0.9 * l0, (kernel, l0, l1)  # 18 steps at batch 1024 (+ 3 tails)
+        finals.append((eng.flat.data.cpu().clone(), l1))
+    assert torch.isfinite(finals[0][0]).all()
+    assert _rel(finals[0][0], finals[1][0]) < 3e-2
+    assert abs(finals[0][1] - finals[1][1]) < 0.02 * finals[1][1]
