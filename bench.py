@@ -347,6 +347,11 @@ def main(argv=None) -> int:
             "epoch_s": round(epoch_s, 4) if epoch_s is not None else None,
             "baseline_epoch_s": base,
             "vs_baseline_time_elapsed": round(base / time_elapsed, 2) if base and time_elapsed else None,
+            "vs_baseline_epoch": round(base / epoch_s, 1) if base and epoch_s else None,
+            "vs_baseline_note": ("vs_baseline = warm timed-window images/s / the reference's images/s over its "
+                                 "whole 1-epoch run (process start to the epoch-0 print, incl. data loading and "
+                                 "validation); the like-for-like ratios are vs_baseline_time_elapsed (the same "
+                                 "cold whole-job span here) and vs_baseline_epoch (a warm epoch + validation)"),
             "train_loss_timed_rank0": round(loss_avg, 4) if loss_avg is not None else None,
         }
         if comm_retry:

@@ -162,21 +162,28 @@ class FusedLeNetTrainer:
         # pixels + labels one step ahead, so lenet_train starts with no dependent index chain
         # (the exact-fp32 kernel, lenet_fused_f32.hip, gathers its samples itself)
         self.fp32 = compute_dtype == torch.float32
-        self.staged = self.B <= stage_max and self.grid == self.B and not self.fp32
-        # split step (lenet_fused.hip KS > 1): split_k workgroups per sample share the backward
-        # conv stages; used whenever the whole grid fits one wave of the GPU (split_k * B <= 256
-        # CUs).  CSED_SPLIT=0 keeps one workgroup per sample.
+        # split step (lenet_fused.hip / lenet_fused_f32.hip KS > 1): split_k workgroups per sample
+        # share the backward conv stages; used whenever the whole grid fits one wave of the GPU
+        # (split_k * B <= 256 CUs).  CSED_SPLIT=0 keeps one workgroup per sample.  The exact-fp32
+        # kernel stages its batch only in the split step.
         split_k = split_factor()
         auto = os.environ.get("CSED_SPLIT", "auto").strip().lower() != "0"
-        self.split = (self.staged and grid is None and split_k * self.B <= 256
+        can_stage = self.B <= stage_max and self.grid == self.B
+        self.split = (can_stage and grid is None and split_k * self.B <= 256
                       and (auto if split is None else bool(split)))
+        self.staged = can_stage and (not self.fp32 or self.split)
         if self.split:
             self.grid = split_k * self.B
             self.slab = torch.empty((self._max_grid(), conv_params), dtype=torch.float32, device=dev)
             self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
         # one staging row per workgroup (split step: row r holds sample r % B)
-        self.xstage = torch.zeros((self.grid, 784), dtype=torch.uint8, device=dev) if self.staged else None
-        self.lstage = torch.zeros(self.grid, dtype=torch.long, device=dev) if self.staged else None
+        # the sample-tile kernel (16-bit, per-rank batch >= tile_min_batch()) stages the first tile
+        # of every workgroup instead: grid * tile_samples() rows (csrc/kernels/lenet_tile.hip)
+        self.tile_staged = (not self.fp32 and not self.staged and self.B >= tile_min_batch()
+                            and self.grid == tile_grid(self.B))
+        srows = self.grid if self.staged else (self.grid * tile_samples() if self.tile_staged else 0)
+        self.xstage = torch.zeros((srows, 784), dtype=torch.uint8, device=dev) if srows else None
+        self.lstage = torch.zeros(srows, dtype=torch.long, device=dev) if srows else None
         self.repack()
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._stepper: tuple | None = None  # (key, csed.LenetStepper), see stepper()
@@ -404,7 +411,7 @@ class FusedLeNetTrainer:
 
     def _stage_current(self) -> None:
         """Gather the batch at the cursor into the staging buffers (epoch start)."""
-        if self.staged:
+        if self.xstage is not None:
             torch.ops.csed.lenet_stage(self.train_data.images, self.train_data.labels, self.perm, self.cursor,
                                        self.B, self.xstage, self.lstage)
 
@@ -431,11 +438,12 @@ class FusedLeNetTrainer:
                      perm: torch.Tensor) -> None:
         ops = torch.ops.csed
         # full steps read the staged batch and stage the next one; the epoch's short tail uses perm
-        st = self.staged and cursor is not None
+        kern = self.kernel_for(B, grid)
+        st = self._stages(kern) and cursor is not None
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
                         self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
                         self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,
-                        self.xstage if st else None, self.lstage if st else None, st, self.kernel_for(B, grid))
+                        self.xstage if st else None, self.lstage if st else None, st, kern)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
         if self.exch is not None:
@@ -453,6 +461,13 @@ class FusedLeNetTrainer:
         else:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
                              self.loss_parts, grid, self.loss_acc, self.mfma)
+
+    def _stages(self, kernel: int) -> bool:
+        """Whether a full step launched with ``kernel`` (kernel_for) reads / writes the staging
+        buffers: the per-sample kernel's (one row per workgroup) or the tile kernel's (first tiles)."""
+        if self.staged:
+            return kernel != 2
+        return self.tile_staged and kernel != 1
 
     def kernel_for(self, B: int, grid: int) -> int:
         """``train_kernel`` for a launch of per-rank batch B on ``grid`` workgroups: the tile kernel
@@ -473,8 +488,8 @@ class FusedLeNetTrainer:
         ops.lenet_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B, self.ctx.rank,
                         self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts, 1.0 / self.global_batch,
                         MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg,
-                        self.xstage if self.staged and grid == self.grid else None,
-                        self.lstage if self.staged and grid == self.grid else None, False,
+                        self.xstage if self._stages(self.kernel_for(self.B, grid)) and grid == self.grid else None,
+                        self.lstage if self._stages(self.kernel_for(self.B, grid)) and grid == self.grid else None, False,
                         self.kernel_for(self.B, grid))
         ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
@@ -512,7 +527,7 @@ class FusedLeNetTrainer:
     def _state(self) -> list[torch.Tensor]:
         """Device tensors a training step advances."""
         return [self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor, self.rng_offset,
-                self.loss_acc] + ([self.xstage, self.lstage] if self.staged else [])
+                self.loss_acc] + ([self.xstage, self.lstage] if self.xstage is not None else [])
 
     def _capture(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph:
         step = self._tail_step if tail else self.step
@@ -587,14 +602,15 @@ class FusedLeNetTrainer:
         if self.comm and self.exch is None:
             return None
         exch_id = -1 if self.exch is None else self.exch.id
-        key = (self.perm.data_ptr(), exch_id, self.staged)
+        key = (self.perm.data_ptr(), exch_id, self.staged, self.train_kernel)
+        st_ok = self._stages(self.kernel_for(self.B, self.grid))
         if self._stepper is None or self._stepper[0] != key:
             st = torch.classes.csed.LenetStepper()
             st.set_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B,
                          self.ctx.rank, self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts,
                          self.grad_scale, MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset,
-                         self.grid, self.mfma, self.xstage if self.staged else None,
-                         self.lstage if self.staged else None, self.staged, self.kernel_for(self.B, self.grid))
+                         self.grid, self.mfma, self.xstage if st_ok else None,
+                         self.lstage if st_ok else None, st_ok, self.kernel_for(self.B, self.grid))
             st.set_update(self.slab, self.grid, self.vslab, self.B, self.flat.data, self.momentum_buf, self.wimg,
                           self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                           self.step_count, self.ticket, self.cursor, self.rng_offset, self.loss_parts, self.grid,

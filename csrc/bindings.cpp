@@ -324,11 +324,13 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   TORCH_CHECK(grid >= 1 && (grid <= B || (xstage.has_value() && grid == csed::lenet_split_k() * B)) && grid <= 1024,
               "lenet_train: 1 <= grid <= B (or split_k * B for a staged batch)");
   TORCH_CHECK(kernel >= 0 && kernel <= 2, "lenet_train: kernel 0 (auto), 1 (per sample) or 2 (sample tiles)");
-  const bool tile = mfma_dtype != csed::kF32 && !xstage.has_value() &&
-                    (kernel == 2 || (kernel == 0 && B >= csed::kLenetTileMinB));
+  const bool tile = mfma_dtype != csed::kF32 && (kernel == 2 || (kernel == 0 && B >= csed::kLenetTileMinB));
   if (tile)
-    TORCH_CHECK(grid == csed::lenet_tile_grid((int)B) && !dbg.has_value(),
-                "lenet_train: the sample-tile kernel runs grid ", csed::lenet_tile_grid((int)B), " (no stage stamps)");
+    TORCH_CHECK(grid == csed::lenet_tile_grid((int)B), "lenet_train: the sample-tile kernel runs grid ",
+                csed::lenet_tile_grid((int)B));
+  // staging rows: the tile kernel stages every workgroup's first tile, the per-sample kernel one
+  // sample per workgroup
+  const int64_t srows = tile ? grid * csed::lenet_tile_samples() : grid;
   TORCH_CHECK(slab.numel() >= grid * csed::lenet_conv_param_count() && loss_parts.numel() >= 2 * grid,
               "lenet_train: slab [grid, 5280] / loss_parts [grid, 2] too small");
   TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_train: vslab [B, 464] too small");
@@ -342,21 +344,24 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   a.std_ = (float)std_; a.drop_p = (float)drop_p; a.seed = (uint64_t)seed; a.rng_offset = optpt<int64_t>(rng_offset);
   a.grid = (int)grid; a.mfma_dtype = lcode(mfma_dtype); a.kernel = (int)kernel;
   if (a.mfma_dtype == csed::kF32)
-    TORCH_CHECK(grid <= 256 && !xstage.has_value(), "lenet_train fp32: grid <= 256, no batch staging");
+    TORCH_CHECK(grid <= 256 && (!xstage.has_value() || grid == csed::lenet_split_k() * B),
+                "lenet_train fp32: grid <= 256; a staged batch runs the split step (grid = split_k * B)");
   if (dbg.has_value()) {
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 32 * grid, "dbg: int64 [grid*32]");
     a.dbg = (uint64_t*)dbg->data_ptr<int64_t>();
   }
   TORCH_CHECK(xstage.has_value() == lstage.has_value(), "lenet_train: xstage and lstage go together");
   if (xstage.has_value()) {
-    TORCH_CHECK(xstage->scalar_type() == at::kByte && xstage->numel() >= grid * 784 && lstage->scalar_type() == at::kLong &&
-                    lstage->numel() >= grid && xstage->is_contiguous() && lstage->is_contiguous(),
-                "lenet_train: staged batch must be uint8 [grid, 784] + int64 [grid] (one row per workgroup)");
+    TORCH_CHECK(xstage->scalar_type() == at::kByte && xstage->numel() >= srows * 784 && lstage->scalar_type() == at::kLong &&
+                    lstage->numel() >= srows && xstage->is_contiguous() && lstage->is_contiguous(),
+                "lenet_train: staged batch must be uint8 [rows, 784] + int64 [rows] (rows: one per workgroup; "
+                "the sample-tile kernel: one per sample of every workgroup's first tile)");
+    TORCH_CHECK(tile || grid == B || grid == csed::lenet_split_k() * B,
+                "lenet_train: the per-sample kernel stages one sample per workgroup (grid == B or split_k * B)");
     a.xstage = xstage->data_ptr<uint8_t>();
     a.lstage = lstage->data_ptr<int64_t>();
     if (stage_next) {
-      TORCH_CHECK(cursor.has_value() && (grid == B || grid == csed::lenet_split_k() * B),
-                  "lenet_train: stage_next needs the cursor and one staging row per workgroup");
+      TORCH_CHECK(cursor.has_value(), "lenet_train: stage_next needs the cursor");
       a.stage_next = 1;
     }
   }
@@ -379,13 +384,13 @@ void lenet_train(const Tensor& images, const Tensor& labels, const Tensor& perm,
 
 csed::LenetStageArgs stage_args(const Tensor& images, const Tensor& labels, const Tensor& perm, int64_t B,
                                 const Tensor& xstage, const Tensor& lstage) {
-  TORCH_CHECK(B >= 1 && B <= csed::lenet_stage_max_batch(), "staged batch must be 1..", csed::lenet_stage_max_batch());
+  TORCH_CHECK(B >= 1, "staging: batch must be positive");
   TORCH_CHECK(images.scalar_type() == at::kByte && images.is_contiguous() && labels.scalar_type() == at::kLong &&
                   perm.scalar_type() == at::kLong && perm.numel() >= 1,
               "staging: images uint8 [N,28,28], labels / perm int64");
-  TORCH_CHECK(xstage.scalar_type() == at::kByte && xstage.numel() >= B * 784 && xstage.is_contiguous() &&
-                  lstage.scalar_type() == at::kLong && lstage.numel() >= B && lstage.is_contiguous(),
-              "staging: xstage uint8 [B, 784], lstage int64 [B]");
+  TORCH_CHECK(xstage.scalar_type() == at::kByte && xstage.is_contiguous() && lstage.scalar_type() == at::kLong &&
+                  lstage.is_contiguous(),
+              "staging: xstage uint8 [rows, 784], lstage int64 [rows]");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(images.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(xstage.data_ptr()) % 16 == 0, "staging: 16-byte aligned buffers");
   csed::LenetStageArgs st{};
@@ -394,8 +399,8 @@ csed::LenetStageArgs stage_args(const Tensor& images, const Tensor& labels, cons
   st.xstage = xstage.data_ptr<uint8_t>(); st.lstage = lstage.data_ptr<int64_t>();
   // one staging row per workgroup: B, or split_k * B for the split step (row r = sample r % B)
   st.rows = (int)lstage.numel();
-  TORCH_CHECK(st.rows >= B && st.rows <= csed::lenet_stage_max_batch() && xstage.numel() >= (int64_t)st.rows * 784,
-              "staging: lstage rows must be B..", csed::lenet_stage_max_batch(), " with xstage [rows, 784]");
+  TORCH_CHECK(st.rows >= 1 && st.rows <= csed::lenet_stage_max_batch() && xstage.numel() >= (int64_t)st.rows * 784,
+              "staging: 1..", csed::lenet_stage_max_batch(), " rows (lstage) with xstage [rows, 784]");
   return st;
 }
 

@@ -1249,12 +1249,12 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
 // mid-kernel, stored at its end); this kernel fills the buffer at epoch start.
 // One block; every thread issues all of its loads before its first store.
 // ---------------------------------------------------------------------------
-constexpr int STAGE_MAXB = 512;
+constexpr int STAGE_MAXB = 1024;  // staging rows (the tile kernel: 256 workgroups x 4 samples)
 constexpr int IMG_U4 = 784 / 16;  // 49 16-byte chunks per image
 
 __device__ __forceinline__ void gather_batch(const LenetStageArgs& st, int64_t step, int64_t* rows_sh) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const int nrows = st.rows > 0 ? st.rows : st.B;  // staging row r holds sample r % B (split step)
+  const int nrows = st.rows;  // staging row r holds sample r % B (split step: 4 rows per sample)
   for (int b = tid; b < nrows; b += nt) {
     const int64_t row = st.perm[min(step * st.B + b % st.B, st.perm_len - 1)];
     rows_sh[b] = row;
@@ -1786,14 +1786,17 @@ int64_t lenet_conv_param_count() { return CNP_PAD; }
 int64_t lenet_vec_len() { return VEC; }
 
 // the sample-tile kernel (lenet_tile.hip) for this launch?  kernel: 0 auto, 1 no, 2 yes
-static bool use_tile(int kernel, int B, int mfma_dtype, bool staged) {
-  if (mfma_dtype == kF32 || staged || kernel == 1) return false;
+// (a staged batch: the tile kernel's staging holds the first tile of every workgroup, rows
+// grid * lenet_tile_samples(); the per-sample kernel's one row per workgroup with grid == B or
+// split_k * B -- the kernel choice decides which, see csrc/bindings.cpp train_args)
+static bool use_tile(int kernel, int B, int mfma_dtype) {
+  if (mfma_dtype == kF32 || kernel == 1) return false;
   return kernel == 2 || B >= kLenetTileMinB;
 }
 
 hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   if (a.mfma_dtype == kF32) return launch_lenet_train_f32(a, 0, nullptr, true, s);  // lenet_fused_f32.hip
-  if (use_tile(a.kernel, a.B, a.mfma_dtype, a.xstage != nullptr)) return launch_lenet_tile(a, 0, nullptr, true, s);
+  if (use_tile(a.kernel, a.B, a.mfma_dtype)) return launch_lenet_tile(a, 0, nullptr, true, s);
   // split step: a staged batch with SPLIT_K workgroups (parts) per sample, one staging row each
   const bool split = a.xstage && a.lstage && a.grid == SPLIT_K * a.B && a.grid <= 256;
   if (a.B <= 0 || a.grid <= 0 || (a.grid > a.B && !split)) return hipErrorInvalidValue;
@@ -1864,7 +1867,8 @@ int lenet_stage_max_batch() { return STAGE_MAXB; }
 int lenet_split_k() { return SPLIT_K; }
 
 hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hipStream_t s) {
-  if (a.B <= 0 || a.B > STAGE_MAXB || a.rows > STAGE_MAXB || !a.xstage || !a.lstage) return hipErrorInvalidValue;
+  // rows: the staging rows (row r = sample r % B of the step); any batch size
+  if (a.B <= 0 || a.rows <= 0 || a.rows > STAGE_MAXB || !a.xstage || !a.lstage) return hipErrorInvalidValue;
   hipLaunchKernelGGL(lenet_stage_kernel, dim3(1), dim3(512), 0, s, a, cursor);
   return hipGetLastError();
 }
@@ -1892,7 +1896,7 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   a.grad_scale = 0.f; a.mean = mean; a.std_ = std_; a.drop_p = 0.f; a.seed = 0; a.rng_offset = nullptr;
   a.grid = (int)std::min<int64_t>(n, 256); a.mfma_dtype = mfma_dtype;
   if (mfma_dtype == kF32) return launch_lenet_train_f32(a, logp_out ? 1 : 0, logp_out, false, s);
-  if (use_tile(kernel, a.B, mfma_dtype, false)) {
+  if (use_tile(kernel, a.B, mfma_dtype)) {
     a.grid = lenet_tile_grid(a.B);  // == min(n, 256) for every n the auto mode sends here
     return launch_lenet_tile(a, logp_out ? 1 : 0, logp_out, false, s);
   }

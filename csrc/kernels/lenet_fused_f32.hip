@@ -83,8 +83,16 @@ __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
 // units [unit_lo(w), unit_lo(w + 1)): at most 3 units spanning at most 2 tiles
 __host__ __device__ constexpr int unit_lo(int w) { return (w * 45) / NW; }
 
-template <bool TRAIN>
+// KS > 1 (split step, staged batches: a.xstage holds one row per workgroup, grid = KS * B):
+// workgroup g is part g / B of sample g % B.  Every part runs the forward (the sample's dependency
+// chain) and dP2; the backward conv stages are divided: part j owns conv2 wgrad N-tiles 4j .. 4j+3
+// (waves 0-3) and the dgrad M-tiles {j, j+4, j+8} (5 units each over waves 4-15), and its conv1
+// wgrad covers those tiles' pool1 pixels.  Part 0 alone writes the fc vectors and the loss; every
+// part stages its row of the next step (as the 16-bit split step, lenet_fused.hip).
+template <bool TRAIN, int KS = 1>
 __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
+  static_assert(KS == 1 || (KS == SPLIT_K && TRAIN), "split step: training only");
+  constexpr bool STAGED = KS > 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* L = reinterpret_cast<float*>(smem);
   float* W1 = L + F_W1;
@@ -116,10 +124,17 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, kq = lane >> 4;
   const int G = gridDim.x, g = blockIdx.x;
+  const int b0 = STAGED ? g % a.B : g, part = STAGED ? g / a.B : 0;
+  const bool own = part == 0;      // writes the sample's fc vectors and loss
+  const int R2 = STAGED ? a.B : G; // slab rows of the conv2 chunks (one per sample in the split step)
   const float inv_std = 1.f / a.std_;
   const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
-  const int nsamp = g < a.B ? (a.B - g + G - 1) / G : 0;
+  const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
   const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
+  const bool stage_next = STAGED && a.stage_next;
+  // this part's dgrad M-tiles: {part, part + 4, part + 8 (part 0)}; all 9 without the split
+  const int ntl = STAGED ? (part == 0 ? 3 : 2) : 9;
+  auto tile_of = [&](int ti) { return STAGED ? part + 4 * ti : ti; };
   auto row_of = [&](int s) { return a.perm[min(pbase + (int64_t)min(s, max(nsamp - 1, 0)) * G, a.perm_len - 1)]; };
 
   // ---------------- once per workgroup: fp32 parameters -> LDS, constant tables
@@ -170,10 +185,16 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   float loss_sum = 0.f, correct = 0.f;
 
   // sample pipeline: pixels (4 per thread) and label of sample s, row of sample s+1
-  uint32_t px = 0;
+  uint32_t px = 0, px_next = 0;
   int lab = 0;
-  int64_t rown = 0;
-  if (nsamp > 0) {
+  int64_t rown = 0, lab_next = 0;
+  if (STAGED) {
+    // the staged batch (row g of the staging buffer); the next step's row for the staging of
+    // step cursor + 1 (loaded here, its pixels at stage 3, stored at the end)
+    px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(tid, 195)];
+    lab = (int)a.lstage[g];
+    if (stage_next) rown = a.perm[min((a.cursor[0] + 1) * (int64_t)a.B + b0, a.perm_len - 1)];
+  } else if (nsamp > 0) {
     const int64_t r0 = row_of(0);
     px = reinterpret_cast<const uint32_t*>(a.images + r0 * 784)[min(tid, 195)];
     lab = (int)a.labels[r0];
@@ -183,8 +204,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   if (a.dbg && threadIdx.x == 0) DBGS[1] = __builtin_amdgcn_s_memtime();
   for (int s = 0; s < nsamp; ++s) {
     const int tid = opaque(threadIdx.x), lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
-    const int b = g + s * G;
+    const int b = b0 + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
+    const bool wvec = TRAIN && own;
     __syncthreads();  // previous sample's readers done (first pass: the preamble's writes)
     STAMP32(2);
     // ---------------- stage 0: pixels, dropout masks; the next sample's loads
@@ -203,7 +225,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       if (tid < 20) SM[S_D2S + tid] = sc;
       else SM[S_D1S + tid - 20] = sc;
     }
-    if (s + 1 < nsamp) {
+    if (!STAGED && s + 1 < nsamp) {
       px = reinterpret_cast<const uint32_t*>(a.images + rown * 784)[min(tid, 195)];
       lab = (int)a.labels[rown];
       rown = row_of(s + 2);
@@ -279,7 +301,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
           const float v = fmaxf(best + PAR[P_C2B + oc], 0.f) * SM[S_D2S + oc];
           P2[oc * 16 + wp] = v;
           I2[oc * 16 + wp] = (uint8_t)bi;
-          if (TRAIN) vs[V_P2 + oc * 16 + wp] = v;
+          if (wvec) vs[V_P2 + oc * 16 + wp] = v;
         }
       }
     }
@@ -287,6 +309,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H (VALU, fixed-order combine)
     STAMP32(5);
+    if (stage_next && wave >= 12) {  // the next step's pixels + label of this staging row
+      px_next = reinterpret_cast<const uint32_t*>(a.images + rown * 784)[min(tid - 768, 195)];
+      lab_next = a.labels[rown];
+    }
     {
       const int o = min(lane, 49), i0 = wave * 20;
       const float* wr = W1 + o * LW1 + i0;
@@ -304,7 +330,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         for (int sg = 0; sg < NW; ++sg) z += RED[sg * 64 + tid];
         const float h = fmaxf(z + PAR[P_F1B + tid], 0.f) * SM[S_D1S + tid];
         SM[S_H + tid] = h;
-        if (TRAIN) vs[V_H + tid] = h;
+        if (wvec) vs[V_H + tid] = h;
       }
     }
     __syncthreads();
@@ -353,7 +379,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         lt = c == t ? lg[c] : lt;
       }
       const float lse = mx + __logf(se);
-      if (lane == 0) {
+      if (lane == 0 && own) {
         loss_sum += lse - lt;
         correct += (amax == t) ? 1.f : 0.f;
       }
@@ -368,7 +394,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         float dl[10];
 #pragma unroll
         for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
-        if (lane < 16) {
+        if (wvec && lane < 16) {
           float mine = 0.f;
 #pragma unroll
           for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
@@ -382,7 +408,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         }
         const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
         SM[S_DZ1 + lane] = dz;
-        if (lane < 50) vs[V_DZ1 + lane] = dz;
+        if (wvec && lane < 50) vs[V_DZ1 + lane] = dz;
       }
     }
     if (!TRAIN) continue;
@@ -413,12 +439,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();
 
     // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers; conv2 dgrad units
+    // (split step: this part's 4 wgrad N-tiles on waves 0-3, its dgrad units on waves 4-15)
     STAMP32(8);
-    {
-      // wgrad: N tile = wave (k = wave*16 + l16 = ic*25 + kh*5 + kw, 250 = ones, > 250 zeros),
+    if (!STAGED || wave < 4) {
+      // wgrad: N tile nt (k = nt*16 + l16 = ic*25 + kh*5 + kw, 250 = ones, > 250 zeros),
       // M tiles oc 0-15 / 16-31, K = the 64 output pixels (pixel 4*ks + kq: row ks>>1,
       // column 4*(ks&1) + kq -> P1 offset (ks>>1)*12 + 4*(ks&1) + kq from the tap's base)
-      const int k = wave * 16 + l16;
+      const int k = (STAGED ? 4 * part + wave : wave) * 16 + l16;
       const float* bsrc;
       if (k < 250) {
         const int ic = k / 25, r = k - 25 * ic;
@@ -435,79 +462,99 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         acc_c2[1] = mma(arow1[4 * ks], bv, acc_c2[1]);
       }
     }
-    {
+    // dgrad units (this part's M-tile ti < ntl, oc block j < 5): wave wd of NWD owns units
+    // [ulo(wd), ulo(wd + 1)) -- at most 2 units, at most 2 M-tiles
+    constexpr int NWD = STAGED ? NW - 4 : NW;
+    const int nu = 5 * ntl;
+    auto ulo = [&](int w) { return (w * nu) / NWD; };
+    const int wd = STAGED ? wave - 4 : wave;
+    if (wd >= 0) {
       // dgrad: dP1[ic][y*12 + x] = sum_{oc, kh, kw} DY2[oc][(y-kh)*8 + x-kw] W2[oc][ic][kh][kw];
       // unit (tile t, j): rows p = 16t + l16, oc = 4j + kq, the 25 taps
-      const int u0 = unit_lo(wave), u1 = unit_lo(wave + 1), t0 = u0 / 5;
+      const int u0 = ulo(wd), u1 = ulo(wd + 1), t0 = u0 / 5;
       f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
       const float* bcol = W2 + kq * LW2 + min(l16, 9) * 25;  // columns >= 10: discarded outputs
+      const float* ZR = L + F_ZEROS;  // >= 37 zeros
       for (int u = u0; u < u1; ++u) {  // wave-uniform
-        const int t = u / 5, j = u - 5 * t;
+        const int ti = u / 5, j = u - 5 * ti, t = tile_of(ti);
         const int p = t * 16 + l16, y = p / 12, x = p - 12 * (p / 12);
-        const float* arow = DY2 + (4 * j + kq) * 64 + y * 8 + x;  // minus kh*8 + kw per tap
+        const float* arow = DY2 + (4 * j + kq) * 64 + y * 8 + x - 36;  // tap (kh, kw): [36 - kh*8 - kw]
         const float* brow = bcol + 4 * j * LW2;
+        // taps with 0 <= y - kh < 8 and 0 <= x - kw < 8, as a 25-bit mask (bit kh*5 + kw): per tap
+        // one bit test selects the row pointer or the zero run, and the load keeps an immediate
+        // offset
+        const uint32_t rb = ((2u << min(4, y)) - 1u) & ~((1u << max(0, y - 7)) - 1u);
+        const uint32_t cb = ((2u << min(4, x)) - 1u) & ~((1u << max(0, x - 7)) - 1u);
+        uint32_t m = 0;
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh) m |= ((rb >> kh) & 1u) ? (cb << (5 * kh)) : 0u;
         f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kh = 0; kh < 5; ++kh) {
 #pragma unroll
           for (int kw = 0; kw < 5; ++kw) {
-            const bool ok = (unsigned)(y - kh) < 8u && (unsigned)(x - kw) < 8u;
-            const float av = ok ? arow[-(kh * 8 + kw)] : 0.f;
-            c = mma(av, brow[kh * 5 + kw], c);
+            const float* ap = (m & (1u << (kh * 5 + kw))) ? arow : ZR;
+            c = mma(ap[36 - (kh * 8 + kw)], brow[kh * 5 + kw], c);
           }
         }
-        if (t == t0) acc0 += c;
+        if (ti == t0) acc0 += c;
         else acc1 += c;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        RED[(wave * 2) * 256 + r * 64 + lane] = acc0[r];
-        RED[(wave * 2 + 1) * 256 + r * 64 + lane] = acc1[r];
+        RED[(wd * 2) * 256 + r * 64 + lane] = acc0[r];
+        RED[(wd * 2 + 1) * 256 + r * 64 + lane] = acc1[r];
       }
     }
     __syncthreads();
 
     // ---------------- stage 7: dgrad combine (fixed wave order), relu / pool1 gate -> G1
+    // (this part's M-tiles only; conv1 wgrad reads only their pixels)
     STAMP32(9);
-    for (int idx = tid; idx < 1440; idx += NT) {
-      const int ic = idx / 144, p = idx - 144 * ic, t = p >> 4, row = p & 15;
+    for (int idx = tid; idx < 160 * ntl; idx += NT) {
+      const int ic = idx / (16 * ntl), rem = idx - 16 * ntl * ic, ti = rem >> 4, row = rem & 15;
+      const int pp = ic * 144 + tile_of(ti) * 16 + row;
       const int e = (row & 3) * 64 + (row >> 2) * 16 + ic;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const int lo = unit_lo(w), hi = unit_lo(w + 1), tw = lo / 5;
-        if (tw == t && lo < hi) v += RED[(w * 2) * 256 + e];
-        else if (tw + 1 == t && (hi - 1) / 5 == t) v += RED[(w * 2 + 1) * 256 + e];
+      for (int w = 0; w < NWD; ++w) {
+        const int lo = ulo(w), hi = ulo(w + 1), tw = lo / 5;
+        if (tw == ti && lo < hi) v += RED[(w * 2) * 256 + e];
+        else if (tw + 1 == ti && (hi - 1) / 5 == ti) v += RED[(w * 2 + 1) * 256 + e];
       }
-      G1[idx] = P1[idx] > 0.f ? v : 0.f;
+      G1[pp] = P1[pp] > 0.f ? v : 0.f;
     }
     __syncthreads();
 
     // ---------------- stage 8: conv1 wgrad over the argmax pixels (VALU) + bias
     STAMP32(10);
     {
+      // this part's pool1 pixels: list index i -> pixel tile_of(i >> 4) * 16 + (i & 15); four
+      // quarters of the list per (oc, tap)
+      const int npx = 16 * ntl, nq = npx / 4;
+      auto px_at = [&](int i) { return tile_of(i >> 4) * 16 + (i & 15); };
       if (tid < 1000) {
-        const int j = tid % 250, part = tid / 250, oc = j / 25, tap = j - 25 * oc;
+        const int j = tid % 250, q4 = tid / 250, oc = j / 25, tap = j - 25 * oc;
         const int koff = (tap / 5) * 28 + (tap % 5);
-        const float* gr = G1 + oc * 144 + 36 * part;
-        const unsigned short* xr = XPOS + oc * 144 + 36 * part;
+        const float* gr = G1 + oc * 144;
+        const unsigned short* xr = XPOS + oc * 144;
         float s0 = 0.f, s1 = 0.f;
-#pragma unroll 6
-        for (int p = 0; p < 36; p += 2) {
-          s0 = fmaf(gr[p], X[xr[p] + koff], s0);
-          s1 = fmaf(gr[p + 1], X[xr[p + 1] + koff], s1);
+        for (int i = q4 * nq; i < (q4 + 1) * nq; i += 2) {
+          const int p0 = px_at(i), p1 = px_at(i + 1);
+          s0 = fmaf(gr[p0], X[xr[p0] + koff], s0);
+          s1 = fmaf(gr[p1], X[xr[p1] + koff], s1);
         }
-        RED[part * 256 + j] = s0 + s1;
+        RED[q4 * 256 + j] = s0 + s1;
       }
       __syncthreads();
       if (tid < 250) {
         acc_c1 += (RED[tid] + RED[256 + tid]) + (RED[512 + tid] + RED[768 + tid]);
-      } else if (tid >= 256 && tid < 266) {  // conv1.b: sum over the 144 gated pooled pixels
+      } else if (tid >= 256 && tid < 266) {  // conv1.b: sum over the gated pooled pixels
         const float* gr = G1 + (tid - 256) * 144;
         float s0 = 0.f, s1 = 0.f;
-        for (int p = 0; p < 144; p += 2) {
-          s0 += gr[p];
-          s1 += gr[p + 1];
+        for (int i = 0; i < npx; i += 2) {
+          s0 += gr[px_at(i)];
+          s1 += gr[px_at(i + 1)];
         }
         acc_c1 += s0 + s1;
       }
@@ -517,24 +564,33 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
 
   // ---------------- epilogue: this workgroup's partial conv gradient + loss
   if (TRAIN) {
-    auto slab_at = [&](int e) { return a.slab + slab_off(slab_slot(e), g, G, G); };  // grid <= B: R2 = G
-    if (tid < 250) *slab_at(O_C1W + tid) = acc_c1;
-    else if (tid >= 256 && tid < 266) *slab_at(O_C1B + tid - 256) = acc_c1;
-    const int k = wave * 16 + l16;
+    // conv1: one slab row per workgroup; conv2: one row per sample (the split step's parts own
+    // disjoint columns of it: N-tiles 4 * part .. + 3, on waves 0-3)
+    auto slab1 = [&](int e) { return a.slab + slab_off(slab_slot(e), g, G, R2); };
+    auto slab2 = [&](int e) { return a.slab + slab_off(slab_slot(e), b0, G, R2); };
+    if (tid < 250) *slab1(O_C1W + tid) = acc_c1;
+    else if (tid >= 256 && tid < 266) *slab1(O_C1B + tid - 256) = acc_c1;
+    if (!STAGED || wave < 4) {
+      const int k = (STAGED ? 4 * part + wave : wave) * 16 + l16;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int oc = mt * 16 + 4 * kq + r;
-        if (oc < 20) {
-          if (k < 250) *slab_at(O_C2W + oc * 250 + k) = acc_c2[mt][r];
-          else if (k == 250) *slab_at(O_C2B + oc) = acc_c2[mt][r];
+        for (int r = 0; r < 4; ++r) {
+          const int oc = mt * 16 + 4 * kq + r;
+          if (oc < 20) {
+            if (k < 250) *slab2(O_C2W + oc * 250 + k) = acc_c2[mt][r];
+            else if (k == 250) *slab2(O_C2B + oc) = acc_c2[mt][r];
+          }
         }
-      }
+    }
+    if (stage_next) {  // this workgroup's staging row for step cursor + 1 (it read row g above)
+      if (tid >= 768 && tid - 768 < 196) reinterpret_cast<uint32_t*>(a.xstage + (int64_t)g * 784)[tid - 768] = px_next;
+      if (tid == 768) a.lstage[g] = lab_next;
+    }
   }
-  if (tid == 0) {
-    a.loss_acc[2 * g] = loss_sum;
-    a.loss_acc[2 * g + 1] = correct;
+  if (tid == 0) {  // (split step: part 0 reports the sample)
+    a.loss_acc[2 * g] = own ? loss_sum : 0.f;
+    a.loss_acc[2 * g + 1] = own ? correct : 0.f;
   }
   if (a.dbg) {
     if (tid == 0) DBGS[12] = __builtin_amdgcn_s_memtime();
@@ -549,8 +605,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
 hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float* logp_out, bool train,
                                   hipStream_t s) {
   using namespace lenet32;
-  if (a.B <= 0 || a.grid <= 0 || a.grid > a.B || a.grid > 256 || a.xstage) return hipErrorInvalidValue;
-  if (train) {
+  // split step: a staged batch with SPLIT_K workgroups (parts) per sample, one staging row each
+  const bool split = train && a.xstage && a.lstage && a.grid == SPLIT_K * a.B && a.grid <= 256;
+  if (a.B <= 0 || a.grid <= 0 || a.grid > 256 || (a.xstage && !split) || (!split && a.grid > a.B))
+    return hipErrorInvalidValue;
+  if (split) {
+    allow_dynamic_lds<lenet_train_f32_kernel<true, SPLIT_K>>(LDS_BYTES);
+    hipLaunchKernelGGL((lenet_train_f32_kernel<true, SPLIT_K>), dim3(a.grid), dim3(NT), LDS_BYTES, s, a, 0,
+                       (float*)nullptr);
+  } else if (train) {
     allow_dynamic_lds<lenet_train_f32_kernel<true>>(LDS_BYTES);
     hipLaunchKernelGGL(lenet_train_f32_kernel<true>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, 0, (float*)nullptr);
   } else {

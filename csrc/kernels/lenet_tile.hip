@@ -62,9 +62,10 @@ constexpr int F_D2S = 0, F_D1S = TS * 20, F_H = F_D1S + TS * 52, F_LAB = F_H + T
 constexpr int D_W1C = 0;                        // u16 [16][32] conv1 B operand
 constexpr int D_PAR = D_W1C + 16 * 32 * 2;      // f32 [592]: c1b 0, c2b 10, f1b 30, f2b 80, f2w 90
 constexpr int D_COFF = D_PAR + 592 * 4;         // i16 [4][16] conv2 (lane group, K-step) -> P1H offset
-constexpr int D_DGT = D_COFF + 64 * 2;          // u8 [4][24] dgrad (lane group, K-step) -> ty | tx << 3 | ocg << 6
-constexpr int D_ZERO = D_DGT + 96;              // 32 B of zeros (out-of-image dgrad fragments)
-constexpr int D_X = D_ZERO + 32;                // u16 [TS][X_LD] normalised pixels
+constexpr int D_DGT = D_COFF + 64 * 2;          // i32 [4][20] dgrad (lane group, K-step) -> rel | tap << 16
+constexpr int D_ONES = D_DGT + 4 * 20 * 4;      // u16 [192] 1.0: the wgrads' bias columns
+constexpr int D_ZERO = D_ONES + 192 * 2;        // u16 [192] 0: padding columns, out-of-image dgrad taps
+constexpr int D_X = D_ZERO + 192 * 2;           // u16 [TS][X_LD] normalised pixels
 constexpr int D_P1H = D_X + TS * X_LD * 2;      // u16 [TS][P1H_SZ]
 constexpr int D_I1 = D_P1H + TS * P1H_SZ * 2;   // u8  [TS][10][144] pool1 argmax
 constexpr int D_P2 = D_I1 + TS * 1440;          // u16 [TS][320] fc1 input
@@ -73,16 +74,20 @@ constexpr int D_F = D_I2 + TS * 320;            // f32 [F_END] masks, fc1 output
 constexpr int D_DZ1B = D_F + F_END * 4;         // u16 [TS][64] dZ1 (dP2's A rows)
 constexpr int D_DC2 = D_DZ1B + TS * 64 * 2;     // u16 [TS][DC2_SZ]
 constexpr int D_DCH = D_DC2 + TS * DC2_SZ * 2;  // u16 [TS][DCH_SZ]
-constexpr int D_G1 = D_DCH + TS * DCH_SZ * 2;   // u16 [TS][10][144] gated dL/dP1 (pooled)
-constexpr int D_TOTAL = D_G1 + TS * 1440 * 2;
+constexpr int D_DBG = D_DCH + TS * DCH_SZ * 2;  // u64 [16] stage stamps (a.dbg, diagnostics)
+constexpr int D_TOTAL = D_DBG + 16 * 8;
 constexpr int W_BYTES = (I_END - I_W2C) * 2;    // static: W2C | W2D | F1 images (LDS-DMA)
 static_assert(D_PAR % 16 == 0 && D_COFF % 16 == 0 && D_DGT % 16 == 0 && D_ZERO % 16 == 0 && D_X % 16 == 0 &&
                   D_P1H % 16 == 0 && D_I1 % 16 == 0 && D_P2 % 16 == 0 && D_I2 % 16 == 0 && D_F % 16 == 0 &&
-                  D_DZ1B % 16 == 0 && D_DC2 % 16 == 0 && D_DCH % 16 == 0 && D_G1 % 16 == 0,
+                  D_DZ1B % 16 == 0 && D_DC2 % 16 == 0 && D_DCH % 16 == 0 && D_ONES % 16 == 0 && D_ZERO % 16 == 0,
               "16-byte aligned regions");
 static_assert(D_TOTAL + W_BYTES <= 160 * 1024, "one workgroup per CU");
 static_assert(5020 * 4 <= TS * P1H_SZ * 2, "conv2 slab row staging fits the dead pool1 images");
-static_assert(NW * 256 * 4 <= D_TOTAL - D_DC2, "conv1 partials fit the dead backward images");
+static_assert(NW * 256 * 4 <= D_DBG - D_DC2, "conv1 partials fit the dead backward images");
+// dL/dconv1, dense [10][576] per sample, written at the end of stage 6 over regions dead by then:
+// samples 0, 1 in the pool1 images, samples 2, 3 in the dL/dconv2 images (contiguous)
+constexpr int DY1_SZ = 10 * 576;
+static_assert(TS == 4 && 2 * DY1_SZ * 2 <= TS * P1H_SZ * 2 && 2 * DY1_SZ * 2 <= D_DBG - D_DC2, "dL/dconv1 images");
 static_assert((W_BYTES / 16) % 256 == 0, "whole LDS-DMA rounds over waves 0-3");
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 
@@ -99,7 +104,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   unsigned short* W1Cs = reinterpret_cast<unsigned short*>(dsm + D_W1C);
   float* PAR = reinterpret_cast<float*>(dsm + D_PAR);
   short* COFF = reinterpret_cast<short*>(dsm + D_COFF);
-  uint8_t* DGT = dsm + D_DGT;
+  int* DGT = reinterpret_cast<int*>(dsm + D_DGT);
+  const unsigned short* ONES = reinterpret_cast<const unsigned short*>(dsm + D_ONES);
   const unsigned short* ZERO = reinterpret_cast<const unsigned short*>(dsm + D_ZERO);
   unsigned short* X = reinterpret_cast<unsigned short*>(dsm + D_X);
   unsigned short* P1H = reinterpret_cast<unsigned short*>(dsm + D_P1H);
@@ -115,7 +121,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   unsigned short* DZ1B = reinterpret_cast<unsigned short*>(dsm + D_DZ1B);
   unsigned short* DC2 = reinterpret_cast<unsigned short*>(dsm + D_DC2);
   unsigned short* DCH = reinterpret_cast<unsigned short*>(dsm + D_DCH);
-  unsigned short* G1 = reinterpret_cast<unsigned short*>(dsm + D_G1);
+  auto DY1 = [&](int s) {  // dense dL/dconv1 of sample s (see DY1_SZ)
+    return reinterpret_cast<unsigned short*>(dsm + (s < 2 ? D_P1H : D_DC2)) + (s & 1) * DY1_SZ;
+  };
+  uint64_t* DBGS = reinterpret_cast<uint64_t*>(dsm + D_DBG);
+  // Diagnostic stamps (a.dbg non-null): thread 0 records s_memtime at kernel entry (0), after
+  // the preamble (1), at stage k's start of the first tile (2 + k), after it (10) and at the end
+  // (11); copied to a.dbg[g * 32 ...] (tools/stage_profile_tile.py).
+#define TSTAMP(i)                                                                   \
+  do {                                                                              \
+    if (a.dbg && tid == 0 && tile == g) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  if (a.dbg && threadIdx.x == 0) DBGS[0] = __builtin_amdgcn_s_memtime();
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -154,17 +171,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       const int kg = (int)kC2Order.fwd[min(4 * tks + tq, 49)];
       const int tap = kg >> 1;
       COFF[t] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
-    } else if (t < 64 + 96) {
+    } else if (t < 64 + 80) {
       // dgrad K slice 4*ks + q = channels 8*ocg .. +7 of flipped tap (ty, tx): it reads
-      // dL/dconv2 at (y + ty - 4, x + tx - 4) (slot 75 is padding: zero weights)
-      const int j = t - 64, q = j / 24, ks = j - 24 * q;
-      uint8_t v = 0;
-      if (ks < DG_KS) {
-        const int kg = (int)kDgOrder.fwd[min(4 * ks + q, 74)];
-        const int tap = kg / 3, ocg = kg - 3 * tap;
-        v = (uint8_t)((tap / 5) | ((tap % 5) << 3) | (ocg << 6));
-      }
-      DGT[j] = v;
+      // dL/dconv2 at (y + ty - 4, x + tx - 4): offset rel from the lane's (y - 4, x - 4) in the
+      // interior image, valid iff bit `tap` of the lane's tap mask is set (slot 75 is padding:
+      // zero weights)
+      const int j = t - 64, q = j / 20, ks = j - 20 * q;
+      const int kg = (int)kDgOrder.fwd[min(4 * min(ks, DG_KS - 1) + q, 74)];
+      const int tap = kg / 3, ocg = kg - 3 * tap, ty = tap / 5, tx = tap % 5;
+      DGT[j] = ((ty * 8 + tx) * DG_OCP + ocg * 8) | (tap << 16);
+    } else if (t < 64 + 80 + 48) {
+      const int j = t - 144;  // 24 x 16 B of ones, 24 x 16 B of zeros
+      const unsigned short o = h16<T>(1.f);
+      reinterpret_cast<u16x8*>(dsm + D_ONES)[j] = j < 24 ? u16x8{o, o, o, o, o, o, o, o} : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   } else {
     // channels 10-23 of the pool1 images and 20-23 of the dL/dconv2 images are never written
@@ -174,24 +193,40 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     for (int i = t; i < TS * P1H_SZ * 2 / 16; i += 512) z[i] = make_uint4(0, 0, 0, 0);
     uint4* zh = reinterpret_cast<uint4*>(DCH);
     for (int i = t; i < TS * DCH_SZ * 2 / 16; i += 512) zh[i] = make_uint4(0, 0, 0, 0);
-    if (t < 2) reinterpret_cast<uint4*>(dsm + D_ZERO)[t] = make_uint4(0, 0, 0, 0);
   }
   // first tile's pixels (threads < TS * 196: sample tid / 196, pixels 4 * (tid % 196) ..),
   // and the row indices of the tile after it
   const int s_me = min(tid / 196, TS - 1), q_me = tid - 196 * (tid / 196);
   const bool px_thread = tid < TS * 196;
-  uint32_t px = 0;
+  uint32_t px = 0, px_next = 0;
   int lab = 0;
-  int64_t nrow = 0;
+  int64_t nrow = 0, srow = 0, lab_next = 0;
+  // Staged (a.xstage: one 784-byte row per sample of every workgroup's FIRST tile, row g * TS + s,
+  // written by the previous step's kernel or lenet_stage at epoch start): the first tile starts
+  // without the dependent cursor -> perm -> image chain (~5 us in front of stage 1 otherwise,
+  // tools/stage_profile_tile.py); this step stages the next step's first tile (stage_next).
+  const bool staged = a.xstage != nullptr;
+  const bool stage_next = TRAIN && staged && a.stage_next;
   if (px_thread && g < ntile) {
-    const int64_t row = perm_at(g * TS + s_me);
-    px = reinterpret_cast<const uint32_t*>(a.images + row * 784)[q_me];
-    if (q_me == 0) lab = (int)a.labels[row];
+    if (staged) {
+      px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)(g * TS + s_me) * 784)[q_me];
+      if (q_me == 0) lab = (int)a.lstage[g * TS + s_me];
+    } else {
+      const int64_t row = perm_at(g * TS + s_me);
+      px = reinterpret_cast<const uint32_t*>(a.images + row * 784)[q_me];
+      if (q_me == 0) lab = (int)a.labels[row];
+    }
+    // (row of the next step's sample g * TS + s: its pixels are loaded at the first tile's stage 4)
+    if (stage_next) srow = a.perm[min((a.cursor[0] + 1) * (int64_t)B + min(g * TS + s_me, B - 1), a.perm_len - 1)];
   }
   if (px_thread && g + G < ntile) nrow = perm_at((g + G) * TS + s_me);
   __syncthreads();  // (also the weight DMA)
+  if (a.dbg && threadIdx.x == 0) DBGS[1] = __builtin_amdgcn_s_memtime();
 
-  f32x4 acc_c2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};  // conv2 wgrad, N-tile = wave
+  // conv2 wgrad, taps wave and wave + 16 (the second for waves 0-9), oc M-tiles 0 / 1
+  f32x4 acc_w[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) acc_w[t][0] = acc_w[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc_c1 = f32x4{0.f, 0.f, 0.f, 0.f};  // conv1 wgrad, N-tile wave & 1, K-steps (wave >> 1) + 8j
   float loss_sum = 0.f, correct = 0.f;
   auto pool4 = [](const f32x4& c, float& best, int& bi) {
@@ -209,6 +244,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     const int s_me = min(tid / 196, TS - 1), q_me = tid - 196 * (tid / 196);
     const int b0 = tile * TS;
     // ---------------- stage 0: normalised pixels, labels, dropout masks
+    TSTAMP(2);
     if (px_thread) {
       const bool ok = b0 + s_me < B;
       u16x4 o;
@@ -231,28 +267,33 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     lds_barrier();
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1H (HWC), I1
+    TSTAMP(3);
     {
+      // M-tile T = wave + 16 i (i < 9): sample T / 36, tile mt = T % 36 of its 576 pool-ordered
+      // pixels -- wave-uniform, so every address is a scalar part plus a lane constant: rows
+      // 4 mt .. 4 mt + 3 of pooled windows lie in pooled row mt / 3, columns 4 (mt % 3) + 0..3
       const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
       const float cb = PAR[P_C1B + min(l16, 9)];
+      const int q1 = l16 & 3;
+      const int xl = (q1 >> 1) * 28 + 2 * (l16 >> 2) + (q1 & 1);  // window pixel of A row l16
+      const unsigned short* xr1 = X + xl + 28 * kq;                 // K slots: row kq of the taps,
+      const unsigned short* xr2 = X + xl + 112 + (kq == 1 ? W1_E1 : 0);  // then 3 taps of row 4
+      const int pl = kq * LD_P1H + min(l16, 9), il = min(l16, 9) * 144 + kq;  // P1H / I1 lane parts
 #pragma unroll
       for (int grp = 0; grp < 3; ++grp) {
         uint32_t rv[3][8];
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
-          const int T9 = wave + NW * (3 * grp + it), s = T9 / 36, mt = T9 - 36 * s;
-          const int m = mt * 16 + l16, p = m >> 2, q = m & 3;
-          const int base = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
-          // K slots of lane group kq (kernels/lenet_images.h w1c_slot): row kq, 3 taps of row 4
-          const unsigned short* r1 = X + s * X_LD + base + 28 * kq;
-          const unsigned short* r2 = X + s * X_LD + base + 112 + (kq == 1 ? W1_E1 : 0);
-          rv[it][0] = lds_u16<0>(r1);
-          rv[it][1] = lds_u16<1>(r1);
-          rv[it][2] = lds_u16<2>(r1);
-          rv[it][3] = lds_u16<3>(r1);
-          rv[it][4] = lds_u16<4>(r1);
-          rv[it][5] = lds_u16<0>(r2);
-          rv[it][6] = lds_u16<1>(r2);
-          rv[it][7] = lds_u16<2>(r2);
+          const int T9 = wave + NW * (3 * grp + it), ss = T9 / 36, mt = T9 - 36 * ss;
+          const int xs = ss * X_LD + (mt / 3) * 56 + 8 * (mt % 3);  // scalar
+          rv[it][0] = lds_u16<0>(xr1 + xs);
+          rv[it][1] = lds_u16<1>(xr1 + xs);
+          rv[it][2] = lds_u16<2>(xr1 + xs);
+          rv[it][3] = lds_u16<3>(xr1 + xs);
+          rv[it][4] = lds_u16<4>(xr1 + xs);
+          rv[it][5] = lds_u16<0>(xr2 + xs);
+          rv[it][6] = lds_u16<1>(xr2 + xs);
+          rv[it][7] = lds_u16<2>(xr2 + xs);
         }
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
@@ -261,14 +302,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 #pragma unroll
           for (int j = 0; j < 8; ++j) raw[j] = (unsigned short)rv[it][j];
           const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
-          const int T9 = wave + NW * (3 * grp + it), s = T9 / 36, mt = T9 - 36 * s;
-          if (l16 < 10) {
-            float best;
-            int bi;
-            pool4(c, best, bi);
-            const int w = mt * 4 + kq;  // pooled position py*12 + px
-            P1H[s * P1H_SZ + (w / 12) * P1H_RP + (w % 12) * LD_P1H + l16] = h16<T>(fmaxf(best + cb, 0.f));
-            I1[s * 1440 + l16 * 144 + w] = (uint8_t)bi;
+          const int T9 = wave + NW * (3 * grp + it), ss = T9 / 36, mt = T9 - 36 * ss;
+          float best;
+          int bi;
+          pool4(c, best, bi);
+          if (l16 < 10) {  // pooled window (mt / 3, 4 (mt % 3) + kq), channel l16
+            P1H[ss * P1H_SZ + (mt / 3) * P1H_RP + (4 * (mt % 3)) * LD_P1H + pl] = h16<T>(fmaxf(best + cb, 0.f));
+            I1[ss * 1440 + 4 * mt + il] = (uint8_t)bi;
           }
         }
       }
@@ -276,6 +316,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     lds_barrier();
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
+    TSTAMP(4);
     {
       const int s = wave >> 2, mt = wave & 3;
       const int m = mt * 16 + l16, p = m >> 2, q = m & 3;
@@ -322,10 +363,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     lds_barrier();
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H (rows = the tile's samples)
+    TSTAMP(5);
     if (wave < 4) {
+      // A rows 4 s = sample s (the other rows zero): C row 4 kq (register 0) of every lane group
+      // is then sample kq, so all 64 lanes hold one (sample, output) each for the epilogue
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
-      const unsigned short* prow = P2 + min(l16, TS - 1) * 320 + kb;
-      const bool live = l16 < TS;
+      const unsigned short* prow = P2 + (l16 >> 2) * 320 + kb;
+      const bool live = (l16 & 3) == 0;
       f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
       for (int ks = 0; ks < 10; ++ks) {
@@ -334,20 +378,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         if (ks & 1) c1 = Mfma<T>::mma(live ? pa : zfrag, fb, c1);
         else c0 = Mfma<T>::mma(live ? pa : zfrag, fb, c0);
       }
-      const f32x4 c = c0 + c1;
-      const int o = wave * 16 + lane;
-      if (lane < 16 && o < 50) {  // C rows 0..3 = samples (lane group 0), column o
-#pragma unroll
-        for (int r = 0; r < TS; ++r) {
-          const float h = fmaxf(c[r] + PAR[P_F1B + o], 0.f) * D1S[r * 52 + o];
-          Hs[r * 64 + o] = h;
-          if (TRAIN && b0 + r < B) a.vslab[(int64_t)(b0 + r) * VEC + V_H + o] = h;
-        }
+      const float cz = c0[0] + c1[0];
+      const int o = wave * 16 + l16;
+      if (o < 50) {  // sample kq, output o
+        const float h = fmaxf(cz + PAR[P_F1B + o], 0.f) * D1S[kq * 52 + o];
+        Hs[kq * 64 + o] = h;
+        if (TRAIN && b0 + kq < B) a.vslab[(int64_t)(b0 + kq) * VEC + V_H + o] = h;
       }
     }
     lds_barrier();
 
     // ---------------- stage 4: fc2 + log_softmax + NLL, dlogits, dZ1 (wave s: sample s)
+    TSTAMP(6);
     if (wave < TS) {
       const int s = wave, b = b0 + s;
       const bool valid = b < B;
@@ -426,6 +468,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       }
     }
     // the next tile's pixels (rows loaded one tile ago), then the rows of the tile after it
+    if (stage_next && tile == g && px_thread) {
+      px_next = reinterpret_cast<const uint32_t*>(a.images + srow * 784)[q_me];
+      if (q_me == 0) lab_next = a.labels[srow];
+    }
     if (px_thread && tile + G < ntile) {
       px = reinterpret_cast<const uint32_t*>(a.images + nrow * 784)[q_me];
       if (q_me == 0) lab = (int)a.labels[nrow];
@@ -436,15 +482,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 
     // ---------------- stage 5: dP2 = dZ1 . W1 (B = fc1 image read transposed), pool2 / relu /
     // Dropout2d backward -> dL/dconv2 as [oc][px] (wgrad A) and HWC interior (dgrad A)
+    TSTAMP(7);
     {
-      const bool live = l16 < TS;
-      const frag dz0 = *reinterpret_cast<const frag*>(DZ1B + min(l16, TS - 1) * 64 + kb);
-      const frag dz1 = *reinterpret_cast<const frag*>(DZ1B + min(l16, TS - 1) * 64 + 32 + kb);
+      // A rows 4 s = dZ1 of sample s: C row 4 kq (register 0) is sample kq (see stage 3)
+      const bool live = (l16 & 3) == 0;
+      const frag dz0 = *reinterpret_cast<const frag*>(DZ1B + (l16 >> 2) * 64 + kb);
+      const frag dz1 = *reinterpret_cast<const frag*>(DZ1B + (l16 >> 2) * 64 + 32 + kb);
       const frag fa0 = live ? dz0 : zfrag, fa1 = live ? dz1 : zfrag;
       const unsigned short* fc0 = F1s + min(kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc1 = F1s + min(kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc2 = F1s + min(32 + kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc3 = F1s + min(32 + kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
+      const int oh0 = 2 * (l16 >> 2), ow0 = 2 * (l16 & 3);  // pool window l16 of the 4 x 4
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         const int t = wave + NW * tt;  // output channel of P2 (wave-uniform: EXEC full for tr reads)
@@ -454,24 +503,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           f32x4 c = Mfma<T>::mma(fa0, __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7)),
                                  f32x4{0.f, 0.f, 0.f, 0.f});
           c = Mfma<T>::mma(fa1, __builtin_bit_cast(frag, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7)), c);
-          if (lane < 16) {  // C row r = sample r, column = pool window `lane` of channel t
-            const int oh0 = 2 * (lane >> 2), ow0 = 2 * (lane & 3);
+          // sample kq, channel t, pool window l16
+          const int pi = kq * 320 + t * 16 + l16;
+          const float gv = f16v<T>(P2[pi]) > 0.f ? c[0] * D2S[kq * 20 + t] : 0.f;
+          const int bi = I2[pi];
+          const uint32_t hg = h16<T>(gv);
 #pragma unroll
-            for (int r = 0; r < TS; ++r) {
-              const int pi = r * 320 + t * 16 + lane;
-              const float gv = f16v<T>(P2[pi]) > 0.f ? c[r] * D2S[r * 20 + t] : 0.f;
-              const int bi = I2[pi];
-              const uint32_t hg = h16<T>(gv);
+          for (int dy = 0; dy < 2; ++dy)
+            reinterpret_cast<uint32_t*>(DC2 + kq * DC2_SZ + t * DC2_LD + (oh0 + dy) * 8 + ow0)[0] =
+                bi == 2 * dy ? hg : (bi == 2 * dy + 1 ? hg << 16 : 0u);
 #pragma unroll
-              for (int dy = 0; dy < 2; ++dy)
-                reinterpret_cast<uint32_t*>(DC2 + r * DC2_SZ + t * DC2_LD + (oh0 + dy) * 8 + ow0)[0] =
-                    bi == 2 * dy ? hg : (bi == 2 * dy + 1 ? hg << 16 : 0u);
-#pragma unroll
-              for (int pos = 0; pos < 4; ++pos)
-                DCH[r * DCH_SZ + ((oh0 + (pos >> 1)) * 8 + ow0 + (pos & 1)) * DG_OCP + t] =
-                    pos == bi ? (unsigned short)hg : (unsigned short)0;
-            }
-          }
+          for (int pos = 0; pos < 4; ++pos)
+            DCH[kq * DCH_SZ + ((oh0 + (pos >> 1)) * 8 + ow0 + (pos & 1)) * DG_OCP + t] =
+                pos == bi ? (unsigned short)hg : (unsigned short)0;
         }
       }
     }
@@ -479,88 +523,124 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 
     // ---------------- stage 6: conv2 wgrad (N-tile = wave; K = 2 x 32 pixels per sample) and
     // conv2 dgrad (36 M-tiles of 16 pool1 pixels: waves 0-3 three, the others two)
-    {
-      const int k = wave * 16 + l16;  // B column: ic * 25 + tap, 250 = bias (ones)
-      const int kc = min(k, 249), ic = kc / 25, r5 = kc - 25 * ic, kh = r5 / 5, kw = r5 - 5 * kh;
-      const unsigned short cst = k == 250 ? one : (unsigned short)0;
+    TSTAMP(8);
+    // conv2 wgrad per tap: dW[oc][ic][t] = sum_px dL/dconv2[oc][px] . P1[ic][px + shift(t)], an
+    // [oc x px] . [px x ic] product for each of the 25 taps (+ a ones "tap" 25: the bias).  Wave w
+    // owns taps w and w + 16 (waves 0-9), both oc M-tiles, K = the tile's 4 x 64 pixels.  The B
+    // fragment (8 pixels of one conv2 output row, channel = lane) comes from the HWC pool1 image
+    // by two ds_read_b64_tr_b16 (a 4-position x 16-channel block each): no 16-bit gathers (the
+    // earlier per-column form read 8 strided u16 per fragment, 6-8-way bank-conflicted: half of
+    // the kernel's LDS cycles were conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE)
+    auto wgrad2 = [&](auto ntap) {
+      constexpr int NTAP = decltype(ntap)::value;
+      const int q4 = l16 >> 2, p4 = l16 & 3;  // this lane's row (position) / channel quad of a block
+      const unsigned short* pb[NTAP];
+      bool is_bias[NTAP];
 #pragma unroll
-      for (int s = 0; s < TS; ++s) {
-        uint32_t rv[2][8];
-        frag fa[2][2];
+      for (int t = 0; t < NTAP; ++t) {
+        const int tap = min(wave + NW * t, 24), kh = tap / 5, kw = tap - 5 * kh;
+        is_bias[t] = wave + NW * t == 25;  // (wave-uniform)
+        pb[t] = P1H + (kq + kh) * P1H_RP + (q4 + kw) * LD_P1H + 4 * p4;
+      }
+      const unsigned short* dl0 = DC2 + min(l16, 19) * DC2_LD + kb;
+      const unsigned short* dl1 = DC2 + min(16 + l16, 19) * DC2_LD + kb;
+      const frag ones = __builtin_bit_cast(frag, u16x8{one, one, one, one, one, one, one, one});
+#pragma unroll
+      for (int ss = 0; ss < TS; ++ss) {
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
-          // output row oy = 4 ps + kq, pixels ox = 0..7: pool1 (ic, oy + kh, kw + ox), HWC
-          const unsigned short* pb = P1H + s * P1H_SZ + (4 * ps + kq + kh) * P1H_RP + kw * LD_P1H + ic;
-          rv[ps][0] = lds_u16<0 * LD_P1H>(pb);
-          rv[ps][1] = lds_u16<1 * LD_P1H>(pb);
-          rv[ps][2] = lds_u16<2 * LD_P1H>(pb);
-          rv[ps][3] = lds_u16<3 * LD_P1H>(pb);
-          rv[ps][4] = lds_u16<4 * LD_P1H>(pb);
-          rv[ps][5] = lds_u16<5 * LD_P1H>(pb);
-          rv[ps][6] = lds_u16<6 * LD_P1H>(pb);
-          rv[ps][7] = lds_u16<7 * LD_P1H>(pb);
-          fa[ps][0] = *reinterpret_cast<const frag*>(DC2 + s * DC2_SZ + min(l16, 19) * DC2_LD + ps * 32 + kb);
-          fa[ps][1] = *reinterpret_cast<const frag*>(DC2 + s * DC2_SZ + min(16 + l16, 19) * DC2_LD + ps * 32 + kb);
-        }
+          // output row oy = 4 ps + kq (lane group), pixels 0..7
+          const frag fa0 = *reinterpret_cast<const frag*>(dl0 + ss * DC2_SZ + ps * 32);
+          const frag fa1 = *reinterpret_cast<const frag*>(dl1 + ss * DC2_SZ + ps * 32);
 #pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
-          lds_wait8(rv[ps]);
-          u16x8 bv;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) bv[j] = k < 250 ? (unsigned short)rv[ps][j] : cst;
-          const frag fb = __builtin_bit_cast(frag, bv);
-          acc_c2[0] = Mfma<T>::mma(fa[ps][0], fb, acc_c2[0]);
-          acc_c2[1] = Mfma<T>::mma(fa[ps][1], fb, acc_c2[1]);
+          for (int t = 0; t < NTAP; ++t) {
+            const unsigned short* q = pb[t] + ss * P1H_SZ + 4 * ps * P1H_RP;
+            const s16x4 r0 = lds_read_tr16(q), r1 = lds_read_tr16(q + 4 * LD_P1H);
+            const frag fb = is_bias[t] ? ones
+                                       : __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc_w[t][0] = Mfma<T>::mma(fa0, fb, acc_w[t][0]);
+            acc_w[t][1] = Mfma<T>::mma(fa1, fb, acc_w[t][1]);
+          }
         }
       }
-    }
+    };
+    if (wave < 10) wgrad2(std::integral_constant<int, 2>{});
+    else wgrad2(std::integral_constant<int, 1>{});
     {
-      // this lane group's dgrad K-slice table (19 bytes of DGT row kq)
-      uint32_t dg[5];
-      {
-        const uint4 d4 = *reinterpret_cast<const uint4*>(DGT + kq * 24);
-        dg[0] = d4.x; dg[1] = d4.y; dg[2] = d4.z; dg[3] = d4.w;
-        dg[4] = *reinterpret_cast<const uint32_t*>(DGT + kq * 24 + 16);
-      }
+      // dgrad.  A row = pool1 pixel (y, x) of the M-tile, K slice (flipped tap (ty, tx), channel
+      // group): dL/dconv2 at (y + ty - 4, x + tx - 4) of the interior image, or the zero run when
+      // that is outside -- one bit of the lane's 25-bit tap mask, computed once per M-tile.
       const unsigned short* wrow = W2d + (kq * 16 + l16) * 8;
-      // M-tiles RT = wave + 16 i (i < NTL): sample RT / 9, pool1 pixels 16 (RT % 9) + row
+      const int* dgt = DGT + kq * 20;
       auto dgrad = [&](auto ntl) {
         constexpr int NTL = decltype(ntl)::value;
-        int sy[NTL], sx[NTL];
         const unsigned short* ab[NTL];
+        uint32_t msk[NTL];
+        int p0[NTL], si[NTL];
 #pragma unroll
         for (int i = 0; i < NTL; ++i) {
-          const int RT = wave + NW * i, s = RT / 9, p = (RT - 9 * s) * 16 + l16;
-          sy[i] = p / 12 - 4;
-          sx[i] = p % 12 - 4;
-          ab[i] = DCH + s * DCH_SZ;
+          const int RT = wave + NW * i, ss = RT / 9;  // wave-uniform
+          const int p = (RT - 9 * ss) * 16 + l16, y = p / 12, x = p - 12 * y;
+          si[i] = ss;
+          p0[i] = (RT - 9 * ss) * 16 + 4 * kq;
+          ab[i] = DCH + ss * DCH_SZ + ((y - 4) * 8 + (x - 4)) * DG_OCP;
+          // taps (ty, tx) with 0 <= y + ty - 4 < 8 and 0 <= x + tx - 4 < 8
+          const uint32_t rb = ((1u << min(5, 12 - y)) - 1u) & ~((1u << max(0, 4 - y)) - 1u);
+          const uint32_t cbits = ((1u << min(5, 12 - x)) - 1u) & ~((1u << max(0, 4 - x)) - 1u);
+          uint32_t m = 0;
+#pragma unroll
+          for (int ty = 0; ty < 5; ++ty) m |= ((rb >> ty) & 1u) ? (cbits << (5 * ty)) : 0u;
+          msk[i] = m;
         }
         f32x4 acc[NTL];
 #pragma unroll
         for (int i = 0; i < NTL; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < DG_KS; ++ks) {
-          const uint32_t e = (dg[ks >> 2] >> (8 * (ks & 3))) & 255u;
-          const int ty = (int)(e & 7u), tx = (int)((e >> 3) & 7u), ocg = (int)(e >> 6);
+          const int e = dgt[ks];
+          const int rel = e & 0xffff, tap = e >> 16;
           const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 512);
 #pragma unroll
           for (int i = 0; i < NTL; ++i) {
-            const int yy = sy[i] + ty, xx = sx[i] + tx;
-            const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
-            const unsigned short* src = ok ? ab[i] + (yy * 8 + xx) * DG_OCP + ocg * 8 : ZERO;
+            const unsigned short* src = ((msk[i] >> tap) & 1u) ? ab[i] + rel : ZERO;
             acc[i] = Mfma<T>::mma(*reinterpret_cast<const frag*>(src), fb, acc[i]);
           }
         }
-        // relu gate (pool1 output > 0), pooled gradient G1[s][ic][p]
+        // relu gate (pool1 output > 0) and pool1 argmax of this lane's 4 pixels, read before the
+        // barrier (the dense dL/dconv1 images overwrite the pool1 images after it)
+        const int ic = min(l16, 9);
+        float v[NTL][4];
+        uint32_t bis[NTL];
+#pragma unroll
+        for (int i = 0; i < NTL; ++i) {
+          bis[i] = *reinterpret_cast<const uint32_t*>(I1 + si[i] * 1440 + ic * 144 + p0[i]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pp = p0[i] + r;  // pooled row p0 / 12 (p0 % 12 is 0, 4 or 8)
+            const float pv = f16v<T>(P1H[si[i] * P1H_SZ + (pp / 12) * P1H_RP + (pp % 12) * LD_P1H + ic]);
+            v[i][r] = pv > 0.f ? acc[i][r] : 0.f;
+          }
+        }
+        lds_barrier();
+        // pool1 backward: each pooled pixel's gradient goes to its window's argmax position of
+        // dL/dconv1 (dense [ic][24 x 24]); this lane's 4 pooled pixels are 8 consecutive conv1
+        // pixels of rows 2 py and 2 py + 1: two 16-byte stores per M-tile
         if (l16 < 10) {
 #pragma unroll
           for (int i = 0; i < NTL; ++i) {
-            const int RT = wave + NW * i, s = RT / 9, p0 = (RT - 9 * s) * 16 + 4 * kq;
+            const int py = p0[i] / 12, px0 = p0[i] - 12 * py;
+            unsigned short* d = DY1(si[i]) + ic * 576 + (2 * py) * 24 + 2 * px0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int pp = p0 + r;
-              const float pv = f16v<T>(P1H[s * P1H_SZ + (pp / 12) * P1H_RP + (pp % 12) * LD_P1H + l16]);
-              G1[s * 1440 + l16 * 144 + pp] = h16<T>(pv > 0.f ? acc[i][r] : 0.f);
+            for (int dy = 0; dy < 2; ++dy) {
+              u16x8 o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int bi = (int)((bis[i] >> (8 * r)) & 255u);
+                const unsigned short h = h16<T>(v[i][r]);
+                o[2 * r] = bi == 2 * dy ? h : (unsigned short)0;
+                o[2 * r + 1] = bi == 2 * dy + 1 ? h : (unsigned short)0;
+              }
+              *reinterpret_cast<u16x8*>(d + dy * 24) = o;
             }
           }
         }
@@ -571,21 +651,20 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     lds_barrier();
 
     // ---------------- stage 7: conv1 wgrad (+ bias column 25): K = the tile's 4 x 576 conv1
-    // pixels, 72 K-steps of 32 over 8 wave pairs; A = dL/dconv1 built from the pooled
-    // gradient and the pool1 argmax, B = X runs (8 pixels of a row at tap offsets)
+    // pixels, 72 K-steps of 32 over 8 wave pairs; A = the dense dL/dconv1 rows (one 16-byte read),
+    // B = X runs (8 pixels of a conv1 output row at the lane's tap offset; the bias / padding
+    // columns read the ones / zeros runs)
+    TSTAMP(9);
     {
       const int kcol = (wave & 1) * 16 + l16, kc = min(kcol, 24), kh = kc / 5, kw = kc - 5 * kh;
-      const unsigned short cst = kcol == 25 ? one : (unsigned short)0;
-      const int oc = min(l16, 9);
-      const bool ocv = l16 < 10;
+      const unsigned short* pconst = kcol == 25 ? ONES : ZERO;
+      const int oc = min(l16, 9);  // A rows 10-15 feed discarded outputs
 #pragma unroll 3
       for (int j = 0; j < 9; ++j) {
-        const int J = (wave >> 1) + 8 * j, s = J / 18, ps = J - 18 * s;
-        const int px0 = ps * 32 + kb, oh = px0 / 24, ow0 = px0 - 24 * oh;
-        const int py = oh >> 1, dy = oh & 1, wx0 = ow0 >> 1;
-        const uint2 gq = *reinterpret_cast<const uint2*>(G1 + s * 1440 + oc * 144 + py * 12 + wx0);
-        const uint32_t iq = *reinterpret_cast<const uint32_t*>(I1 + s * 1440 + oc * 144 + py * 12 + wx0);
-        const unsigned short* xb = X + s * X_LD + (oh + kh) * 28 + ow0 + kw;
+        const int J = (wave >> 1) + 8 * j, ss = J / 18, ps = J - 18 * ss;  // wave-uniform
+        const int r = 4 * ps + kq, oh = r / 3, ow0 = 8 * (r - 3 * oh);      // conv1 pixels 8 r .. 8 r + 7
+        const frag fa = *reinterpret_cast<const frag*>(DY1(ss) + oc * 576 + 8 * r);
+        const unsigned short* xb = kcol < 25 ? X + ss * X_LD + (oh + kh) * 28 + ow0 + kw : pconst;
         uint32_t rv[8];
         rv[0] = lds_u16<0>(xb);
         rv[1] = lds_u16<1>(xb);
@@ -595,25 +674,22 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         rv[5] = lds_u16<5>(xb);
         rv[6] = lds_u16<6>(xb);
         rv[7] = lds_u16<7>(xb);
-        u16x8 av;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const unsigned short gv = (unsigned short)(((i < 2 ? gq.x : gq.y) >> (16 * (i & 1))) & 0xffffu);
-          const int bi = (int)((iq >> (8 * i)) & 255u);
-          av[2 * i] = (ocv && bi == 2 * dy) ? gv : (unsigned short)0;
-          av[2 * i + 1] = (ocv && bi == 2 * dy + 1) ? gv : (unsigned short)0;
-        }
         lds_wait8(rv);
         u16x8 bv;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) bv[jj] = kcol < 25 ? (unsigned short)rv[jj] : cst;
-        acc_c1 = Mfma<T>::mma(__builtin_bit_cast(frag, av), __builtin_bit_cast(frag, bv), acc_c1);
+        for (int jj = 0; jj < 8; ++jj) bv[jj] = (unsigned short)rv[jj];
+        acc_c1 = Mfma<T>::mma(fa, __builtin_bit_cast(frag, bv), acc_c1);
       }
     }
     lds_barrier();
+    TSTAMP(10);
   }
 
   // ---------------- epilogue: this workgroup's partial conv gradient (slab row g) + loss
+  if (stage_next && px_thread && g < ntile) {  // the next step's first tile of this workgroup
+    reinterpret_cast<uint32_t*>(a.xstage + (int64_t)(g * TS + s_me) * 784)[q_me] = px_next;
+    if (q_me == 0) a.lstage[g * TS + s_me] = lab_next;
+  }
   if (wave < TS && lane == 0) {
     LOSS[2 * wave] = loss_sum;
     LOSS[2 * wave + 1] = correct;
@@ -623,14 +699,21 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     float* SLF = reinterpret_cast<float*>(dsm + D_P1H);  // dead pool1 images: conv2 row, slot order
 #pragma unroll
     for (int r = 0; r < 4; ++r) RED[wave * 256 + (4 * kq + r) * 16 + l16] = acc_c1[r];
-    const int k = wave * 16 + l16;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int t = 0; t < 2; ++t) {
+      const int tap = wave + NW * t;  // C[oc][ic] of tap `tap`; tap 25: the bias (column 0)
+      if (tap <= 25) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int oc = mt * 16 + 4 * kq + r;
-        if (oc < 20 && k <= 250) SLF[k * 20 + oc] = acc_c2[mt][r];  // slab slot S_C2 + k*20 + oc
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int oc = mt * 16 + 4 * kq + r;
+            // slab slot S_C2 + k*20 + oc, k = ic*25 + tap (250: bias)
+            if (oc < 20 && (tap < 25 ? l16 < 10 : l16 == 0))
+              SLF[(tap < 25 ? l16 * 25 + tap : 250) * 20 + oc] = acc_w[t][mt][r];
+          }
       }
+    }
     __syncthreads();
     auto slab_at = [&](int e) { return a.slab + slab_off(slab_slot(e), g, G, G); };
     if (tid < 512) {  // conv1: fixed-order sum of the 8 wave-pair partials of each N-tile
@@ -660,6 +743,12 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     a.loss_acc[2 * g] = l;
     a.loss_acc[2 * g + 1] = c;
   }
+  if (a.dbg) {
+    if (tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (tid < 16) a.dbg[g * 32 + tid] = DBGS[tid];
+  }
+#undef TSTAMP
 }
 
 }  // namespace lenet_tile
@@ -670,7 +759,9 @@ int lenet_tile_grid(int B) { return std::min(256, (B + lenet_tile::TS - 1) / len
 
 hipError_t launch_lenet_tile(const LenetTrainArgs& a, int write_logp, float* logp_out, bool train, hipStream_t s) {
   using namespace lenet_tile;
-  if (a.B <= 0 || a.grid != lenet_tile_grid(a.B) || a.xstage || a.mfma_dtype == kF32) return hipErrorInvalidValue;
+  if (a.B <= 0 || a.grid != lenet_tile_grid(a.B) || a.mfma_dtype == kF32 || (a.xstage && !a.lstage) ||
+      (a.stage_next && (!a.xstage || !a.cursor)))
+    return hipErrorInvalidValue;
   const size_t lds = (size_t)D_TOTAL;
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     if (train) {

@@ -63,7 +63,8 @@ def _kernel_masks(eng, B):
 
 @pytest.mark.parametrize("dt,B,split", [(torch.bfloat16, 64, True), (torch.bfloat16, 8, True),
                                         (torch.bfloat16, 64, False), (torch.float16, 100, False),
-                                        (torch.float32, 64, False), (torch.float32, 100, False)])
+                                        (torch.float32, 64, False), (torch.float32, 100, False),
+                                        (torch.float32, 64, True), (torch.float32, 8, True)])
 def test_kernel_masks_equal_host_philox(dt, B, split):
     p, seed = 0.5, 1234
     data = synthetic_mnist(256, seed=2)

@@ -126,3 +126,67 @@ def test_f32_training_with_dropout_converges():
     l1, c1 = eng.evaluate(test)
     assert l1 < 0.7 * l0 and c1 > 400, (l0, l1, c1)
     assert eng.capture_comm_ok is True
+
+
+@pytest.mark.parametrize("B", [64, 8, 16])
+def test_f32_split_step_matches_cpu_reference_and_unsplit(B):
+    """The exact-fp32 split step (4 workgroups per sample, staged batch): gradients within 1e-4
+    of the CPU fp32 Net, fc gradients and loss bitwise the one-workgroup-per-sample kernel's, conv
+    gradients equal to it up to summation order."""
+    data = synthetic_mnist(256, seed=11)
+    order = torch.randperm(256, generator=torch.Generator().manual_seed(B))[:B]
+    res = []
+    for split in (True, False):
+        torch.manual_seed(1)
+        net = Net()
+        eng = FusedLeNetTrainer(net.to(DEV), data, lr=0.01, momentum=0.5, global_batch=B,
+                                compute_dtype=torch.float32, drop_p=0.0, split=split)
+        assert eng.split == split and eng.staged == split and eng.grid == (4 * B if split else B)
+        eng.set_epoch_order(order)
+        g = eng.gradient()
+        torch.cuda.synchronize()
+        res.append((g.cpu(), eng.loss_acc.cpu().clone()))
+    torch.manual_seed(1)
+    ref = Net()
+    ref.eval()
+    out = ref(_x(data, order))
+    F.nll_loss(out, data.labels[order]).backward()
+    (gs, ls), (g1, l1) = res
+    assert torch.equal(ls, l1)
+    off = 0
+    for name, p in ref.named_parameters():
+        n = p.numel()
+        assert _rel(gs[off:off + n].view_as(p), p.grad) < 1e-4, name
+        if name.startswith("fc"):
+            assert torch.equal(gs[off:off + n], g1[off:off + n]), name
+        else:
+            assert _rel(gs[off:off + n], g1[off:off + n]) < 1e-5, name
+        off += n
+
+
+def test_f32_split_step_graphs_native_and_eager_bitwise():
+    """Staged split steps across two epochs (with the tail): graph replay, the native step
+    executor and per-step launches end with bitwise-equal parameters and momentum."""
+    data = synthetic_mnist(64 * 5 + 17, seed=5)
+    finals = []
+    for mode in ("graph", "native", "python"):
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.5, global_batch=64,
+                                compute_dtype=torch.float32)
+        assert eng.split and eng.staged and eng.grid == 256
+        eng.native_max = 64 if mode == "native" else 0
+        g = torch.Generator().manual_seed(7)
+        for _ in range(2):
+            eng.set_epoch_order(torch.randperm(len(data), generator=g))
+            if mode == "python":
+                for _ in range(eng.full_steps()):
+                    eng.step()
+            else:
+                eng.run_steps(eng.full_steps(), 2, use_graph=mode == "graph")
+            eng.last_partial_step(use_graph=mode == "graph")
+        torch.cuda.synchronize()
+        finals.append((eng.flat.data.clone(), eng.momentum_buf.clone(), eng.loss_acc.clone()))
+    for other in finals[1:]:
+        for a, b in zip(finals[0], other):
+            assert torch.equal(a, b)
+    assert torch.isfinite(finals[0][0]).all()

@@ -34,7 +34,8 @@ def summarize(path: str):
     acc = defaultdict(lambda: defaultdict(list))
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name", "")
-        short = "lenet_train" if "lenet_train" in name else ("lenet_update" if "lenet_update" in name else None)
+        short = ("lenet_train" if "lenet_train" in name else "lenet_tile" if "lenet_tile" in name
+                 else "lenet_update" if "lenet_update" in name else None)
         if short is None:
             continue
         acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))

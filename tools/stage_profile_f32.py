@@ -15,8 +15,9 @@ from csed_514_project_distributed_training_using_pytorch_amd.data import synthet
 from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer  # noqa: E402
 from csed_514_project_distributed_training_using_pytorch_amd.models import Net  # noqa: E402
 
-NAMES = ["preamble", "stage 0 pixels+masks", "1 conv1", "2 conv2", "3 fc1 (VALU)", "4 fc2+loss+dZ1",
-         "5 dP2 (VALU)+pool2 bwd", "6 conv2 wgrad+dgrad", "7 dgrad combine", "8 conv1 wgrad (VALU)"]
+NAMES = ["preamble", "(sample loop entry)", "0 pixels+masks", "1 conv1", "2 conv2", "3 fc1 (VALU)",
+         "4 fc2+loss+dZ1", "5 dP2 (VALU)+pool2 bwd", "6 conv2 wgrad+dgrad", "7 dgrad combine",
+         "8 conv1 wgrad (VALU)"]
 
 
 def main():
