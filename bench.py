@@ -335,6 +335,8 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": round(value / base_ips, 2) if base_ips else None,
+            "vs_baseline_basis": "warm-rate: timed-window images/s / the reference's whole-run images/s "
+                                 "(like-for-like: vs_baseline_time_elapsed, vs_baseline_epoch)",
             "dtype": args.dtype if args.device == "cuda" else "fp32",
             "data": "synthetic (60000 x 1x28x28 uint8, class-conditional stroke mixture; random-init weights)",
             "config": {"model": "Net (ref src/model.py, 21,840 params)", "global_batch": args.global_batch,

@@ -28,3 +28,29 @@ def test_scaling_report_from_bench_lines_and_scale_json(tmp_path):
     assert "17.53" in md and "5.00" in md  # the reference's curve alongside
     assert "100.0%" in rows[0]  # N = 1 efficiency
     assert (tmp_path / "rep" / "scaling.png").stat().st_size > 1000
+
+
+def test_scaling_report_prediction_from_loopback_log(tmp_path):
+    """Predicted columns: per-rank step at batch 64/N from a loopback log + the hop; the epoch
+    keeps the N = 1 record's non-step remainder; measured / predicted for the records given."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scaling_report as sr
+
+    lb = tmp_path / "lb.log"
+    lb.write_text("B= 64 N=1 update 5.87 us  step  15.00 us  stamps ...\n"
+                  "B= 32 N=2 update 6.24 us  step  16.00 us\nB= 16 N=4 update 6.39 us  step  16.50 us\n"
+                  "B=  8 N=8 update 6.81 us  step  17.00 us  comm_errors 0\nnoise\n")
+    steps = sr.load_loopback(lb)
+    assert steps == {(64, 1): 15.0, (32, 2): 16.0, (16, 4): 16.5, (8, 8): 17.0}
+    by_n = {1: {"n_gpus": 1, "value": 64 / 15e-6, "ms_per_step": 0.015, "epoch_s": 938 * 15e-6 + 0.002}}
+    pred = sr.predict(by_n, steps, hop_us=1.0)
+    assert abs(pred[1]["step_us"] - 15.0) < 1e-9 and abs(pred[8]["step_us"] - 18.0) < 1e-9
+    assert abs(pred[8]["epoch_s"] - (938 * 18e-6 + 0.002)) < 1e-9
+    assert abs(pred[2]["images_s"] - 64 / 17e-6) < 1e-3
+    rows = sr.table(by_n, pred)
+    assert [r["n"] for r in rows] == [1, 2, 4, 8] and abs(rows[0]["vs_pred"] - 1.0) < 1e-9
+    assert rows[3]["vs_pred"] is None  # no N = 8 record yet: prediction only
+    md = sr.markdown(rows, "t")
+    assert "predicted epoch s" in md
+    # the built-in table covers every N of the strong-scaling curve
+    assert all(n in sr.predict({}, sr.LOOPBACK_STEP_US, 1.0) for n in (1, 2, 4, 8))

@@ -17,15 +17,70 @@ Columns: images/s (bench ``value``, whole job), ms/step, the warm epoch (``epoch
 steps + the 10k validation), the reference's own quantity (``time_elapsed_s``: process start
 -> end of epoch-0 validation), the reference time, speed-up on both, and strong-scaling
 efficiency value_N / (N * value_1).
+
+Prediction (``--predict``, on by default).  At global batch 64 each of N ranks runs a step of
+per-rank batch 64/N whose exchange pushes to N-1 peers.  Both parts were measured on one GPU
+with the exchange looped back to N virtual ranks (``tools/exchange_loopback.py``,
+profiles/dp_exchange_r3.md section 2): ``LOOPBACK_STEP_US[(B, N)]`` is that graph-replayed
+step.  The predicted N-GPU step adds one xGMI one-way hop (``--hop-us``, 1 us assumed: the
+loopback push never leaves the device) and the predicted epoch keeps the N=1 record's
+non-step remainder (validation + tail):
+
+    step_N  = LOOPBACK_STEP_US[(64 / N, N)] + hop          (N > 1; N = 1: no exchange, no hop)
+    epoch_N = 938 * step_N + (epoch_s_1 - 938 * ms_per_step_1)
+
+A loopback log (``--loopback-log``, the ``B=.. N=.. ... step X us`` lines of
+exchange_loopback.py) replaces the built-in table.  The driver's SCALE record is then checked
+against the prediction in the ``measured / predicted`` column.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import re
 import sys
 from pathlib import Path
 
 REF_EPOCH_S = {1: 17.53, 2: 11.29, 4: 7.60, 8: 5.00}  # BASELINE.md (reference README.md:20)
+STEPS_PER_EPOCH = 938
+GLOBAL_BATCH = 64
+# graph-replayed lenet_train + lenet_update step (us) at per-rank batch B with the in-kernel
+# exchange looped back to N virtual ranks, one MI355X (gpurun_out/r3y_loopback.log,
+# profiles/dp_exchange_r3.md section 2)
+LOOPBACK_STEP_US = {
+    (8, 1): 13.77, (8, 2): 16.09, (8, 4): 16.29, (8, 8): 16.73,
+    (16, 1): 14.05, (16, 2): 16.24, (16, 4): 16.48, (16, 8): 17.00,
+    (32, 1): 14.24, (32, 2): 16.57, (32, 4): 16.80, (32, 8): 17.26,
+    (64, 1): 15.05, (64, 2): 17.19, (64, 4): 17.49, (64, 8): 17.98,
+}
+_LB_LINE = re.compile(r"B=\s*(\d+)\s+N=(\d+).*?step\s+([0-9.]+)\s*us")
+
+
+def load_loopback(path) -> dict[tuple[int, int], float]:
+    """(per-rank B, N) -> step us from exchange_loopback.py output."""
+    out = {}
+    for line in Path(path).read_text().splitlines():
+        m = _LB_LINE.search(line)
+        if m:
+            out[(int(m.group(1)), int(m.group(2)))] = float(m.group(3))
+    return out
+
+
+def predict(by_n: dict[int, dict], steps_us: dict, hop_us: float, ns=(1, 2, 4, 8)) -> dict[int, dict]:
+    """Predicted per-N step (us), images/s and warm epoch (s) at global batch 64."""
+    r1 = by_n.get(1) or {}
+    rest = None
+    if r1.get("epoch_s") and r1.get("ms_per_step"):
+        rest = max(0.0, r1["epoch_s"] - STEPS_PER_EPOCH * r1["ms_per_step"] * 1e-3)
+    out = {}
+    for n in ns:
+        b = GLOBAL_BATCH // n
+        if (b, n) not in steps_us:
+            continue
+        step = steps_us[(b, n)] + (hop_us if n > 1 else 0.0)
+        out[n] = {"step_us": step, "images_s": GLOBAL_BATCH / (step * 1e-6),
+                  "epoch_s": STEPS_PER_EPOCH * step * 1e-6 + rest if rest is not None else None}
+    return out
 
 
 def _walk(obj, out: list) -> None:
@@ -64,10 +119,13 @@ def load_records(paths) -> dict[int, dict]:
     return dict(sorted(by_n.items()))
 
 
-def table(by_n: dict[int, dict]) -> list[dict]:
+def table(by_n: dict[int, dict], pred: dict[int, dict] | None = None) -> list[dict]:
     base = by_n.get(1, {}).get("value")
+    pred = pred or {}
     rows = []
-    for n, r in by_n.items():
+    for n in sorted(set(by_n) | set(pred)):
+        r = by_n.get(n, {"value": None})
+        p = pred.get(n, {})
         ref = REF_EPOCH_S.get(n)
         ep, te = r.get("epoch_s"), r.get("time_elapsed_s")
         rows.append({
@@ -77,6 +135,8 @@ def table(by_n: dict[int, dict]) -> list[dict]:
             "speedup_time_elapsed": ref / te if ref and te else None,
             "efficiency": r["value"] / (n * base) if base and r.get("value") else None,
             "dtype": r.get("dtype"), "allreduce": (r.get("config") or {}).get("allreduce"),
+            "pred_images_s": p.get("images_s"), "pred_epoch_s": p.get("epoch_s"),
+            "vs_pred": r["value"] / p["images_s"] if r.get("value") and p.get("images_s") else None,
         })
     return rows
 
@@ -88,16 +148,20 @@ def _f(v, fmt):
 def markdown(rows: list[dict], title: str) -> str:
     out = [f"## {title}", "",
            "| GPUs | images/s | ms/step | epoch s (warm) | time_elapsed s (ref quantity) | reference s | "
-           "speed-up (epoch) | speed-up (time_elapsed) | scaling eff. | all-reduce |",
-           "|---:|---:|---:|---:|---:|---:|---:|---:|---:|---|"]
+           "speed-up (epoch) | speed-up (time_elapsed) | scaling eff. | all-reduce | predicted images/s | "
+           "predicted epoch s | measured / predicted |",
+           "|---:|---:|---:|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|"]
     for r in rows:
         out.append(f"| {r['n']} | {_f(r['images_s'], ',.0f')} | {_f(r['ms_step'], '.4f')} | "
                    f"{_f(r['epoch_s'], '.4f')} | {_f(r['time_elapsed_s'], '.3f')} | {_f(r['ref_s'], '.2f')} | "
                    f"{_f(r['speedup_epoch'], ',.0f')}x | {_f(r['speedup_time_elapsed'], '.1f')}x | "
-                   f"{_f(r['efficiency'], '.1%')} | {r['allreduce'] or '-'} |")
+                   f"{_f(r['efficiency'], '.1%')} | {r['allreduce'] or '-'} | {_f(r['pred_images_s'], ',.0f')} | "
+                   f"{_f(r['pred_epoch_s'], '.4f')} | {_f(r['vs_pred'], '.2f')} |")
     out += ["", "Reference: 1 / 2 / 4 / 8 GCP e2-standard-8 CPU VMs, gloo over TCP (BASELINE.md).  Scaling is "
             "strong (global batch 64 split over the GPUs, ref src/train_dist.py:133), so per-GPU work shrinks "
-            "to 8 images per step at N = 8."]
+            "to 8 images per step at N = 8.  Predicted columns: the one-GPU loopback measurement of the "
+            "per-rank step (per-rank batch 64/N, exchange with N-1 virtual peers) + one xGMI hop; see the "
+            "module docstring of tools/scaling_report.py."]
     return "\n".join(out) + "\n"
 
 
@@ -118,6 +182,9 @@ def plot(rows: list[dict], path: Path, title: str) -> bool:
     pts = [(r["n"], r["epoch_s"]) for r in rows if r["epoch_s"]]
     if pts:
         ax.plot(*zip(*pts), "^-", color="tab:blue", label="MI355X, warm epoch (938 steps + validation)")
+    pts = [(r["n"], r["pred_epoch_s"]) for r in rows if r.get("pred_epoch_s")]
+    if pts:
+        ax.plot(*zip(*pts), "^--", color="tab:cyan", label="MI355X, predicted warm epoch (loopback + hop)")
     ax.set_xscale("log", base=2)
     ax.set_yscale("log")
     ax.set_xticks(ns)
@@ -139,12 +206,18 @@ def main(argv=None) -> int:
     ap.add_argument("inputs", nargs="+")
     ap.add_argument("--out", default="profiles/scaling")
     ap.add_argument("--title", default="Time to train 1 epoch vs number of GPUs (MNIST Net, global batch 64)")
+    ap.add_argument("--no-predict", dest="predict", action="store_false")
+    ap.add_argument("--hop-us", type=float, default=1.0, help="assumed xGMI one-way hop added for N > 1")
+    ap.add_argument("--loopback-log", help="exchange_loopback.py output replacing the built-in step table")
     a = ap.parse_args(argv)
     by_n = load_records(a.inputs)
     if not by_n:
         print("no bench records found", file=sys.stderr)
         return 1
-    rows = table(by_n)
+    pred = None
+    if a.predict:
+        pred = predict(by_n, load_loopback(a.loopback_log) if a.loopback_log else LOOPBACK_STEP_US, a.hop_us)
+    rows = table(by_n, pred)
     out = Path(a.out)
     out.parent.mkdir(parents=True, exist_ok=True)
     md = markdown(rows, a.title)
