@@ -53,6 +53,12 @@ using namespace csed::lenet;
 constexpr int TS = 4;               // samples per tile
 constexpr int NT = 1024, NW = 16;   // 16 waves, 4 per SIMD
 constexpr int X_LD = 800;           // u16 per sample image (784 + pad)
+// The normalised images are kept twice, the second copy shifted left by one pixel (X_1[i] =
+// X[i + 1]): any run of pixels X[o ..] is then 4-byte aligned in copy o & 1, so the conv1 A
+// operand (stage 1) and the conv1 wgrad B operand (stage 7), 5 / 3 / 8-pixel runs at every
+// alignment, are read as dwords instead of one ds_read_u16 per pixel.  (Four copies, for 8-byte
+// alignment, do not fit next to the weight images.)  Copy pitch 1602 dwords (== 2 mod 32).
+constexpr int XCP = TS * X_LD + 4;
 constexpr int P1H_SZ = 12 * P1H_RP; // u16 per sample: pool1 output, HWC [12][P1H_RP] (channels 10-23 zero)
 constexpr int DC2_LD = 72, DC2_SZ = 20 * DC2_LD;  // dL/dconv2 [oc][64 px] (+pad), wgrad A operand
 constexpr int DCH_SZ = 64 * DG_OCP;              // dL/dconv2 HWC interior [64 pos][24 ch], dgrad A operand
@@ -65,8 +71,8 @@ constexpr int D_COFF = D_PAR + 592 * 4;         // i16 [4][16] conv2 (lane group
 constexpr int D_DGT = D_COFF + 64 * 2;          // i32 [4][20] dgrad (lane group, K-step) -> rel | tap << 16
 constexpr int D_ONES = D_DGT + 4 * 20 * 4;      // u16 [192] 1.0: the wgrads' bias columns
 constexpr int D_ZERO = D_ONES + 192 * 2;        // u16 [192] 0: padding columns, out-of-image dgrad taps
-constexpr int D_X = D_ZERO + 192 * 2;           // u16 [TS][X_LD] normalised pixels
-constexpr int D_P1H = D_X + TS * X_LD * 2;      // u16 [TS][P1H_SZ]
+constexpr int D_X = D_ZERO + 192 * 2;           // u16 [2 copies][XCP]: [TS][X_LD] normalised pixels
+constexpr int D_P1H = D_X + (2 * XCP * 2 + 15) / 16 * 16;  // u16 [TS][P1H_SZ]
 constexpr int D_I1 = D_P1H + TS * P1H_SZ * 2;   // u8  [TS][10][144] pool1 argmax
 constexpr int D_P2 = D_I1 + TS * 1440;          // u16 [TS][320] fc1 input
 constexpr int D_I2 = D_P2 + TS * 320 * 2;       // u8  [TS][320] pool2 argmax
@@ -86,7 +92,9 @@ static_assert(5020 * 4 <= TS * P1H_SZ * 2, "conv2 slab row staging fits the dead
 static_assert(NW * 256 * 4 <= D_DBG - D_DC2, "conv1 partials fit the dead backward images");
 // dL/dconv1, dense [10][576] per sample, written at the end of stage 6 over regions dead by then:
 // samples 0, 1 in the pool1 images, samples 2, 3 in the dL/dconv2 images (contiguous)
-constexpr int DY1_SZ = 10 * 576;
+// row pitch 584 (not 576): stage 7's A reads (10 rows x 4 lane-group columns per 16-lane group)
+// go from 3-way to the unavoidable 2-way bank conflicts
+constexpr int DY1_LD = 584, DY1_SZ = 10 * DY1_LD;
 static_assert(TS == 4 && 2 * DY1_SZ * 2 <= TS * P1H_SZ * 2 && 2 * DY1_SZ * 2 <= D_DBG - D_DC2, "dL/dconv1 images");
 static_assert((W_BYTES / 16) % 256 == 0, "whole LDS-DMA rounds over waves 0-3");
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
@@ -252,6 +260,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       for (int j = 0; j < 4; ++j)
         o[j] = ok ? h16<T>(((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std) : (unsigned short)0;
       *reinterpret_cast<u16x4*>(X + s_me * X_LD + 4 * q_me) = o;
+      unsigned short* x1 = X + XCP + s_me * X_LD + 4 * q_me - 1;
+      if (q_me > 0) x1[0] = o[0];
+      *reinterpret_cast<uint32_t*>(x1 + 1) = o[1] | ((uint32_t)o[2] << 16);
+      x1[3] = o[3];
       if (q_me == 0) LAB[s_me] = lab;
     }
     if (tid < TS * 70) {
@@ -276,31 +288,31 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       const float cb = PAR[P_C1B + min(l16, 9)];
       const int q1 = l16 & 3;
       const int xl = (q1 >> 1) * 28 + 2 * (l16 >> 2) + (q1 & 1);  // window pixel of A row l16
-      const unsigned short* xr1 = X + xl + 28 * kq;                 // K slots: row kq of the taps,
-      const unsigned short* xr2 = X + xl + 112 + (kq == 1 ? W1_E1 : 0);  // then 3 taps of row 4
+      // K slots: the 5 taps of row kq (2 dwords of the aligned copy + 1 pixel), then 3 taps of
+      // row 4 (1 dword + 1 pixel); the tile offset xs below is even, so the copy is a lane constant
+      const int o1 = xl + 28 * kq, o2 = xl + 112 + (kq == 1 ? W1_E1 : 0);
+      const uint32_t* xr1 = reinterpret_cast<const uint32_t*>(X + (o1 & 1) * XCP + (o1 & ~1));
+      const unsigned short* xe1 = X + o1 + 4;
+      const uint32_t* xr2 = reinterpret_cast<const uint32_t*>(X + (o2 & 1) * XCP + (o2 & ~1));
+      const unsigned short* xe2 = X + o2 + 2;
       const int pl = kq * LD_P1H + min(l16, 9), il = min(l16, 9) * 144 + kq;  // P1H / I1 lane parts
 #pragma unroll
       for (int grp = 0; grp < 3; ++grp) {
-        uint32_t rv[3][8];
+        uint32_t r0[3], r1[3], e4[3], r2[3], e2[3];
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
           const int T9 = wave + NW * (3 * grp + it), ss = T9 / 36, mt = T9 - 36 * ss;
-          const int xs = ss * X_LD + (mt / 3) * 56 + 8 * (mt % 3);  // scalar
-          rv[it][0] = lds_u16<0>(xr1 + xs);
-          rv[it][1] = lds_u16<1>(xr1 + xs);
-          rv[it][2] = lds_u16<2>(xr1 + xs);
-          rv[it][3] = lds_u16<3>(xr1 + xs);
-          rv[it][4] = lds_u16<4>(xr1 + xs);
-          rv[it][5] = lds_u16<0>(xr2 + xs);
-          rv[it][6] = lds_u16<1>(xr2 + xs);
-          rv[it][7] = lds_u16<2>(xr2 + xs);
+          const int xs = ss * X_LD + (mt / 3) * 56 + 8 * (mt % 3);  // scalar, even
+          r0[it] = xr1[xs / 2];
+          r1[it] = xr1[xs / 2 + 1];
+          e4[it] = xe1[xs];
+          r2[it] = xr2[xs / 2];
+          e2[it] = xe2[xs];
         }
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
-          lds_wait8(rv[it]);
-          u16x8 raw;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) raw[j] = (unsigned short)rv[it][j];
+          // [t0 t1 | t2 t3 | t4 u0 | u1 u2]: row kq's 5 taps, then row 4's 3
+          const uint4 raw = make_uint4(r0[it], r1[it], e4[it] | (r2[it] << 16), (r2[it] >> 16) | (e2[it] << 16));
           const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
           const int T9 = wave + NW * (3 * grp + it), ss = T9 / 36, mt = T9 - 36 * ss;
           float best;
@@ -545,22 +557,28 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       const unsigned short* dl0 = DC2 + min(l16, 19) * DC2_LD + kb;
       const unsigned short* dl1 = DC2 + min(16 + l16, 19) * DC2_LD + kb;
       const frag ones = __builtin_bit_cast(frag, u16x8{one, one, one, one, one, one, one, one});
+      // K block j = (sample ss = j / 2, output rows 4 (j % 2) + kq): its operands are read while
+      // block j - 1 multiplies (software pipeline, as the dgrad below)
+      frag fa[2][2], fb[2][NTAP];
+      auto load = [&](int j, frag(&a_)[2], frag(&b_)[NTAP]) {
+        const int ss = j >> 1, ps = j & 1;
+        a_[0] = *reinterpret_cast<const frag*>(dl0 + ss * DC2_SZ + ps * 32);
+        a_[1] = *reinterpret_cast<const frag*>(dl1 + ss * DC2_SZ + ps * 32);
 #pragma unroll
-      for (int ss = 0; ss < TS; ++ss) {
+        for (int t = 0; t < NTAP; ++t) {
+          const unsigned short* q = pb[t] + ss * P1H_SZ + 4 * ps * P1H_RP;
+          const s16x4 r0 = lds_read_tr16(q), r1 = lds_read_tr16(q + 4 * LD_P1H);
+          b_[t] = is_bias[t] ? ones : __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      };
+      load(0, fa[0], fb[0]);
 #pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
-          // output row oy = 4 ps + kq (lane group), pixels 0..7
-          const frag fa0 = *reinterpret_cast<const frag*>(dl0 + ss * DC2_SZ + ps * 32);
-          const frag fa1 = *reinterpret_cast<const frag*>(dl1 + ss * DC2_SZ + ps * 32);
+      for (int j = 0; j < 2 * TS; ++j) {
+        if (j + 1 < 2 * TS) load(j + 1, fa[(j + 1) & 1], fb[(j + 1) & 1]);
 #pragma unroll
-          for (int t = 0; t < NTAP; ++t) {
-            const unsigned short* q = pb[t] + ss * P1H_SZ + 4 * ps * P1H_RP;
-            const s16x4 r0 = lds_read_tr16(q), r1 = lds_read_tr16(q + 4 * LD_P1H);
-            const frag fb = is_bias[t] ? ones
-                                       : __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
-            acc_w[t][0] = Mfma<T>::mma(fa0, fb, acc_w[t][0]);
-            acc_w[t][1] = Mfma<T>::mma(fa1, fb, acc_w[t][1]);
-          }
+        for (int t = 0; t < NTAP; ++t) {
+          acc_w[t][0] = Mfma<T>::mma(fa[j & 1][0], fb[j & 1][t], acc_w[t][0]);
+          acc_w[t][1] = Mfma<T>::mma(fa[j & 1][1], fb[j & 1][t], acc_w[t][1]);
         }
       }
     };
@@ -595,16 +613,23 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         f32x4 acc[NTL];
 #pragma unroll
         for (int i = 0; i < NTL; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < DG_KS; ++ks) {
+        // operands of K-step ks + 1 are read while K-step ks multiplies (software pipeline: a
+        // read-then-wait-then-MFMA chain exposes the full LDS latency on every MFMA)
+        frag fa[2][NTL], fb[2];
+        auto load = [&](int ks, frag(&a_)[NTL], frag& b_) {
           const int e = dgt[ks];
           const int rel = e & 0xffff, tap = e >> 16;
-          const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 512);
+          b_ = *reinterpret_cast<const frag*>(wrow + ks * 512);
 #pragma unroll
-          for (int i = 0; i < NTL; ++i) {
-            const unsigned short* src = ((msk[i] >> tap) & 1u) ? ab[i] + rel : ZERO;
-            acc[i] = Mfma<T>::mma(*reinterpret_cast<const frag*>(src), fb, acc[i]);
-          }
+          for (int i = 0; i < NTL; ++i)
+            a_[i] = *reinterpret_cast<const frag*>(((msk[i] >> tap) & 1u) ? ab[i] + rel : ZERO);
+        };
+        load(0, fa[0], fb[0]);
+#pragma unroll
+        for (int ks = 0; ks < DG_KS; ++ks) {
+          if (ks + 1 < DG_KS) load(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+#pragma unroll
+          for (int i = 0; i < NTL; ++i) acc[i] = Mfma<T>::mma(fa[ks & 1][i], fb[ks & 1], acc[i]);
         }
         // relu gate (pool1 output > 0) and pool1 argmax of this lane's 4 pixels, read before the
         // barrier (the dense dL/dconv1 images overwrite the pool1 images after it)
@@ -629,7 +654,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 #pragma unroll
           for (int i = 0; i < NTL; ++i) {
             const int py = p0[i] / 12, px0 = p0[i] - 12 * py;
-            unsigned short* d = DY1(si[i]) + ic * 576 + (2 * py) * 24 + 2 * px0;
+            unsigned short* d = DY1(si[i]) + ic * DY1_LD + (2 * py) * 24 + 2 * px0;
 #pragma unroll
             for (int dy = 0; dy < 2; ++dy) {
               u16x8 o;
@@ -663,22 +688,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       for (int j = 0; j < 9; ++j) {
         const int J = (wave >> 1) + 8 * j, ss = J / 18, ps = J - 18 * ss;  // wave-uniform
         const int r = 4 * ps + kq, oh = r / 3, ow0 = 8 * (r - 3 * oh);      // conv1 pixels 8 r .. 8 r + 7
-        const frag fa = *reinterpret_cast<const frag*>(DY1(ss) + oc * 576 + 8 * r);
-        const unsigned short* xb = kcol < 25 ? X + ss * X_LD + (oh + kh) * 28 + ow0 + kw : pconst;
-        uint32_t rv[8];
-        rv[0] = lds_u16<0>(xb);
-        rv[1] = lds_u16<1>(xb);
-        rv[2] = lds_u16<2>(xb);
-        rv[3] = lds_u16<3>(xb);
-        rv[4] = lds_u16<4>(xb);
-        rv[5] = lds_u16<5>(xb);
-        rv[6] = lds_u16<6>(xb);
-        rv[7] = lds_u16<7>(xb);
-        lds_wait8(rv);
-        u16x8 bv;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) bv[jj] = (unsigned short)rv[jj];
-        acc_c1 = Mfma<T>::mma(fa, __builtin_bit_cast(frag, bv), acc_c1);
+        const frag fa = *reinterpret_cast<const frag*>(DY1(ss) + oc * DY1_LD + 8 * r);
+        // pixels X[o .. o + 7], o = (oh + kh) * 28 + ow0 + kw == kw (mod 2): copy kw & 1
+        const uint32_t* xb = reinterpret_cast<const uint32_t*>(
+            kcol < 25 ? X + (kw & 1) * XCP + ss * X_LD + (oh + kh) * 28 + ow0 + (kw & ~1) : pconst);
+        acc_c1 = Mfma<T>::mma(fa, __builtin_bit_cast(frag, make_uint4(xb[0], xb[1], xb[2], xb[3])), acc_c1);
       }
     }
     lds_barrier();
