@@ -133,12 +133,28 @@ def run_cpu(args, ctx, t_start: float) -> dict:
             "time_elapsed_s": all_reduce_max(ctx, time.time() - t_start)}
 
 
+def start_native_data():
+    """The data set, generated natively (csrc/data/synth_mnist.cpp) in a background thread
+    that runs while ``import torch`` does: this file loads data/native_synth.py by path (numpy +
+    ctypes, not the package, which imports torch).  None when the library is not built."""
+    import importlib.util
+
+    path = os.path.join(ROOT, "csed_514_project_distributed_training_using_pytorch_amd", "data", "native_synth.py")
+    spec = importlib.util.spec_from_file_location("_csed_native_synth", path)
+    ns = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ns)
+    if not ns.available():
+        return None
+    return ns.Job(60000, 10000, seed=0)
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn(args, argv)
     t_start = float(os.environ.get("CSED_BENCH_T0", T_START))
+    native_job = start_native_data() if args.device == "cuda" and not os.environ.get("CSED_TORCH_DATA") else None
 
     import torch
     import torch.distributed as dist
@@ -153,7 +169,7 @@ def main(argv=None) -> int:
         return 2
     backend = None if args.backend == "auto" else args.backend
     data_job = None
-    if args.device == "cuda":  # the data set builds (CPU threads) while the GPU context comes up
+    if args.device == "cuda" and native_job is None:  # the data set builds (CPU threads) while the GPU context comes up
         from concurrent.futures import ThreadPoolExecutor
 
         from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
@@ -180,7 +196,16 @@ def main(argv=None) -> int:
 
         dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
         with prof.range("bench:data"):
-            train, test = data_job.result()
+            if native_job is not None:
+                from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNISTData
+
+                (xi, xl), (ti, tl) = native_job.result()
+                train = MNISTData(torch.from_numpy(xi), torch.from_numpy(xl), synthetic=True)
+                test = MNISTData(torch.from_numpy(ti), torch.from_numpy(tl), synthetic=True)
+                data_src = "native generator (csrc/data/synth_mnist.cpp), overlapped with import torch"
+            else:
+                train, test = data_job.result()
+                data_src = "data/mnist.py:synthetic_mnist (torch CPU ops)"
         use_graph = not args.no_graph
 
         def sync_barrier():
@@ -339,6 +364,7 @@ def main(argv=None) -> int:
                                  "(like-for-like: vs_baseline_time_elapsed, vs_baseline_epoch)",
             "dtype": args.dtype if args.device == "cuda" else "fp32",
             "data": "synthetic (60000 x 1x28x28 uint8, class-conditional stroke mixture; random-init weights)",
+            "data_source": data_src if args.device == "cuda" else "data/mnist.py:synthetic_mnist",
             "config": {"model": "Net (ref src/model.py, 21,840 params)", "global_batch": args.global_batch,
                        "seq_len": None, "parallelism": f"dp{n}", "optimizer": "SGD lr=0.02 momentum=0.5",
                        "engine": cfg_engine, "hip_graph": hip_graph, "allreduce": allreduce, "step": step_kind,

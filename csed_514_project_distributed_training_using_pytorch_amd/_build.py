@@ -144,12 +144,36 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     return SO_PATH
 
 
+DATA_SO = PKG_DIR / "_csed_data.so"
+
+
+def build_data_lib(force: bool = False, verbose: bool = True) -> Path:
+    """Host-only native data generator (``csrc/data/synth_mnist.cpp`` -> ``_csed_data.so``):
+    plain g++, no torch and no HIP, so it loads before ``import torch``."""
+    src = CSRC / "data" / "synth_mnist.cpp"
+    if not force and DATA_SO.exists() and DATA_SO.stat().st_mtime >= src.stat().st_mtime:
+        return DATA_SO
+    cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++")
+    if not cxx:
+        raise RuntimeError("no host C++ compiler for the data generator")
+    tmp = DATA_SO.with_suffix(".so.tmp")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-ffp-contract=off", "-march=x86-64-v2", str(src), "-o", str(tmp)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, DATA_SO)
+    if verbose:
+        print(f"[csed build] built {DATA_SO}", flush=True)
+    return DATA_SO
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.jobs)
+    build_data_lib(force=a.force)
     return 0
 
 
