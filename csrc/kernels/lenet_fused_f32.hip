@@ -26,6 +26,8 @@
 // MFMA f32 16x16x4 operand layout: lane l holds A[row l&15][k 4*ks + (l>>4)] and
 // B[k 4*ks + (l>>4)][col l&15]; accumulator register j holds C[4*(l>>4) + j][l&15].  Padding
 // rows / columns of A / B only feed discarded outputs; K padding reads exact zeros.
+#include <type_traits>
+
 #include "common.h"
 #include "dispatch.h"
 #include "kernels/lenet_layout.h"
@@ -57,8 +59,9 @@ constexpr int F_END = F_RED + 8192;
 constexpr int B_I1 = F_END * 4;               // u8  [1440] pool1 argmax
 constexpr int B_I2 = B_I1 + 1440;             // u8  [320]  pool2 argmax
 constexpr int B_XPOS = B_I2 + 320;            // u16 [1440] X offset of the pool1 argmax pixel
-constexpr int B_K2 = B_XPOS + 2880;           // u16 [256]  conv2 fwd: k -> P1 offset
-constexpr int B_DBG = B_K2 + 512;             // u64 [16]   stage stamps (a.dbg, diagnostics)
+constexpr int B_K2 = B_XPOS + 2880;           // u16 [4][64] conv2 fwd: (lane group q, K-step ks) -> P1 offset of k = 4 ks + q
+constexpr int B_K2L = B_K2 + 512;             // u16 [256]  the same offsets in k order (conv2 fwd VALU part)
+constexpr int B_DBG = B_K2L + 512;            // u64 [16]   stage stamps (a.dbg, diagnostics)
 constexpr int LDS_BYTES = B_DBG + 16 * 8;
 static_assert(LDS_BYTES <= 160 * 1024, "lds");
 static_assert(F_W2 % 4 == 0 && F_W1B % 4 == 0 && F_PAR % 4 == 0 && F_X % 4 == 0 && F_P1 % 4 == 0 &&
@@ -78,6 +81,8 @@ __device__ __forceinline__ int opaque(int x) {
 __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+
+__device__ int64_t kF32Zero = 0;  // the counter an absent cursor / Philox offset reads
 
 // conv2 dgrad work units: (tile t < 9, oc block j < 5) of 25 K-steps, tile-major; wave w owns
 // units [unit_lo(w), unit_lo(w + 1)): at most 3 units spanning at most 2 tiles
@@ -110,6 +115,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   uint8_t* I2 = smem + B_I2;
   unsigned short* XPOS = reinterpret_cast<unsigned short*>(smem + B_XPOS);
   unsigned short* K2 = reinterpret_cast<unsigned short*>(smem + B_K2);
+  unsigned short* K2L = reinterpret_cast<unsigned short*>(smem + B_K2L);
   uint64_t* DBGS = reinterpret_cast<uint64_t*>(smem + B_DBG);
   // Diagnostic stamps (a.dbg non-null): thread 0 records s_memtime at kernel entry (0), after the
   // preamble (1), at stage k's start of the first sample (2 + k, k = 0..8), at its end (11) and at
@@ -118,7 +124,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   do {                                                                      \
     if (a.dbg && tid == 0 && s == 0) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-  if (a.dbg && threadIdx.x == 0) DBGS[0] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && threadIdx.x == 0) {
+    DBGS[0] = __builtin_amdgcn_s_memtime();
+    DBGS[13] = __builtin_amdgcn_s_memrealtime();  // (100 MHz, one clock for every XCD: skew)
+  }
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -128,38 +137,69 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   const bool own = part == 0;      // writes the sample's fc vectors and loss
   const int R2 = STAGED ? a.B : G; // slab rows of the conv2 chunks (one per sample in the split step)
   const float inv_std = 1.f / a.std_;
-  const uint64_t rng_off = TRAIN ? rng_offset(0, a.rng_offset) : 0;
+  // The step counters load into VGPRs through an opaque lane index and without a branch (an
+  // absent counter reads a zero word): a uniform load is moved to SGPRs with a wait right
+  // behind it, in front of the whole preamble (as lenet_tile.hip)
+  const int lane0 = opaque(0);
+  const int64_t cur0 = (a.cursor ? a.cursor : &kF32Zero)[lane0];
+  const uint64_t rng_off = TRAIN ? (uint64_t)((a.rng_offset ? a.rng_offset : &kF32Zero)[lane0]) << 20 : 0;
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
-  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + g;
+  const int64_t pbase = cur0 * (int64_t)a.B + g;
   const bool stage_next = STAGED && a.stage_next;
   // this part's dgrad M-tiles: {part, part + 4, part + 8 (part 0)}; all 9 without the split
   const int ntl = STAGED ? (part == 0 ? 3 : 2) : 9;
   auto tile_of = [&](int ti) { return STAGED ? part + 4 * ti : ti; };
   auto row_of = [&](int s) { return a.perm[min(pbase + (int64_t)min(s, max(nsamp - 1, 0)) * G, a.perm_len - 1)]; };
 
+  // sample pipeline: pixels (4 per thread) and label of sample s, row of sample s+1
+  uint32_t px = 0, px_next = 0;
+  int lab = 0;
+  int64_t rown = 0, lab_next = 0;
+  if (STAGED) {
+    // the staged batch (row g of the staging buffer), loaded before the weights; the next
+    // step's row (for the staging of step cursor + 1) is looked up at stage 0, its pixels
+    // loaded at stage 3 and stored at the end
+    px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(tid, 195)];
+    // (the label's low dword only, into a VGPR: no wait until stage 0 -- a 64-bit load whose
+    // dead high half is re-used at once is waited for on the spot)
+    lab = reinterpret_cast<const int*>(a.lstage + g)[2 * lane0];
+  }
+
   // ---------------- once per workgroup: fp32 parameters -> LDS, constant tables
   {
+    // every global load of the preamble is issued before the first LDS store (one round trip)
     const float4* f1 = reinterpret_cast<const float4*>(a.params + O_F1W);  // 4000 float4
-    for (int q = tid; q < 4000; q += NT) {
-      const float4 v = f1[q];
-      const int e = 4 * q, o = e / 320, i = e - o * 320;  // 320 % 4 == 0: no row crossing
-      float* d = W1 + o * LW1 + i;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    constexpr int NF1 = (4000 + NT - 1) / NT, NW2 = (20 * LW2 + NT - 1) / NT;
+    float4 v1[NF1];
+    float v2[NW2];
+#pragma unroll
+    for (int j = 0; j < NF1; ++j) v1[j] = f1[min(tid + j * NT, 3999)];
+#pragma unroll
+    for (int j = 0; j < NW2; ++j) {
+      const int q = min(tid + j * NT, 20 * LW2 - 1), oc = q / LW2, k = q - oc * LW2;
+      v2[j] = a.params[O_C2W + oc * 250 + min(k, 249)];
     }
-    for (int q = tid; q < 20 * LW2; q += NT) {
-      const int oc = q / LW2, k = q - oc * LW2;
-      W2[q] = k < 250 ? a.params[O_C2W + oc * 250 + k] : 0.f;
+    const int n1 = min(tid, 447) / 28, k1 = min(tid, 447) - 28 * (min(tid, 447) / 28);
+    const float vb = a.params[O_C1W + min(n1, 9) * 25 + min(k1, 24)];
+    const int qp = min(tid, 589);
+    const float vp = a.params[qp < 10 ? O_C1B + qp : qp < 30 ? O_C2B + qp - 10 : qp < 80 ? O_F1B + qp - 30
+                                                        : qp < 90 ? O_F2B + qp - 80 : O_F2W + qp - 90];
+#pragma unroll
+    for (int j = 0; j < NF1; ++j) {
+      const int q = tid + j * NT;
+      if (q < 4000) {
+        const int e = 4 * q, o = e / 320, i = e - o * 320;  // 320 % 4 == 0: no row crossing
+        float* d = W1 + o * LW1 + i;
+        d[0] = v1[j].x; d[1] = v1[j].y; d[2] = v1[j].z; d[3] = v1[j].w;
+      }
     }
-    if (tid < 448) {
-      const int n = tid / 28, k = tid - n * 28;
-      W1B[tid] = (n < 10 && k < 25) ? a.params[O_C1W + n * 25 + k] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NW2; ++j) {
+      const int q = tid + j * NT, k = q - (q / LW2) * LW2;
+      if (q < 20 * LW2) W2[q] = k < 250 ? v2[j] : 0.f;
     }
-    if (tid < 590) {
-      const int q = tid;
-      const int src = q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30
-                                                                : q < 90 ? O_F2B + q - 80 : O_F2W + q - 90;
-      PAR[q] = a.params[src];
-    }
+    if (tid < 448) W1B[tid] = (n1 < 10 && k1 < 25) ? vb : 0.f;
+    if (tid < 590) PAR[tid] = vp;
     if (tid < 96) {
       L[F_ONES + tid] = 1.f;
       L[F_ZEROS + tid] = 0.f;
@@ -167,8 +207,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     if (tid < 4) X[784 + tid] = 0.f;
     if (tid == 0) DY2[1280] = 0.f;
     if (tid < 256) {  // conv2 fwd A offsets: k = ic*25 + kh*5 + kw -> ic*144 + kh*12 + kw (K pad -> k 249)
-      const int k = min(tid, 249), ic = k / 25, r = k - 25 * ic;
+      const int k = min(4 * (tid & 63) + (tid >> 6), 249), ic = k / 25, r = k - 25 * ic;
       K2[tid] = (unsigned short)(ic * 144 + (r / 5) * 12 + (r % 5));
+      const int kl = min(tid, 249), icl = kl / 25, rl = kl - 25 * icl;
+      K2L[tid] = (unsigned short)(icl * 144 + (rl / 5) * 12 + (rl % 5));
     }
   }
   // conv1 A offsets of this lane's 7 K-steps (tap k = 4*ks + kq, K pad clamped to tap 24)
@@ -184,17 +226,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   float acc_c1 = 0.f;                                                      // conv1 wgrad (tid < 260)
   float loss_sum = 0.f, correct = 0.f;
 
-  // sample pipeline: pixels (4 per thread) and label of sample s, row of sample s+1
-  uint32_t px = 0, px_next = 0;
-  int lab = 0;
-  int64_t rown = 0, lab_next = 0;
-  if (STAGED) {
-    // the staged batch (row g of the staging buffer); the next step's row for the staging of
-    // step cursor + 1 (loaded here, its pixels at stage 3, stored at the end)
-    px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)g * 784)[min(tid, 195)];
-    lab = (int)a.lstage[g];
-    if (stage_next) rown = a.perm[min((a.cursor[0] + 1) * (int64_t)a.B + b0, a.perm_len - 1)];
-  } else if (nsamp > 0) {
+  if (!STAGED && nsamp > 0) {
     const int64_t r0 = row_of(0);
     px = reinterpret_cast<const uint32_t*>(a.images + r0 * 784)[min(tid, 195)];
     lab = (int)a.labels[r0];
@@ -210,6 +242,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     __syncthreads();  // previous sample's readers done (first pass: the preamble's writes)
     STAMP32(2);
     // ---------------- stage 0: pixels, dropout masks; the next sample's loads
+    if (stage_next && wave >= 12) rown = a.perm[min((cur0 + 1) * (int64_t)a.B + b0, a.perm_len - 1)];
     if (tid < 196) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -239,18 +272,31 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
 #pragma unroll
       for (int ks = 0; ks < 7; ++ks) bv[ks] = W1B[l16 * 28 + 4 * ks + kq];
       const float cb = PAR[P_C1B + min(l16, 9)];
+      // the 3 (waves 0-3) or 2 M-tiles of this wave: all A reads first, then independent MFMA
+      // chains interleaved (each chain in K order, as one tile at a time)
+      auto tiles = [&](auto nti) {
+        constexpr int NTI = decltype(nti)::value;
+        float av[NTI][7];
 #pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        const int mt = wave + it * NW;
-        if (mt < 36) {
+        for (int it = 0; it < NTI; ++it) {
+          const int mt = wave + it * NW;
           const int m = mt * 16 + l16, p = m >> 2, q = m & 3;
           const int base = (2 * (p / 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1);
-          float av[7];
 #pragma unroll
-          for (int ks = 0; ks < 7; ++ks) av[ks] = X[base + c1k[ks]];
-          f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int ks = 0; ks < 7; ++ks) av[it][ks] = X[base + c1k[ks]];
+        }
+        f32x4 cc[NTI];
 #pragma unroll
-          for (int ks = 0; ks < 7; ++ks) c = mma(av[ks], bv[ks], c);
+        for (int it = 0; it < NTI; ++it) cc[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 7; ++ks)
+#pragma unroll
+          for (int it = 0; it < NTI; ++it) cc[it] = mma(av[it][ks], bv[ks], cc[it]);
+#pragma unroll
+        for (int it = 0; it < NTI; ++it) {
+          const int mt = wave + it * NW;
+          {
+          const f32x4 c = cc[it];
           if (l16 < 10) {
             float best = c[0];
             int bi = 0;
@@ -264,45 +310,122 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
           }
         }
       }
+      };
+      if (wave < 36 - 2 * NW) tiles(std::integral_constant<int, 3>{});
+      else tiles(std::integral_constant<int, 2>{});
     }
     __syncthreads();
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
+    // oc 0-15: one MFMA N-tile, 4 M-tiles x 2 K halves on waves 0-3 / 8-11.  oc 16-19 (a second
+    // N-tile would be 3/4 padding, and the fp32 MFMA rate bounds this stage): VALU on waves
+    // 4-7 / 12-15, lane = pixel, 4 accumulators, K split 8 ways; both run at once.
     STAMP32(4);
     {
-      const int tile = wave & 7, half = wave >> 3;  // K-steps [0, 32) / [32, 63)
-      const int mt = tile & 3, nt = tile >> 2;
-      const int m = mt * 16 + l16, w = m >> 2, q = m & 3;
-      const int abase = (2 * (w >> 2) + (q >> 1)) * 12 + 2 * (w & 3) + (q & 1);
-      const float* wrow = W2 + min(nt * 16 + l16, 19) * LW2;  // rows >= 20 feed discarded columns
-      f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int ks0 = half * 32, nks = half ? 31 : 32;
-#pragma unroll 8
-      for (int u = 0; u < nks; ++u) {
-        const int k = 4 * (ks0 + u) + kq;
-        c = mma(P1[abase + K2[k]], wrow[k], c);
-      }
-      if (half) {
+      const bool mf = (wave & 4) == 0;
+      const int half = wave >> 3, mt = wave & 3;  // MFMA: K-steps [0, 32) / [32, 63)
+      if (mf) {
+        const int m = mt * 16 + l16, w = m >> 2, q = m & 3;
+        const int abase = (2 * (w >> 2) + (q >> 1)) * 12 + 2 * (w & 3) + (q & 1);
+        const float* wrow = W2 + l16 * LW2;
+        // K-steps ks0 .. ks0 + NK - 1 in order, their operands read 8 K-steps at a time (the
+        // lane's offsets are one 16-byte read of its K2 row), so no MFMA waits on a table read
+        // followed by a dependent operand read
+        const unsigned short* kt = K2 + kq * 64;
+        // (the next 8 K-steps' operands are read while these 8 multiply; offsets one chunk
+        // further ahead)
+        auto run = [&](auto nk, int ks0) {
+          constexpr int NK = decltype(nk)::value, NC = (NK + 7) / 8;
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+          float av[2][8], bv[2][8];
+          auto ld = [&](int c8, const u16x8& o, float(&aa)[8], float(&bb)[8]) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) RED[tile * 256 + r * 64 + lane] = c[r];
+            for (int j = 0; j < 8; ++j)
+              if (8 * c8 + j < NK) {
+                aa[j] = P1[abase + o[j]];
+                bb[j] = wrow[4 * (ks0 + 8 * c8 + j) + kq];
+              }
+          };
+          u16x8 o = *reinterpret_cast<const u16x8*>(kt + ks0);
+          ld(0, o, av[0], bv[0]);
+#pragma unroll
+          for (int c8 = 0; c8 < NC; ++c8) {
+            if (c8 + 1 < NC) {
+              o = *reinterpret_cast<const u16x8*>(kt + ks0 + 8 * (c8 + 1));
+              ld(c8 + 1, o, av[(c8 + 1) & 1], bv[(c8 + 1) & 1]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (8 * c8 + j < NK) acc = mma(av[c8 & 1][j], bv[c8 & 1][j], acc);
+          }
+          return acc;
+        };
+        const f32x4 c = half ? run(std::integral_constant<int, 31>{}, 32) : run(std::integral_constant<int, 32>{}, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) RED[(half * 4 + mt) * 256 + r * 64 + lane] = c[r];
+      } else {
+        // k in [32 vw, 32 vw + 32) of 250; lane = pixel m (pool-fused order, as the MFMA rows)
+        const int vw = mt + 4 * half, k0 = 32 * vw, m = lane, w = m >> 2, q = m & 3;
+        const float* pa = P1 + (2 * (w >> 2) + (q >> 1)) * 12 + 2 * (w & 3) + (q & 1);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c8 = 0; c8 < 4; ++c8) {
+          const int kb = k0 + 8 * c8;  // (k >= 250: zero weights, clamped offsets)
+          const u16x8 o = *reinterpret_cast<const u16x8*>(K2L + kb);
+          float av[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) av[j] = pa[o[j]];
+#pragma unroll
+          for (int oc = 0; oc < 4; ++oc) {
+            const float4 w0 = *reinterpret_cast<const float4*>(W2 + (16 + oc) * LW2 + kb);
+            const float4 w1 = *reinterpret_cast<const float4*>(W2 + (16 + oc) * LW2 + kb + 4);
+            acc[oc] = fmaf(av[0], w0.x, acc[oc]);
+            acc[oc] = fmaf(av[1], w0.y, acc[oc]);
+            acc[oc] = fmaf(av[2], w0.z, acc[oc]);
+            acc[oc] = fmaf(av[3], w0.w, acc[oc]);
+            acc[oc] = fmaf(av[4], w1.x, acc[oc]);
+            acc[oc] = fmaf(av[5], w1.y, acc[oc]);
+            acc[oc] = fmaf(av[6], w1.z, acc[oc]);
+            acc[oc] = fmaf(av[7], w1.w, acc[oc]);
+          }
+        }
+#pragma unroll
+        for (int oc = 0; oc < 4; ++oc) RED[2048 + vw * 256 + oc * 64 + m] = acc[oc];
       }
       __syncthreads();
-      if (!half) {
-        const int oc = nt * 16 + l16;
+      auto emit = [&](int oc, int wp, float best, int bi) {
+        const float v = fmaxf(best + PAR[P_C2B + oc], 0.f) * SM[S_D2S + oc];
+        P2[oc * 16 + wp] = v;
+        I2[oc * 16 + wp] = (uint8_t)bi;
+        if (wvec) vs[V_P2 + oc * 16 + wp] = v;
+      };
+      if (wave < 4) {  // oc 0-15: the two K halves, then pool (window wp = 4 mt + kq, pixels r)
+        float c[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] += RED[tile * 256 + r * 64 + lane];
-        if (oc < 20) {
-          float best = c[0];
-          int bi = 0;
+        for (int r = 0; r < 4; ++r) c[r] = RED[mt * 256 + r * 64 + lane] + RED[(4 + mt) * 256 + r * 64 + lane];
+        float best = c[0];
+        int bi = 0;
 #pragma unroll
-          for (int r = 1; r < 4; ++r)
-            if (c[r] > best) { best = c[r]; bi = r; }
-          const int wp = mt * 4 + kq;
-          const float v = fmaxf(best + PAR[P_C2B + oc], 0.f) * SM[S_D2S + oc];
-          P2[oc * 16 + wp] = v;
-          I2[oc * 16 + wp] = (uint8_t)bi;
-          if (wvec) vs[V_P2 + oc * 16 + wp] = v;
+        for (int r = 1; r < 4; ++r)
+          if (c[r] > best) { best = c[r]; bi = r; }
+        emit(l16, mt * 4 + kq, best, bi);
+      } else if (wave == 4) {  // oc 16-19: the 8 K parts in order, then pool (lane: oc, window)
+        const int o4 = lane >> 4, wp = lane & 15;
+        float c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = 0.f;
+#pragma unroll
+          for (int v8 = 0; v8 < 8; ++v8) t += RED[2048 + v8 * 256 + o4 * 64 + 4 * wp + r];
+          c[r] = t;
         }
+        float best = c[0];
+        int bi = 0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r)
+          if (c[r] > best) { best = c[r]; bi = r; }
+        emit(16 + o4, wp, best, bi);
       }
     }
     __syncthreads();
@@ -417,14 +540,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     // ---------------- stage 5: dP2 = dZ1 . W1 (VALU), pool2 / relu / Dropout2d backward -> DY2
     STAMP32(7);
     {
-      if (tid < 960) {
-        const int i = tid % 320, part = tid / 320, o0 = 17 * part, o1 = min(o0 + 17, 50);
+      if (wave < 15) {
+        // output range pr (fc1 units 17 pr .. 17 pr + 16) on waves 5 pr .. 5 pr + 4, so the
+        // bounds are wave-uniform; column i = 64 (wave % 5) + lane
+        const int pr = wave / 5, i = (wave - 5 * pr) * 64 + lane, o0 = 17 * pr, o1 = min(o0 + 17, 50);
         float d0 = 0.f, d1 = 0.f;
-        for (int o = o0; o < o1; o += 2) {
-          d0 = fmaf(SM[S_DZ1 + o], W1[o * LW1 + i], d0);
+#pragma unroll
+        for (int u = 0; u < 17; u += 2) {  // (the same two chains as a loop over o in [o0, o1))
+          const int o = o0 + u;
+          if (o < o1) d0 = fmaf(SM[S_DZ1 + o], W1[o * LW1 + i], d0);
           if (o + 1 < o1) d1 = fmaf(SM[S_DZ1 + o + 1], W1[(o + 1) * LW1 + i], d1);
         }
-        RED[part * 320 + i] = d0 + d1;
+        RED[pr * 320 + i] = d0 + d1;
       }
       __syncthreads();
       if (tid < 320) {
@@ -475,31 +602,75 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
       const float* bcol = W2 + kq * LW2 + min(l16, 9) * 25;  // columns >= 10: discarded outputs
       const float* ZR = L + F_ZEROS;  // >= 37 zeros
-      for (int u = u0; u < u1; ++u) {  // wave-uniform
-        const int ti = u / 5, j = u - 5 * ti, t = tile_of(ti);
-        const int p = t * 16 + l16, y = p / 12, x = p - 12 * (p / 12);
-        const float* arow = DY2 + (4 * j + kq) * 64 + y * 8 + x - 36;  // tap (kh, kw): [36 - kh*8 - kw]
-        const float* brow = bcol + 4 * j * LW2;
-        // taps with 0 <= y - kh < 8 and 0 <= x - kw < 8, as a 25-bit mask (bit kh*5 + kw): per tap
-        // one bit test selects the row pointer or the zero run, and the load keeps an immediate
-        // offset
-        const uint32_t rb = ((2u << min(4, y)) - 1u) & ~((1u << max(0, y - 7)) - 1u);
-        const uint32_t cb = ((2u << min(4, x)) - 1u) & ~((1u << max(0, x - 7)) - 1u);
-        uint32_t m = 0;
+      // this wave's (wave-uniform) 1-3 units run interleaved, each as two MFMA chains (even /
+      // odd taps): a single 25-MFMA dependent chain per unit is latency-bound
+      auto units = [&](auto nu_c) {
+        constexpr int NU = decltype(nu_c)::value;
+        const float* arow[NU];
+        const float* brow[NU];
+        uint32_t msk[NU];
+        f32x4 ce[NU], co[NU];
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh) m |= ((rb >> kh) & 1u) ? (cb << (5 * kh)) : 0u;
-        f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < NU; ++i) {
+          const int u = u0 + i, ti = u / 5, j = u - 5 * ti, t = tile_of(ti);
+          const int p = t * 16 + l16, y = p / 12, x = p - 12 * (p / 12);
+          arow[i] = DY2 + (4 * j + kq) * 64 + y * 8 + x - 36;  // tap (kh, kw): [36 - kh*8 - kw]
+          brow[i] = bcol + 4 * j * LW2;
+          // taps with 0 <= y - kh < 8 and 0 <= x - kw < 8, as a 25-bit mask (bit kh*5 + kw): per
+          // tap one bit test selects the row pointer or the zero run, and the load keeps an
+          // immediate offset
+          const uint32_t rb = ((2u << min(4, y)) - 1u) & ~((1u << max(0, y - 7)) - 1u);
+          const uint32_t cb = ((2u << min(4, x)) - 1u) & ~((1u << max(0, x - 7)) - 1u);
+          uint32_t m = 0;
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh) {
+          for (int kh = 0; kh < 5; ++kh) m |= ((rb >> kh) & 1u) ? (cb << (5 * kh)) : 0u;
+          msk[i] = m;
+          ce[i] = co[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // the NU x 25 (unit, tap) steps in chunks of 8, the operands of chunk c + 1 read while
+        // chunk c multiplies (software pipeline: a read -> wait -> MFMA chain exposes the LDS
+        // latency on every MFMA)
+        constexpr int S = NU * 25, NC = (S + 7) / 8;
+        float a_[2][8], b_[2][8];
+        auto ld = [&](int c, float(&aa)[8], float(&bb)[8]) {
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) {
-            const float* ap = (m & (1u << (kh * 5 + kw))) ? arow : ZR;
-            c = mma(ap[36 - (kh * 8 + kw)], brow[kh * 5 + kw], c);
+          for (int j = 0; j < 8; ++j) {
+            const int st = 8 * c + j;
+            if (st < S) {
+              const int i = st / 25, tap = st - 25 * i, kh = tap / 5, kw = tap - 5 * kh;
+              const float* ap = (msk[i] & (1u << tap)) ? arow[i] : ZR;
+              aa[j] = ap[36 - (kh * 8 + kw)];
+              bb[j] = brow[i][tap];
+            }
+          }
+        };
+        ld(0, a_[0], b_[0]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (c + 1 < NC) ld(c + 1, a_[(c + 1) & 1], b_[(c + 1) & 1]);
+          // (keeps the scheduler from sinking those reads back next to their MFMAs)
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int st = 8 * c + j;
+            if (st < S) {
+              const int i = st / 25, tap = st - 25 * i;
+              if (tap & 1) co[i] = mma(a_[c & 1][j], b_[c & 1][j], co[i]);
+              else ce[i] = mma(a_[c & 1][j], b_[c & 1][j], ce[i]);
+            }
           }
         }
-        if (ti == t0) acc0 += c;
-        else acc1 += c;
-      }
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+          const f32x4 c = ce[i] + co[i];
+          if ((u0 + i) / 5 == t0) acc0 += c;
+          else acc1 += c;
+        }
+      };
+      const int nun = u1 - u0;  // (wave-uniform; at most 3: 45 units over 16 waves)
+      if (nun == 3) units(std::integral_constant<int, 3>{});
+      else if (nun == 2) units(std::integral_constant<int, 2>{});
+      else if (nun == 1) units(std::integral_constant<int, 1>{});
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         RED[(wd * 2) * 256 + r * 64 + lane] = acc0[r];
@@ -593,7 +764,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     a.loss_acc[2 * g + 1] = own ? correct : 0.f;
   }
   if (a.dbg) {
-    if (tid == 0) DBGS[12] = __builtin_amdgcn_s_memtime();
+    if (tid == 0) {
+      DBGS[12] = __builtin_amdgcn_s_memtime();
+      DBGS[14] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
     if (tid < 16) a.dbg[g * 32 + tid] = DBGS[tid];
   }

@@ -99,6 +99,9 @@ static_assert(TS == 4 && 2 * DY1_SZ * 2 <= TS * P1H_SZ * 2 && 2 * DY1_SZ * 2 <= 
 static_assert((W_BYTES / 16) % 256 == 0, "whole LDS-DMA rounds over waves 0-3");
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 
+__device__ int64_t kTileZero = 0;  // the counter an absent cursor / Philox offset reads (global memory: a
+                                 // __constant__ word would turn the loads into flat ones, which lgkmcnt waits count)
+
 template <typename T, bool TRAIN>
 __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
   struct Kargs { LenetTrainArgs a; int write_logp; float* logp_out; };
@@ -140,7 +143,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   do {                                                                              \
     if (a.dbg && tid == 0 && tile == g) DBGS[(i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-  if (a.dbg && threadIdx.x == 0) DBGS[0] = __builtin_amdgcn_s_memtime();
+  if (a.dbg && threadIdx.x == 0) {
+    DBGS[0] = __builtin_amdgcn_s_memtime();
+    DBGS[12] = __builtin_amdgcn_s_memrealtime();  // (100 MHz, one clock for every XCD: skew)
+  }
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -148,11 +154,35 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   const int G = a.grid, g = blockIdx.x, B = a.B;
   const int ntile = (B + TS - 1) / TS;
   const float inv_std = 1.f / a.std_;
-  const uint64_t rng_ctr = (TRAIN && a.rng_offset) ? (uint64_t)a.rng_offset[0] : 0ull;
-  const int64_t pbase = (a.cursor ? a.cursor[0] : 0) * (int64_t)B;
+  // The preamble's global loads are ordered so that nothing waits on a chain: the step counters
+  // and the staged first tile first, then the weight DMA; the rows that depend on the cursor
+  // (cursor -> perm) are loaded after the barrier and first used at stage 4.
+  // (through an opaque lane index the two counters load into VGPRs: a uniform load would be
+  // moved to SGPRs with a wait right behind it, in front of everything else)
+  // (and without a branch: an absent counter reads a zero word)
+  const int lane0 = opaque(0);
+  const int64_t cur0 = (a.cursor ? a.cursor : &kTileZero)[lane0];
+  const uint64_t rng_ctr = (uint64_t)((TRAIN && a.rng_offset) ? a.rng_offset : &kTileZero)[lane0];
+  const int64_t pbase = cur0 * (int64_t)B;
   auto perm_at = [&](int b) { return a.perm[min(pbase + (int64_t)min(b, B - 1), a.perm_len - 1)]; };
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   const unsigned short one = h16<T>(1.f);
+  // first tile's pixels (threads < TS * 196: sample tid / 196, pixels 4 * (tid % 196) ..)
+  const int s_me = min(tid / 196, TS - 1), q_me = tid - 196 * (tid / 196);
+  const bool px_thread = tid < TS * 196;
+  uint32_t px = 0, px_next = 0;
+  int lab = 0;
+  int64_t nrow = 0, srow = 0, lab_next = 0;
+  // Staged (a.xstage: one 784-byte row per sample of every workgroup's FIRST tile, row g * TS + s,
+  // written by the previous step's kernel or lenet_stage at epoch start): the first tile starts
+  // without the dependent cursor -> perm -> image chain (~5 us in front of stage 1 otherwise,
+  // tools/stage_profile_tile.py); this step stages the next step's first tile (stage_next).
+  const bool staged = a.xstage != nullptr;
+  const bool stage_next = TRAIN && staged && a.stage_next;
+  if (staged && px_thread && g < ntile) {
+    px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)(g * TS + s_me) * 784)[q_me];
+    if (q_me == 0) lab = reinterpret_cast<const int*>(a.lstage + g * TS + s_me)[0];  // (low dword)
+  }
 
   // ---------------- once per workgroup: weight images, fp32 params, tables, zero padding
   if (wave < 4) {
@@ -162,32 +192,39 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     for (int u = 0; u < W_BYTES / 16 / 256; ++u)
       __builtin_amdgcn_global_load_lds((glb_void*)(const_cast<uint4*>(src + u * 256 + tid)),
                                        (lds_void*)(wsm + (u * 256 + wave * 64) * 16), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the images are in LDS before the barrier
   } else if (wave < 8) {
     const int t = tid - 256;
     auto par_index = [](int q) {
       return q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30 : q < 90 ? O_F2B + q - 80
                                                                                           : O_F2W + q - 90;
     };
+    // every global load of these waves first (unconditional, clamped indices), then the stores:
+    // one round trip instead of one per dependent store
+    float pv[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * 256, 589))];
+    const uint4 w1c = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[min(t, 63)];
+    // conv2 A offset of K-step ks for lane group q: K slice kC2Order[4*ks + q] = channels
+    // 8*(kg&1) .. +7 of tap kg>>1 (slices >= 50 meet zero weights)
+    const int tq = (t >> 4) & 3, tks = t & 15;
+    const int kg2 = (int)kC2Order.fwd[min(4 * tks + tq, 49)];
+    // dgrad K slice 4*ks + q = channels 8*ocg .. +7 of flipped tap (ty, tx): it reads
+    // dL/dconv2 at (y + ty - 4, x + tx - 4): offset rel from the lane's (y - 4, x - 4) in the
+    // interior image, valid iff bit `tap` of the lane's tap mask is set (slot 75 is padding:
+    // zero weights)
+    const int jd = min(max(t - 64, 0), 79), qd = jd / 20, ksd = jd - 20 * qd;
+    const int kgd = (int)kDgOrder.fwd[min(4 * min(ksd, DG_KS - 1) + qd, 74)];
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      if (t + j * 256 < 590) PAR[t + j * 256] = a.params[par_index(t + j * 256)];
+      if (t + j * 256 < 590) PAR[t + j * 256] = pv[j];
     if (t < 64) {
-      reinterpret_cast<uint4*>(W1Cs)[t] = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t];
-      // conv2 A offset of K-step ks for lane group q: K slice kC2Order[4*ks + q] = channels
-      // 8*(kg&1) .. +7 of tap kg>>1 (slices >= 50 meet zero weights)
-      const int tq = t >> 4, tks = t & 15;
-      const int kg = (int)kC2Order.fwd[min(4 * tks + tq, 49)];
-      const int tap = kg >> 1;
-      COFF[t] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
+      reinterpret_cast<uint4*>(W1Cs)[t] = w1c;
+      const int tap = kg2 >> 1;
+      COFF[t] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg2 & 1) * 8);
     } else if (t < 64 + 80) {
-      // dgrad K slice 4*ks + q = channels 8*ocg .. +7 of flipped tap (ty, tx): it reads
-      // dL/dconv2 at (y + ty - 4, x + tx - 4): offset rel from the lane's (y - 4, x - 4) in the
-      // interior image, valid iff bit `tap` of the lane's tap mask is set (slot 75 is padding:
-      // zero weights)
-      const int j = t - 64, q = j / 20, ks = j - 20 * q;
-      const int kg = (int)kDgOrder.fwd[min(4 * min(ks, DG_KS - 1) + q, 74)];
-      const int tap = kg / 3, ocg = kg - 3 * tap, ty = tap / 5, tx = tap % 5;
-      DGT[j] = ((ty * 8 + tx) * DG_OCP + ocg * 8) | (tap << 16);
+      const int tap = kgd / 3, ocg = kgd - 3 * tap, ty = tap / 5, tx = tap % 5;
+      DGT[jd] = ((ty * 8 + tx) * DG_OCP + ocg * 8) | (tap << 16);
     } else if (t < 64 + 80 + 48) {
       const int j = t - 144;  // 24 x 16 B of ones, 24 x 16 B of zeros
       const unsigned short o = h16<T>(1.f);
@@ -202,34 +239,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     uint4* zh = reinterpret_cast<uint4*>(DCH);
     for (int i = t; i < TS * DCH_SZ * 2 / 16; i += 512) zh[i] = make_uint4(0, 0, 0, 0);
   }
-  // first tile's pixels (threads < TS * 196: sample tid / 196, pixels 4 * (tid % 196) ..),
-  // and the row indices of the tile after it
-  const int s_me = min(tid / 196, TS - 1), q_me = tid - 196 * (tid / 196);
-  const bool px_thread = tid < TS * 196;
-  uint32_t px = 0, px_next = 0;
-  int lab = 0;
-  int64_t nrow = 0, srow = 0, lab_next = 0;
-  // Staged (a.xstage: one 784-byte row per sample of every workgroup's FIRST tile, row g * TS + s,
-  // written by the previous step's kernel or lenet_stage at epoch start): the first tile starts
-  // without the dependent cursor -> perm -> image chain (~5 us in front of stage 1 otherwise,
-  // tools/stage_profile_tile.py); this step stages the next step's first tile (stage_next).
-  const bool staged = a.xstage != nullptr;
-  const bool stage_next = TRAIN && staged && a.stage_next;
-  if (px_thread && g < ntile) {
-    if (staged) {
-      px = reinterpret_cast<const uint32_t*>(a.xstage + (int64_t)(g * TS + s_me) * 784)[q_me];
-      if (q_me == 0) lab = (int)a.lstage[g * TS + s_me];
-    } else {
-      const int64_t row = perm_at(g * TS + s_me);
-      px = reinterpret_cast<const uint32_t*>(a.images + row * 784)[q_me];
-      if (q_me == 0) lab = (int)a.labels[row];
-    }
-    // (row of the next step's sample g * TS + s: its pixels are loaded at the first tile's stage 4)
-    if (stage_next) srow = a.perm[min((a.cursor[0] + 1) * (int64_t)B + min(g * TS + s_me, B - 1), a.perm_len - 1)];
+  if (!staged && px_thread && g < ntile) {
+    const int64_t row = perm_at(g * TS + s_me);
+    px = reinterpret_cast<const uint32_t*>(a.images + row * 784)[q_me];
+    if (q_me == 0) lab = (int)a.labels[row];
   }
-  if (px_thread && g + G < ntile) nrow = perm_at((g + G) * TS + s_me);
   __syncthreads();  // (also the weight DMA)
   if (a.dbg && threadIdx.x == 0) DBGS[1] = __builtin_amdgcn_s_memtime();
+  // rows used at stage 4 of the first tile: the next step's sample g * TS + s (staging) and the
+  // sample of the tile after this one
+  if (stage_next && px_thread && g < ntile)
+    srow = a.perm[min((cur0 + 1) * (int64_t)B + min(g * TS + s_me, B - 1), a.perm_len - 1)];
+  if (px_thread && g + G < ntile) nrow = perm_at((g + G) * TS + s_me);
 
   // conv2 wgrad, taps wave and wave + 16 (the second for waves 0-9), oc M-tiles 0 / 1
   f32x4 acc_w[2][2];
@@ -319,8 +340,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           int bi;
           pool4(c, best, bi);
           if (l16 < 10) {  // pooled window (mt / 3, 4 (mt % 3) + kq), channel l16
-            P1H[ss * P1H_SZ + (mt / 3) * P1H_RP + (4 * (mt % 3)) * LD_P1H + pl] = h16<T>(fmaxf(best + cb, 0.f));
-            I1[ss * 1440 + 4 * mt + il] = (uint8_t)bi;
+            const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
+            P1H[ss * P1H_SZ + (mt / 3) * P1H_RP + (4 * (mt % 3)) * LD_P1H + pl] = hv;
+            // argmax of the window, or 4 where the relu gate (stored pool1 output > 0) is shut
+            I1[ss * 1440 + 4 * mt + il] = (uint8_t)((hv & 0x7fff) ? bi : 4);
           }
         }
       }
@@ -543,15 +566,17 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     // by two ds_read_b64_tr_b16 (a 4-position x 16-channel block each): no 16-bit gathers (the
     // earlier per-column form read 8 strided u16 per fragment, 6-8-way bank-conflicted: half of
     // the kernel's LDS cycles were conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE)
-    auto wgrad2 = [&](auto ntap) {
+    // (NTAP taps per wave; BIAS: the second "tap" is the ones column -- wave 9 -- decided at
+    // compile time, so no per-fragment select)
+    auto wgrad2 = [&](auto ntap, auto bias) {
       constexpr int NTAP = decltype(ntap)::value;
+      constexpr bool BIAS = decltype(bias)::value;
       const int q4 = l16 >> 2, p4 = l16 & 3;  // this lane's row (position) / channel quad of a block
       const unsigned short* pb[NTAP];
-      bool is_bias[NTAP];
+      constexpr bool is_bias[2] = {false, BIAS};
 #pragma unroll
       for (int t = 0; t < NTAP; ++t) {
         const int tap = min(wave + NW * t, 24), kh = tap / 5, kw = tap - 5 * kh;
-        is_bias[t] = wave + NW * t == 25;  // (wave-uniform)
         pb[t] = P1H + (kq + kh) * P1H_RP + (q4 + kw) * LD_P1H + 4 * p4;
       }
       const unsigned short* dl0 = DC2 + min(l16, 19) * DC2_LD + kb;
@@ -566,9 +591,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         a_[1] = *reinterpret_cast<const frag*>(dl1 + ss * DC2_SZ + ps * 32);
 #pragma unroll
         for (int t = 0; t < NTAP; ++t) {
-          const unsigned short* q = pb[t] + ss * P1H_SZ + 4 * ps * P1H_RP;
-          const s16x4 r0 = lds_read_tr16(q), r1 = lds_read_tr16(q + 4 * LD_P1H);
-          b_[t] = is_bias[t] ? ones : __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+          if (is_bias[t]) {
+            b_[t] = ones;
+          } else {
+            const unsigned short* q = pb[t] + ss * P1H_SZ + 4 * ps * P1H_RP;
+            const s16x4 r0 = lds_read_tr16(q), r1 = lds_read_tr16(q + 4 * LD_P1H);
+            b_[t] = __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
         }
       };
       load(0, fa[0], fb[0]);
@@ -582,8 +611,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         }
       }
     };
-    if (wave < 10) wgrad2(std::integral_constant<int, 2>{});
-    else wgrad2(std::integral_constant<int, 1>{});
+    if (wave == 9) wgrad2(std::integral_constant<int, 2>{}, std::true_type{});
+    else if (wave < 10) wgrad2(std::integral_constant<int, 2>{}, std::false_type{});
+    else wgrad2(std::integral_constant<int, 1>{}, std::false_type{});
     {
       // dgrad.  A row = pool1 pixel (y, x) of the M-tile, K slice (flipped tap (ty, tx), channel
       // group): dL/dconv2 at (y + ty - 4, x + tx - 4) of the interior image, or the zero run when
@@ -631,21 +661,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 #pragma unroll
           for (int i = 0; i < NTL; ++i) acc[i] = Mfma<T>::mma(fa[ks & 1][i], fb[ks & 1], acc[i]);
         }
-        // relu gate (pool1 output > 0) and pool1 argmax of this lane's 4 pixels, read before the
+        // pool1 argmax codes of this lane's 4 pixels (4: relu gate shut, stage 1), read before the
         // barrier (the dense dL/dconv1 images overwrite the pool1 images after it)
         const int ic = min(l16, 9);
-        float v[NTL][4];
         uint32_t bis[NTL];
 #pragma unroll
-        for (int i = 0; i < NTL; ++i) {
+        for (int i = 0; i < NTL; ++i)
           bis[i] = *reinterpret_cast<const uint32_t*>(I1 + si[i] * 1440 + ic * 144 + p0[i]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int pp = p0[i] + r;  // pooled row p0 / 12 (p0 % 12 is 0, 4 or 8)
-            const float pv = f16v<T>(P1H[si[i] * P1H_SZ + (pp / 12) * P1H_RP + (pp % 12) * LD_P1H + ic]);
-            v[i][r] = pv > 0.f ? acc[i][r] : 0.f;
-          }
-        }
         lds_barrier();
         // pool1 backward: each pooled pixel's gradient goes to its window's argmax position of
         // dL/dconv1 (dense [ic][24 x 24]); this lane's 4 pooled pixels are 8 consecutive conv1
@@ -655,18 +677,20 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           for (int i = 0; i < NTL; ++i) {
             const int py = p0[i] / 12, px0 = p0[i] - 12 * py;
             unsigned short* d = DY1(si[i]) + ic * DY1_LD + (2 * py) * 24 + 2 * px0;
+            // window code c = 2 dy + dx: the gradient's 16 bits shifted to u16 slot c of the
+            // window's two rows (dword dy = row 2 py + dy, half dx)
+            uint32_t o[2][4];
 #pragma unroll
-            for (int dy = 0; dy < 2; ++dy) {
-              u16x8 o;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int bi = (int)((bis[i] >> (8 * r)) & 255u);
-                const unsigned short h = h16<T>(v[i][r]);
-                o[2 * r] = bi == 2 * dy ? h : (unsigned short)0;
-                o[2 * r + 1] = bi == 2 * dy + 1 ? h : (unsigned short)0;
-              }
-              *reinterpret_cast<u16x8*>(d + dy * 24) = o;
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t c = (bis[i] >> (8 * r)) & 255u;
+              const uint32_t hb = c < 4 ? (uint32_t)h16<T>(acc[i][r]) : 0u;
+              const uint64_t w = (uint64_t)hb << (16 * (c & 3));
+              o[0][r] = (uint32_t)w;
+              o[1][r] = (uint32_t)(w >> 32);
             }
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)
+              *reinterpret_cast<uint4*>(d + dy * 24) = make_uint4(o[dy][0], o[dy][1], o[dy][2], o[dy][3]);
           }
         }
       };
@@ -758,7 +782,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     a.loss_acc[2 * g + 1] = c;
   }
   if (a.dbg) {
-    if (tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
+    if (tid == 0) {
+      DBGS[11] = __builtin_amdgcn_s_memtime();
+      DBGS[13] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
     if (tid < 16) a.dbg[g * 32 + tid] = DBGS[tid];
   }

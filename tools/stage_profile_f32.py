@@ -41,6 +41,19 @@ def main():
         print(f"fp32 B={B} grid={grid}: kernel {tot:.0f} cycles (median over workgroups)")
         for name, v in zip(NAMES, med):
             print(f"  {name:26s} {v:8.0f}  {100 * v / tot:5.1f}%")
+        if grid == 4 * B:  # split step: workgroup g is part g // B of sample g % B
+            parts = [d[p * B:(p + 1) * B].median(0).values.tolist() for p in range(4)]
+            print("  per part (median):   " + "  ".join(f"{'part ' + str(p):>8s}" for p in range(4)))
+            for i, name in enumerate(NAMES):
+                print(f"  {name:22s} " + "  ".join(f"{parts[p][i]:8.0f}" for p in range(4)))
+        # workgroup start / end skew on the 100 MHz realtime clock (10 ns ticks, all XCDs)
+        t0, t1 = st[:, 13], st[:, 14]
+        base = t0.min()
+        start, end, dur = (t0 - base) * 0.01, (t1 - base) * 0.01, (t1 - t0) * 0.01
+        q = torch.tensor([0.0, 0.5, 0.9, 1.0], dtype=torch.double)
+        print(f"  realtime (us): span {end.max().item():.2f}; start p0/50/90/100 "
+              f"{' / '.join(f'{v:.2f}' for v in start.quantile(q).tolist())}; per-WG duration p0/50/90/100 "
+              f"{' / '.join(f'{v:.2f}' for v in dur.quantile(q).tolist())}")
 
 
 if __name__ == "__main__":

@@ -39,6 +39,15 @@ def main():
         print(f"tile kernel B={B} grid={grid}: kernel {tot:.0f} cycles, first tile {tile:.0f} (median over WGs)")
         for name, v in zip(NAMES, d):
             print(f"  {name:22s} {v:8.0f}")
+        # workgroup start / end skew on the 100 MHz realtime clock (10 ns ticks, all XCDs)
+        t0, t1 = st[:, 12], st[:, 13]
+        base = t0.min()
+        start, end, dur = (t0 - base) * 0.01, (t1 - base) * 0.01, (t1 - t0) * 0.01
+        q = torch.tensor([0.0, 0.5, 0.9, 1.0], dtype=torch.double)
+        print(f"  realtime (us): span {end.max().item():.2f}; start p0/50/90/100 "
+              f"{' / '.join(f'{v:.2f}' for v in start.quantile(q).tolist())}; per-WG duration p0/50/90/100 "
+              f"{' / '.join(f'{v:.2f}' for v in dur.quantile(q).tolist())}; end p0/50/90/100 "
+              f"{' / '.join(f'{v:.2f}' for v in end.quantile(q).tolist())}")
 
 
 if __name__ == "__main__":
