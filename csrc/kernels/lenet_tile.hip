@@ -80,8 +80,9 @@ constexpr int D_F = D_I2 + TS * 320;            // f32 [F_END] masks, fc1 output
 constexpr int D_DZ1B = D_F + F_END * 4;         // u16 [TS][64] dZ1 (dP2's A rows)
 constexpr int D_DC2 = D_DZ1B + TS * 64 * 2;     // u16 [TS][DC2_SZ]
 constexpr int D_DCH = D_DC2 + TS * DC2_SZ * 2;  // u16 [TS][DCH_SZ]
-constexpr int D_DBG = D_DCH + TS * DCH_SZ * 2;  // u64 [16] stage stamps (a.dbg, diagnostics)
-constexpr int D_TOTAL = D_DBG + 16 * 8;
+constexpr int D_DBG = D_DCH + TS * DCH_SZ * 2;  // u64 [32] stage stamps (a.dbg, diagnostics)
+constexpr int D_MSK = D_DBG + 32 * 8;            // f32 [TS][20] | [TS][52]: the second dropout-mask buffer
+constexpr int D_TOTAL = D_MSK + TS * 72 * 4;
 constexpr int W_BYTES = (I_END - I_W2C) * 2;    // static: W2C | W2D | F1 images (LDS-DMA)
 static_assert(D_PAR % 16 == 0 && D_COFF % 16 == 0 && D_DGT % 16 == 0 && D_ZERO % 16 == 0 && D_X % 16 == 0 &&
                   D_P1H % 16 == 0 && D_I1 % 16 == 0 && D_P2 % 16 == 0 && D_I2 % 16 == 0 && D_F % 16 == 0 &&
@@ -102,7 +103,12 @@ constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 __device__ int64_t kTileZero = 0;  // the counter an absent cursor / Philox offset reads (global memory: a
                                  // __constant__ word would turn the loads into flat ones, which lgkmcnt waits count)
 
-template <typename T, bool TRAIN>
+// ONE_TILE: every workgroup has exactly one tile (B <= TS * grid, the 8-GPU share of the
+// large-batch config).  Then nothing is gained by hoisting the stages' wave-uniform addresses out
+// of the tile loop, and hoisted they cost ~430 scalar instructions per wave in front of it (SGPR
+// spills, 1 SALU instruction per 4 cycles per SIMD: the four waves of a SIMD reached stage 0's
+// barrier 1.7k cycles apart); with several tiles the hoisting pays (computed once).
+template <typename T, bool TRAIN, bool ONE_TILE>
 __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
   struct Kargs { LenetTrainArgs a; int write_logp; float* logp_out; };
   prefetch_kernargs<(int)sizeof(Kargs)>();
@@ -124,8 +130,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   unsigned short* P2 = reinterpret_cast<unsigned short*>(dsm + D_P2);
   uint8_t* I2 = dsm + D_I2;
   float* Fs = reinterpret_cast<float*>(dsm + D_F);
-  float* D2S = Fs + F_D2S;
-  float* D1S = Fs + F_D1S;
+  // Dropout keep-scales, double-buffered by tile parity: a tile's masks are drawn ahead of it
+  // by waves that are otherwise idle (the first tile's in the preamble, the next tile's during
+  // the loss stage), not in front of its conv1
+  float* const MSK_D2S[2] = {Fs + F_D2S, reinterpret_cast<float*>(dsm + D_MSK)};
+  float* const MSK_D1S[2] = {Fs + F_D1S, reinterpret_cast<float*>(dsm + D_MSK) + TS * 20};
   float* Hs = Fs + F_H;
   int* LAB = reinterpret_cast<int*>(Fs + F_LAB);
   float* LOSS = Fs + F_LOSS;
@@ -167,6 +176,23 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   auto perm_at = [&](int b) { return a.perm[min(pbase + (int64_t)min(b, B - 1), a.perm_len - 1)]; };
   const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   const unsigned short one = h16<T>(1.f);
+  // keep-scales of tile tl (Philox, as lenet_train: key (rank * B + batch position) * 70 +
+  // unit), thread t < TS * 70 of the drawing waves
+  auto draw_masks = [&](int tl, int par, int t) {
+    if (t < TS * 70) {
+      const int s = t / 70, u = t - 70 * s;
+      float sc = 1.f;
+      if (TRAIN) {
+        // (the key through an opaque copy: its ten round keys are not hoisted and spilled)
+        uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+        asm volatile("" : "+s"(k0), "+s"(k1));
+        const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)B + tl * TS + s) * 70ull + u;
+        sc = dropout_keep(((uint64_t)k1 << 32) | k0, rng_ctr << 20, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
+      }
+      if (u < 20) MSK_D2S[par][s * 20 + u] = sc;
+      else MSK_D1S[par][s * 52 + u - 20] = sc;
+    }
+  };
   // first tile's pixels (threads < TS * 196: sample tid / 196, pixels 4 * (tid % 196) ..)
   const int s_me = min(tid / 196, TS - 1), q_me = tid - 196 * (tid / 196);
   const bool px_thread = tid < TS * 196;
@@ -238,6 +264,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     for (int i = t; i < TS * P1H_SZ * 2 / 16; i += 512) z[i] = make_uint4(0, 0, 0, 0);
     uint4* zh = reinterpret_cast<uint4*>(DCH);
     for (int i = t; i < TS * DCH_SZ * 2 / 16; i += 512) zh[i] = make_uint4(0, 0, 0, 0);
+    if (g < ntile) draw_masks(g, 0, t);  // the first tile's dropout masks
   }
   if (!staged && px_thread && g < ntile) {
     const int64_t row = perm_at(g * TS + s_me);
@@ -246,11 +273,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   }
   __syncthreads();  // (also the weight DMA)
   if (a.dbg && threadIdx.x == 0) DBGS[1] = __builtin_amdgcn_s_memtime();
-  // rows used at stage 4 of the first tile: the next step's sample g * TS + s (staging) and the
-  // sample of the tile after this one
-  if (stage_next && px_thread && g < ntile)
-    srow = a.perm[min((cur0 + 1) * (int64_t)B + min(g * TS + s_me, B - 1), a.perm_len - 1)];
-  if (px_thread && g + G < ntile) nrow = perm_at((g + G) * TS + s_me);
 
   // conv2 wgrad, taps wave and wave + 16 (the second for waves 0-9), oc M-tiles 0 / 1
   f32x4 acc_w[2][2];
@@ -266,12 +288,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       if (c[r] > best) { best = c[r]; bi = r; }
   };
 
+  const int wave_o = wave;
   for (int tile = g; tile < ntile; tile += G) {
     // Lane indices through an opaque copy per tile: otherwise hipcc hoists every lane-dependent
     // LDS address of every stage out of the tile loop into long-lived registers (spills).
     const int tid = opaque(threadIdx.x), lane = tid & 63, l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
+    // and, with one tile, the wave index too (see ONE_TILE)
+    const int wave = ONE_TILE ? __builtin_amdgcn_readfirstlane(tid >> 6) : wave_o;
     const int s_me = min(tid / 196, TS - 1), q_me = tid - 196 * (tid / 196);
     const int b0 = tile * TS;
+    const int par = ((tile - g) / G) & 1;  // (uniform) this tile's mask buffer
+    float* const D2S = MSK_D2S[par];
+    float* const D1S = MSK_D1S[par];
     // ---------------- stage 0: normalised pixels, labels, dropout masks
     TSTAMP(2);
     if (px_thread) {
@@ -287,16 +315,16 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       x1[3] = o[3];
       if (q_me == 0) LAB[s_me] = lab;
     }
-    if (tid < TS * 70) {
-      const int s = tid / 70, u = tid - 70 * s;
-      float sc = 1.f;
-      if (TRAIN) {
-        const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)B + b0 + s) * 70ull + u;
-        sc = dropout_keep(a.seed, rng_ctr << 20, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
-      }
-      if (u < 20) D2S[s * 20 + u] = sc;
-      else D1S[s * 52 + u - 20] = sc;
+    if (a.dbg && tid == 0 && tile == g) DBGS[14] = __builtin_amdgcn_s_memtime();  // pixels in
+    if (tile == g) {
+      // rows used at stage 4 of the first tile: the next step's sample g * TS + s (staging)
+      // and the sample of the tile after this one -- loaded only now, after the pixels have
+      // been consumed (a wait on the pixels is a vmcnt(0), which would wait on these too)
+      if (stage_next && px_thread)
+        srow = a.perm[min((cur0 + 1) * (int64_t)B + min(g * TS + s_me, B - 1), a.perm_len - 1)];
+      if (px_thread && g + G < ntile) nrow = perm_at((g + G) * TS + s_me);
     }
+    if (a.dbg && lane == 0 && tile == g) DBGS[16 + wave] = __builtin_amdgcn_s_memtime();  // arrivals
     lds_barrier();
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1H (HWC), I1
@@ -425,6 +453,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 
     // ---------------- stage 4: fc2 + log_softmax + NLL, dlogits, dZ1 (wave s: sample s)
     TSTAMP(6);
+    // the next tile's dropout masks, on the 12 waves this stage leaves idle
+    if (wave >= TS && tile + G < ntile) draw_masks(tile + G, par ^ 1, tid - 64 * TS);
     if (wave < TS) {
       const int s = wave, b = b0 + s;
       const bool valid = b < B;
@@ -787,7 +817,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       DBGS[13] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
-    if (tid < 16) a.dbg[g * 32 + tid] = DBGS[tid];
+    if (tid < 32) a.dbg[g * 32 + tid] = DBGS[tid];
   }
 #undef TSTAMP
 }
@@ -804,16 +834,22 @@ hipError_t launch_lenet_tile(const LenetTrainArgs& a, int write_logp, float* log
       (a.stage_next && (!a.xstage || !a.cursor)))
     return hipErrorInvalidValue;
   const size_t lds = (size_t)D_TOTAL;
+  const bool one = a.B <= TS * a.grid;
+#define CSED_TILE_LAUNCH(TR, ONE, WL, LP)                                                           \
+  do {                                                                                               \
+    allow_dynamic_lds<lenet_tile_kernel<scalar_t, TR, ONE>>(lds);                                    \
+    hipLaunchKernelGGL((lenet_tile_kernel<scalar_t, TR, ONE>), dim3(a.grid), dim3(NT), lds, s, a, WL, LP); \
+  } while (0)
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     if (train) {
-      allow_dynamic_lds<lenet_tile_kernel<scalar_t, true>>(lds);
-      hipLaunchKernelGGL((lenet_tile_kernel<scalar_t, true>), dim3(a.grid), dim3(NT), lds, s, a, 0, (float*)nullptr);
+      if (one) CSED_TILE_LAUNCH(true, true, 0, (float*)nullptr);
+      else CSED_TILE_LAUNCH(true, false, 0, (float*)nullptr);
     } else {
-      allow_dynamic_lds<lenet_tile_kernel<scalar_t, false>>(lds);
-      hipLaunchKernelGGL((lenet_tile_kernel<scalar_t, false>), dim3(a.grid), dim3(NT), lds, s, a, write_logp,
-                         logp_out);
+      if (one) CSED_TILE_LAUNCH(false, true, write_logp, logp_out);
+      else CSED_TILE_LAUNCH(false, false, write_logp, logp_out);
     }
   });
+#undef CSED_TILE_LAUNCH
   return hipGetLastError();
 }
 

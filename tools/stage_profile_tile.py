@@ -39,6 +39,10 @@ def main():
         print(f"tile kernel B={B} grid={grid}: kernel {tot:.0f} cycles, first tile {tile:.0f} (median over WGs)")
         for name, v in zip(NAMES, d):
             print(f"  {name:22s} {v:8.0f}")
+        px = (st[:, 14] - st[:, 2]).median().item()
+        print(f"  (stage 0: staged pixels in and written after {px:.0f} cycles)")
+        arr = [(st[:, 16 + w] - st[:, 2]).median().item() for w in range(16)]
+        print("  stage-0 barrier arrival per wave (cycles after stage start): " + " ".join(f"{v:.0f}" for v in arr))
         # workgroup start / end skew on the 100 MHz realtime clock (10 ns ticks, all XCDs)
         t0, t1 = st[:, 12], st[:, 13]
         base = t0.min()
