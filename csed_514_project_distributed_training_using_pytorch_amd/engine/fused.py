@@ -42,6 +42,8 @@ from ..parallel.ipc import (allreduce_mode, make_allreduce, open_exchange, open_
                             wait_timeout_s)
 from ..utils.flat import FlatParams
 
+N_VEC = 464  # per-sample fc vector length (kernels/lenet_layout.h VEC)
+
 
 def _clear_hip_error() -> None:
     """Reset this thread's sticky HIP error after a failed stream capture.  Our ops report
@@ -128,6 +130,7 @@ class FusedLeNetTrainer:
         self.lr, self.momentum, self.dampening = float(lr), float(momentum), float(dampening)
         self.weight_decay, self.nesterov = float(weight_decay), bool(nesterov)
         self.mfma = _native.MFMA_CODE[compute_dtype]
+        self.compute_dtype = compute_dtype
         self.drop_p = float(drop_p)
         self.seed = int(seed)  # masks decorrelate across ranks through the rank id in the element index
         self.train_data = train.to(self.device)
@@ -149,7 +152,9 @@ class FusedLeNetTrainer:
         self.wimg = torch.zeros(wimg_elems, dtype=torch.int16, device=dev)
         # per-WG conv partial gradients and per-sample fc vectors (see lenet_fused.hip)
         self.slab = torch.empty((self._max_grid(), conv_params), dtype=torch.float32, device=dev)
-        self.vslab = torch.zeros((self.B, vec_len), dtype=torch.float32, device=dev)
+        # (fp32 [B, 464] for the exact-fp32 kernel; the 16-bit kernels keep raw 16-bit values
+        # feature-major, [464, round_up(B, 64)], in the same bytes: fc_vectors() decodes either)
+        self.vslab = torch.zeros(((self.B + 63) // 64 * 64, vec_len), dtype=torch.float32, device=dev)
         self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(2, dtype=torch.float32, device=dev)  # running (loss sum, correct)
         self.step_count = torch.zeros(1, dtype=torch.long, device=dev)
@@ -225,6 +230,42 @@ class FusedLeNetTrainer:
     def grad_scale(self) -> float:
         """Loss-gradient scale of a full step: 1 / (global batch) (x 1 / loopback_world)."""
         return 1.0 / (self.global_batch * max(1, self.loopback_world))
+
+    # 16-bit steps run their backward at per-sample scale (dlogits = softmax - onehot, so fp16
+    # gradient images stay normal numbers at any batch) and lenet_update applies the 1 / (global
+    # batch) in fp32 (its grad_post); the exact-fp32 kernel takes the scale in-kernel.  For a
+    # power-of-two batch both give bit-identical bf16 results.
+    def _train_scale(self, grad_scale: float) -> float:
+        return grad_scale if self.fp32 else 1.0
+
+    def _post_scale(self, grad_scale: float) -> float:
+        return 1.0 if self.fp32 else grad_scale
+
+    def _vec16(self, B: int) -> torch.Tensor:
+        """The 16-bit kernels' fc-vector slab of a batch of B: raw [round_up(B, 64) / 4, 464, 4]
+        (sample quads, kernels/lenet_layout.h)."""
+        q = (B + 63) // 64 * 16
+        return self.vslab.view(-1).view(torch.int16)[:q * N_VEC * 4].view(q, N_VEC, 4)
+
+    def fc_vectors(self, B: int | None = None) -> torch.Tensor:
+        """The step's per-sample fc vectors (P2 | dZ1 | H | dlogits) as fp32 [B, 464], decoded
+        from either slab layout (kernels/lenet_layout.h)."""
+        B = self.B if B is None else int(B)
+        if self.fp32:
+            return self.vslab[:B].clone()
+        v = self._vec16(B).transpose(1, 2).reshape(-1, N_VEC)[:B]  # [quad, 4, 464] -> [sample, 464]
+        return v.contiguous().view(self.compute_dtype).float()
+
+    def set_fc_vectors(self, v: torch.Tensor) -> None:
+        """Fill the fc-vector slab from fp32 [B, 464] values (rounded to the compute dtype)."""
+        B = v.shape[0]
+        self.vslab.zero_()
+        if self.fp32:
+            self.vslab[:B].copy_(v)
+            return
+        buf = torch.zeros(((B + 63) // 64 * 64, N_VEC), dtype=self.compute_dtype, device=self.device)
+        buf[:B] = v.to(device=self.device, dtype=self.compute_dtype)
+        self._vec16(B).copy_(buf.view(torch.int16).view(-1, 4, N_VEC).transpose(1, 2))
 
     @property
     def allreduce_kind(self) -> str:
@@ -302,7 +343,7 @@ class FusedLeNetTrainer:
         ok = True
         for _ in range(rounds):
             self.slab.copy_(torch.randint(-8, 9, self.slab.shape, generator=gen, dtype=torch.float32))
-            self.vslab.copy_(torch.randint(-4, 5, self.vslab.shape, generator=gen, dtype=torch.float32))
+            self.set_fc_vectors(torch.randint(-4, 5, (self.B, N_VEC), generator=gen, dtype=torch.float32))
             local = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
             fused = torch.empty_like(local)
             ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, local, *common)
@@ -441,17 +482,19 @@ class FusedLeNetTrainer:
         kern = self.kernel_for(B, grid)
         st = self._stages(kern) and cursor is not None
         ops.lenet_train(self.train_data.images, self.train_data.labels, perm, cursor, B, self.ctx.rank, self.wimg,
-                        self.flat.data, self.slab, self.vslab, self.loss_parts, grad_scale, MNIST_MEAN, MNIST_STD,
-                        self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,
+                        self.flat.data, self.slab, self.vslab, self.loss_parts, self._train_scale(grad_scale),
+                        MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, None,
                         self.xstage if st else None, self.lstage if st else None, st, kern)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket)
+        post = self._post_scale(grad_scale)
         if self.exch is not None:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
-                             self.loss_parts, grid, self.loss_acc, self.mfma, None, self.exch.id, self.exch_timeout_s)
+                             self.loss_parts, grid, self.loss_acc, self.mfma, None, self.exch.id, self.exch_timeout_s,
+                             post)
         elif self.comm:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, self.flat.grad, *common, None, None, False,
-                             self.loss_parts, grid, self.loss_acc, self.mfma)
+                             self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post)
             if self.allreduce is not None:
                 self.allreduce(self.flat.grad)
             else:
@@ -460,7 +503,7 @@ class FusedLeNetTrainer:
                              True, None, 0, None, self.mfma)
         else:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
-                             self.loss_parts, grid, self.loss_acc, self.mfma)
+                             self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post)
 
     def _stages(self, kernel: int) -> bool:
         """Whether a full step launched with ``kernel`` (kernel_for) reads / writes the staging
@@ -486,14 +529,16 @@ class FusedLeNetTrainer:
         g = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
         ops = torch.ops.csed
         ops.lenet_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B, self.ctx.rank,
-                        self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts, 1.0 / self.global_batch,
+                        self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts,
+                        self._train_scale(1.0 / self.global_batch),
                         MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset, grid, self.mfma, dbg,
                         self.xstage if self._stages(self.kernel_for(self.B, grid)) and grid == self.grid else None,
                         self.lstage if self._stages(self.kernel_for(self.B, grid)) and grid == self.grid else None, False,
                         self.kernel_for(self.B, grid))
         ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
-                         self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma)
+                         self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma, None, -1,
+                         2.0, self._post_scale(1.0 / self.global_batch))
         return g
 
     def step(self) -> None:
@@ -608,13 +653,15 @@ class FusedLeNetTrainer:
             st = torch.classes.csed.LenetStepper()
             st.set_train(self.train_data.images, self.train_data.labels, self.perm, self.cursor, self.B,
                          self.ctx.rank, self.wimg, self.flat.data, self.slab, self.vslab, self.loss_parts,
-                         self.grad_scale, MNIST_MEAN, MNIST_STD, self.drop_p, self.seed, self.rng_offset,
+                         self._train_scale(self.grad_scale), MNIST_MEAN, MNIST_STD, self.drop_p, self.seed,
+                         self.rng_offset,
                          self.grid, self.mfma, self.xstage if st_ok else None,
                          self.lstage if st_ok else None, st_ok, self.kernel_for(self.B, self.grid))
             st.set_update(self.slab, self.grid, self.vslab, self.B, self.flat.data, self.momentum_buf, self.wimg,
                           self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                           self.step_count, self.ticket, self.cursor, self.rng_offset, self.loss_parts, self.grid,
-                          self.loss_acc, self.mfma, exch_id, self.exch_timeout_s if exch_id >= 0 else 2.0)
+                          self.loss_acc, self.mfma, exch_id, self.exch_timeout_s if exch_id >= 0 else 2.0,
+                          self._post_scale(self.grad_scale))
             self._stepper = (key, st)
         return self._stepper[1]
 

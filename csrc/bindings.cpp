@@ -310,6 +310,12 @@ void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
                                     cur_stream(params)));
 }
 
+// bytes of the fc-vector slab of a batch: fp32 rows per sample, or the 16-bit steps' rows per
+// feature (kernels/lenet_layout.h: 464 x round_up(B, 64) raw 16-bit values)
+int64_t vec_bytes(int64_t B, int64_t mfma_dtype) {
+  return lcode(mfma_dtype) == csed::kF32 ? B * csed::lenet_vec_len() * 4 : csed::lenet_vec_len() * ((B + 63) / 64 * 64) * 2;
+}
+
 csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, const Tensor& perm,
                                 const optional<Tensor>& cursor, int64_t B, int64_t rank, const Tensor& wimg,
                                 const Tensor& params, Tensor& slab, Tensor& vslab, Tensor& loss_parts,
@@ -333,7 +339,8 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   const int64_t srows = tile ? grid * csed::lenet_tile_samples() : grid;
   TORCH_CHECK(slab.numel() >= grid * csed::lenet_conv_param_count() && loss_parts.numel() >= 2 * grid,
               "lenet_train: slab [grid, 5280] / loss_parts [grid, 2] too small");
-  TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_train: vslab [B, 464] too small");
+  TORCH_CHECK(vslab.scalar_type() == at::kFloat && vslab.numel() * 4 >= vec_bytes(B, mfma_dtype),
+              "lenet_train: vslab too small (fp32 [B, 464]; 16-bit steps: 464 x round_up(B, 64) x 2 bytes)");
   if (!cursor.has_value()) TORCH_CHECK(perm.numel() >= B, "perm shorter than the batch");
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0);
   csed::LenetTrainArgs a{};
@@ -419,7 +426,7 @@ csed::LenetUpdateArgs update_args(const Tensor& slab, int64_t grid, const Tensor
                                   const optional<Tensor>& cursor, const optional<Tensor>& rng_offset, bool apply_sgd,
                                   const optional<Tensor>& loss_parts, const optional<Tensor>& loss_acc,
                                   int64_t mfma_dtype, const optional<Tensor>& dbg, int64_t exch_id,
-                                  double exch_timeout_s) {
+                                  double exch_timeout_s, double grad_post) {
   dev(slab, "slab"); dev(params, "params"); dev(momentum, "momentum"); dev(wimg, "wimg");
   TORCH_CHECK(params.numel() == csed::lenet_param_count() && momentum.numel() == params.numel(),
               "lenet_update: params / momentum must hold the 21840 flat LeNet parameters");
@@ -428,7 +435,9 @@ csed::LenetUpdateArgs update_args(const Tensor& slab, int64_t grid, const Tensor
   csed::LenetUpdateArgs a{};
   a.slab = slab.data_ptr<float>(); a.grid = (int)grid;
   a.vslab = vslab.data_ptr<float>(); a.B = (int)B;
-  TORCH_CHECK(vslab.numel() >= B * csed::lenet_vec_len(), "lenet_update: vslab too small");
+  TORCH_CHECK(vslab.scalar_type() == at::kFloat && vslab.numel() * 4 >= vec_bytes(B, mfma_dtype),
+              "lenet_update: vslab too small");
+  a.grad_post = (float)grad_post;
   a.grad_in = optpt<float>(grad_in); a.grad_out = optpt<float>(grad_out);
   a.params = params.data_ptr<float>(); a.momentum = momentum.data_ptr<float>(); a.wimg = (uint16_t*)wimg.data_ptr();
   a.lr = (float)lr; a.mom = (float)mom; a.dampening = (float)dampening; a.weight_decay = (float)weight_decay;
@@ -450,12 +459,12 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
                   double weight_decay, bool nesterov, Tensor& step, Tensor& ticket, const optional<Tensor>& cursor,
                   const optional<Tensor>& rng_offset, bool apply_sgd, const optional<Tensor>& loss_parts,
                   int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg,
-                  int64_t exch_id, double exch_timeout_s) {
+                  int64_t exch_id, double exch_timeout_s, double grad_post) {
   const c10::DeviceGuard gd(params.device());
   const csed::LenetUpdateArgs a =
       update_args(slab, grid, vslab, B, grad_in, grad_out, params, momentum, wimg, lr, mom, dampening, weight_decay,
                   nesterov, step, ticket, cursor, rng_offset, apply_sgd, loss_parts, loss_acc, mfma_dtype, dbg,
-                  exch_id, exch_timeout_s);
+                  exch_id, exch_timeout_s, grad_post);
   CHECK_HIP(csed::launch_lenet_update(a, optpt<float>(loss_parts), (int)nparts, optpt<float>(loss_acc),
                                       cur_stream(params)));
 }
@@ -505,10 +514,10 @@ struct LenetStepper : torch::CustomClassHolder {
   void set_update(Tensor slab, int64_t grid, Tensor vslab, int64_t B, Tensor params, Tensor momentum, Tensor wimg,
                   double lr, double mom, double dampening, double weight_decay, bool nesterov, Tensor step,
                   Tensor ticket, Tensor cursor, Tensor rng_offset, Tensor loss_parts_t, int64_t nparts_,
-                  Tensor loss_acc_t, int64_t mfma_dtype, int64_t exch_id, double exch_timeout_s) {
+                  Tensor loss_acc_t, int64_t mfma_dtype, int64_t exch_id, double exch_timeout_s, double grad_post) {
     ua = update_args(slab, grid, vslab, B, c10::nullopt, c10::nullopt, params, momentum, wimg, lr, mom, dampening,
                      weight_decay, nesterov, step, ticket, cursor, rng_offset, true, loss_parts_t, loss_acc_t,
-                     mfma_dtype, c10::nullopt, exch_id, exch_timeout_s);
+                     mfma_dtype, c10::nullopt, exch_id, exch_timeout_s, grad_post);
     loss_parts = loss_parts_t.data_ptr<float>();
     loss_acc = loss_acc_t.data_ptr<float>();
     nparts = nparts_;
@@ -549,7 +558,7 @@ TORCH_LIBRARY(csed, m) {
         "Tensor(c!) momentum, Tensor(d!) wimg, float lr, float mom, float dampening, float weight_decay, "
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
         "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
-        "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0) -> ()");
+        "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0, float grad_post=1.0) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
         "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype, int kernel=0) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "

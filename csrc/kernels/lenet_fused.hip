@@ -472,7 +472,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   auto sample = [&](const int s, const int tid, const int lane, const int l16, const int kq, const int kb) {
     const int b = b0 + s * G;
     const bool wvec = TRAIN && own_vec;
-    float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
+    // fc vectors, 16-bit sample quads (kernels/lenet_layout.h): feature f of sample b at
+    // vs[4 f], the values exactly as the forward / backward used them
+    unsigned short* vs = TRAIN ? reinterpret_cast<unsigned short*>(a.vslab) + vec16_index(0, b) : nullptr;
+    constexpr int vld = 4;
     if (a.dbg && lane == 0 && s == 0 && wave < 8) DBGS[24 + wave] = __builtin_amdgcn_s_memtime();
     lds_barrier();  // previous sample's readers are done (first pass: preamble LDS writes)
     // ---------------- stage 0: normalise the prefetched pixels, dropout masks;
@@ -607,7 +610,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[oc]);
         P2[oc * 16 + w] = hv;
         I2[oc * 16 + w] = (uint8_t)bi;
-        if (wvec) vs[V_P2 + oc * 16 + w] = f16v<T>(hv);  // fc1 input, exactly as the forward used it
+        if (wvec) vs[(V_P2 + oc * 16 + w) * vld] = hv;  // fc1 input, exactly as the forward used it
       }
     }
     __syncthreads();
@@ -635,7 +638,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (o < 50) {
           const float h = fmaxf(c[0] + PAR[P_F1B + o], 0.f) * D1S[o];
           Hs[o] = h;
-          if (wvec) vs[V_H + o] = h;
+          if (wvec) vs[(V_H + o) * vld] = h16<T>(h);
         }
       }
     }
@@ -737,7 +740,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           float mine = 0.f;
 #pragma unroll
           for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
-          vs[V_DLOG + lane] = mine;
+          vs[(V_DLOG + lane) * vld] = h16<T>(mine);
         }
         // dZ1[o] = gate(o) * sum_c dl[c] * W2[c][o]   (lane o; every lane has all dl[c])
         float dh0 = 0.f, dh1 = 0.f;
@@ -747,8 +750,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           else dh0 = fmaf(dl[c], w2c[c], dh0);
         }
         const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
-        DZ1B[lane] = h16<T>(dz);
-        if (wvec && lane < 50) vs[V_DZ1 + lane] = dz;
+        const unsigned short dzh = h16<T>(dz);
+        DZ1B[lane] = dzh;
+        if (wvec && lane < 50) vs[(V_DZ1 + lane) * vld] = dzh;
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -1492,7 +1496,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     __syncthreads();
     USTAMP(3);
     if (ht < 64 && live_pb && pi >= 0) {
-      float g[1] = {(part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])};
+      float g[1] = {((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post};
       if (EXCH) {
         const int idx[1] = {pi};
         const bool live[1] = {true};
@@ -1574,9 +1578,85 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       image_slots(max(pidx[r], 0), fd[r], d1);
       if (pidx[r] < 0) fd[r] = -1;
     }
-    // this wave's samples [k0, k1): a multiple-of-4 share of the batch
-    const int kw = ((B + wpt - 1) / wpt + 3) & ~3;
+    // this wave's samples [k0, k1): a multiple-of-4 (16-bit layout: of-32) share of the batch
+    constexpr bool FC16 = !std::is_same<T, float>::value;
+    constexpr int KG = FC16 ? 32 : 4;
+    const int kw = ((B + wpt - 1) / wpt + KG - 1) & ~(KG - 1);
     const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
+    f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (FC16) {
+      // 16-bit vectors in sample quads (kernels/lenet_layout.h): K-step s = samples s .. s+31
+      // on the 16x16x32 MFMA, lane (l16, kq) holding A[o][s + 8kq .. +8] and B[s + 8kq .. +8][i],
+      // each two 8-byte loads (quads (s + 8kq) / 4 and the next; a lane group's 16 lanes read
+      // one 128-byte line).  The bias column (i == cols) is ones, columns past it zeros,
+      // and samples past k1 (a partial last K-step, stale columns of a shorter batch, the
+      // duplicate loads of a group's steps past the end) are masked to exact zeros: the same
+      // sum in a fixed order, whatever the batch.
+      if (live_wave && k0 < k1) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        typedef typename Mfma<T>::frag frag16;
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        const unsigned short* vh = reinterpret_cast<const unsigned short*>(vslab);
+        // quad q of row r at vh + (q * VEC + r) * 4; K-step s starts at quad s / 4
+        const unsigned short* pa = vh + vec16_index(a_off + o, 8 * kq);
+        const unsigned short* pb = vh + vec16_index(b_off + min(i, cols - 1), 8 * kq);
+        const uint32_t one2 = std::is_same<T, __bf16>::value ? 0x3F803F80u : 0x3C003C00u;
+        const uint32_t bsel = i < cols ? 0xffffffffu : 0u;             // loaded B values
+        const uint32_t bone = i == cols ? one2 : 0u;                   // the ones column
+        const int nsteps = (k1 - k0 + 31) >> 5;                        // (uniform)
+        f32x4 c1 = c;
+        auto run = [&](auto nb_) {
+          constexpr int NB = decltype(nb_)::value;
+          const int ng = (nsteps + NB - 1) / NB;
+          u4 a0[NB], b0[NB], a1[NB], b1[NB];
+          auto ld = [&](int gi, u4 (&av)[NB], u4 (&bv)[NB]) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+              const int s = min(k0 + (gi * NB + u) * 32, (k1 - 1) & ~31);  // clamped: a valid step
+              const int64_t q = (int64_t)(s >> 2) * VEC * 4;                    // its first quad
+              const u2 a_lo = *reinterpret_cast<const u2*>(pa + q), a_hi = *reinterpret_cast<const u2*>(pa + q + VEC * 4);
+              const u2 b_lo = *reinterpret_cast<const u2*>(pb + q), b_hi = *reinterpret_cast<const u2*>(pb + q + VEC * 4);
+              av[u] = u4{a_lo[0], a_lo[1], a_hi[0], a_hi[1]};
+              bv[u] = u4{b_lo[0], b_lo[1], b_hi[0], b_hi[1]};
+            }
+          };
+          auto mm = [&](int gi, const u4 (&av)[NB], const u4 (&bv)[NB]) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+              const int n = k1 - (k0 + (gi * NB + u) * 32) - 8 * kq;  // live samples of this lane
+              u4 fa, fb;
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+                const uint32_t m = n >= 2 * d + 2 ? 0xffffffffu : (n == 2 * d + 1 ? 0x0000ffffu : 0u);
+                fa[d] = av[u][d] & m;
+                fb[d] = ((bv[u][d] & bsel) | bone) & m;
+              }
+              if (u & 1)
+                c1 = Mfma<T>::mma(__builtin_bit_cast(frag16, fa), __builtin_bit_cast(frag16, fb), c1);
+              else
+                c = Mfma<T>::mma(__builtin_bit_cast(frag16, fa), __builtin_bit_cast(frag16, fb), c);
+            }
+          };
+          ld(0, a0, b0);
+          for (int gi = 0; gi < ng; gi += 2) {
+            const bool more = gi + 1 < ng;
+            if (more) ld(gi + 1, a1, b1);
+            __builtin_amdgcn_sched_barrier(0);  // a group's loads stay ahead of its MFMAs
+            USTAMP(1);
+            mm(gi, a0, b0);
+            if (more) {
+              if (gi + 2 < ng) ld(gi + 2, a0, b0);
+              __builtin_amdgcn_sched_barrier(0);
+              mm(gi + 1, a1, b1);
+            }
+          }
+        };
+        if (nsteps <= 1) run(std::integral_constant<int, 1>{});
+        else if (nsteps <= 2) run(std::integral_constant<int, 2>{});
+        else run(std::integral_constant<int, 4>{});
+        c += c1;
+      }
+    } else {
     // K = samples; 16x16x4 f32 MFMA: lane holds A[o][s0 + 4u + kq] and B[s0 + 4u + kq][i]
     // Loads and masking are separate phases: a chunk's 32 loads are all issued before any
     // select consumes one (a select right behind its load pair let the scheduler wait on
@@ -1617,7 +1697,6 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         bv[u] = ok ? (i < cols ? rb : (i == cols ? 1.f : 0.f)) : 0.f;
       }
     };
-    f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
     auto small_k = [&](auto nc) {
       constexpr int NC = decltype(nc)::value;
       float a0[NC], b0[NC];
@@ -1652,6 +1731,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         }
       }
     }
+    }  // fp32 vectors
     USTAMP(2);
     // Retire the p / m prefetch now: after the first finish_param's stores, hipcc would
     // wait for them with vmcnt(0), i.e. for those stores too (one store round trip per
@@ -1672,7 +1752,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       for (int r = 0; r < 4; ++r) {
         float v = c[r];
         for (int w = 1; w < wpt; ++w) v += pfc[(wave + w) * 256 + r * 64 + lane];
-        g[r] = v;
+        g[r] = v * a.grad_post;
       }
       if (EXCH) {
         int idx[4];

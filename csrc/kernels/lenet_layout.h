@@ -47,8 +47,21 @@ __host__ __device__ inline int slab_off(int s, int row, int G, int R2) {
   return r * 64 + (s & 63);
 }
 
-// per-sample vector slab (fp32): fc1 input P2 | dL/dz1 | fc1 output H | dL/dlogits
+// per-sample vector slab: fc1 input P2 | dL/dz1 | fc1 output H | dL/dlogits
 constexpr int V_P2 = 0, V_DZ1 = 320, V_H = 384, V_DLOG = 448, VEC = 464;
+// Two layouts of it:
+//  * exact fp32 (lenet_fused_f32.hip): float [B][VEC], a row per sample;
+//  * 16-bit steps (lenet_train, lenet_tile): raw bf16 / fp16 in sample quads,
+//    [B / 4][VEC][4]: feature f of sample b at vec16_index(f, b).  lenet_update forms the fc
+//    weight gradients dW = dZ^T X with K = samples on the 16x16x32 MFMA, whose fragments hold 8
+//    consecutive K per lane: two 8-byte loads per operand and K-step, and the 16 lanes of a lane
+//    group read 16 consecutive features of one quad, i.e. one whole 128-byte line (the
+//    per-sample fp32 rows needed 8 strided scalar loads, and twice the bytes).  A quad is one
+//    sample tile of lenet_tile.hip, so a tile's vectors are one contiguous 3,712-byte run that
+//    no other workgroup (XCD) shares a line of.  Features never written (dZ1 rows 50..63, H rows
+//    50..63, dlogits rows 10..15) stay zero; samples past B are stale and masked by the reader.
+__host__ __device__ constexpr int64_t vec16_index(int f, int b) { return ((int64_t)(b >> 2) * VEC + f) * 4 + (b & 3); }
+__host__ __device__ constexpr int64_t vec16_bytes(int B) { return (int64_t)((B + 63) & ~63) * VEC * 2; }
 
 // Split step: workgroups per sample (the backward conv stages are divided among them)
 constexpr int SPLIT_K = 4;

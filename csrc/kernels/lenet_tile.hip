@@ -162,6 +162,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   const int l16 = lane & 15, kq = lane >> 4, kb = 8 * kq;
   const int G = a.grid, g = blockIdx.x, B = a.B;
   const int ntile = (B + TS - 1) / TS;
+  // fc vectors, 16-bit sample quads = tiles (lenet_layout.h): feature f of sample b at
+  // VH[vec16_index(f, b)], a tile's vectors one contiguous run
+  unsigned short* const VH = reinterpret_cast<unsigned short*>(a.vslab);
   const float inv_std = 1.f / a.std_;
   // The preamble's global loads are ordered so that nothing waits on a chain: the step counters
   // and the staged first tile first, then the weight DMA; the rows that depend on the cursor
@@ -419,7 +422,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           const unsigned short hv = h16<T>(fmaxf(best + PAR[P_C2B + oc], 0.f) * D2S[s * 20 + oc]);
           P2[s * 320 + oc * 16 + w] = hv;
           I2[s * 320 + oc * 16 + w] = (uint8_t)bi;
-          if (TRAIN && b < B) a.vslab[(int64_t)b * VEC + V_P2 + oc * 16 + w] = f16v<T>(hv);
+          if (TRAIN && b < B) VH[vec16_index(V_P2 + oc * 16 + w, b)] = hv;
         }
       }
     }
@@ -446,7 +449,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       if (o < 50) {  // sample kq, output o
         const float h = fmaxf(cz + PAR[P_F1B + o], 0.f) * D1S[kq * 52 + o];
         Hs[kq * 64 + o] = h;
-        if (TRAIN && b0 + kq < B) a.vslab[(int64_t)(b0 + kq) * VEC + V_H + o] = h;
+        if (TRAIN && b0 + kq < B) VH[vec16_index(V_H + o, b0 + kq)] = h16<T>(h);
       }
     }
     lds_barrier();
@@ -514,12 +517,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         float dl[10];
 #pragma unroll
         for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
-        float* vs = a.vslab + (int64_t)b * VEC;
+        unsigned short* vs = VH + vec16_index(0, b);
+        constexpr int vld = 4;
         if (valid && lane < 16) {
           float mine = 0.f;
 #pragma unroll
           for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
-          vs[V_DLOG + lane] = mine;
+          vs[(V_DLOG + lane) * vld] = h16<T>(mine);
         }
         float dh0 = 0.f, dh1 = 0.f;
 #pragma unroll
@@ -528,8 +532,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           else dh0 = fmaf(dl[c], w2c[c], dh0);
         }
         const float dz = (valid && lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
-        DZ1B[s * 64 + lane] = h16<T>(dz);
-        if (valid && lane < 50) vs[V_DZ1 + lane] = dz;
+        const unsigned short dzh = h16<T>(dz);
+        DZ1B[s * 64 + lane] = dzh;
+        if (valid && lane < 50) vs[(V_DZ1 + lane) * vld] = dzh;
       }
     }
     // the next tile's pixels (rows loaded one tile ago), then the rows of the tile after it

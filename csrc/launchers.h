@@ -140,9 +140,10 @@ struct LenetTrainArgs {
   const uint16_t* wimg;      // packed 16-bit weight images
   const float* params;       // flat fp32 master params [21840]
   float* slab;               // [grid, 5280] per-workgroup partial conv grads
-  float* vslab;              // [B, 464] per-sample fc vectors (P2 | dZ1 | H | dlogits)
+  float* vslab;              // fc vectors (P2 | dZ1 | H | dlogits): fp32 [B, 464], or for the
+                             // 16-bit kernels raw 16-bit [464, vec_ld(B)] (kernels/lenet_layout.h)
   float* loss_acc;           // [grid, 2] per-workgroup (loss sum, correct count)
-  float grad_scale;          // 1 / (global batch)
+  float grad_scale;          // dlogits scale: 1 / (global batch), or 1 with lenet_update's grad_post
   float mean, std_;
   float drop_p;
   uint64_t seed;
@@ -189,6 +190,10 @@ int64_t lenet_vec_len();           // 464 floats of per-sample fc vectors
 struct LenetUpdateArgs {
   const float* slab; int grid;
   const float* vslab; int B;         // per-sample fc vectors of the step and their count
+  // multiplies the reduced (rank-local) gradient before the exchange / export / SGD: the 16-bit
+  // steps run their backward at per-sample scale (grad_scale 1, so fp16 gradients stay normal
+  // numbers) and apply 1 / (global batch) here in fp32; 1 where the train kernel pre-scaled
+  float grad_post;
   const float* grad_in;
   float* grad_out;
   float* params; float* momentum; uint16_t* wimg;

@@ -55,7 +55,7 @@ def _kernel_masks(eng, B):
     vector slab the training kernel wrote for the batch at the cursor."""
     eng.gradient()
     torch.cuda.synchronize()
-    v = eng.vslab[:B].cpu()
+    v = eng.fc_vectors(B).cpu()
     p2 = v[:, V_P2:V_P2 + 320].view(B, 20, 16) != 0
     h = v[:, V_H:V_H + 50] != 0
     return p2.any(2), bool((p2.all(2) == p2.any(2)).all()), h
@@ -101,7 +101,7 @@ def test_mask_statistics_steps_and_ranks():
                         eng.flat.data, eng.slab, eng.vslab, eng.loss_parts, 1.0 / B, MNIST_MEAN, MNIST_STD, p,
                         99, eng.rng_offset, eng.grid, eng.mfma, None, None, None, False)
         torch.cuda.synchronize()
-        v = eng.vslab[:B].cpu()
+        v = eng.fc_vectors(B).cpu()
         r2 = (v[:, V_P2:V_P2 + 320].view(B, 20, 16) != 0).any(2)
         r1 = v[:, V_H:V_H + 50] != 0
         h2, h1 = host_masks(99, 0, 1, B, p)

@@ -35,7 +35,7 @@ def test_loopback_exchange_returns_world_copies(world, B):
               eng.nesterov, eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
     for _ in range(4):
         eng.slab.copy_(torch.randint(-8, 9, eng.slab.shape, generator=gen, dtype=torch.float32))
-        eng.vslab.copy_(torch.randint(-4, 5, eng.vslab.shape, generator=gen, dtype=torch.float32))
+        eng.set_fc_vectors(torch.randint(-4, 5, (eng.B, 464), generator=gen, dtype=torch.float32))
         local = torch.empty(N_PARAMS, device=eng.device)
         fused = torch.empty_like(local)
         ops.lenet_update(eng.slab, eng.grid, eng.vslab, eng.B, None, local, *common)

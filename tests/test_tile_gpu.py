@@ -37,7 +37,7 @@ def _grads(B, kernel, dt=torch.bfloat16, drop_p=0.5, n=None, seed=23, counter=3)
     eng.rng_offset.fill_(counter)
     g = eng.gradient()
     torch.cuda.synchronize()
-    return g.cpu(), eng.loss_acc.cpu().clone(), eng.vslab[:B].cpu().clone()
+    return g.cpu(), eng.loss_acc.cpu().clone(), eng.fc_vectors(B).cpu()
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
