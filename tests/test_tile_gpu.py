@@ -61,20 +61,28 @@ def test_tile_matches_per_sample_kernel(B, dt):
         off += n
 
 
-def test_tile_gradient_matches_cpu_reference():
-    """Dropout off: the tile kernel's gradient against the fp32 CPU Net (16-bit bands, as
-    test_fused_gpu.test_fused_gradient_matches_reference)."""
-    B = 1024
-    data = synthetic_mnist(2048, seed=11)
+# measured (tools/grad_bands.py, profiles/r3/grad_bands.txt): bf16 B=1024 conv <= 2.6e-2, fc <= 1.5e-2;
+# fp16 B=1024 conv <= 1.3e-2, fc <= 3.6e-3; fp16 B=8192 conv <= 3.7e-3, fc <= 1.6e-3 (the 16-bit
+# backward runs at per-sample scale, lenet_update applies 1 / B in fp32: with 1 / B inside the
+# fp16 backward, conv1's error at B = 8192 was 6-7e-3)
+@pytest.mark.parametrize("B,dt,conv_bound,fc_bound", [(1024, torch.bfloat16, 0.06, 0.03),
+                                                      (1024, torch.float16, 0.03, 0.008),
+                                                      (8192, torch.float16, 0.01, 0.004)])
+def test_tile_gradient_matches_cpu_reference(B, dt, conv_bound, fc_bound):
+    """Dropout off: the tile kernel's gradient against the fp32 CPU Net (16-bit bands: the conv
+    gradients follow max-pool / ReLU decisions that 16-bit rounding can flip, see
+    test_fused_gpu.test_reference_sensitivity)."""
+    n = max(2048, B)
+    data = synthetic_mnist(n, seed=11)
     torch.manual_seed(1)
     net, ref = Net(), Net()
     ref.load_state_dict(net.state_dict())
-    eng = FusedLeNetTrainer(net.to(DEV), data, global_batch=B, drop_p=0.0)
+    eng = FusedLeNetTrainer(net.to(DEV), data, global_batch=B, compute_dtype=dt, drop_p=0.0)
     assert eng.kernel_for(B, eng.grid) == 0 and eng.grid == tile_grid(B)  # auto -> tile kernel
-    order = torch.randperm(2048, generator=torch.Generator().manual_seed(0))[:B]
+    order = torch.randperm(n, generator=torch.Generator().manual_seed(0))[:B]
     eng.set_epoch_order(order)
     g = eng.gradient().cpu()
-    x = ((data.images[order].float() / 255.0 - MNIST_MEAN) / MNIST_STD).to(torch.bfloat16).float().view(-1, 1, 28, 28)
+    x = ((data.images[order].float() / 255.0 - MNIST_MEAN) / MNIST_STD).to(dt).float().view(-1, 1, 28, 28)
     ref.eval()
     out = ref(x)
     loss = F.nll_loss(out, data.labels[order])
@@ -85,7 +93,7 @@ def test_tile_gradient_matches_cpu_reference():
     for name, p in ref.named_parameters():
         n = p.numel()
         rel = _rel(g[off:off + n].view_as(p), p.grad)
-        assert rel < (6e-2 if name.startswith("fc") else 0.2), f"{name}: {rel:.3e}"
+        assert rel < (fc_bound if name.startswith("fc") else conv_bound), f"{name}: {rel:.3e}"
         off += n
 
 
