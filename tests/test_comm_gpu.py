@@ -130,6 +130,11 @@ def _worker(rank, world, port, q):
         res["fused_split_equals_ipc_split"] = p_is is None or torch.equal(p_is, p_fs)
         # both sum the same rank-local gradients in rank order: bitwise-identical training
         res["fused_equals_ipc"] = p_ipc is None or torch.equal(p_ipc, p_fused)
+        for name, (x, y) in (("ipc", (p_ipc, p_fused)), ("ipc_split", (p_is, p_fs))):
+            if x is not None:  # (diagnostics for a mismatch)
+                d = (x - y).abs()
+                res[f"maxdiff_{name}"] = float(d.max())
+                res[f"ndiff_{name}"] = int((d > 0).sum())
         q.put((rank, res))
         dist.destroy_process_group()
     except Exception as e:  # report, do not hang the parent
@@ -176,7 +181,8 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         assert res["step_fused"] == "two kernels", res
         assert res["native_fused"] and res["native_fused_split"], res
         assert not res.get("native_ipc", False), res
-        assert res["fused_equals_ipc"] and res["fused_split_equals_ipc_split"], res
+        diag = {k: v for k, v in res.items() if k.startswith(("maxdiff", "ndiff", "engine_errors", "errors"))}
+        assert res["fused_equals_ipc"] and res["fused_split_equals_ipc_split"], (r, diag)
         assert res["split_fused_split"] and not res["split_fused"], res
 
 
