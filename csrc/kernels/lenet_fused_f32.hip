@@ -91,7 +91,7 @@ __host__ __device__ constexpr int unit_lo(int w) { return (w * 45) / NW; }
 // KS > 1 (split step, staged batches: a.xstage holds one row per workgroup, grid = KS * B):
 // workgroup g is part g / B of sample g % B.  Every part runs the forward (the sample's dependency
 // chain) and dP2; the backward conv stages are divided: part j owns conv2 wgrad N-tiles 4j .. 4j+3
-// (waves 0-3) and the dgrad M-tiles {j, j+4, j+8} (5 units each over waves 4-15), and its conv1
+// (waves 0-3) and the dgrad M-tiles {j, j+4} plus a share of tile 8 (over waves 4-15), and its conv1
 // wgrad covers those tiles' pool1 pixels.  Part 0 alone writes the fc vectors and the loss; every
 // part stages its row of the next step (as the 16-bit split step, lenet_fused.hip).
 template <bool TRAIN, int KS = 1>
@@ -146,9 +146,17 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
   const int64_t pbase = cur0 * (int64_t)a.B + g;
   const bool stage_next = STAGED && a.stage_next;
-  // this part's dgrad M-tiles: {part, part + 4, part + 8 (part 0)}; all 9 without the split
-  const int ntl = STAGED ? (part == 0 ? 3 : 2) : 9;
-  auto tile_of = [&](int ti) { return STAGED ? part + 4 * ti : ti; };
+  // this part's dgrad M-tiles: {part, part + 4, 8}; all 9 without the split.  Tile 8 is shared:
+  // its K = (oc, tap) sum is split by oc block over the parts (part 0: block 4, parts 1 / 2:
+  // blocks 0 / 1, part 3: blocks 2 and 3), so every part runs 11-12 dgrad units on its 12 dgrad
+  // waves -- one each -- instead of part 0 running 15 (two on some waves: the step's critical
+  // path, profiles/tile_r3.md §3).  Each part's partial dL/dP1 of tile 8 goes through the
+  // (linear) relu / pool1 gate and conv1 wgrad on its own; the slab reduction adds the parts.
+  const int ntl = STAGED ? 3 : 9;
+  auto tile_of = [&](int ti) { return STAGED ? (ti < 2 ? part + 4 * ti : 8) : ti; };
+  // dgrad units of this part: u < 10 (or unsplit): tile u / 5, oc block u % 5; u >= 10: tile 8,
+  // oc block blk8 + u - 10
+  const int blk8 = part == 0 ? 4 : part - 1;
   auto row_of = [&](int s) { return a.perm[min(pbase + (int64_t)min(s, max(nsamp - 1, 0)) * G, a.perm_len - 1)]; };
 
   // sample pipeline: pixels (4 per thread) and label of sample s, row of sample s+1
@@ -589,10 +597,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         acc_c2[1] = mma(arow1[4 * ks], bv, acc_c2[1]);
       }
     }
-    // dgrad units (this part's M-tile ti < ntl, oc block j < 5): wave wd of NWD owns units
-    // [ulo(wd), ulo(wd + 1)) -- at most 2 units, at most 2 M-tiles
+    // dgrad units (this part's M-tile ti < ntl, oc block j < 5; see blk8): wave wd of NWD owns
+    // units [ulo(wd), ulo(wd + 1)) -- at most 3 units (unsplit), at most 2 M-tiles
     constexpr int NWD = STAGED ? NW - 4 : NW;
-    const int nu = 5 * ntl;
+    const int nu = STAGED ? 10 + (part == 3 ? 2 : 1) : 5 * ntl;
     auto ulo = [&](int w) { return (w * nu) / NWD; };
     const int wd = STAGED ? wave - 4 : wave;
     if (wd >= 0) {
@@ -612,7 +620,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         f32x4 ce[NU], co[NU];
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-          const int u = u0 + i, ti = u / 5, j = u - 5 * ti, t = tile_of(ti);
+          const int u = u0 + i, ti = u / 5, j = (STAGED && ti == 2) ? blk8 + u - 10 : u - 5 * ti, t = tile_of(ti);
           const int p = t * 16 + l16, y = p / 12, x = p - 12 * (p / 12);
           arow[i] = DY2 + (4 * j + kq) * 64 + y * 8 + x - 36;  // tap (kh, kw): [36 - kh*8 - kw]
           brow[i] = bcol + 4 * j * LW2;
