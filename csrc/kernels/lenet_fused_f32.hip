@@ -695,11 +695,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       const int pp = ic * 144 + tile_of(ti) * 16 + row;
       const int e = (row & 3) * 64 + (row >> 2) * 16 + ic;
       float v = 0.f;
+      if (STAGED) {
+        // one unit per wave (nu = 11 or 12 units on NWD = 12 waves): unit u is on wave u + off
+        // (ulo: with 11 units wave 0 has none), its sum in the wave's first accumulator; the
+        // units of tile ti in unit order -- the same order as the general loop below
+        const int off = nu == NWD ? 0 : 1, ua = 5 * ti, ub = ti < 2 ? ua + 5 : nu;
+        for (int u = ua; u < ub; ++u) v += RED[((u + off) * 2) * 256 + e];
+      } else {
 #pragma unroll
-      for (int w = 0; w < NWD; ++w) {
-        const int lo = ulo(w), hi = ulo(w + 1), tw = lo / 5;
-        if (tw == ti && lo < hi) v += RED[(w * 2) * 256 + e];
-        else if (tw + 1 == ti && (hi - 1) / 5 == ti) v += RED[(w * 2 + 1) * 256 + e];
+        for (int w = 0; w < NWD; ++w) {
+          const int lo = ulo(w), hi = ulo(w + 1), tw = lo / 5;
+          if (tw == ti && lo < hi) v += RED[(w * 2) * 256 + e];
+          else if (tw + 1 == ti && (hi - 1) / 5 == ti) v += RED[(w * 2 + 1) * 256 + e];
+        }
       }
       G1[pp] = P1[pp] > 0.f ? v : 0.f;
     }
