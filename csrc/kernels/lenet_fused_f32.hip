@@ -38,19 +38,30 @@ namespace lenet32 {
 using namespace csed::lenet;  // parameter order, slab and vector-slab layouts (lenet_layout.h)
 constexpr int NT = 1024, NW = 16;
 constexpr int LW1 = 321;  // fc1 weight row stride (odd: the fc1-forward lanes walk rows)
-constexpr int LW2 = 260;  // conv2 weight row stride (== 4 mod 64: conflict-free B fragments)
+// conv2 weight row pitch: 258 == 2 (mod 4).  ds_read_b32 banks are (a/4) mod 32 per 32-lane half:
+// the conv2 fwd B reads (lane = oc row l16 x K slot kq) hit 32 distinct banks only for a pitch
+// == 2 (mod 4) (260: rows l16 and l16 + 8 on one bank), and the dgrad B reads (lane = ic column
+// x oc row kq, rows 4j + kq) are conflict-free with it too.  Even, so rows are 8-byte aligned
+// (the VALU part reads float2 runs)
+constexpr int LW2 = 258;
 
 // LDS carve, floats (every region 16-byte aligned)
 constexpr int F_W1 = 0;                       // fc1.w  [50][LW1]
-constexpr int F_W2 = F_W1 + 16052;            // conv2.w [20][LW2], cols 250..259 zero
+constexpr int F_W2 = F_W1 + 16052;            // conv2.w [20][LW2], cols 250..257 zero
 constexpr int F_W1B = F_W2 + 20 * LW2;        // conv1 B operand [16 n][28 k], zero padded
 constexpr int F_PAR = F_W1B + 448;            // c1b 0, c2b 10, f1b 30, f2b 80, f2w 90 (500)
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 constexpr int F_X = F_PAR + 592;              // normalised pixels [784] (+ pad)
 constexpr int F_P1 = F_X + 788;               // pool1 output [10][144]
 constexpr int F_P2 = F_P1 + 1444;             // pool2 output = fc1 input [20][16]
-constexpr int F_DY2 = F_P2 + 320;             // dL/dconv2 [20][64], zero word at 1280
-constexpr int F_G1 = F_DY2 + 1284;            // gated dL/dP1 [10][144]
+// dL/dconv2 row pitch: 78 == 14 (mod 32).  ds_read_b32 banks are (a/4) mod 32 per 32-lane half
+// (MI355X_MICROARCH.md, LDS): the conv2 wgrad A reads (lane = oc row l16 x pixel kq) need the
+// pitch == 2 (mod 4) to hit 32 distinct banks (pitch 64: 16 rows on one bank, 16-way), and the
+// dgrad A reads (lane = pixel l16 x oc row kq, 12 consecutive pixels per row) need the two rows of
+// a half 12-20 banks apart: both hold for 78 (and 82)
+constexpr int DY2_LD = 78;
+constexpr int F_DY2 = F_P2 + 320;             // dL/dconv2 [20][DY2_LD], zero word at 20 * DY2_LD
+constexpr int F_G1 = F_DY2 + (20 * DY2_LD + 4) / 4 * 4;  // gated dL/dP1 [10][144]
 constexpr int F_ONES = F_G1 + 1440;           // 96 ones (conv2 wgrad bias column)
 constexpr int F_ZEROS = F_ONES + 96;          // 96 zeros (its padding columns)
 constexpr int F_SM = F_ZEROS + 96;            // D2S 0, D1S 32, H 96, DZ1 160, label 224
@@ -213,7 +224,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       L[F_ZEROS + tid] = 0.f;
     }
     if (tid < 4) X[784 + tid] = 0.f;
-    if (tid == 0) DY2[1280] = 0.f;
+    if (tid == 0) DY2[20 * DY2_LD] = 0.f;
     if (tid < 256) {  // conv2 fwd A offsets: k = ic*25 + kh*5 + kw -> ic*144 + kh*12 + kw (K pad -> k 249)
       const int k = min(4 * (tid & 63) + (tid >> 6), 249), ic = k / 25, r = k - 25 * ic;
       K2[tid] = (unsigned short)(ic * 144 + (r / 5) * 12 + (r % 5));
@@ -386,8 +397,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
           for (int j = 0; j < 8; ++j) av[j] = pa[o[j]];
 #pragma unroll
           for (int oc = 0; oc < 4; ++oc) {
-            const float4 w0 = *reinterpret_cast<const float4*>(W2 + (16 + oc) * LW2 + kb);
-            const float4 w1 = *reinterpret_cast<const float4*>(W2 + (16 + oc) * LW2 + kb + 4);
+            const float* wr = W2 + (16 + oc) * LW2 + kb;
+            const float2 w0a = *reinterpret_cast<const float2*>(wr), w0b = *reinterpret_cast<const float2*>(wr + 2);
+            const float2 w1a = *reinterpret_cast<const float2*>(wr + 4), w1b = *reinterpret_cast<const float2*>(wr + 6);
+            const float4 w0 = make_float4(w0a.x, w0a.y, w0b.x, w0b.y), w1 = make_float4(w1a.x, w1a.y, w1b.x, w1b.y);
             acc[oc] = fmaf(av[0], w0.x, acc[oc]);
             acc[oc] = fmaf(av[1], w0.y, acc[oc]);
             acc[oc] = fmaf(av[2], w0.z, acc[oc]);
@@ -568,7 +581,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         const float gv = P2[tid] > 0.f ? dp * SM[S_D2S + oc] : 0.f;
         const int bi = I2[tid], oy0 = 2 * (w >> 2), ox0 = 2 * (w & 3);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) DY2[oc * 64 + (oy0 + (q >> 1)) * 8 + ox0 + (q & 1)] = q == bi ? gv : 0.f;
+        for (int q = 0; q < 4; ++q) DY2[oc * DY2_LD + (oy0 + (q >> 1)) * 8 + ox0 + (q & 1)] = q == bi ? gv : 0.f;
       }
     }
     __syncthreads();
@@ -588,8 +601,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       } else {
         bsrc = L + (k == 250 ? F_ONES : F_ZEROS) + kq;
       }
-      const float* arow0 = DY2 + l16 * 64 + kq;
-      const float* arow1 = DY2 + min(16 + l16, 19) * 64 + kq;  // rows >= 20: discarded outputs
+      const float* arow0 = DY2 + l16 * DY2_LD + kq;
+      const float* arow1 = DY2 + min(16 + l16, 19) * DY2_LD + kq;  // rows >= 20: discarded outputs
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks) {
         const float bv = bsrc[(ks >> 1) * 12 + 4 * (ks & 1)];
@@ -622,7 +635,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         for (int i = 0; i < NU; ++i) {
           const int u = u0 + i, ti = u / 5, j = (STAGED && ti == 2) ? blk8 + u - 10 : u - 5 * ti, t = tile_of(ti);
           const int p = t * 16 + l16, y = p / 12, x = p - 12 * (p / 12);
-          arow[i] = DY2 + (4 * j + kq) * 64 + y * 8 + x - 36;  // tap (kh, kw): [36 - kh*8 - kw]
+          arow[i] = DY2 + (4 * j + kq) * DY2_LD + y * 8 + x - 36;  // tap (kh, kw): [36 - kh*8 - kw]
           brow[i] = bcol + 4 * j * LW2;
           // taps with 0 <= y - kh < 8 and 0 <= x - kw < 8, as a 25-bit mask (bit kh*5 + kw): per
           // tap one bit test selects the row pointer or the zero run, and the load keeps an
