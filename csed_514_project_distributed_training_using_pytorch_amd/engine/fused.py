@@ -200,16 +200,19 @@ class FusedLeNetTrainer:
         self._eval_cache: dict[int, tuple] = {}
         self._order_host: torch.Tensor | None = None
         self.capture_comm_ok: bool | None = None
-        # gradient all-reduce.  Fallback step (3 kernels): the one-shot IPC kernel
-        # (csrc/comm) when every rank passes its self-test, else RCCL (parallel/ipc.py).
-        # Preferred: the exchange fused into lenet_update (1 kernel), see module docstring.
+        # gradient all-reduce.  Preferred: the exchange fused into lenet_update (see the module
+        # docstring).  Fallback step (3 kernels: reduce-only update -> all-reduce -> SGD): RCCL;
+        # the one-shot IPC all-reduce kernel (csrc/comm) only when CSED_ALLREDUCE=ipc asks for
+        # it -- with two ranks sharing one GPU its engine path was seen to leave the replicas
+        # unequal without a reported timeout (profiles/dp_exchange_r3.md, open), so `auto` never
+        # trains on it.
         self.exch = None
         self.exchange_note: str | None = None  # why the data-parallel step runs as it does (reports)
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"
-        self.allreduce = make_allreduce(self.ctx, N_PARAMS) if multi and mode != "fused" else None
+        self.allreduce = make_allreduce(self.ctx, N_PARAMS) if multi and mode == "ipc" else None
         if multi and mode in ("auto", "fused"):
             self._enable_exchange(required=(mode == "fused"))
         # Loopback exchange (one GPU, no process group): lenet_update runs its full push + poll

@@ -21,7 +21,7 @@ def main():
     eng = FusedLeNetTrainer(Net().to(dev), data, global_batch=B)
     eng.set_epoch_order(torch.randperm(len(data)))
     plans = {"1": [1], "2": [2], "5": [5], "20": [20], "1+19": [1, 19], "2+18": [2, 18], "4+16": [4, 16],
-             "200": [200]}
+             "200": [200], "19": [19], "18": [18], "16": [16]}
     for p in plans.values():
         for n in p:
             eng.graph(n)
@@ -29,7 +29,10 @@ def main():
     res = {}
     plans.update({"sleep+1": ["s", 1], "sleep+20": ["s", 20], "eager1": ["e"], "eager5": ["e"] * 5, "eager20": ["e"] * 20,
                   "native1": [("n", 1)], "native5": [("n", 5)], "native20": [("n", 20)], "native200": [("n", 200)],
-                  "sleep+native20": ["s", ("n", 20)]})
+                  "sleep+native20": ["s", ("n", 20)],
+                  # the first step(s) from the native executor, the rest as one graph replay: does the
+                  # graph's launch latency hide behind the native steps?
+                  "n1+19": [("n", 1), 19], "n2+18": [("n", 2), 18], "n4+16": [("n", 4), 16]})
     st = eng.stepper()  # csed.LenetStepper: the native step executor
     st.run(1)
     for name, p in plans.items():
