@@ -202,10 +202,8 @@ class FusedLeNetTrainer:
         self.capture_comm_ok: bool | None = None
         # gradient all-reduce.  Preferred: the exchange fused into lenet_update (see the module
         # docstring).  Fallback step (3 kernels: reduce-only update -> all-reduce -> SGD): RCCL;
-        # the one-shot IPC all-reduce kernel (csrc/comm) only when CSED_ALLREDUCE=ipc asks for
-        # it -- with two ranks sharing one GPU its engine path was seen to leave the replicas
-        # unequal without a reported timeout (profiles/dp_exchange_r3.md, open), so `auto` never
-        # trains on it.
+        # the one-shot IPC all-reduce kernel (csrc/comm) when CSED_ALLREDUCE=ipc asks for it
+        # (`auto` keeps one IPC path, the fused one: one self-test and timing less at bring-up).
         self.exch = None
         self.exchange_note: str | None = None  # why the data-parallel step runs as it does (reports)
         self.exch_timeout_s = wait_timeout_s()
