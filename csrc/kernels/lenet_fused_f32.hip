@@ -52,8 +52,12 @@ constexpr int F_W1B = F_W2 + 20 * LW2;        // conv1 B operand [16 n][28 k], z
 constexpr int F_PAR = F_W1B + 448;            // c1b 0, c2b 10, f1b 30, f2b 80, f2w 90 (500)
 constexpr int P_C1B = 0, P_C2B = 10, P_F1B = 30, P_F2B = 80, P_F2W = 90;
 constexpr int F_X = F_PAR + 592;              // normalised pixels [784] (+ pad)
-constexpr int F_P1 = F_X + 788;               // pool1 output [10][144]
-constexpr int F_P2 = F_P1 + 1444;             // pool2 output = fc1 input [20][16]
+// pool1 output / gated dL/dP1 channel pitch: 146 == 2 (mod 4), so conv1's epilogue stores (lane =
+// channel l16 < 10 x pooled pixel kq) hit 20 distinct banks (ds_write_b32: (a/4) mod 32 per
+// 32-lane half; pitch 144 put the 10 channels on 2 banks, 5-way)
+constexpr int P1_LD = 146, XPOS_LD = 148;  // (XPOS: u16, 74 dwords == 10 mod 32: 10 distinct banks)
+constexpr int F_P1 = F_X + 788;               // pool1 output [10][P1_LD]
+constexpr int F_P2 = F_P1 + (10 * P1_LD + 3) / 4 * 4;  // pool2 output = fc1 input [20][16]
 // dL/dconv2 row pitch: 78 == 14 (mod 32).  ds_read_b32 banks are (a/4) mod 32 per 32-lane half
 // (MI355X_MICROARCH.md, LDS): the conv2 wgrad A reads (lane = oc row l16 x pixel kq) need the
 // pitch == 2 (mod 4) to hit 32 distinct banks (pitch 64: 16 rows on one bank, 16-way), and the
@@ -61,16 +65,15 @@ constexpr int F_P2 = F_P1 + 1444;             // pool2 output = fc1 input [20][1
 // a half 12-20 banks apart: both hold for 78 (and 82)
 constexpr int DY2_LD = 78;
 constexpr int F_DY2 = F_P2 + 320;             // dL/dconv2 [20][DY2_LD], zero word at 20 * DY2_LD
-constexpr int F_G1 = F_DY2 + (20 * DY2_LD + 4) / 4 * 4;  // gated dL/dP1 [10][144]
-constexpr int F_ONES = F_G1 + 1440;           // 96 ones (conv2 wgrad bias column)
+constexpr int F_G1 = F_DY2 + (20 * DY2_LD + 4) / 4 * 4;  // gated dL/dP1 [10][P1_LD]
+constexpr int F_ONES = F_G1 + (10 * P1_LD + 3) / 4 * 4;  // 96 ones (conv2 wgrad bias column)
 constexpr int F_ZEROS = F_ONES + 96;          // 96 zeros (its padding columns)
 constexpr int F_SM = F_ZEROS + 96;            // D2S 0, D1S 32, H 96, DZ1 160, label 224
 constexpr int F_RED = F_SM + 256;             // reduction scratch [8192]
 constexpr int F_END = F_RED + 8192;
-constexpr int B_I1 = F_END * 4;               // u8  [1440] pool1 argmax
-constexpr int B_I2 = B_I1 + 1440;             // u8  [320]  pool2 argmax
-constexpr int B_XPOS = B_I2 + 320;            // u16 [1440] X offset of the pool1 argmax pixel
-constexpr int B_K2 = B_XPOS + 2880;           // u16 [4][64] conv2 fwd: (lane group q, K-step ks) -> P1 offset of k = 4 ks + q
+constexpr int B_I2 = F_END * 4;               // u8  [320]  pool2 argmax
+constexpr int B_XPOS = B_I2 + 320;            // u16 [10][XPOS_LD] X offset of the pool1 argmax pixel
+constexpr int B_K2 = B_XPOS + 10 * XPOS_LD * 2;           // u16 [4][64] conv2 fwd: (lane group q, K-step ks) -> P1 offset of k = 4 ks + q
 constexpr int B_K2L = B_K2 + 512;             // u16 [256]  the same offsets in k order (conv2 fwd VALU part)
 constexpr int B_DBG = B_K2L + 512;            // u64 [16]   stage stamps (a.dbg, diagnostics)
 constexpr int LDS_BYTES = B_DBG + 16 * 8;
@@ -122,7 +125,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   float* G1 = L + F_G1;
   float* SM = L + F_SM;
   float* RED = L + F_RED;
-  uint8_t* I1 = smem + B_I1;
   uint8_t* I2 = smem + B_I2;
   unsigned short* XPOS = reinterpret_cast<unsigned short*>(smem + B_XPOS);
   unsigned short* K2 = reinterpret_cast<unsigned short*>(smem + B_K2);
@@ -227,9 +229,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     if (tid == 0) DY2[20 * DY2_LD] = 0.f;
     if (tid < 256) {  // conv2 fwd A offsets: k = ic*25 + kh*5 + kw -> ic*144 + kh*12 + kw (K pad -> k 249)
       const int k = min(4 * (tid & 63) + (tid >> 6), 249), ic = k / 25, r = k - 25 * ic;
-      K2[tid] = (unsigned short)(ic * 144 + (r / 5) * 12 + (r % 5));
+      K2[tid] = (unsigned short)(ic * P1_LD + (r / 5) * 12 + (r % 5));
       const int kl = min(tid, 249), icl = kl / 25, rl = kl - 25 * icl;
-      K2L[tid] = (unsigned short)(icl * 144 + (rl / 5) * 12 + (rl % 5));
+      K2L[tid] = (unsigned short)(icl * P1_LD + (rl / 5) * 12 + (rl % 5));
     }
   }
   // conv1 A offsets of this lane's 7 K-steps (tap k = 4*ks + kq, K pad clamped to tap 24)
@@ -284,7 +286,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     }
     __syncthreads();
 
-    // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, XPOS
+    // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, XPOS (the argmax pixel)
     STAMP32(3);
     {
       float bv[7];
@@ -323,9 +325,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
             for (int r = 1; r < 4; ++r)
               if (c[r] > best) { best = c[r]; bi = r; }
             const int w = mt * 4 + kq, py = w / 12, pxw = w - 12 * py;  // pooled position
-            P1[l16 * 144 + w] = fmaxf(best + cb, 0.f);
-            I1[l16 * 144 + w] = (uint8_t)bi;
-            XPOS[l16 * 144 + w] = (unsigned short)((2 * py + (bi >> 1)) * 28 + 2 * pxw + (bi & 1));
+            P1[l16 * P1_LD + w] = fmaxf(best + cb, 0.f);
+            XPOS[l16 * XPOS_LD + w] = (unsigned short)((2 * py + (bi >> 1)) * 28 + 2 * pxw + (bi & 1));
           }
         }
       }
@@ -562,15 +563,21 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     STAMP32(7);
     {
       if (wave < 15) {
-        // output range pr (fc1 units 17 pr .. 17 pr + 16) on waves 5 pr .. 5 pr + 4, so the
-        // bounds are wave-uniform; column i = 64 (wave % 5) + lane
-        const int pr = wave / 5, i = (wave - 5 * pr) * 64 + lane, o0 = 17 * pr, o1 = min(o0 + 17, 50);
+        // output range pr (fc1 units 16 pr .. 16 pr + 15; the last 32 .. 49) on waves 5 pr ..
+        // 5 pr + 4, so the bounds are wave-uniform; column i = 64 (wave % 5) + lane.  The range's
+        // dZ1 values come as five broadcast float4 reads (stage 4 writes zeros past unit 49)
+        const int pr = wave / 5, i = (wave - 5 * pr) * 64 + lane, o0 = 16 * pr, n = pr < 2 ? 16 : 18;
+        float dz[20];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const float4 v4 = *reinterpret_cast<const float4*>(SM + S_DZ1 + o0 + 4 * k);
+          dz[4 * k] = v4.x; dz[4 * k + 1] = v4.y; dz[4 * k + 2] = v4.z; dz[4 * k + 3] = v4.w;
+        }
         float d0 = 0.f, d1 = 0.f;
 #pragma unroll
-        for (int u = 0; u < 17; u += 2) {  // (the same two chains as a loop over o in [o0, o1))
-          const int o = o0 + u;
-          if (o < o1) d0 = fmaf(SM[S_DZ1 + o], W1[o * LW1 + i], d0);
-          if (o + 1 < o1) d1 = fmaf(SM[S_DZ1 + o + 1], W1[(o + 1) * LW1 + i], d1);
+        for (int u = 0; u < 20; u += 2) {  // (two chains over o in [o0, o0 + n))
+          if (u < n) d0 = fmaf(dz[u], W1[(o0 + u) * LW1 + i], d0);
+          if (u + 1 < n) d1 = fmaf(dz[u + 1], W1[(o0 + u + 1) * LW1 + i], d1);
         }
         RED[pr * 320 + i] = d0 + d1;
       }
@@ -597,7 +604,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       const float* bsrc;
       if (k < 250) {
         const int ic = k / 25, r = k - 25 * ic;
-        bsrc = P1 + ic * 144 + (r / 5) * 12 + (r % 5) + kq;
+        bsrc = P1 + ic * P1_LD + (r / 5) * 12 + (r % 5) + kq;
       } else {
         bsrc = L + (k == 250 ? F_ONES : F_ZEROS) + kq;
       }
@@ -705,7 +712,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     STAMP32(9);
     for (int idx = tid; idx < 160 * ntl; idx += NT) {
       const int ic = idx / (16 * ntl), rem = idx - 16 * ntl * ic, ti = rem >> 4, row = rem & 15;
-      const int pp = ic * 144 + tile_of(ti) * 16 + row;
+      const int pp = ic * P1_LD + tile_of(ti) * 16 + row;
       const int e = (row & 3) * 64 + (row >> 2) * 16 + ic;
       float v = 0.f;
       if (STAGED) {
@@ -736,8 +743,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       if (tid < 1000) {
         const int j = tid % 250, q4 = tid / 250, oc = j / 25, tap = j - 25 * oc;
         const int koff = (tap / 5) * 28 + (tap % 5);
-        const float* gr = G1 + oc * 144;
-        const unsigned short* xr = XPOS + oc * 144;
+        const float* gr = G1 + oc * P1_LD;
+        const unsigned short* xr = XPOS + oc * XPOS_LD;
         float s0 = 0.f, s1 = 0.f;
         for (int i = q4 * nq; i < (q4 + 1) * nq; i += 2) {
           const int p0 = px_at(i), p1 = px_at(i + 1);
@@ -750,7 +757,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       if (tid < 250) {
         acc_c1 += (RED[tid] + RED[256 + tid]) + (RED[512 + tid] + RED[768 + tid]);
       } else if (tid >= 256 && tid < 266) {  // conv1.b: sum over the gated pooled pixels
-        const float* gr = G1 + (tid - 256) * 144;
+        const float* gr = G1 + (tid - 256) * P1_LD;
         float s0 = 0.f, s1 = 0.f;
         for (int i = 0; i < npx; i += 2) {
           s0 += gr[px_at(i)];
