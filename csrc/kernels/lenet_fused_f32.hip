@@ -96,6 +96,14 @@ __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// A workgroup barrier that waits for this wave's LDS operations only.  __syncthreads() also
+// waits for every outstanding vector-memory operation (vmcnt(0)): inside the sample loop that
+// made waves 12-15 wait at stage 0's barrier for the next step's perm row and at stage 3's for
+// its pixels (loads meant to stay in flight until the epilogue), and part 0's waves for their
+// vector-slab stores.  Every barrier of the sample loop is this one: no data crosses waves
+// through global memory there.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ int64_t kF32Zero = 0;  // the counter an absent cursor / Philox offset reads
 
 // conv2 dgrad work units: (tile t < 9, oc block j < 5) of 25 K-steps, tile-major; wave w owns
@@ -260,7 +268,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     const int b = b0 + s * G;
     float* vs = TRAIN ? a.vslab + (int64_t)b * VEC : nullptr;
     const bool wvec = TRAIN && own;
-    __syncthreads();  // previous sample's readers done (first pass: the preamble's writes)
+    lds_sync();  // previous sample's readers done (first pass: the preamble's writes)
     STAMP32(2);
     // ---------------- stage 0: pixels, dropout masks; the next sample's loads
     if (stage_next && wave >= 12) rown = a.perm[min((cur0 + 1) * (int64_t)a.B + b0, a.perm_len - 1)];
@@ -284,7 +292,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       lab = (int)a.labels[rown];
       rown = row_of(s + 2);
     }
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, XPOS (the argmax pixel)
     STAMP32(3);
@@ -334,7 +342,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       if (wave < 36 - 2 * NW) tiles(std::integral_constant<int, 3>{});
       else tiles(std::integral_constant<int, 2>{});
     }
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
     // oc 0-15: one MFMA N-tile, 4 M-tiles x 2 K halves on waves 0-3 / 8-11.  oc 16-19 (a second
@@ -415,7 +423,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
 #pragma unroll
         for (int oc = 0; oc < 4; ++oc) RED[2048 + vw * 256 + oc * 64 + m] = acc[oc];
       }
-      __syncthreads();
+      lds_sync();
       auto emit = [&](int oc, int wp, float best, int bi) {
         const float v = fmaxf(best + PAR[P_C2B + oc], 0.f) * SM[S_D2S + oc];
         P2[oc * 16 + wp] = v;
@@ -450,7 +458,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         emit(16 + o4, wp, best, bi);
       }
     }
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H (VALU, fixed-order combine)
     STAMP32(5);
@@ -461,14 +469,21 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     {
       const int o = min(lane, 49), i0 = wave * 20;
       const float* wr = W1 + o * LW1 + i0;
+      // this wave's 20 inputs as five broadcast float4 reads (i0 = 20 * wave: 16-byte aligned)
+      float pv[20];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float4 v4 = *reinterpret_cast<const float4*>(P2 + i0 + 4 * k);
+        pv[4 * k] = v4.x; pv[4 * k + 1] = v4.y; pv[4 * k + 2] = v4.z; pv[4 * k + 3] = v4.w;
+      }
       float z0 = 0.f, z1 = 0.f;
 #pragma unroll
       for (int u = 0; u < 20; u += 2) {
-        z0 = fmaf(wr[u], P2[i0 + u], z0);
-        z1 = fmaf(wr[u + 1], P2[i0 + u + 1], z1);
+        z0 = fmaf(wr[u], pv[u], z0);
+        z1 = fmaf(wr[u + 1], pv[u + 1], z1);
       }
       RED[wave * 64 + lane] = z0 + z1;
-      __syncthreads();
+      lds_sync();
       if (tid < 50) {
         float z = 0.f;
 #pragma unroll
@@ -478,7 +493,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         if (wvec) vs[V_H + tid] = h;
       }
     }
-    __syncthreads();
+    // (no barrier: fc1's outputs are written by wave 0, the loss stage's only wave, which reads
+    // them next; RED is next written after stage 4's barrier)
 
     // ---------------- stage 4: fc2, log_softmax, NLL, dlogits, dZ1 (wave 0)
     STAMP32(6);
@@ -557,7 +573,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       }
     }
     if (!TRAIN) continue;
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 5: dP2 = dZ1 . W1 (VALU), pool2 / relu / Dropout2d backward -> DY2
     STAMP32(7);
@@ -581,7 +597,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         }
         RED[pr * 320 + i] = d0 + d1;
       }
-      __syncthreads();
+      lds_sync();
       if (tid < 320) {
         const int oc = tid >> 4, w = tid & 15;
         const float dp = (RED[tid] + RED[320 + tid]) + RED[640 + tid];
@@ -591,7 +607,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         for (int q = 0; q < 4; ++q) DY2[oc * DY2_LD + (oy0 + (q >> 1)) * 8 + ox0 + (q & 1)] = q == bi ? gv : 0.f;
       }
     }
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers; conv2 dgrad units
     // (split step: this part's 4 wgrad N-tiles on waves 0-3, its dgrad units on waves 4-15)
@@ -705,7 +721,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         RED[(wd * 2 + 1) * 256 + r * 64 + lane] = acc1[r];
       }
     }
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 7: dgrad combine (fixed wave order), relu / pool1 gate -> G1
     // (this part's M-tiles only; conv1 wgrad reads only their pixels)
@@ -731,7 +747,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       }
       G1[pp] = P1[pp] > 0.f ? v : 0.f;
     }
-    __syncthreads();
+    lds_sync();
 
     // ---------------- stage 8: conv1 wgrad over the argmax pixels (VALU) + bias
     STAMP32(10);
@@ -753,7 +769,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         }
         RED[q4 * 256 + j] = s0 + s1;
       }
-      __syncthreads();
+      lds_sync();
       if (tid < 250) {
         acc_c1 += (RED[tid] + RED[256 + tid]) + (RED[512 + tid] + RED[768 + tid]);
       } else if (tid >= 256 && tid < 266) {  // conv1.b: sum over the gated pooled pixels
