@@ -576,7 +576,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
-    __syncthreads();  // also the weight DMA (first pass): conv2 reads W2C next
+    // the weight DMA (waves 0-3, preamble) is in LDS before conv2 reads W2C.  Every barrier of the
+    // sample loop is LDS-only: __syncthreads() also waits vmcnt(0) in every wave, i.e. for the
+    // next step's perm row / pixels loaded for the epilogue and for the vector-slab stores
+    if (wave < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2
     STAMP(2);
@@ -613,7 +617,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         if (wvec) vs[(V_P2 + oc * 16 + w) * vld] = hv;  // fc1 input, exactly as the forward used it
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H   (waves 0-3; the idle waves
     // zeroing / X copies moved to stage 4, where 15 waves are idle)
@@ -642,7 +646,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- stage 4: fc2 + log_softmax + NLL, then dlogits and the fc1
     // pre-activation gradient dZ1 (wave 0; everything stays inside the wave)
@@ -757,7 +761,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       __builtin_amdgcn_s_setprio(0);
     }
     if (!TRAIN) return;
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- stage 5: dP2 = dZ1 . W1 on the MFMA (B = fc1 image read
     // transposed), fused with the pool2 / relu / Dropout2d backward -> dC2 (2 layouts)
@@ -801,7 +805,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     if constexpr (KS > 1) {
       // ---------------- stage 6 (split step): this part's conv2 wgrad N-tile on waves 12-15,
@@ -900,7 +904,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         WSTAMP(11, 29);
       }
       WSTAMP(12, 27);
-      __syncthreads();
+      lds_barrier();
       STAMP(7);
       if (tid < T3 * 256) {
         // dgrad: fixed-order sum of the K parts, then the relu / pool1 backward into DC1
@@ -918,7 +922,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       }
       WSTAMP(0, 30);
       WSTAMP(12, 31);
-      __syncthreads();
+      lds_barrier();
     } else {
     // ---------------- stage 6: conv2 wgrad (+bias column 250) into registers, and
       // conv2 dgrad -> dP1 -> relu/pool1 backward -> dC1
@@ -1017,7 +1021,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   #pragma unroll
         for (int r = 0; r < 4; ++r) RED[w8 * 256 + (4 * kq + r) * 16 + l16] = c8[r];
       }
-      __syncthreads();
+      lds_barrier();
       STAMP(7);
       if (TRAIN && STAGED && tid >= 256) store_c2(tid - 256, NT - 256);  // write latency hides under stage 8
       if (tid < 256) {  // tile 8: fixed-order sum of the 8 shares, then the pool1/relu backward
@@ -1029,7 +1033,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           dgrad_out<T>(DC1, P1, I1, ci, 128 + rr, v);
         }
       }
-      __syncthreads();
+      lds_barrier();
   
     }
 
@@ -1080,14 +1084,14 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   if (a.dbg && tid == 0) DBGS[11] = __builtin_amdgcn_s_memtime();
   // ---------------- epilogue: write this workgroup's partial gradient + loss
   if (TRAIN) {
-    __syncthreads();
+    lds_barrier();
     // conv1: the four step-slices of each tile; partial of wave w at part(w): RED for
     // waves 0-7, the dead DC2H image for 8-15
     auto part = [&](int w) { return w < 8 ? RED + w * 256 : reinterpret_cast<float*>(DC2H) + (w - 8) * 256; };
 #pragma unroll
     for (int r = 0; r < 4; ++r) part(wave)[(4 * (lane >> 4) + r) * 16 + l16] = acc_c1[r];
     if (!STAGED) stage_c2();  // (staged: stored at stage 7)
-    __syncthreads();
+    lds_barrier();
     if (tid < 512) {  // conv1 combine (fixed order)
       const int nt = tid >> 8, oc = (tid >> 4) & 15, col = tid & 15;
       float v = 0.f;
