@@ -333,9 +333,14 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1H (HWC), I1
     TSTAMP(3);
     {
-      // M-tile T = wave + 16 i (i < 9): sample T / 36, tile mt = T % 36 of its 576 pool-ordered
-      // pixels -- wave-uniform, so every address is a scalar part plus a lane constant: rows
-      // 4 mt .. 4 mt + 3 of pooled windows lie in pooled row mt / 3, columns 4 (mt % 3) + 0..3
+      // M-tile T = 9 wave + k (k < 9): sample wave / 4, tile mt = 9 (wave % 4) + k of its 576
+      // pool-ordered pixels -- rows 4 mt .. 4 mt + 3 of pooled windows lie in pooled row mt / 3,
+      // columns 4 (mt % 3) + 0..3.  With k a compile-time constant every address is one scalar
+      // base per wave plus immediates (mt / 3 = 3 (wave % 4) + k / 3, mt % 3 = k % 3); the
+      // earlier T = wave + 16 k needed ~200 scalar instructions per wave (divisions by 36 and
+      // 3) that, not hoisted in the one-tile instantiation, queued on each SIMD's scalar issue
+      // (one SALU instruction per 4 cycles for the SIMD's four waves: conv1 7.1k vs 5.6k cycles)
+      const int wsmp = wave >> 2, wq = wave & 3;  // this wave's sample, quarter of its tiles
       const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
       const float cb = PAR[P_C1B + min(l16, 9)];
       const int q1 = l16 & 3;
@@ -353,8 +358,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         uint32_t r0[3], r1[3], e4[3], r2[3], e2[3];
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
-          const int T9 = wave + NW * (3 * grp + it), ss = T9 / 36, mt = T9 - 36 * ss;
-          const int xs = ss * X_LD + (mt / 3) * 56 + 8 * (mt % 3);  // scalar, even
+          const int k = 3 * grp + it;  // (compile-time)
+          const int xs = wsmp * X_LD + wq * 168 + (k / 3) * 56 + 8 * (k % 3);  // scalar, even
           r0[it] = xr1[xs / 2];
           r1[it] = xr1[xs / 2 + 1];
           e4[it] = xe1[xs];
@@ -366,15 +371,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           // [t0 t1 | t2 t3 | t4 u0 | u1 u2]: row kq's 5 taps, then row 4's 3
           const uint4 raw = make_uint4(r0[it], r1[it], e4[it] | (r2[it] << 16), (r2[it] >> 16) | (e2[it] << 16));
           const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
-          const int T9 = wave + NW * (3 * grp + it), ss = T9 / 36, mt = T9 - 36 * ss;
+          const int k = 3 * grp + it, mt3 = 3 * wq + k / 3, mtr = k % 3;  // mt / 3, mt % 3
           float best;
           int bi;
           pool4(c, best, bi);
           if (l16 < 10) {  // pooled window (mt / 3, 4 (mt % 3) + kq), channel l16
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
-            P1H[ss * P1H_SZ + (mt / 3) * P1H_RP + (4 * (mt % 3)) * LD_P1H + pl] = hv;
+            P1H[wsmp * P1H_SZ + mt3 * P1H_RP + (4 * mtr) * LD_P1H + pl] = hv;
             // argmax of the window, or 4 where the relu gate (stored pool1 output > 0) is shut
-            I1[ss * 1440 + 4 * mt + il] = (uint8_t)((hv & 0x7fff) ? bi : 4);
+            I1[wsmp * 1440 + 4 * (3 * mt3 + mtr) + il] = (uint8_t)((hv & 0x7fff) ? bi : 4);
           }
         }
       }
