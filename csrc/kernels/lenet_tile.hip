@@ -748,14 +748,18 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       const int kcol = (wave & 1) * 16 + l16, kc = min(kcol, 24), kh = kc / 5, kw = kc - 5 * kh;
       const unsigned short* pconst = kcol == 25 ? ONES : ZERO;
       const int oc = min(l16, 9);  // A rows 10-15 feed discarded outputs
-#pragma unroll 3
+      // K-steps 9 w2 + j (j < 9) of wave pair w2: all in sample w2 / 2 (= wave / 4), rows
+      // r = 36 (w2 % 2) + 4 j + kq -- one base per wave and compile-time steps (the earlier
+      // w2 + 8 j spread a pair over the samples: divisions by 18 per step on the scalar issue)
+      const int ss = wave >> 2, rb = 36 * ((wave >> 1) & 1) + kq;
+      const unsigned short* arow = DY1(ss) + oc * DY1_LD;
+      // pixels X[o .. o + 7], o = (oh + kh) * 28 + ow0 + kw == kw (mod 2): copy kw & 1
+      const unsigned short* xrow = X + (kw & 1) * XCP + ss * X_LD + kh * 28 + (kw & ~1);
+#pragma unroll
       for (int j = 0; j < 9; ++j) {
-        const int J = (wave >> 1) + 8 * j, ss = J / 18, ps = J - 18 * ss;  // wave-uniform
-        const int r = 4 * ps + kq, oh = r / 3, ow0 = 8 * (r - 3 * oh);      // conv1 pixels 8 r .. 8 r + 7
-        const frag fa = *reinterpret_cast<const frag*>(DY1(ss) + oc * DY1_LD + 8 * r);
-        // pixels X[o .. o + 7], o = (oh + kh) * 28 + ow0 + kw == kw (mod 2): copy kw & 1
-        const uint32_t* xb = reinterpret_cast<const uint32_t*>(
-            kcol < 25 ? X + (kw & 1) * XCP + ss * X_LD + (oh + kh) * 28 + ow0 + (kw & ~1) : pconst);
+        const int r = rb + 4 * j, oh = r / 3, ow0 = 8 * (r - 3 * oh);  // conv1 pixels 8 r .. 8 r + 7
+        const frag fa = *reinterpret_cast<const frag*>(arow + 8 * r);
+        const uint32_t* xb = reinterpret_cast<const uint32_t*>(kcol < 25 ? xrow + oh * 28 + ow0 : pconst);
         acc_c1 = Mfma<T>::mma(fa, __builtin_bit_cast(frag, make_uint4(xb[0], xb[1], xb[2], xb[3])), acc_c1);
       }
     }
