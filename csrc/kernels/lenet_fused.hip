@@ -870,7 +870,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       static_assert(3 * 4 * 256 * 4 <= S_XC - S_C1T && 2 * 6 * 256 * 4 <= S_XC - S_C1T, "dgrad partials");
       const int T3 = part == 0 ? 3 : 2;  // dgrad tiles part, part + 4 (, part + 8)
       const int P = T3 == 3 ? 4 : 6;     // K parts per tile
-      if (wave < 12) {
+      // (T3 / P as compile-time constants in the body: with them at run time, wave % T3,
+      // wave / T3 and pp * DG_KS / P were emulated 32-bit divisions on each wave's scalar
+      // issue, one SALU instruction per 4 cycles for a SIMD's waves)
+      auto dgrad_split = [&](auto t3c) {
+        constexpr int T3 = decltype(t3c)::value, P = T3 == 3 ? 4 : 6;
         const int ts = wave % T3, pp = wave / T3;
         const int mw = (part + 4 * ts) * 16 + l16;
         const int ks0 = pp * DG_KS / P, ks1 = (pp + 1) * DG_KS / P;  // at most 5 K-steps
@@ -902,6 +906,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         WSTAMP(0, 25);
         WSTAMP(4, 28);
         WSTAMP(11, 29);
+      };
+      if (wave < 12) {
+        if (part == 0) dgrad_split(std::integral_constant<int, 3>{});
+        else dgrad_split(std::integral_constant<int, 2>{});
       }
       WSTAMP(12, 27);
       lds_barrier();
