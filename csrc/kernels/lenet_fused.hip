@@ -193,6 +193,24 @@ constexpr int UP_C = 16, UP_S = 32, UP_MAXL = 8, UP_NT = UP_C * UP_S;
 // owns conv2 wgrad columns [64j, 64j+64) and dgrad tiles {j, j+4, j+8}, and its conv1
 // wgrad covers the conv1 pixels of those tiles.  Part 0 alone writes the fc vector slab and
 // the loss partials.  The backward conv stages are a third of the per-sample chain.
+// Split step, stage 8: the conv1-wgrad K-steps (32 conv1 pixels each) under part j's dgrad tiles
+// j, j + 4 (, j + 8 for part 0) -- the rest of the part's dL/dconv1 is zero
+struct SplitNeed { uint32_t m[4]; };
+__host__ __device__ constexpr SplitNeed split_need_table() {
+  SplitNeed r{};
+  for (int part = 0; part < 4; ++part) {
+    uint32_t need = 0;
+    for (int ts = 0; ts < (part == 0 ? 3 : 2); ++ts) {
+      const int t = part + 4 * ts, py0 = (16 * t) / 12, py1 = (16 * t + 15) / 12;
+      const int ps0 = (48 * py0) / 32, ps1 = (48 * (py1 + 1) - 1) / 32;
+      need |= ((2u << ps1) - 1) & ~((1u << ps0) - 1);
+    }
+    r.m[part] = need;
+  }
+  return r;
+}
+__device__ constexpr SplitNeed kSplitNeed = split_need_table();
+
 template <typename T, bool TRAIN, bool STAGED, int KS = 1>
 __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
   static_assert(KS == 1 || (KS == SPLIT_K && STAGED && TRAIN), "split step: staged training only");
@@ -251,7 +269,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // (a.grid, not gridDim.x: every launcher sets it, and it is in the prefetched argument lines)
   const int G = a.grid, g = blockIdx.x;
   // this workgroup's (first) sample and, in the split step, which part of it
-  const int b0 = KS > 1 ? g % a.B : g, part = KS > 1 ? g / a.B : 0;
+  // (part = g / B for g < 4 B, as three compares: a run-time division is a long emulated
+  // sequence on every wave's scalar issue)
+  const int part = KS > 1 ? (g >= a.B) + (g >= 2 * a.B) + (g >= 3 * a.B) : 0, b0 = g - part * a.B;
   const bool own_vec = part == 0;  // writes the sample's fc vectors and loss
   const int R2 = min(G, a.B);      // rows of the slab's conv2 chunks
   // staged: this thread's conv1 address row, first in the vector memory queue
@@ -1066,15 +1086,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       }
       // split step: only the K-steps (32 conv1 pixels each) under this part's dgrad tiles
       // carry gradient (the rest of DC1 is zero)
-      uint32_t need = (1u << 18) - 1;
-      if (KS > 1) {
-        need = 0;
-        for (int ts = 0; ts < (part == 0 ? 3 : 2); ++ts) {
-          const int t = part + 4 * ts, py0 = (16 * t) / 12, py1 = (16 * t + 15) / 12;
-          const int ps0 = (48 * py0) / 32, ps1 = (48 * (py1 + 1) - 1) / 32;
-          need |= ((2u << ps1) - 1) & ~((1u << ps0) - 1);
-        }
-      }
+      // (a compile-time table per part: computed here it was ~45 scalar instructions per wave)
+      const uint32_t need = KS > 1 ? kSplitNeed.m[part & 3] : (1u << 18) - 1;
 #pragma unroll
       for (int i = 0; i < 3; ++i)
         if ((KS == 1 || wave < 12) && (wave >> 1) + (KS > 1 ? 6 : 8) * i < 18 &&
@@ -1233,6 +1246,15 @@ __host__ __device__ constexpr int fc_blocks(int B) {
   return (FC_TILES + fc_tiles_per_block(B) - 1) / fc_tiles_per_block(B);
 }
 __host__ __device__ constexpr int update_blocks(int B) { return fc_blocks(B) + NB_CONV; }
+// (update_role shifts by log2 of both: they must stay powers of two)
+__host__ __device__ constexpr bool fc_shapes_pow2() {
+  for (int B : {1, 32, 64, 128, 129, 256, 257, 512, 513, 1024, 8192}) {
+    const int w = fc_waves_per_tile(B), t = fc_tiles_per_block(B);
+    if ((w & (w - 1)) || (t & (t - 1))) return false;
+  }
+  return true;
+}
+static_assert(fc_shapes_pow2(), "fc waves per tile / tiles per block: powers of two");
 constexpr int NB_FC = FC_TILES;                     // FC blocks at most (one tile each)
 // FC tile of workgroup b (one tile per workgroup): b = 8 * slot + xcd takes position
 // 11 * xcd + slot of the fc1 tiles in column-block-major order (q -> row block q % 4, column
@@ -1442,8 +1464,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
 
-  // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (the exchange's fixed map)
-  const int nb_fc = fc_tpb > 0 ? (FC_TILES + fc_tpb - 1) / fc_tpb : fc_blocks(B);
+  // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (the exchange's fixed map).
+  // Tiles per block and waves per tile are powers of two: shifts, not run-time divisions (a
+  // division by a run-time value is a long emulated sequence on every wave's scalar issue)
+  const int tpb_ = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
+  const int nb_fc = (FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_);
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
@@ -1541,13 +1566,13 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // as the chunk path.  Splitting K over waves instead (B = 32 /
     // 64: 2 / 4 waves per tile + an LDS combine) was slower: +0.1 / +0.4 us per step.
     const bool small = B <= 32;
-    const int wpt = fc_waves_per_tile(B);
-    const int tpb = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
-    const bool live_wave = wave / wpt < tpb;      // (uniform) waves past the block's tiles idle
+    const int wpt = fc_waves_per_tile(B), lw = __builtin_ctz(wpt);  // (1, 2, 4 or 8)
+    const int tpb = tpb_;
+    const bool live_wave = (wave >> lw) < tpb;    // (uniform) waves past the block's tiles idle
     // one tile per workgroup: XCD-grouped tiles.  Workgroup b runs on XCD b % 8; the tiles
     // in (fc1 column-block, row-block) order are dealt out 11 per XCD, so an XCD's tiles share
     // their column blocks (B operand rows of the vector slab) and its L2 fetches each line once
-    const int tile_w = tpb == 1 ? fc_tile_of_block(blk) : blk * tpb + wave / wpt, sub = wave % wpt;
+    const int tile_w = tpb == 1 ? fc_tile_of_block(blk) : blk * tpb + (wave >> lw), sub = wave & (wpt - 1);
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
     const int tile = min(tile_w, FC_TILES - 1);   // they compute a valid tile, store nothing
     const bool fc1 = tile < FC1_TILES;
@@ -1593,7 +1618,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // this wave's samples [k0, k1): a multiple-of-4 (16-bit layout: of-32) share of the batch
     constexpr bool FC16 = !std::is_same<T, float>::value;
     constexpr int KG = FC16 ? 32 : 4;
-    const int kw = ((B + wpt - 1) / wpt + KG - 1) & ~(KG - 1);
+    const int kw = (((B + wpt - 1) >> lw) + KG - 1) & ~(KG - 1);
     const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
     f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (FC16) {

@@ -154,7 +154,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, kq = lane >> 4;
   const int G = gridDim.x, g = blockIdx.x;
-  const int b0 = STAGED ? g % a.B : g, part = STAGED ? g / a.B : 0;
+  // (part = g / B for g < 4 B, as three compares: a run-time division is a long emulated
+  // sequence on every wave's scalar issue)
+  const int part = STAGED ? (g >= a.B) + (g >= 2 * a.B) + (g >= 3 * a.B) : 0, b0 = g - part * a.B;
   const bool own = part == 0;      // writes the sample's fc vectors and loss
   const int R2 = STAGED ? a.B : G; // slab rows of the conv2 chunks (one per sample in the split step)
   const float inv_std = 1.f / a.std_;
