@@ -529,40 +529,39 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
       for (int c = 0; c < 10; ++c)
         lg[c] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, zp), 4 * c)) +
                 PAR[P_F2B + c];
+      // lane c < 10 holds logit c as well (bpermute from lane 4c, the same sum as lg[c]): the
+      // label's logit, the argmax and the per-lane stores below read it instead of ten
+      // compare / select steps each
+      const int lc = min(lane, 9), tu = __builtin_amdgcn_readfirstlane(t);
+      const float zl = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(16 * lc, __builtin_bit_cast(int, zp))) +
+                       PAR[P_F2B + lc];
       float mx = lg[0];
-      int amax = 0;
 #pragma unroll
-      for (int c = 1; c < 10; ++c)
-        if (lg[c] > mx) { mx = lg[c]; amax = c; }
-      float ex[10], se = 0.f, lt = 0.f;
+      for (int c = 1; c < 10; ++c) mx = fmaxf(mx, lg[c]);
+      // first index attaining the max (torch argmax)
+      const int amax = __builtin_ctzll(__ballot(lane < 10 && zl == mx));
+      float ex[10], se = 0.f;
 #pragma unroll
       for (int c = 0; c < 10; ++c) {
         ex[c] = __expf(lg[c] - mx);
         se += ex[c];
-        lt = c == t ? lg[c] : lt;
       }
-      const float lse = mx + __logf(se);
+      const float lt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, zl), tu));
+      // se is in [1, 10]: the hardware log2 / reciprocal (1 ulp) need no denormal or
+      // special-case handling
+      const float lse = mx + __builtin_amdgcn_logf(se) * 0.693147180559945309f;
       if (lane == 0 && own) {
         loss_sum += lse - lt;
         correct += (amax == t) ? 1.f : 0.f;
       }
       if (write_logp && lane < 10) {
-        float mine = 0.f;
-#pragma unroll
-        for (int c = 0; c < 10; ++c) mine = lane == c ? lg[c] : mine;
-        logp_out[(int64_t)b * 10 + lane] = mine - lse;
+        logp_out[(int64_t)b * 10 + lane] = zl - lse;
       }
       if (TRAIN) {
-        const float gs = a.grad_scale * (1.f / se);
+        const float gs = a.grad_scale * __builtin_amdgcn_rcpf(se);
         float dl[10];
 #pragma unroll
         for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
-        if (wvec && lane < 16) {
-          float mine = 0.f;
-#pragma unroll
-          for (int c = 0; c < 10; ++c) mine = lane == c ? dl[c] : mine;
-          vs[V_DLOG + lane] = mine;
-        }
         float dh0 = 0.f, dh1 = 0.f;
 #pragma unroll
         for (int c = 0; c < 10; ++c) {
@@ -572,6 +571,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
         const float dz = (lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
         SM[S_DZ1 + lane] = dz;
         if (wvec && lane < 50) vs[V_DZ1 + lane] = dz;
+        if (wvec && lane < 16) {
+          // lane c's dlogit, computed as dl[c] is (lanes 10-15 store the zero padding)
+          const float mine = lane < 10 ? __expf(zl - mx) * gs - (lane == tu ? a.grad_scale : 0.f) : 0.f;
+          vs[V_DLOG + lane] = mine;
+        }
       }
     }
     if (!TRAIN) continue;
