@@ -546,55 +546,62 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, P1H
     STAMP(1);
     {
-      // 36 tiles over 8 waves: gather all five tiles' fragments, then the MFMAs
-      // 36 tiles over 16 waves: at most 3 per wave
-      uint32_t rv[3][8];
+      // 36 tiles over 16 waves: 3 on waves 0-3, 2 on the others (a compile-time count, so
+      // the 2-tile waves issue no reads for a dead third tile -- a quarter of the stage's LDS
+      // reads).  All fragments are gathered first, the independent MFMAs issued back to
+      // back, then one epilogue region for all tiles (per-tile branches serialised each
+      // tile's MFMA latency and epilogue chain behind the previous one's)
       // per-thread tables (kC1Tab row / preamble, waves 8-15)
       const u16x4 xo = STAGED ? __builtin_bit_cast(u16x4, make_uint2(c1row.x, c1row.y)) : C1T[tid];
       const u16x4 ho = STAGED ? __builtin_bit_cast(u16x4, make_uint2(c1row.z, c1row.w)) : C1H[tid];
+      auto tiles = [&](auto nti) {
+        constexpr int NTI = decltype(nti)::value;
+        uint32_t rv[NTI][8];
 #pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        const int pb = xo[it];
-        // K slots of lane group kq (see w1c_slot): row kq, then 3 taps of row 4
-        const unsigned short* r1 = Xs + pb + 28 * kq;
-        const unsigned short* r2 = Xs + pb + 112 + (kq == 1 ? W1_E1 : 0);
-        rv[it][0] = lds_u16<0>(r1);
-        rv[it][1] = lds_u16<1>(r1);
-        rv[it][2] = lds_u16<2>(r1);
-        rv[it][3] = lds_u16<3>(r1);
-        rv[it][4] = lds_u16<4>(r1);
-        rv[it][5] = lds_u16<0>(r2);
-        rv[it][6] = lds_u16<1>(r2);
-        rv[it][7] = lds_u16<2>(r2);
-      }
-      u16x8 raw[3];
+        for (int it = 0; it < NTI; ++it) {
+          const int pb = xo[it];
+          // K slots of lane group kq (see w1c_slot): row kq, then 3 taps of row 4
+          const unsigned short* r1 = Xs + pb + 28 * kq;
+          const unsigned short* r2 = Xs + pb + 112 + (kq == 1 ? W1_E1 : 0);
+          rv[it][0] = lds_u16<0>(r1);
+          rv[it][1] = lds_u16<1>(r1);
+          rv[it][2] = lds_u16<2>(r1);
+          rv[it][3] = lds_u16<3>(r1);
+          rv[it][4] = lds_u16<4>(r1);
+          rv[it][5] = lds_u16<0>(r2);
+          rv[it][6] = lds_u16<1>(r2);
+          rv[it][7] = lds_u16<2>(r2);
+        }
+        const float cb = PAR[P_C1B + min(l16, 9)];
+        const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
+        f32x4 c[NTI];
 #pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        lds_wait8(rv[it]);
+        for (int it = 0; it < NTI; ++it) {
+          lds_wait8(rv[it]);
+          u16x8 raw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[it][j] = (unsigned short)rv[it][j];
-      }
-      const float cb = PAR[P_C1B + min(l16, 9)];
-      const frag fb1 = *reinterpret_cast<const frag*>(W1Cs + l16 * 32 + kb);
+          for (int j = 0; j < 8; ++j) raw[j] = (unsigned short)rv[it][j];
+          c[it] = Mfma<T>::mma(__builtin_bit_cast(frag, raw), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
+        }
+        if (l16 < 10) {
 #pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        const int mt = wave + it * NW;
-        if (mt < 36) {
-          const f32x4 c = Mfma<T>::mma(__builtin_bit_cast(frag, raw[it]), fb1, f32x4{0.f, 0.f, 0.f, 0.f});
-          if (l16 < 10) {
-            float best = c[0];
+          for (int it = 0; it < NTI; ++it) {
+            float best = c[it][0];
             int bi = 0;
 #pragma unroll
             for (int r = 1; r < 4; ++r)
-              if (c[r] > best) { best = c[r]; bi = r; }
-            const int w = mt * 4 + kq;  // pooled position py*12 + px
+              if (c[it][r] > best) { best = c[it][r]; bi = r; }
+            const int w = (wave + it * NW) * 4 + kq;  // pooled position py*12 + px
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
             P1[l16 * 144 + w] = hv;
             I1[l16 * 144 + w] = (uint8_t)bi;
             P1H[ho[it] + l16] = hv;
           }
         }
-      }
+      };
+      static_assert(36 - 2 * NW == 4, "conv1: 3 tiles on waves 0-3, 2 on the rest");
+      if (wave < 36 - 2 * NW) tiles(std::integral_constant<int, 3>{});
+      else tiles(std::integral_constant<int, 2>{});
     }
     // the weight DMA (waves 0-3, preamble) is in LDS before conv2 reads W2C.  Every barrier of the
     // sample loop is LDS-only: __syncthreads() also waits vmcnt(0) in every wave, i.e. for the
