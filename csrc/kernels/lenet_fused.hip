@@ -289,7 +289,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // argument loads would wait for it)
   typedef const __attribute__((address_space(1))) int64_t* gptr64;
   const uint64_t rng_ctr = (uint64_t)((gptr64)rngp)[opaque(0)];
-  const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
   // (staged: a deferred per-lane load, only the next-step row needs it; the multi-sample path
@@ -655,13 +654,21 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
     if (wave < 4) {
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
+      // A = the fc1 input broadcast to all 16 rows: output row r depends on A row r only, and
+      // only row 0 is kept, so no lane needs masking.  All 20 operand reads are issued before
+      // the first MFMA (one LDS round trip, not one per K-step pair)
+      frag pa[10], fb[10];
+#pragma unroll
+      for (int ks = 0; ks < 10; ++ks) {
+        pa[ks] = *reinterpret_cast<const frag*>(P2 + ks * 32 + kb);
+        fb[ks] = *reinterpret_cast<const frag*>(wrow + ks * 32);
+      }
+      __builtin_amdgcn_sched_barrier(0);
       f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;  // even / odd K-step chains
 #pragma unroll
       for (int ks = 0; ks < 10; ++ks) {
-        const frag pa = *reinterpret_cast<const frag*>(P2 + ks * 32 + kb);
-        const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 32);
-        if (ks & 1) c1 = Mfma<T>::mma(l16 == 0 ? pa : zfrag, fb, c1);
-        else c0 = Mfma<T>::mma(l16 == 0 ? pa : zfrag, fb, c0);
+        if (ks & 1) c1 = Mfma<T>::mma(pa[ks], fb[ks], c1);
+        else c0 = Mfma<T>::mma(pa[ks], fb[ks], c0);
       }
       const f32x4 c = c0 + c1;
       if (lane < 16) {
@@ -798,28 +805,43 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // transposed), fused with the pool2 / relu / Dropout2d backward -> dC2 (2 layouts)
     STAMP(5);
     {
-      // A = dZ1 as row 0 (K = fc1 output o, 64 = 2 steps); tile t = output channel t of P2
+      // A = dZ1 in every row (K = fc1 output o, 64 = 2 steps: only C row 0 is kept, and row r
+      // depends on A row r only); tile t = output channel t of P2
       const frag dz0 = *reinterpret_cast<const frag*>(DZ1B + kb);
       const frag dz1 = *reinterpret_cast<const frag*>(DZ1B + 32 + kb);
-      const frag fa0 = l16 == 0 ? dz0 : zfrag, fa1 = l16 == 0 ? dz1 : zfrag;
       // lane 4q+p reads rows o = ks*32 + kb + {0,4} + q (rows >= 50: the zero row)
       const unsigned short* fc0 = F1s + min(kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc1 = F1s + min(kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc2 = F1s + min(32 + kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc3 = F1s + min(32 + kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
+      // output channels t = wave + 16 tt: 2 on waves 0-3, 1 on the others (compile-time
+      // counts: both tiles' transposed reads and MFMAs before either epilogue)
+      auto tiles = [&](auto ntt) {
+        constexpr int NTT = decltype(ntt)::value;
+        s16x4 r[NTT][4];
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int t = wave + NW * tt;  // wave-uniform: EXEC stays full for the transposed reads
-        if (t < 20) {
-          const s16x4 r0 = lds_read_tr16(fc0 + t * 16), r1 = lds_read_tr16(fc1 + t * 16);
-          const s16x4 r2 = lds_read_tr16(fc2 + t * 16), r3 = lds_read_tr16(fc3 + t * 16);
-          f32x4 c = Mfma<T>::mma(fa0, __builtin_bit_cast(frag, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7)),
-                                 f32x4{0.f, 0.f, 0.f, 0.f});
-          c = Mfma<T>::mma(fa1, __builtin_bit_cast(frag, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7)), c);
-          if (lane < 16) {
+        for (int tt = 0; tt < NTT; ++tt) {
+          const int t = wave + NW * tt;  // wave-uniform: EXEC stays full for the transposed reads
+          r[tt][0] = lds_read_tr16(fc0 + t * 16);
+          r[tt][1] = lds_read_tr16(fc1 + t * 16);
+          r[tt][2] = lds_read_tr16(fc2 + t * 16);
+          r[tt][3] = lds_read_tr16(fc3 + t * 16);
+        }
+        f32x4 c[NTT];
+#pragma unroll
+        for (int tt = 0; tt < NTT; ++tt) {
+          c[tt] = Mfma<T>::mma(dz0, __builtin_bit_cast(frag, __builtin_shufflevector(r[tt][0], r[tt][1], 0, 1, 2, 3, 4, 5, 6, 7)),
+                               f32x4{0.f, 0.f, 0.f, 0.f});
+          c[tt] = Mfma<T>::mma(dz1, __builtin_bit_cast(frag, __builtin_shufflevector(r[tt][2], r[tt][3], 0, 1, 2, 3, 4, 5, 6, 7)),
+                               c[tt]);
+        }
+        if (lane < 16) {
+#pragma unroll
+          for (int tt = 0; tt < NTT; ++tt) {
+            const int t = wave + NW * tt;
             // C row 0: lane w holds dP2[t][w]; unpool window w of channel t
             const int pi = t * 16 + lane;
-            const float gv = f16v<T>(P2[pi]) > 0.f ? c[0] * D2S[t] : 0.f;
+            const float gv = f16v<T>(P2[pi]) > 0.f ? c[tt][0] * D2S[t] : 0.f;
             const int bi = I2[pi];
             const int oh0 = 2 * (lane >> 2), ow0 = 2 * (lane & 3);
             const uint32_t hg = h16<T>(gv);
@@ -834,7 +856,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
             }
           }
         }
-      }
+      };
+      static_assert(20 - NW == 4, "dP2: 2 channels on waves 0-3, 1 on the rest");
+      if (wave < 20 - NW) tiles(std::integral_constant<int, 2>{});
+      else tiles(std::integral_constant<int, 1>{});
     }
     lds_barrier();
 
