@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     if (wave < TS) {
       const int s = wave, b = b0 + s;
       const bool valid = b < B;
-      const int t = LAB[s];
+      const int t = LAB[s + opaque(0)];  // (lane-variant index: no early readfirstlane wait)
       const float* H = Hs + s * 64;
       const int o = min(lane, 49);
       float w2c[10];
@@ -497,7 +497,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       // lane c < 10 holds logit c as well (bpermute from lane 4c, the same sum as lg[c]): the
       // label's logit, the argmax and the per-lane stores below read it instead of ten
       // compare / select steps each
-      const int lc = min(lane, 9), tu = __builtin_amdgcn_readfirstlane(t);
+      const int lc = min(lane, 9);
       const float zl = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(16 * lc, __builtin_bit_cast(int, zp))) +
                        PAR[P_F2B + lc];
       float mx = lg[0];
@@ -511,7 +511,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         ex[c] = __expf(lg[c] - mx);
         se += ex[c];
       }
-      const float lt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, zl), tu));
+      // (t stays a VGPR: a wave-uniform copy in an SGPR made hipcc wait for the label's LDS read
+      // ahead of every other read of the stage)
+      const float lt = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(4 * t, __builtin_bit_cast(int, zl)));
       // se is in [1, 10]: the hardware log2 / reciprocal (1 ulp) need no denormal or
       // special-case handling
       const float lse = mx + __builtin_amdgcn_logf(se) * 0.693147180559945309f;
@@ -541,7 +543,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         if (valid && lane < 50) vs[(V_DZ1 + lane) * vld] = dzh;
         if (valid && lane < 16) {
           // lane c's dlogit, computed as dl[c] is (lanes 10-15 store the zero padding)
-          const float mine = lane < 10 ? __expf(zl - mx) * gs - (lane == tu ? a.grad_scale : 0.f) : 0.f;
+          const float mine = lane < 10 ? __expf(zl - mx) * gs - (lane == t ? a.grad_scale : 0.f) : 0.f;
           vs[(V_DLOG + lane) * vld] = h16<T>(mine);
         }
       }
