@@ -289,6 +289,26 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // argument loads would wait for it)
   typedef const __attribute__((address_space(1))) int64_t* gptr64;
   const uint64_t rng_ctr = (uint64_t)((gptr64)rngp)[opaque(0)];
+  // Stage 0's LDS work (the preamble's, for a staged sample): zero the HWC conv1 image (thread
+  // i of 512) -- conv1 writes channels 0-9 of each position at stage 1; channels 10-15 meet zero
+  // conv2 weights in the K sum, so they must hold finite values (zero), not whatever the LDS
+  // last held (DC2 / DC1 rows >= 20 / >= 10 only feed discarded output rows and need no init);
+  // and the dropout scales of sample b (thread i < 70: Dropout2d's 20 channels, then dropout's
+  // 50 units)
+  auto zero_p1h = [&](int i) {
+    constexpr int NZ = (S_DC2 - S_P1H) / 16;
+    uint4* z = reinterpret_cast<uint4*>(P1H);
+    for (; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
+  };
+  auto dropout_scales = [&](int i, int b) {
+    float sc = 1.f;
+    if (TRAIN) {
+      const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)a.B + b) * 70ull + i;
+      sc = dropout_keep(a.seed, rng_ctr << 20, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
+    }
+    if (i < 20) D2S[i] = sc;
+    else D1S[i - 20] = sc;
+  };
   // samples of this workgroup: b = g, g + G, ...; sample s reads perm[cursor*B + b]
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
   // (staged: a deferred per-lane load, only the next-step row needs it; the multi-sample path
@@ -424,6 +444,14 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       conv1_tables(tid);
     }
     if (tid - 512 < 16) CONSTB[tid - 512] = tid - 512 < 8 ? (unsigned short)0 : h16<T>(1.f);
+    if (STAGED) {
+      // the staged sample's stage 0, on these otherwise idle waves while waves 0-7 wait for
+      // the preamble's loads: its dropout masks and the zero HWC conv1 image (see stage 0),
+      // so the sample starts at conv1 with one barrier fewer
+      const int tz = tid - 512;
+      zero_p1h(tz);
+      if (tz < 70) dropout_scales(tz, b0);
+    }
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
   // chain) and the row indices of samples 0..63 (one per lane); these waits do
@@ -504,15 +532,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // one wave-role branch there made hipcc wait vmcnt(0) -- for the weight DMA -- at the end
     // of the DMA branch of waves 0-3)
     if (KS > 1 && stage_next && wave >= 12 && s == 0) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
-    if (wave >= 8) {
-      // idle waves: zero the HWC conv1 image.  conv1 writes channels 0-9 of each
-      // position at stage 1; channels 10-15 meet zero conv2 weights in the K sum, so
-      // they must hold finite values (zero), not whatever the LDS last held.  (DC2 /
-      // DC1 rows >= 20 / >= 10 only feed discarded output rows and need no init.)
-      constexpr int NZ = (S_DC2 - S_P1H) / 16;
-      uint4* z = reinterpret_cast<uint4*>(P1H);
-      for (int i = tid - 512; i < NZ; i += 512) z[i] = make_uint4(0, 0, 0, 0);
-    }
+    if (!STAGED && wave >= 8) zero_p1h(tid - 512);  // (staged: in the preamble)
     // label of this sample: staged -> LDS (preamble), else the register pipeline
     const int t_lab = STAGED ? 0 : (s == 0 ? lab : __builtin_amdgcn_readlane(labv, s & 63));
     {
@@ -523,15 +543,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           o[j] = h16<T>(((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std);
         put_x(tid, o);
       }
-      if (tid < 70) {
-        float sc = 1.f;
-        if (TRAIN) {
-          const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)a.B + b) * 70ull + tid;
-          sc = dropout_keep(a.seed, rng_ctr << 20, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
-        }
-        if (tid < 20) D2S[tid] = sc;
-        else D1S[tid - 20] = sc;
-      }
+      if (!STAGED && tid < 70) dropout_scales(tid, b);  // (staged: in the preamble)
       if (!STAGED && s + 1 < nsamp) {
         const int sn = s + 1;
         if ((sn & 63) == 0) rowv = perm_at(min(sn + lane, nsamp - 1));
@@ -540,7 +552,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         px = reinterpret_cast<const uint32_t*>(a.images + rn * 784)[min(tid, 195)];
       }
     }
-    lds_barrier();
+    if (!STAGED) lds_barrier();  // (staged: stage 0 writes no LDS, the preamble did its part)
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, I1, P1H
     STAMP(1);
