@@ -196,6 +196,26 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     lab = reinterpret_cast<const int*>(a.lstage + g)[2 * lane0];
   }
 
+  // Stage 0's LDS work for sample b: the normalised pixels, the label and the dropout scales
+  // (the 16-bit kernel's Philox stream: identical masks for a given step)
+  auto stage0 = [&](int tid, int b) {
+    if (tid < 196) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        X[4 * tid + j] = ((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std;
+    }
+    if (tid == 0) reinterpret_cast<int*>(SM)[S_LAB] = lab;
+    if (tid < 70) {
+      float sc = 1.f;
+      if (TRAIN) {
+        const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)a.B + b) * 70ull + tid;
+        sc = dropout_keep(a.seed, rng_off, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
+      }
+      if (tid < 20) SM[S_D2S + tid] = sc;
+      else SM[S_D1S + tid - 20] = sc;
+    }
+  };
+
   // ---------------- once per workgroup: fp32 parameters -> LDS, constant tables
   {
     // every global load of the preamble is issued before the first LDS store (one round trip)
@@ -215,6 +235,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     const int qp = min(tid, 589);
     const float vp = a.params[qp < 10 ? O_C1B + qp : qp < 30 ? O_C2B + qp - 10 : qp < 80 ? O_F1B + qp - 30
                                                         : qp < 90 ? O_F2B + qp - 80 : O_F2W + qp - 90];
+    // the staged sample's stage 0 while the parameter loads are in flight (its pixels, label and
+    // step counter were loaded first), so the sample starts at conv1 with one barrier fewer
+    if (STAGED) stage0(tid, b0);
 #pragma unroll
     for (int j = 0; j < NF1; ++j) {
       const int q = tid + j * NT;
@@ -274,27 +297,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_f32_kernel(LenetTrainArgs a
     STAMP32(2);
     // ---------------- stage 0: pixels, dropout masks; the next sample's loads
     if (stage_next && wave >= 12) rown = a.perm[min((cur0 + 1) * (int64_t)a.B + b0, a.perm_len - 1)];
-    if (tid < 196) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        X[4 * tid + j] = ((float)((px >> (8 * j)) & 255u) * (1.f / 255.f) - a.mean) * inv_std;
-    }
-    if (tid == 0) reinterpret_cast<int*>(SM)[S_LAB] = lab;
-    if (tid < 70) {
-      float sc = 1.f;
-      if (TRAIN) {  // the 16-bit kernel's Philox stream: identical masks for a given step
-        const uint64_t e = (uint64_t)(a.rank_stride * (int64_t)a.B + b) * 70ull + tid;
-        sc = dropout_keep(a.seed, rng_off, e, a.drop_p) ? 1.f / (1.f - a.drop_p) : 0.f;
-      }
-      if (tid < 20) SM[S_D2S + tid] = sc;
-      else SM[S_D1S + tid - 20] = sc;
-    }
+    if (!STAGED) stage0(tid, b);  // (staged: in the preamble)
     if (!STAGED && s + 1 < nsamp) {
       px = reinterpret_cast<const uint32_t*>(a.images + rown * 784)[min(tid, 195)];
       lab = (int)a.labels[rown];
       rown = row_of(s + 2);
     }
-    lds_sync();
+    if (!STAGED) lds_sync();  // (staged: stage 0 writes no LDS, the preamble did its part)
 
     // ---------------- stage 1: conv1 + bias + maxpool + relu -> P1, XPOS (the argmax pixel)
     STAMP32(3);
