@@ -177,7 +177,6 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
   const uint64_t rng_ctr = (uint64_t)((TRAIN && a.rng_offset) ? a.rng_offset : &kTileZero)[lane0];
   const int64_t pbase = cur0 * (int64_t)B;
   auto perm_at = [&](int b) { return a.perm[min(pbase + (int64_t)min(b, B - 1), a.perm_len - 1)]; };
-  const frag zfrag = __builtin_bit_cast(frag, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   const unsigned short one = h16<T>(1.f);
   // keep-scales of tile tl (Philox, as lenet_train: key (rank * B + batch position) * 70 +
   // unit), thread t < TS * 70 of the drawing waves
@@ -436,18 +435,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     // ---------------- stage 3: fc1 + bias + relu + dropout -> H (rows = the tile's samples)
     TSTAMP(5);
     if (wave < 4) {
-      // A rows 4 s = sample s (the other rows zero): C row 4 kq (register 0) of every lane group
-      // is then sample kq, so all 64 lanes hold one (sample, output) each for the epilogue
+      // A rows 4 s .. 4 s + 3 = sample s: C row 4 kq (register 0) of every lane group is then
+      // sample kq, so all 64 lanes hold one (sample, output) each for the epilogue (rows
+      // 4 s + 1 .. 3 repeat it into registers 1-3, unused: C row r depends on A row r only).
+      // (Issuing all 20 operand reads up front, as lenet_fused.hip does, spills here: 128 VGPRs)
       const unsigned short* wrow = F1s + min(wave * 16 + l16, R_F1) * LD_F1 + kb;
       const unsigned short* prow = P2 + (l16 >> 2) * 320 + kb;
-      const bool live = (l16 & 3) == 0;
       f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
       for (int ks = 0; ks < 10; ++ks) {
         const frag pa = *reinterpret_cast<const frag*>(prow + ks * 32);
         const frag fb = *reinterpret_cast<const frag*>(wrow + ks * 32);
-        if (ks & 1) c1 = Mfma<T>::mma(live ? pa : zfrag, fb, c1);
-        else c0 = Mfma<T>::mma(live ? pa : zfrag, fb, c0);
+        if (ks & 1) c1 = Mfma<T>::mma(pa, fb, c1);
+        else c0 = Mfma<T>::mma(pa, fb, c0);
       }
       const float cz = c0[0] + c1[0];
       const int o = wave * 16 + l16;
@@ -565,11 +565,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
     // Dropout2d backward -> dL/dconv2 as [oc][px] (wgrad A) and HWC interior (dgrad A)
     TSTAMP(7);
     {
-      // A rows 4 s = dZ1 of sample s: C row 4 kq (register 0) is sample kq (see stage 3)
-      const bool live = (l16 & 3) == 0;
-      const frag dz0 = *reinterpret_cast<const frag*>(DZ1B + (l16 >> 2) * 64 + kb);
-      const frag dz1 = *reinterpret_cast<const frag*>(DZ1B + (l16 >> 2) * 64 + 32 + kb);
-      const frag fa0 = live ? dz0 : zfrag, fa1 = live ? dz1 : zfrag;
+      // A rows 4 s .. 4 s + 3 = dZ1 of sample s: C row 4 kq (register 0) is sample kq (see stage 3)
+      const frag fa0 = *reinterpret_cast<const frag*>(DZ1B + (l16 >> 2) * 64 + kb);
+      const frag fa1 = *reinterpret_cast<const frag*>(DZ1B + (l16 >> 2) * 64 + 32 + kb);
       const unsigned short* fc0 = F1s + min(kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc1 = F1s + min(kb + 4 + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
       const unsigned short* fc2 = F1s + min(32 + kb + (l16 >> 2), R_F1) * LD_F1 + 4 * (l16 & 3);
