@@ -70,7 +70,25 @@ def parse(argv=None) -> argparse.Namespace:
                          "time; use with --global-batch 64/N")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: plumbing only (launch/rendezvous/JSON contract), stock PyTorch ops")
+    ap.add_argument("--inject-exchange-fault", action="store_true",
+                    help="fault-injection test hook: the last rank's exchange pushes go to a dead-end buffer "
+                         "(in loopback mode: every virtual peer is dead), so peer waits time out; the bench "
+                         "must detect it and re-measure on the process-group all-reduce (config.comm_retry)")
     return ap.parse_args(argv)
+
+
+def reduce_max(ctx, values: dict) -> dict:
+    """{name: seconds} -> the max over ranks of each entry (one collective)."""
+    import torch
+    import torch.distributed as dist
+
+    if not ctx.is_distributed or not values:
+        return dict(values)
+    keys = sorted(values)
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(values[k]) for k in keys], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return dict(zip(keys, t.tolist()))
 
 
 def spawn(args: argparse.Namespace, argv: list[str]) -> int:
@@ -154,14 +172,19 @@ def main(argv=None) -> int:
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn(args, argv)
     t_start = float(os.environ.get("CSED_BENCH_T0", T_START))
+    # bring-up phases (s) on this rank; the JSON reports the max over ranks of each
+    # (the reference's time_elapsed runs from process start, ref src/train_dist.py:119)
+    phases = {"spawn": T_START - t_start}
     native_job = start_native_data() if args.device == "cuda" and not os.environ.get("CSED_TORCH_DATA") else None
 
+    t_mark = time.time()
     import torch
     import torch.distributed as dist
 
     from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import (
         all_reduce_max, barrier, init_distributed)
     from csed_514_project_distributed_training_using_pytorch_amd.utils import prof
+    phases["import"] = time.time() - t_mark
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
@@ -178,7 +201,9 @@ def main(argv=None) -> int:
         data_job = pool.submit(lambda: (synthetic_mnist(60000, seed=0, train=True),
                                         synthetic_mnist(10000, seed=0, train=False)))
         pool.shutdown(wait=False)
+    t_mark = time.time()
     ctx = init_distributed(world_size=world, device=args.device, backend=backend)
+    phases["process_group"] = time.time() - t_mark
     n = ctx.world_size
     if ctx.is_distributed and dist.get_world_size() != args.gpus:
         raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
@@ -189,12 +214,14 @@ def main(argv=None) -> int:
         cfg_engine, allreduce, step_kind, hip_graph = r["engine"], r["allreduce"], "eager", False
         time_elapsed, epoch0_s, epoch_s, val, loss_avg, comm_err, comm_retry = r["time_elapsed_s"], None, None, \
             None, None, 0, None
+        data_src = None
     else:
         from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
         from csed_514_project_distributed_training_using_pytorch_amd.models import Net
         from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
 
         dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+        t_mark = time.time()
         with prof.range("bench:data"):
             if native_job is not None:
                 from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNISTData
@@ -206,6 +233,7 @@ def main(argv=None) -> int:
             else:
                 train, test = data_job.result()
                 data_src = "data/mnist.py:synthetic_mnist (torch CPU ops)"
+        phases["data_wait"] = time.time() - t_mark
         use_graph = not args.no_graph
 
         def sync_barrier():
@@ -214,11 +242,16 @@ def main(argv=None) -> int:
                 barrier(ctx)
                 torch.cuda.synchronize(ctx.device)
 
-        def run_once():
+        def run_once(loopback_world: int, inject: bool, ph: dict):
+            t_mark = time.time()
             torch.manual_seed(1)
             net = Net().to(ctx.device)
             eng = FusedLeNetTrainer(net, train, lr=0.02, momentum=0.5, global_batch=args.global_batch, ctx=ctx,
-                                    compute_dtype=dt, grid=args.grid or None, loopback_world=args.loopback_world)
+                                    compute_dtype=dt, grid=args.grid or None, loopback_world=loopback_world)
+            ph["engine"] = time.time() - t_mark
+            ph.update({f"engine.{k}": v for k, v in eng.bringup_s.items()})
+            if inject and eng.exch is not None and (loopback_world or ctx.rank == ctx.world_size - 1):
+                eng.inject_exchange_fault()
             sampler = ShardSampler(len(train), ctx.world_size, ctx.rank, shuffle=True, seed=42)
             state = {"epoch": 0, "pos": 0}
             spg = args.steps_per_graph
@@ -245,17 +278,22 @@ def main(argv=None) -> int:
 
             new_epoch()
             full = eng.full_steps()
+            t_mark = time.time()
             if use_graph:  # every graph this run replays: epoch, tail, timed K (from an epoch start)
                 with prof.range("bench:capture"):
                     eng.prepare(spg, ks=(full, *epoch_chunks(args.steps, 0, full)))
+            ph["capture"] = time.time() - t_mark
+            t_mark = time.time()
             eng._device_data(test)  # test set upload is data loading (ref: DataLoader), not epoch work
+            ph["test_upload"] = time.time() - t_mark
             # 2. epoch 0, cold: the reference's time_elapsed (process start -> epoch-0 validation)
             sync_barrier()
             te = time.perf_counter()
             with prof.range("bench:epoch0"):
                 full_epoch()
             sync_barrier()
-            epoch0 = all_reduce_max(ctx, time.perf_counter() - te)
+            ph["epoch0"] = time.perf_counter() - te
+            epoch0 = all_reduce_max(ctx, ph["epoch0"])
             t_el = all_reduce_max(ctx, time.time() - t_start)
             # 3. warm-up, then a rehearsal of the timed sequence (same graphs, same order)
             with prof.range("bench:warmup"):
@@ -306,12 +344,13 @@ def main(argv=None) -> int:
 
         from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc
 
-        r = run_once()
+        r = run_once(args.loopback_world, args.inject_exchange_fault, phases)
         comm_retry = None
         if r["err"] and os.environ.get("CSED_ALLREDUCE", "auto").lower() != "rccl":
             # a peer wait of the IPC exchange timed out somewhere: release the IPC buffers on
             # every rank (collective) and measure again on the process group's all-reduce
-            # (RCCL on GPUs), so the reported number is a valid training run
+            # (RCCL on GPUs; loopback mode: the plain one-GPU step), so the reported number is
+            # a valid training run
             comm_retry = r["eng"].allreduce_kind
             r["eng"].close()
             del r
@@ -320,7 +359,9 @@ def main(argv=None) -> int:
             sync_barrier()
             _ipc.LAST_TIMING = None
             os.environ["CSED_ALLREDUCE"] = "rccl"
-            r = run_once()
+            retry_phases = {}
+            r = run_once(0, False, retry_phases)
+            phases.update({f"retry.{k}": v for k, v in retry_phases.items()})
         eng = r["eng"]
         elapsed, time_elapsed, epoch0_s, epoch_s, val = r["elapsed"], r["t_el"], r["epoch0"], r["epoch_s"], r["val"]
         comm_err = r["err"]
@@ -345,6 +386,7 @@ def main(argv=None) -> int:
         if _ipc.LAST_NOTE:
             extra["allreduce_note"] = _ipc.LAST_NOTE
 
+    bringup = {k: round(v, 4) for k, v in reduce_max(ctx, phases).items()}
     value = args.steps * args.global_batch / elapsed
     base = BASELINE_EPOCH_S.get(n)
     base_ips = 60000.0 / base if base else None
@@ -381,6 +423,12 @@ def main(argv=None) -> int:
                                  "validation); the like-for-like ratios are vs_baseline_time_elapsed (the same "
                                  "cold whole-job span here) and vs_baseline_epoch (a warm epoch + validation)"),
             "train_loss_timed_rank0": round(loss_avg, 4) if loss_avg is not None else None,
+            # where time_elapsed_s goes, max over ranks of each phase (s): spawn (launcher ->
+            # this process), import (torch + package), process_group (rendezvous, RCCL
+            # communicator), data_wait (the generator overlapped with import; what is left),
+            # engine (incl. engine.ipc_open / engine.self_test of the fused exchange), capture
+            # (HIP graphs), test_upload, epoch0 (938 steps + validation)
+            "bringup_s": bringup,
         }
         if comm_retry:
             rec["config"]["comm_retry"] = f"{comm_retry} path timed out; re-measured on the process-group all-reduce"

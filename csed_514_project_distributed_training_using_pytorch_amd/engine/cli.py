@@ -235,6 +235,10 @@ def dist_main(argv=None) -> int:
                     help="every E epochs, compare a bitwise hash of the parameters across ranks "
                          "(all-reduce MIN/MAX) and abort on divergence (0 = off)")
     ap.add_argument("--progress", action="store_true", help="tqdm bars (syncs every step, like the reference)")
+    ap.add_argument("--inject-exchange-fault", type=int, default=None, metavar="EPOCH",
+                    help="fault-injection test hook: in epoch EPOCH the last rank's exchange pushes go to a "
+                         "dead-end buffer (its peers' waits time out); the epoch must be re-run on the "
+                         "process-group all-reduce")
     ap.add_argument("--reference-metrics", action="store_true",
                     help="reproduce the reference's metric quirks (loss/bs sums, mean-of-batch-means val)")
     _common_flags(ap)
@@ -285,8 +289,10 @@ def dist_main(argv=None) -> int:
             # the IPC exchange paths raise a device error word when a peer wait times out (the
             # kernel then finishes with an incomplete sum instead of hanging): snapshot the
             # training state so the epoch can be re-run on the process group's all-reduce
-            ipc_live = ctx.is_distributed and (eng.exch is not None or eng.allreduce is not None)
+            ipc_live = ctx.is_distributed and eng.exch is not None
             snap = [t.clone() for t in eng._state()] if ipc_live else None
+            if ipc_live and args.inject_exchange_fault == i and ctx.rank == ctx.world_size - 1:
+                eng.inject_exchange_fault()
             n_hist = (len(hist.train_losses), len(hist.train_counter))
             eng.set_epoch_order(order)
             epoch_order = order

@@ -12,10 +12,13 @@ The data-parallel gradient all-reduce (ref src/train_dist.py:83, DDP's one
 87,360-byte bucket) is fused into lenet_update: each update lane pushes its
 rank-local gradient value straight into every peer's IPC-mapped receive buffer
 and sums what the peers pushed (csrc/comm buffers, LL-tagged words).  It is
-enabled after a collective bring-up and an exact self-test, and (in ``auto``
-mode, RCCL process group) only if it times faster than the fallback step:
+enabled after a collective bring-up and an exact self-test; if either fails, or
+``CSED_ALLREDUCE=rccl`` asks for it, the step runs as the fallback
 
-    lenet_update (reduce only) -> all-reduce (one-shot IPC kernel or RCCL) -> SGD kernel
+    lenet_update (reduce only) -> RCCL all-reduce -> SGD kernel
+
+(``CSED_TIME_PATHS=1`` additionally times both in ``auto`` mode and keeps the
+faster; off by default, since it costs three graph captures at bring-up.)
 
 All per-step state (batch cursor into this rank's epoch permutation, Philox
 offset, optimizer step) lives on the device, so a sequence of steps is
@@ -38,8 +41,7 @@ from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
 from ..parallel.comm import DistContext
-from ..parallel.ipc import (allreduce_mode, make_allreduce, open_exchange, open_loopback_exchange,
-                            wait_timeout_s)
+from ..parallel.ipc import allreduce_mode, open_exchange, open_loopback_exchange, wait_timeout_s
 from ..utils.flat import FlatParams
 
 N_VEC = 464  # per-sample fc vector length (kernels/lenet_layout.h VEC)
@@ -201,16 +203,14 @@ class FusedLeNetTrainer:
         self._order_host: torch.Tensor | None = None
         self.capture_comm_ok: bool | None = None
         # gradient all-reduce.  Preferred: the exchange fused into lenet_update (see the module
-        # docstring).  Fallback step (3 kernels: reduce-only update -> all-reduce -> SGD): RCCL;
-        # the one-shot IPC all-reduce kernel (csrc/comm) when CSED_ALLREDUCE=ipc asks for it
-        # (`auto` keeps one IPC path, the fused one: one self-test and timing less at bring-up).
+        # docstring).  Fallback step (3 kernels: reduce-only update -> RCCL all-reduce -> SGD).
         self.exch = None
         self.exchange_note: str | None = None  # why the data-parallel step runs as it does (reports)
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
+        self.bringup_s: dict[str, float] = {}  # exchange bring-up phases (s), for the bench JSON
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"
-        self.allreduce = make_allreduce(self.ctx, N_PARAMS) if multi and mode == "ipc" else None
         if multi and mode in ("auto", "fused"):
             self._enable_exchange(required=(mode == "fused"))
         # Loopback exchange (one GPU, no process group): lenet_update runs its full push + poll
@@ -276,20 +276,29 @@ class FusedLeNetTrainer:
             return "none"
         if self.exch is not None:
             return "fused-ipc"
-        return "ipc-oneshot" if self.allreduce is not None else "rccl"
+        return "rccl"
 
     # ------------------------------------------------- fused gradient exchange
     def _enable_exchange(self, required: bool) -> None:
-        """Bring up lenet_update's in-kernel exchange (collective on every rank):
-        open the IPC buffers, self-test them with the update kernel itself, and in
-        auto mode on RCCL keep it only if a captured step is faster than the fallback's."""
+        """Bring up lenet_update's in-kernel exchange (collective on every rank): open the IPC
+        buffers and self-test them with the update kernel itself.  With ``CSED_TIME_PATHS=1``
+        (auto mode, RCCL) the fused, fallback and exchange-free steps are also timed and the
+        faster of the first two is kept; by default a passing self-test keeps the fused path
+        (three graph captures and timings less inside the job's bring-up, i.e. inside the
+        reference's time_elapsed)."""
+        import time
+
+        t0 = time.perf_counter()
         ex, why = open_exchange(self.ctx, exch_words())
+        t1 = time.perf_counter()
+        self.bringup_s["ipc_open"] = t1 - t0
         ok = ex is not None
         if ok:
             self.exch = ex
             ok = self._vote(self._exchange_self_test())
             if not ok:
                 why = "self-test mismatch or timeout on some rank"
+        self.bringup_s["self_test"] = time.perf_counter() - t1
         if not ok:
             if ex is not None:
                 try:
@@ -302,7 +311,8 @@ class FusedLeNetTrainer:
                 raise RuntimeError(f"CSED_ALLREDUCE=fused but the fused exchange is unusable ({why})")
             return
         self.exchange_note = "fused exchange on (self-test passed)"
-        if not required and self.ctx.backend == "nccl":
+        if not required and self.ctx.backend == "nccl" and os.environ.get("CSED_TIME_PATHS", "0") == "1":
+            t2 = time.perf_counter()
             t_fused = self._time_steps()
             saved, self.exch = self.exch, None
             t_fallback = self._time_steps()
@@ -323,7 +333,8 @@ class FusedLeNetTrainer:
                                    "local_step_us": fin(t_local),
                                    "exchange_us": fin(t_fused - t_local) if max(t_fused, t_local) != float("inf")
                                    else None,
-                                   "fallback": "ipc-oneshot" if self.allreduce is not None else "rccl"}
+                                   "fallback": "rccl"}
+            self.bringup_s["path_timing"] = time.perf_counter() - t2
 
     def _vote(self, ok: bool) -> bool:
         dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
@@ -403,21 +414,31 @@ class FusedLeNetTrainer:
             torch.cuda.synchronize(self.device)
             self.exch.close()
             self.exch = None
-        if (self.exch is not None or self.allreduce is not None) and dist.is_initialized():
+        if self.exch is not None and dist.is_initialized():
             torch.cuda.synchronize(self.device)
             if self.ctx.backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
-        for comm in (self.exch, self.allreduce):
-            if comm is not None:
-                comm.close()
-        self.exch = self.allreduce = None
+        if self.exch is not None:
+            self.exch.close()
+        self.exch = None
 
     def comm_errors(self) -> int:
-        """Nonzero if an IPC exchange ever timed out waiting for a peer (synchronous)."""
-        e = self.exch.error() if self.exch is not None else 0
-        return e | (self.allreduce.error() if self.allreduce is not None else 0)
+        """Nonzero if the IPC exchange ever timed out waiting for a peer (synchronous)."""
+        return self.exch.error() if self.exch is not None else 0
+
+    def inject_exchange_fault(self, on: bool = True) -> None:
+        """Fault injection (tests, ``--inject-exchange-fault``): this rank's exchange pushes go
+        to a private dead-end buffer (csrc/comm ipc_set_mute), so to its peers -- or, in
+        loopback mode, to itself -- it is a dead rank whose words never arrive: their waits run
+        into CSED_IPC_TIMEOUT_S and raise the error word.  Captured graphs and the native
+        executor hold the old mapping, so both are dropped."""
+        if self.exch is None:
+            raise RuntimeError("no IPC exchange to inject a fault into")
+        self.exch.mute(on)
+        self._graphs.clear()
+        self._stepper = None
 
     def _max_grid(self) -> int:
         return max(self.grid, 1)
@@ -496,10 +517,7 @@ class FusedLeNetTrainer:
         elif self.comm:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, self.flat.grad, *common, None, None, False,
                              self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post)
-            if self.allreduce is not None:
-                self.allreduce(self.flat.grad)
-            else:
-                dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
+            dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
             ops.lenet_update(self.slab, grid, self.vslab, B, self.flat.grad, None, *common, cursor, self.rng_offset,
                              True, None, 0, None, self.mfma)
         else:

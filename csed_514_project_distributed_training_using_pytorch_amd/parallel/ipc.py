@@ -12,10 +12,13 @@ error word, and bitwise agreement with the process group's own all-reduce.  The
 ranks then agree (MIN over the process group) and the path is enabled only if
 every rank passed; otherwise callers keep using RCCL.  In ``auto`` mode the two
 are then timed on the real buffer and the faster one is kept (the slowest
-rank's numbers decide, so all ranks agree).  ``CSED_ALLREDUCE`` = ``auto``
-(default) | ``ipc`` (use it; fail if unusable) | ``rccl`` (never try) | ``fused``
-(the fused engine's in-kernel exchange, engine/fused.py; this kernel is then only
-its fallback).
+rank's numbers decide, so all ranks agree).  It is a standalone collective
+(:func:`make_allreduce`, ``tools/allreduce_bench.py``, the loopback tests); the
+fused engine does not train on it.
+
+``CSED_ALLREDUCE`` selects the fused engine's gradient path: ``auto`` (default:
+the in-kernel exchange if its self-test passes, else RCCL) | ``fused`` (the
+in-kernel exchange or fail) | ``rccl`` (never try IPC).
 
 The same IPC buffers also back the fused engine's in-kernel exchange
 (:func:`open_exchange`): lenet_update pushes its reduced gradient to every peer
@@ -113,6 +116,13 @@ class IpcAllReduce:
     def error(self, reset: bool = False) -> int:
         return int(torch.ops.csed.ipc_error(self.id, reset))
 
+    def mute(self, on: bool = True) -> None:
+        """Fault injection: while on, this rank's pushes go to a dead-end buffer (csrc/comm
+        ipc_set_mute), so its peers' waits time out as if it had died.  Launches resolved
+        after the call see it (re-capture graphs)."""
+        with torch.cuda.device(self.ctx.device):
+            torch.ops.csed.ipc_set_mute(self.id, bool(on))
+
     def close(self) -> None:
         """Unmap the peers and free this rank's buffers (call after a process-group barrier,
         so that no peer is still pushing into them).  Idempotent."""
@@ -191,10 +201,14 @@ def wait_timeout_s() -> float:
 
 
 def allreduce_mode() -> str:
-    """``CSED_ALLREDUCE``: auto (default) | fused | ipc | rccl (see engine/fused.py)."""
+    """``CSED_ALLREDUCE``: auto (default) | fused | rccl (see engine/fused.py)."""
     mode = os.environ.get("CSED_ALLREDUCE", "auto").lower()
-    if mode not in ("auto", "fused", "ipc", "rccl"):
-        raise ValueError(f"CSED_ALLREDUCE={mode!r}: expected auto, fused, ipc or rccl")
+    if mode == "ipc":
+        raise ValueError("CSED_ALLREDUCE=ipc was removed as a training path: the one-shot IPC kernel "
+                         "depends on co-scheduling when ranks share a GPU and could not be tested "
+                         "strictly; use auto / fused (the in-kernel exchange) or rccl")
+    if mode not in ("auto", "fused", "rccl"):
+        raise ValueError(f"CSED_ALLREDUCE={mode!r}: expected auto, fused or rccl")
     return mode
 
 
@@ -241,21 +255,24 @@ def open_loopback_exchange(device: torch.device, words: int, world: int, blocks:
     return ar
 
 
-def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
-    """The IPC all-reduce if every rank can use it (see module docstring), else None.
+def make_allreduce(ctx: DistContext, n: int, mode: str = "auto") -> IpcAllReduce | None:
+    """The standalone one-shot IPC all-reduce if every rank can use it (see module docstring),
+    else None.  ``mode``: ``auto`` (keep it only where it times faster than the process group)
+    | ``ipc`` (use it; raise if unusable) | ``rccl`` (None).
 
     Every rank runs the same sequence of collectives whatever fails locally:
     create -> vote -> all-gather handles -> open -> vote -> self-test -> vote.
     """
     global LAST_NOTE
-    mode = allreduce_mode()
+    if mode not in ("auto", "ipc", "rccl"):
+        raise ValueError(f"make_allreduce mode {mode!r}: expected auto, ipc or rccl")
     if mode == "rccl" or not ctx.is_distributed or ctx.device.type != "cuda":
         return None
     shared = ranks_per_gpu(ctx)
     if shared > MAX_RANKS_PER_GPU:
         LAST_NOTE = f"ipc all-reduce off: {shared} ranks share one GPU (needs <= {MAX_RANKS_PER_GPU})"
         if mode == "ipc":
-            raise RuntimeError(f"CSED_ALLREDUCE=ipc but {LAST_NOTE}")
+            raise RuntimeError(f"ipc all-reduce required but {LAST_NOTE}")
         return None
     if shared > 1 and mode != "ipc":
         # Ranks sharing a GPU (a rehearsal setup, never a real node): the auto mode keeps the
@@ -263,7 +280,7 @@ def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
         # GPU interleaves the processes' queues: tools/dp_step_bench.py --gloo still records one
         # 2 s timed-out wait per run on one shared MI355X (profiles/dp_exchange_r3.md), which the
         # fused exchange (one waiting point per step, inside lenet_update) does not show.
-        LAST_NOTE = f"ipc all-reduce off: {shared} ranks share one GPU (auto mode; CSED_ALLREDUCE=ipc forces it)"
+        LAST_NOTE = f"ipc all-reduce off: {shared} ranks share one GPU (auto mode; mode='ipc' forces it)"
         return None
     ar, why = _open(ctx, n, blocks=32)
     ok = ar is not None
@@ -272,7 +289,7 @@ def make_allreduce(ctx: DistContext, n: int) -> IpcAllReduce | None:
         why = why or ("" if ok else "self-test mismatch or timeout on some rank")
     if not ok:
         if mode == "ipc":
-            raise RuntimeError(f"CSED_ALLREDUCE=ipc but the IPC all-reduce is unusable ({why or 'a peer failed'})")
+            raise RuntimeError(f"ipc all-reduce required but it is unusable ({why or 'a peer failed'})")
         LAST_NOTE = f"ipc all-reduce off: {why or 'a peer failed'}"
         return None
     if mode == "auto" and ctx.backend == "nccl":

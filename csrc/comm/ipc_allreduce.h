@@ -24,7 +24,12 @@ hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double 
 // Unmap the peers, free the buffers and retire the id (after a process-group barrier:
 // no peer may still be pushing into this rank's buffer).
 hipError_t ipc_destroy(int id);
-// Error word: nonzero if a wait ever timed out (synchronous read).
+// Fault injection: while muted this rank's pushes go to a private dead-end buffer, so its
+// peers see a dead rank (their waits time out).  Takes effect for launches resolved after the
+// call (kernel arguments captured in a graph keep the mapping they were captured with).
+hipError_t ipc_set_mute(int id, bool mute);
+// Error word: nonzero if a wait ever timed out (synchronous read).  Once set, the exchange
+// kernels stop waiting (one poll per call) until it is reset.
 hipError_t ipc_error(int id, int* err_out, bool reset);
 
 // Device view of an opened exchange buffer, for kernels that carry their own

@@ -58,6 +58,10 @@ __global__ void __launch_bounds__(kThreads) ipc_allreduce_kernel(const float* __
                                                                  int64_t* __restrict__ counters, int* err,
                                                                  uint64_t timeout_ticks) {
   const int tid = threadIdx.x, blk = blockIdx.x;
+  // once any wait of this buffer has timed out the replicas are already inconsistent (the
+  // caller re-runs on the process group): later calls poll once and never wait again, so a
+  // dead peer costs one timeout, not one per call
+  const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   __shared__ int64_t t_sh;
   if (tid == 0) t_sh = counters[blk] + 1;
   __syncthreads();
@@ -82,7 +86,7 @@ __global__ void __launch_bounds__(kThreads) ipc_allreduce_kernel(const float* __
   // an element pair are loaded together (unconditionally, from clamped rows) and
   // re-polled together, so a pair costs one memory round trip, not one per peer.
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  bool timed_out = false;
+  bool timed_out = failed;
   // relaxed system-scope atomic loads: never cached or hoisted, but not ordered
   // against each other either, so all 16 of a pair issue before the first wait
   uint64_t* mine = peers.base[rank] + slot;
@@ -134,6 +138,11 @@ struct IpcComm {
   PeerBufs peers{};
   int world = 0, rank = -1;
   bool loopback = false;  // peers are slots of this rank's own buffer (ipc_open_loopback)
+  // fault injection (ipc_set_mute): while muted, ipc_peers hands out a private dead-end buffer
+  // in place of every peer's receive buffer, so this rank's pushes never arrive -- to its
+  // peers it is a dead rank (their waits time out and raise the error word)
+  bool muted = false;
+  uint64_t* sink = nullptr;
 };
 
 std::vector<IpcComm*>& registry() {
@@ -227,15 +236,34 @@ hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double 
   IpcComm* c = get(id);
   if (!c || c->world < 1 || n > c->cap || n % 4) return hipErrorInvalidValue;
   const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  PeerBufs p = c->peers;
+  if (c->muted)  // (ipc_set_mute: pushes go to the dead-end buffer)
+    for (int r = 0; r < c->world; ++r)
+      if (r != c->rank) p.base[r] = c->sink + (int64_t)r * c->cap;
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(c->blocks), dim3(kThreads), 0, s, in, out, n / 2, c->cap,
-                     c->world, c->rank, c->peers, c->counters, c->err, ticks);
+                     c->world, c->rank, p, c->counters, c->err, ticks);
   return hipGetLastError();
+}
+
+hipError_t ipc_set_mute(int id, bool mute) {
+  IpcComm* c = get(id);
+  if (!c || c->world < 1) return hipErrorInvalidValue;
+  if (mute && !c->sink) {
+    const size_t bytes = 2 * (size_t)kMaxRanks * (size_t)c->cap * sizeof(uint64_t);
+    hipError_t e = hipMalloc(&c->sink, bytes);
+    if (e == hipSuccess) e = hipMemset(c->sink, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+  }
+  c->muted = mute;
+  return hipSuccess;
 }
 
 hipError_t ipc_peers(int id, IpcPeers* out) {
   IpcComm* c = get(id);
   if (!c || c->world < 1) return hipErrorInvalidValue;
-  for (int r = 0; r < kMaxRanks; ++r) out->base[r] = c->peers.base[r];
+  for (int r = 0; r < kMaxRanks; ++r)
+    out->base[r] = (c->muted && r != c->rank && r < c->world) ? c->sink + (int64_t)r * c->cap : c->peers.base[r];
   out->counters = c->counters;
   out->err = c->err;
   out->cap = c->cap;
@@ -255,7 +283,7 @@ hipError_t ipc_destroy(int id) {
       const hipError_t e2 = hipIpcCloseMemHandle(c->peers.base[r]);
       if (e == hipSuccess) e = e2;
     }
-  for (void* p : {(void*)c->buf, (void*)c->counters, (void*)c->err})
+  for (void* p : {(void*)c->buf, (void*)c->counters, (void*)c->err, (void*)c->sink})
     if (p) {
       const hipError_t e2 = hipFree(p);
       if (e == hipSuccess) e = e2;

@@ -62,6 +62,8 @@ int64_t ipc_error(int64_t id, bool reset) {
   return e;
 }
 
+void ipc_set_mute(int64_t id, bool mute) { COMM_CHECK(csed::comm::ipc_set_mute((int)id, mute)); }
+
 void ipc_destroy(int64_t id) { COMM_CHECK(csed::comm::ipc_destroy((int)id)); }
 
 }  // namespace
@@ -74,4 +76,5 @@ TORCH_LIBRARY_FRAGMENT(csed, m) {
   m.def("ipc_allreduce(int id, Tensor input, Tensor(a!) out, float timeout_s=2.0) -> ()", &ipc_allreduce);
   m.def("ipc_error(int id, bool reset=False) -> int", &ipc_error);
   m.def("ipc_destroy(int id) -> ()", &ipc_destroy);
+  m.def("ipc_set_mute(int id, bool mute) -> ()", &ipc_set_mute);
 }

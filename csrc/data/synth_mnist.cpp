@@ -63,7 +63,8 @@ void make_sample(const float* protos, int classes, const Stream& st, const Up& u
   const float* pb = protos + ((int64_t)other * kStyles + ostyle) * kPix;
   const float dw = r[3] * 0.6f;
   // the blended source with a 2-pixel zero border: bilinear taps need no bounds checks (sample
-  // coordinates are clamped to [-2, 29], where every tap outside the image reads zero anyway)
+  // coordinates are clamped to [-2, 28]: both taps of a clamped coordinate lie in the zero
+  // border, so the clamp changes no output, and the right / lower tap of 28 is border index 31)
   constexpr int kP = kSide + 4;
   float src[kP * kP];
   std::fill(src, src + kP * kP, 0.0f);
@@ -108,8 +109,8 @@ void make_sample(const float* protos, int classes, const Stream& st, const Up& u
       const float gx = t00 * cx + t01 * cy + tx + ex;
       const float gy = t10 * cx + t11 * cy + ty + ey;
       // grid_sample, bilinear, zero padding, align_corners=False
-      const float ix = std::min(std::max(((gx + 1.0f) * kSide - 1.0f) * 0.5f, -2.0f), 29.0f);
-      const float iy = std::min(std::max(((gy + 1.0f) * kSide - 1.0f) * 0.5f, -2.0f), 29.0f);
+      const float ix = std::min(std::max(((gx + 1.0f) * kSide - 1.0f) * 0.5f, -2.0f), 28.0f);
+      const float iy = std::min(std::max(((gy + 1.0f) * kSide - 1.0f) * 0.5f, -2.0f), 28.0f);
       const float fx = std::floor(ix), fy = std::floor(iy);
       const int x0 = (int)fx + 2, y0 = (int)fy + 2;  // in the bordered image
       const float wx1 = ix - fx, wy1 = iy - fy, wx0 = 1.0f - wx1, wy0 = 1.0f - wy1;

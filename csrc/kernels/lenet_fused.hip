@@ -1509,7 +1509,10 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
   // exchange tag of this call (uniform load; written back after the block's last poll)
   const uint32_t xt = EXCH ? (uint32_t)(px.counters[blk] + 1) : 0u;
-  bool timed_out = false;
+  // a wait of this exchange has timed out before (the error word is set): the replicas are
+  // already inconsistent and the caller re-runs the epoch on the process group, so this call
+  // polls once and never waits -- a dead peer costs one timeout, not one per step
+  bool timed_out = EXCH && __hip_atomic_load(px.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 #define USTAMP(k) \
   if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);

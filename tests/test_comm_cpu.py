@@ -11,8 +11,7 @@ from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc
 from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import DistContext
 
 
-@pytest.mark.parametrize("value,mode", [(None, "auto"), ("auto", "auto"), ("FUSED", "fused"), ("ipc", "ipc"),
-                                        ("rccl", "rccl")])
+@pytest.mark.parametrize("value,mode", [(None, "auto"), ("auto", "auto"), ("FUSED", "fused"), ("rccl", "rccl")])
 def test_allreduce_mode(monkeypatch, value, mode):
     if value is None:
         monkeypatch.delenv("CSED_ALLREDUCE", raising=False)
@@ -21,10 +20,19 @@ def test_allreduce_mode(monkeypatch, value, mode):
     assert ipc.allreduce_mode() == mode
 
 
-def test_allreduce_mode_rejects_unknown(monkeypatch):
-    monkeypatch.setenv("CSED_ALLREDUCE", "nvlink")
+@pytest.mark.parametrize("value", ["nvlink", "ipc"])
+def test_allreduce_mode_rejects_unknown(monkeypatch, value):
+    # "ipc" (the one-shot kernel as a training path) was removed in round 4: only gradient paths
+    # with a strict test remain selectable
+    monkeypatch.setenv("CSED_ALLREDUCE", value)
     with pytest.raises(ValueError):
         ipc.allreduce_mode()
+
+
+def test_make_allreduce_mode_checked():
+    single = DistContext(0, 1, 0, torch.device("cpu"), None)
+    with pytest.raises(ValueError):
+        ipc.make_allreduce(single, 21840, mode="fused")
 
 
 def test_no_ipc_without_distributed_gpu(monkeypatch):

@@ -43,7 +43,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         ctx = DistContext(rank, world, local, dev, "nccl")
     data = synthetic_mnist(60000, seed=0)
-    modes = ["fused", "ipc"] + ([] if args.gloo else ["rccl"])
+    modes = ["fused"] + ([] if args.gloo else ["rccl"])
     out = {}
     for mode in modes:
         os.environ["CSED_ALLREDUCE"] = mode

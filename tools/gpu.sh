@@ -1,0 +1,105 @@
+# One parameterised GPU-box script for every record in profiles/ (replaces the round-1..3
+# one-off wrappers).  Each task writes gpurun_out/<tag>_*; steps are chained with && and
+# each GPU step has its own time limit.
+#
+#   gpurun --timeout 1100 -- bash tools/gpu.sh <task>[,<task>...] [tag]
+#
+# tasks
+#   suite     the whole GPU test suite + smoke()                            (GPUTEST-style record)
+#   bench     the driver's command, default / fp32 / per-rank-8 / large-batch benches (JSON lines)
+#   rehearse  2-rank gloo rehearsal of the multi-rank bench flow on the one GPU
+#   trace     rocprofv3 kernel traces: default (B=64), per-rank 8, B=1024 / 8192 fp16, fp32 64 / 8
+#   stages    in-kernel stage stamps (train B=64 / 8, tile B=1024, fp32 B=64) + update stamps
+#   exchange  loopback exchange table (tools/exchange_loopback.py) + step breakdown
+#             (tools/exchange_trace.py) + the exchange / fault-injection / comm tests
+#   pmc       three rocprofv3 --pmc passes over the train kernel (B=64), one over B=8,
+#             and three over the tile kernel (B=1024)
+#   ab        same-box A/B of ab/A_C.so vs ab/B_C.so (tools/ab_build.sh REV) at global batch
+#             64 and 8 (+ AB_ARGS), N_AB alternations (default 3)
+#   abenv     same-box A/B of one build under ENV_A vs ENV_B (BENCH_ARGS / AB_ARGS / N_AB)
+TASKS=${1:?task list}
+T=${2:-run}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out
+mkdir -p $O
+py() { timeout -k 10 "$@"; }
+
+task_suite() {
+  cd $R && py 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > $O/${T}_tests.log 2>&1
+  local rc=$?
+  grep -E "passed|failed" $O/${T}_tests.log | tail -1 > $O/${T}_tests_summary.txt
+  [ $rc -le 1 ] && py 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/${T}_smoke.log 2>&1 && [ $rc -eq 0 ]
+}
+
+task_bench() {
+  cd $R && py 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/${T}_bench_driver.json 2>$O/${T}_bench_driver.err && \
+  py 200 python bench.py > $O/${T}_bench_default.json 2>$O/${T}_bench_default.err && \
+  py 200 python bench.py --dtype fp32 > $O/${T}_bench_fp32.json 2>$O/${T}_bench_fp32.err && \
+  py 200 python bench.py --global-batch 8 --steps 3000 --warmup 300 --no-epoch > $O/${T}_bench_b8.json 2>$O/${T}_bench_b8.err && \
+  py 200 python bench.py --global-batch 8 --loopback-world 8 --steps 3000 --warmup 300 --no-epoch > $O/${T}_bench_lb8.json 2>$O/${T}_bench_lb8.err && \
+  py 200 python bench.py --global-batch 1024 --dtype fp16 --steps 300 --warmup 30 --no-epoch > $O/${T}_bench_1024.json 2>$O/${T}_bench_1024.err && \
+  py 200 python bench.py --global-batch 8192 --dtype fp16 --steps 40 --warmup 5 > $O/${T}_bench_8192.json 2>$O/${T}_bench_8192.err
+}
+
+task_rehearse() {
+  cd $R && py 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/${T}_reh_n1.json 2>$O/${T}_reh_n1.err && \
+  py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 > $O/${T}_reh_gloo2.json 2>$O/${T}_reh_gloo2.err
+}
+
+task_trace() {
+  cd /tmp && export TMPDIR=/tmp && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt64 -o run -- python3 $R/bench.py --steps 300 --warmup 30 --no-epoch > $O/${T}_kt64.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt8 -o run -- python3 $R/bench.py --global-batch 8 --steps 300 --warmup 30 --no-epoch > $O/${T}_kt8.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt1024 -o run -- python3 $R/bench.py --global-batch 1024 --dtype fp16 --steps 200 --warmup 20 --no-epoch > $O/${T}_kt1024.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt8192 -o run -- python3 $R/bench.py --global-batch 8192 --dtype fp16 --steps 40 --warmup 5 --no-epoch > $O/${T}_kt8192.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_ktf32 -o run -- python3 $R/bench.py --dtype fp32 --steps 300 --warmup 30 --no-epoch > $O/${T}_ktf32.log 2>&1
+}
+
+task_stages() {
+  cd $R && py 120 python tools/stage_profile.py 64 > $O/${T}_stage64.log 2>&1 && \
+  py 120 python tools/stage_profile.py 8 > $O/${T}_stage8.log 2>&1 && \
+  py 120 python tools/stage_profile_tile.py 1024 > $O/${T}_stage_tile1024.log 2>&1 && \
+  py 120 python tools/stage_profile_f32.py 64 > $O/${T}_stage_f32.log 2>&1 && \
+  py 120 python tools/update_profile.py 8 > $O/${T}_update8.log 2>&1 && \
+  py 120 python tools/update_profile.py 8192 > $O/${T}_update8192.log 2>&1
+}
+
+task_exchange() {
+  cd $R && py 300 python -u tools/exchange_loopback.py 8 16 32 64 > $O/${T}_loopback.log 2>&1 && \
+  py 300 python -u tools/exchange_trace.py --batch 8 16 32 64 --worlds 1 2 4 8 > $O/${T}_xtrace.log 2>&1 && \
+  py 600 python -u -m pytest tests/test_exchange_loopback_gpu.py tests/test_fault_injection_gpu.py tests/test_comm_gpu.py -v --timeout 240 --timeout-method thread > $O/${T}_xtests.log 2>&1
+}
+
+pmc3() {  # pmc3 <tag> <kernel_counters.py args>
+  local t=$1; shift
+  cd /tmp && export TMPDIR=/tmp && \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_INSTS_BRANCH --output-format csv -d $O/${t}1 -o run -- python3 $R/tools/kernel_counters.py "$@" > $O/${t}1.log 2>&1 && \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY --output-format csv -d $O/${t}2 -o run -- python3 $R/tools/kernel_counters.py "$@" > $O/${t}2.log 2>&1 && \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_IDX_ACTIVE SQ_IFETCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_VMEM --output-format csv -d $O/${t}3 -o run -- python3 $R/tools/kernel_counters.py "$@" > $O/${t}3.log 2>&1 && \
+  cd $R && python3 tools/kernel_counters.py --summarize $O/${t}1/run_counter_collection.csv $O/${t}2/run_counter_collection.csv $O/${t}3/run_counter_collection.csv > $O/${t}_summary.log 2>&1
+}
+
+task_pmc() {
+  pmc3 ${T}_pmc64 64 200 && pmc3 ${T}_pmc8 8 200 && pmc3 ${T}_pmc1024 1024 100
+}
+
+task_ab() {
+  cd $R && rm -f $O/${T}_ab.log && \
+  for i in $(seq ${N_AB:-3}); do for b in 64 8; do for v in A B; do
+    echo "$v B=$b $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py --global-batch $b --steps 3000 --warmup 300 --no-epoch $AB_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_ab.log || return 1
+  done; done; done
+}
+
+task_abenv() {
+  cd $R && rm -f $O/${T}_abenv.log && \
+  for i in $(seq ${N_AB:-3}); do for v in A B; do
+    if [ $v = A ]; then E="$ENV_A"; else E="$ENV_B"; fi
+    echo "$v $(env $E timeout -k 10 100 python bench.py ${BENCH_ARGS:---steps 3000 --warmup 300 --no-epoch} $AB_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abenv.log || return 1
+  done; done
+}
+
+for task in ${TASKS//,/ }; do
+  echo "[gpu.sh] $task $(date +%T)"
+  task_$task || { echo "[gpu.sh] $task failed rc=$?"; exit 1; }
+done
+echo "[gpu.sh] done"
