@@ -1450,32 +1450,56 @@ __device__ __forceinline__ uint64_t ll_word(float v, uint32_t t) {
   return ((uint64_t)t << 32) | (uint64_t)__float_as_uint(v);
 }
 
-// v[k] (this rank's value of exchange word idx[k], for live[k]) := sum over ranks.
-template <int K>
-__device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t t, const int (&idx)[K],
+// The exchange's peer addresses for one call, resolved at block entry (the pointer loads from
+// the argument segment issue with the block's first loads instead of as a dependent scalar
+// chain inside the exchange): dst[p] = this rank's sender slot in peer p's buffer for this
+// call's tag parity; src = sender slot 0 of this rank's own buffer (peer p's words at + p * cap).
+// R: the launch's world bound (2, 4 or 8 >= px.world; peers p >= world are never pushed to and
+// their polls are clamped to row world - 1).
+template <int R>
+struct XPtrs {
+  uint64_t* dst[R];
+  const uint64_t* src;
+};
+template <int R>
+__device__ __forceinline__ XPtrs<R> xptrs(const comm::IpcPeers& px, uint32_t t) {
+  static_assert(R >= 2 && R <= comm::kIpcMaxRanks, "world bound");
+  XPtrs<R> x;
+  // receive buffer layout (csrc/comm/ipc_allreduce.h): [2 slots][kIpcMaxRanks senders][cap]
+  const int64_t slot = (int64_t)(t & 1) * comm::kIpcMaxRanks * px.cap;
+#pragma unroll
+  for (int p = 0; p < R; ++p) x.dst[p] = px.base[min(p, px.world - 1)] + slot + (int64_t)px.rank * px.cap;
+  x.src = px.base[px.rank] + slot;
+  return x;
+}
+
+// v[k] (this rank's value of exchange word w0 + 64 k) := sum over ranks, in rank order (so every
+// rank gets identical bits).  A wave's lanes hold consecutive w0, so each push / poll
+// instruction of a wave moves one contiguous 512-byte run.  live[k]: words whose tags must match
+// (the others are pushed and summed but never waited for).
+template <int K, int R>
+__device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                              const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
                                              bool& timed_out) {
-  constexpr int R = comm::kIpcMaxRanks;
-  const int64_t slot = (int64_t)(t & 1) * R * px.cap;
+  // 1. push (write-through, system scope: see comm::push_word) to every peer
 #pragma unroll
-  for (int p = 0; p < R; ++p) {
-    if (p < px.world && p != px.rank) {
-      uint64_t* dst = px.base[p] + slot + (int64_t)px.rank * px.cap;
+  for (int p = 0; p < R; ++p)
+    if (p < px.world && p != px.rank)
 #pragma unroll
-      for (int k = 0; k < K; ++k)  // write-through (system scope): see comm::push_word
-        if (live[k]) __hip_atomic_store(dst + idx[k], ll_word(v[k], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  const uint64_t* mine = px.base[px.rank] + slot;
+      for (int k = 0; k < K; ++k)
+        __hip_atomic_store(x.dst[p] + w0 + 64 * k, ll_word(v[k], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 2. poll this rank's receive buffer for every peer's words of tag t (all loads issued before
+  //    the first wait: one memory round trip per pass)
+  const int64_t cap = px.cap;
+  const int wl = px.world - 1;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t w[R][K];
   while (true) {
-    // relaxed system-scope loads: never cached or hoisted, all issued before the first wait
 #pragma unroll
     for (int p = 0; p < R; ++p)
 #pragma unroll
       for (int k = 0; k < K; ++k)
-        w[p][k] = __hip_atomic_load(mine + (int64_t)min(p, px.world - 1) * px.cap + idx[k], __ATOMIC_RELAXED,
+        w[p][k] = __hip_atomic_load(x.src + (int64_t)min(p, wl) * cap + w0 + 64 * k, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_SYSTEM);
     bool ready = true;
 #pragma unroll
@@ -1498,8 +1522,9 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, uint32_t 
 }
 
 // Update workgroup blk of nblk (UP_NT threads).  part: float4[UP_S][UP_C], part2:
-// float[4][UP_C*4] in LDS.
-template <typename T, bool EXCH>
+// float[4][UP_C*4] in LDS.  XW: 0 = no exchange, else the fused exchange's world bound
+// (2, 4 or 8 >= px.world).
+template <typename T, int XW>
 __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
                             int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
                             int nblk, int tid, float4* part_, float* part2_, int fc_tpb) {
@@ -1508,7 +1533,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
   // exchange tag of this call (uniform load; written back after the block's last poll)
+  constexpr bool EXCH = XW > 0;
+  constexpr int XR = EXCH ? XW : 2;
   const uint32_t xt = EXCH ? (uint32_t)(px.counters[blk] + 1) : 0u;
+  XPtrs<XR> xp;
+  if constexpr (EXCH) xp = xptrs<XR>(px, xt);
   // a wait of this exchange has timed out before (the error word is set): the replicas are
   // already inconsistent and the caller re-runs the epoch on the process group, so this call
   // polls once and never waits -- a dead peer costs one timeout, not one per step
@@ -1588,9 +1617,10 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     if (ht < 64 && live_pb && pi >= 0) {
       float g[1] = {((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post};
       if (EXCH) {
-        const int idx[1] = {pi};
+        // exchange word = the slab slot (contiguous over the lanes: one 512-byte run per wave
+        // and peer; the parameter index is 250 apart between neighbouring conv2 slots)
         const bool live[1] = {true};
-        ll_allreduce<1>(px, xt, idx, live, g, timeout_ticks, timed_out);
+        ll_allreduce<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out);
       }
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
@@ -1845,14 +1875,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         g[r] = v * a.grad_post;
       }
       if (EXCH) {
-        int idx[4];
+        // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + r * 64 + lane
         bool live[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          idx[r] = CNP_PAD + tile * 256 + r * 64 + lane;
-          live[r] = pidx[r] >= 0;
-        }
-        ll_allreduce<4>(px, xt, idx, live, g, timeout_ticks, timed_out);
+        for (int r = 0; r < 4; ++r) live[r] = pidx[r] >= 0;
+        ll_allreduce<4, XR>(px, xp, xt, CNP_PAD + tile * 256 + lane, live, g, timeout_ticks, timed_out);
       }
       if (vec) {
         // MFMA layout (row 4kq + r, column l16) -> row layout through this wave's LDS slot
@@ -1906,7 +1933,7 @@ struct UpdateKargs {
   LenetUpdateArgs a; const float* vslab; int B; float* loss_parts; int nparts; float* loss_acc;
   uint64_t timeout_ticks; int fc_tpb;
 };
-template <typename T, bool EXCH>
+template <typename T, int XW>
 __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
                                                              int B, float* loss_parts, int nparts,
                                                              float* loss_acc, uint64_t timeout_ticks, int fc_tpb,
@@ -1914,7 +1941,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   prefetch_kernargs<sizeof(UpdateKargs) + sizeof(comm::IpcPeers)>();  // (+ gridDim.x after px)
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
-  update_role<T, EXCH>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
+  update_role<T, XW>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
                        threadIdx.x, &part[0][0], &part2[0][0], fc_tpb);
 }
 
@@ -2017,14 +2044,21 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
-      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, true>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                         a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
+      if (px.world <= 2)
+        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 2>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+                           a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
+      else if (px.world <= 4)
+        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 4>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+                           a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
+      else
+        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 8>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
+                           a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
     });
     return hipGetLastError();
   }
   const int nblocks = update_blocks(a.B);
   CSED_DISPATCH_UPDATE(a.mfma_dtype, {
-    hipLaunchKernelGGL((lenet_update_kernel<scalar_t, false>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
+    hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 0>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
                        a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 0, px);
   });
   return hipGetLastError();

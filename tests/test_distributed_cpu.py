@@ -160,6 +160,27 @@ def test_bench_self_spawns_ranks_cpu():
     assert rec["time_elapsed_s"] > 0
 
 
+def test_bench_eight_ranks_bringup_phases_cpu():
+    """bench.py --gpus 8 --device cpu: the driver's 8-rank launch shape on the CPU (spawn, eight
+    concurrent `import torch`, an 8-rank rendezvous).  The JSON's bringup_s carries the per-phase
+    breakdown of time_elapsed_s (max over ranks) that the driver's SCALE run records."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--device", "cpu", "--steps", "2",
+                        "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(js) == 1, r.stdout
+    import json
+
+    rec = json.loads(js[0])
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
+    ph = rec["bringup_s"]
+    assert {"spawn", "import", "process_group"} <= set(ph), ph
+    assert all(v >= 0 for v in ph.values()), ph
+    # every phase is a part of the span it is measured in
+    assert ph["spawn"] + ph["import"] + ph["process_group"] <= rec["time_elapsed_s"] + 1e-3, rec
+
+
 def test_bench_rejects_world_size_mismatch_cpu():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup",

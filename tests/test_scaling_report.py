@@ -54,3 +54,24 @@ def test_scaling_report_prediction_from_loopback_log(tmp_path):
     assert "predicted epoch s" in md
     # the built-in table covers every N of the strong-scaling curve
     assert all(n in sr.predict({}, sr.LOOPBACK_STEP_US, 1.0) for n in (1, 2, 4, 8))
+
+
+def test_scaling_report_predicts_time_elapsed():
+    """Predicted time_elapsed: launch phases at N from a CPU record, the N = 1 GPU bring-up, the
+    exchange bring-up of a 2-rank rehearsal (N > 1 only) and epoch 0 at the predicted step."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scaling_report as sr
+
+    ph1 = {"spawn": 0.0, "import": 1.4, "process_group": 0.0, "data_wait": 0.1, "engine": 0.05, "capture": 0.2,
+           "test_upload": 0.01}
+    by_n = {1: {"n_gpus": 1, "value": 1.0, "ms_per_step": 0.014, "epoch_s": 0.013, "epoch0_s": 0.05,
+                "bringup_s": ph1}}
+    steps = {(64, 1): 14.0, (8, 8): 13.0}
+    pred = sr.predict(by_n, steps, hop_us=1.0)
+    cpu = {8: {"n_gpus": 8, "bringup_s": {"spawn": 0.3, "import": 3.0, "process_group": 1.0}}}
+    reh = {"n_gpus": 2, "bringup_s": {"engine.ipc_open": 0.02, "engine.self_test": 0.03}}
+    te = sr.predict_time_elapsed(by_n, pred, cpu, reh)
+    base = 0.1 + 0.05 + 0.2 + 0.01
+    assert abs(te[1] - (1.4 + base + 0.05)) < 1e-9
+    assert abs(te[8] - (4.3 + base + 0.05 + 0.05 + 938 * 0.0e-6)) < 1e-9  # step_8 = 13 + 1 hop = step_1
+    assert sr.predict_time_elapsed({}, pred, cpu, reh) == {}

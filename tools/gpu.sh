@@ -7,7 +7,8 @@
 # tasks
 #   suite     the whole GPU test suite + smoke()                            (GPUTEST-style record)
 #   bench     the driver's command, default / fp32 / per-rank-8 / large-batch benches (JSON lines)
-#   rehearse  2-rank gloo rehearsal of the multi-rank bench flow on the one GPU
+#   rehearse  N=1 and a 2-rank gloo rehearsal of the multi-rank bench flow on the one GPU, and
+#             bench.py --device cpu --gpus 2/4/8 (N concurrent imports + rendezvous, bringup_s)
 #   trace     rocprofv3 kernel traces: default (B=64), per-rank 8, B=1024 / 8192 fp16, fp32 64 / 8
 #   stages    in-kernel stage stamps (train B=64 / 8, tile B=1024, fp32 B=64) + update stamps
 #   exchange  loopback exchange table (tools/exchange_loopback.py) + step breakdown
@@ -43,7 +44,10 @@ task_bench() {
 
 task_rehearse() {
   cd $R && py 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/${T}_reh_n1.json 2>$O/${T}_reh_n1.err && \
-  py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 > $O/${T}_reh_gloo2.json 2>$O/${T}_reh_gloo2.err
+  py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 > $O/${T}_reh_gloo2.json 2>$O/${T}_reh_gloo2.err && \
+  for n in 2 4 8; do
+    py 300 python bench.py --gpus $n --device cpu --steps 2 --warmup 1 > $O/${T}_reh_cpu$n.json 2>$O/${T}_reh_cpu$n.err || return 1
+  done
 }
 
 task_trace() {

@@ -32,6 +32,21 @@ non-step remainder (validation + tail):
 A loopback log (``--loopback-log``, the ``B=.. N=.. ... step X us`` lines of
 exchange_loopback.py) replaces the built-in table.  The driver's SCALE record is then checked
 against the prediction in the ``measured / predicted`` column.
+
+Predicted ``time_elapsed`` (the reference's own quantity: process start -> end of epoch-0
+validation, ref src/train_dist.py:119,112).  bench.py's ``bringup_s`` splits it into phases
+(max over ranks).  For N ranks:
+
+    time_elapsed_N = spawn_N + import_N + process_group_N      (--cpu-bringup: bench.py --gpus N
+                                                                 --device cpu on the GPU box: N
+                                                                 concurrent imports + rendezvous)
+                   + data_wait_1 + engine_1 + capture_1 + test_upload_1     (the N = 1 GPU record)
+                   + exchange bring-up (engine.ipc_open + engine.self_test of --rehearsal, a
+                     2-rank gloo run sharing the GPU; 0 at N = 1)
+                   + epoch0_1 + 938 * (step_N - step_1)        (the epoch at the predicted step)
+
+What it leaves out: RCCL's communicator set-up over N GPUs (the CPU rehearsal's rendezvous is
+gloo) and xGMI peer mapping (the rehearsal maps one GPU's memory).
 """
 from __future__ import annotations
 
@@ -80,6 +95,29 @@ def predict(by_n: dict[int, dict], steps_us: dict, hop_us: float, ns=(1, 2, 4, 8
         step = steps_us[(b, n)] + (hop_us if n > 1 else 0.0)
         out[n] = {"step_us": step, "images_s": GLOBAL_BATCH / (step * 1e-6),
                   "epoch_s": STEPS_PER_EPOCH * step * 1e-6 + rest if rest is not None else None}
+    return out
+
+
+def predict_time_elapsed(by_n: dict[int, dict], pred: dict[int, dict], cpu_by_n: dict[int, dict],
+                         rehearsal: dict | None) -> dict[int, float]:
+    """Predicted time_elapsed_s per N (see the module docstring); N needs a CPU record."""
+    r1 = by_n.get(1) or {}
+    ph1 = r1.get("bringup_s") or {}
+    if not ph1 or not r1.get("epoch0_s") or 1 not in pred:
+        return {}
+    base = sum(ph1.get(k, 0.0) for k in ("data_wait", "engine", "capture", "test_upload"))
+    xb = 0.0
+    if rehearsal:
+        rph = rehearsal.get("bringup_s") or {}
+        xb = rph.get("engine.ipc_open", 0.0) + rph.get("engine.self_test", 0.0)
+    out = {}
+    for n, p in pred.items():
+        c = (cpu_by_n.get(n) or {}).get("bringup_s") if n > 1 else ph1
+        if not c:
+            continue
+        launch = sum(c.get(k, 0.0) for k in ("spawn", "import", "process_group"))
+        ep0 = r1["epoch0_s"] + STEPS_PER_EPOCH * (p["step_us"] - pred[1]["step_us"]) * 1e-6
+        out[n] = launch + base + (xb if n > 1 else 0.0) + ep0
     return out
 
 
@@ -136,6 +174,7 @@ def table(by_n: dict[int, dict], pred: dict[int, dict] | None = None) -> list[di
             "efficiency": r["value"] / (n * base) if base and r.get("value") else None,
             "dtype": r.get("dtype"), "allreduce": (r.get("config") or {}).get("allreduce"),
             "pred_images_s": p.get("images_s"), "pred_epoch_s": p.get("epoch_s"),
+            "pred_time_elapsed_s": p.get("time_elapsed_s"),
             "vs_pred": r["value"] / p["images_s"] if r.get("value") and p.get("images_s") else None,
         })
     return rows
@@ -149,18 +188,21 @@ def markdown(rows: list[dict], title: str) -> str:
     out = [f"## {title}", "",
            "| GPUs | images/s | ms/step | epoch s (warm) | time_elapsed s (ref quantity) | reference s | "
            "speed-up (epoch) | speed-up (time_elapsed) | scaling eff. | all-reduce | predicted images/s | "
-           "predicted epoch s | measured / predicted |",
-           "|---:|---:|---:|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|"]
+           "predicted epoch s | predicted time_elapsed s | measured / predicted |",
+           "|---:|---:|---:|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|---:|"]
     for r in rows:
         out.append(f"| {r['n']} | {_f(r['images_s'], ',.0f')} | {_f(r['ms_step'], '.4f')} | "
                    f"{_f(r['epoch_s'], '.4f')} | {_f(r['time_elapsed_s'], '.3f')} | {_f(r['ref_s'], '.2f')} | "
                    f"{_f(r['speedup_epoch'], ',.0f')}x | {_f(r['speedup_time_elapsed'], '.1f')}x | "
                    f"{_f(r['efficiency'], '.1%')} | {r['allreduce'] or '-'} | {_f(r['pred_images_s'], ',.0f')} | "
-                   f"{_f(r['pred_epoch_s'], '.4f')} | {_f(r['vs_pred'], '.2f')} |")
+                   f"{_f(r['pred_epoch_s'], '.4f')} | {_f(r.get('pred_time_elapsed_s'), '.3f')} | "
+                   f"{_f(r['vs_pred'], '.2f')} |")
     out += ["", "Reference: 1 / 2 / 4 / 8 GCP e2-standard-8 CPU VMs, gloo over TCP (BASELINE.md).  Scaling is "
             "strong (global batch 64 split over the GPUs, ref src/train_dist.py:133), so per-GPU work shrinks "
             "to 8 images per step at N = 8.  Predicted columns: the one-GPU loopback measurement of the "
-            "per-rank step (per-rank batch 64/N, exchange with N-1 virtual peers) + one xGMI hop; see the "
+            "per-rank step (per-rank batch 64/N, exchange with N-1 virtual peers) + one xGMI hop; predicted "
+            "time_elapsed: N concurrent imports + rendezvous measured on the CPU, the N = 1 GPU bring-up, "
+            "the exchange bring-up of a 2-rank rehearsal and epoch 0 at the predicted step; see the "
             "module docstring of tools/scaling_report.py."]
     return "\n".join(out) + "\n"
 
@@ -209,6 +251,9 @@ def main(argv=None) -> int:
     ap.add_argument("--no-predict", dest="predict", action="store_false")
     ap.add_argument("--hop-us", type=float, default=1.0, help="assumed xGMI one-way hop added for N > 1")
     ap.add_argument("--loopback-log", help="exchange_loopback.py output replacing the built-in step table")
+    ap.add_argument("--cpu-bringup", nargs="*", default=[],
+                    help="bench.py --device cpu --gpus N JSON lines (spawn / import / rendezvous at N ranks)")
+    ap.add_argument("--rehearsal", help="a 2-rank gloo GPU rehearsal's JSON line (exchange bring-up phases)")
     a = ap.parse_args(argv)
     by_n = load_records(a.inputs)
     if not by_n:
@@ -217,6 +262,10 @@ def main(argv=None) -> int:
     pred = None
     if a.predict:
         pred = predict(by_n, load_loopback(a.loopback_log) if a.loopback_log else LOOPBACK_STEP_US, a.hop_us)
+        reh = load_records([a.rehearsal]).get(2) if a.rehearsal else None
+        for n, t in predict_time_elapsed(by_n, pred, load_records(a.cpu_bringup) if a.cpu_bringup else {},
+                                         reh).items():
+            pred[n]["time_elapsed_s"] = t
     rows = table(by_n, pred)
     out = Path(a.out)
     out.parent.mkdir(parents=True, exist_ok=True)
