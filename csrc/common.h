@@ -4,6 +4,8 @@
 // instruction set; there is no other target.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 namespace csed {
@@ -110,13 +112,31 @@ __device__ __forceinline__ void prefetch_kernargs() {
 // Raise a kernel's dynamic-LDS limit once per instantiation (host side).  The attribute
 // is a property of the function, not of a launch: setting it on every launch was host
 // work on every step of the native executor (csrc/bindings.cpp LenetStepper).
+// One record per kernel instantiation and device, set only after the attribute call succeeded
+// (a failed or other-device first call is retried; the launch right after a failure reports the
+// error through hipGetLastError).  Launches may come from several host threads: atomics.
 template <auto KERNEL>
-inline void allow_dynamic_lds(size_t bytes) {
-  static size_t done = 0;  // one flag per kernel instantiation
-  if (done >= bytes) return;
-  hipFuncSetAttribute((const void*)KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  done = bytes;
+inline hipError_t allow_dynamic_lds(size_t bytes) {
+  constexpr int kMaxDevices = 64;
+  static std::atomic<size_t> done[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = kMaxDevices - 1;
+  if (done[dev].load(std::memory_order_acquire) >= bytes) return hipSuccess;
+  const hipError_t e =
+      hipFuncSetAttribute((const void*)KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) {
+    size_t cur = done[dev].load(std::memory_order_relaxed);
+    while (cur < bytes && !done[dev].compare_exchange_weak(cur, bytes, std::memory_order_release)) {
+    }
+  }
+  return e;
 }
+// allow_dynamic_lds for a launcher returning hipError_t: a failed attribute call is returned.
+#define CSED_ALLOW_LDS(bytes, ...)                                              \
+  do {                                                                          \
+    const hipError_t csed_lds_e_ = ::csed::allow_dynamic_lds<__VA_ARGS__>(bytes); \
+    if (csed_lds_e_ != hipSuccess) return csed_lds_e_;                          \
+  } while (0)
 
 // ---------------------------------------------------------------------------
 // Counter-based RNG (Philox4x32-10).  Dropout masks are a pure function of

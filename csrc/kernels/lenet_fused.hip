@@ -1444,33 +1444,36 @@ __device__ __forceinline__ void finish_param4(const LenetUpdateArgs& a, int i, f
 // are 512-byte contiguous runs.  Every wait is bounded by a wall-clock timeout
 // that raises the comm error word instead of hanging the GPU.
 // ---------------------------------------------------------------------------
-constexpr int EXCH_WORDS = CNP_PAD + FC_TILES * 256;  // 27840
+constexpr int EXCH_WORDS = CNP_PAD + FC_TILES * 256;  // 27904
 
 __device__ __forceinline__ uint64_t ll_word(float v, uint32_t t) {
   return ((uint64_t)t << 32) | (uint64_t)__float_as_uint(v);
 }
 
-// The exchange's peer addresses for one call, resolved at block entry (the pointer loads from
-// the argument segment issue with the block's first loads instead of as a dependent scalar
-// chain inside the exchange): dst[p] = this rank's sender slot in peer p's buffer for this
-// call's tag parity; src = sender slot 0 of this rank's own buffer (peer p's words at + p * cap).
-// R: the launch's world bound (2, 4 or 8 >= px.world; peers p >= world are never pushed to and
-// their polls are clamped to row world - 1).
+// The exchange's peer addresses, resolved at block entry (the pointer loads from the argument
+// segment issue with the block's first loads instead of as a dependent scalar chain inside the
+// exchange), for slot parity 0: dst[p] = this rank's sender slot in peer p's buffer; src =
+// sender slot 0 of this rank's own buffer (peer p's words at + p * cap).  A call's parity
+// (tag & 1) adds slot_words(): the tag itself is a per-lane load nobody waits for before the
+// exchange.  R: the launch's world bound (2, 4 or 8 >= px.world; peers p >= world are never
+// pushed to and their polls are clamped to row world - 1).
 template <int R>
 struct XPtrs {
   uint64_t* dst[R];
   const uint64_t* src;
 };
 template <int R>
-__device__ __forceinline__ XPtrs<R> xptrs(const comm::IpcPeers& px, uint32_t t) {
+__device__ __forceinline__ XPtrs<R> xptrs(const comm::IpcPeers& px) {
   static_assert(R >= 2 && R <= comm::kIpcMaxRanks, "world bound");
   XPtrs<R> x;
-  // receive buffer layout (csrc/comm/ipc_allreduce.h): [2 slots][kIpcMaxRanks senders][cap]
-  const int64_t slot = (int64_t)(t & 1) * comm::kIpcMaxRanks * px.cap;
 #pragma unroll
-  for (int p = 0; p < R; ++p) x.dst[p] = px.base[min(p, px.world - 1)] + slot + (int64_t)px.rank * px.cap;
-  x.src = px.base[px.rank] + slot;
+  for (int p = 0; p < R; ++p) x.dst[p] = px.base[min(p, px.world - 1)] + (int64_t)px.rank * px.cap;
+  x.src = px.base[px.rank];
   return x;
+}
+// receive buffer layout (csrc/comm/ipc_allreduce.h): [2 slots][kIpcMaxRanks senders][cap]
+__device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t t) {
+  return (int64_t)(t & 1u) * comm::kIpcMaxRanks * px.cap;
 }
 
 // v[k] (this rank's value of exchange word w0 + 64 k) := sum over ranks, in rank order (so every
@@ -1481,13 +1484,14 @@ template <int K, int R>
 __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                              const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
                                              bool& timed_out) {
+  const int64_t so = slot_words(px, t) + w0;
   // 1. push (write-through, system scope: see comm::push_word) to every peer
 #pragma unroll
   for (int p = 0; p < R; ++p)
     if (p < px.world && p != px.rank)
 #pragma unroll
       for (int k = 0; k < K; ++k)
-        __hip_atomic_store(x.dst[p] + w0 + 64 * k, ll_word(v[k], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(x.dst[p] + so + 64 * k, ll_word(v[k], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // 2. poll this rank's receive buffer for every peer's words of tag t (all loads issued before
   //    the first wait: one memory round trip per pass)
   const int64_t cap = px.cap;
@@ -1499,7 +1503,7 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
     for (int p = 0; p < R; ++p)
 #pragma unroll
       for (int k = 0; k < K; ++k)
-        w[p][k] = __hip_atomic_load(x.src + (int64_t)min(p, wl) * cap + w0 + 64 * k, __ATOMIC_RELAXED,
+        w[p][k] = __hip_atomic_load(x.src + (int64_t)min(p, wl) * cap + so + 64 * k, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_SYSTEM);
     bool ready = true;
 #pragma unroll
@@ -1532,12 +1536,16 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
-  // exchange tag of this call (uniform load; written back after the block's last poll)
+  // exchange tag of this call (written back after the block's last poll): a per-lane load
+  // through an opaque lane offset, so it is a VGPR nothing waits for before the exchange (a
+  // uniform load is an SGPR the block's first address math waits for: one more round trip in
+  // front of its slab loads)
   constexpr bool EXCH = XW > 0;
   constexpr int XR = EXCH ? XW : 2;
-  const uint32_t xt = EXCH ? (uint32_t)(px.counters[blk] + 1) : 0u;
+  typedef const __attribute__((address_space(1))) int64_t* gcptr64;
+  const uint32_t xt = EXCH ? (uint32_t)(((gcptr64)px.counters)[blk + opaque(0)] + 1) : 0u;
   XPtrs<XR> xp;
-  if constexpr (EXCH) xp = xptrs<XR>(px, xt);
+  if constexpr (EXCH) xp = xptrs<XR>(px);
   // a wait of this exchange has timed out before (the error word is set): the replicas are
   // already inconsistent and the caller re-runs the epoch on the process group, so this call
   // polls once and never waits -- a dead peer costs one timeout, not one per step
@@ -2002,15 +2010,15 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(S_TOTAL - S_X);  // dynamic activations; weights are static LDS
   CSED_DISPATCH_MFMA(a.mfma_dtype, {
     if (split) {
-      allow_dynamic_lds<lenet_train_kernel<scalar_t, true, true, SPLIT_K>>(lds);
+      CSED_ALLOW_LDS(lds, lenet_train_kernel<scalar_t, true, true, SPLIT_K>);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true, SPLIT_K>), dim3(a.grid), dim3(NT), lds, s,
                          a, 0, (float*)nullptr);
     } else if (a.xstage) {
-      allow_dynamic_lds<lenet_train_kernel<scalar_t, true, true>>(lds);
+      CSED_ALLOW_LDS(lds, lenet_train_kernel<scalar_t, true, true>);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, true>), dim3(a.grid), dim3(NT), lds, s, a, 0,
                          (float*)nullptr);
     } else {
-      allow_dynamic_lds<lenet_train_kernel<scalar_t, true, false>>(lds);
+      CSED_ALLOW_LDS(lds, lenet_train_kernel<scalar_t, true, false>);
       hipLaunchKernelGGL((lenet_train_kernel<scalar_t, true, false>), dim3(a.grid), dim3(NT), lds, s, a, 0,
                          (float*)nullptr);
     }
@@ -2106,7 +2114,7 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   }
   const size_t lds = (size_t)(S_TOTAL - S_X);
   CSED_DISPATCH_MFMA(mfma_dtype, {
-    allow_dynamic_lds<lenet_train_kernel<scalar_t, false, false>>(lds);
+    CSED_ALLOW_LDS(lds, lenet_train_kernel<scalar_t, false, false>);
     hipLaunchKernelGGL((lenet_train_kernel<scalar_t, false, false>), dim3(a.grid), dim3(NT), lds, s, a,
                        logp_out ? 1 : 0, logp_out);
   });

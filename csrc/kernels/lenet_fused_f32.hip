@@ -853,14 +853,14 @@ hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float
   if (a.B <= 0 || a.grid <= 0 || a.grid > 256 || (a.xstage && !split) || (!split && a.grid > a.B))
     return hipErrorInvalidValue;
   if (split) {
-    allow_dynamic_lds<lenet_train_f32_kernel<true, SPLIT_K>>(LDS_BYTES);
+    CSED_ALLOW_LDS(LDS_BYTES, lenet_train_f32_kernel<true, SPLIT_K>);
     hipLaunchKernelGGL((lenet_train_f32_kernel<true, SPLIT_K>), dim3(a.grid), dim3(NT), LDS_BYTES, s, a, 0,
                        (float*)nullptr);
   } else if (train) {
-    allow_dynamic_lds<lenet_train_f32_kernel<true>>(LDS_BYTES);
+    CSED_ALLOW_LDS(LDS_BYTES, lenet_train_f32_kernel<true>);
     hipLaunchKernelGGL(lenet_train_f32_kernel<true>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, 0, (float*)nullptr);
   } else {
-    allow_dynamic_lds<lenet_train_f32_kernel<false>>(LDS_BYTES);
+    CSED_ALLOW_LDS(LDS_BYTES, lenet_train_f32_kernel<false>);
     hipLaunchKernelGGL(lenet_train_f32_kernel<false>, dim3(a.grid), dim3(NT), LDS_BYTES, s, a, write_logp,
                        logp_out);
   }

@@ -855,7 +855,7 @@ hipError_t launch_lenet_tile(const LenetTrainArgs& a, int write_logp, float* log
   const bool one = a.B <= TS * a.grid;
 #define CSED_TILE_LAUNCH(TR, ONE, WL, LP)                                                           \
   do {                                                                                               \
-    allow_dynamic_lds<lenet_tile_kernel<scalar_t, TR, ONE>>(lds);                                    \
+    CSED_ALLOW_LDS(lds, lenet_tile_kernel<scalar_t, TR, ONE>);                                    \
     hipLaunchKernelGGL((lenet_tile_kernel<scalar_t, TR, ONE>), dim3(a.grid), dim3(NT), lds, s, a, WL, LP); \
   } while (0)
   CSED_DISPATCH_MFMA(a.mfma_dtype, {

@@ -48,7 +48,7 @@ def test_no_ipc_without_distributed_gpu(monkeypatch):
 
 
 def test_exchange_buffer_layout():
-    """lenet_update's exchange words: conv params 0..5279 map to themselves, each of the
+    """lenet_update's exchange words: the conv slab slots 0..5375 (one word each), each of the
     88 fc tiles owns 256 words after the conv slab row (csrc/kernels/lenet_layout.h: conv1's
     260 slots padded to 5 chunks, conv2's 5020 to 79: 84 chunks of 64 = 5376)."""
     from csed_514_project_distributed_training_using_pytorch_amd.ops import _native

@@ -109,4 +109,4 @@ def test_dist_epoch_rerun_after_injected_fault_matches_clean_run(tmp_path):
         assert torch.equal(sd_fault[k], sd_clean[k]), k
     # and the epoch lines: two epochs per rank in each run, the faulted epoch printed once
     for r in (r_fault, r_clean):
-        assert sum(ln.startswith("Epoch=") for ln in r.stdout.splitlines()) == 2 * 2, r.stdout
+        assert r.stdout.count("Epoch=") == 2 * 2, r.stdout  # (two ranks' lines may share a line)

@@ -116,9 +116,10 @@ def test_tile_eval_matches_per_sample_eval():
 
 
 def test_tile_training_epoch_matches_per_sample_and_converges():
-    """Two epochs at per-rank batch 1024 (graph-replayed, with the epoch tail on the tile kernel
-    too): the tile-kernel and per-sample trainings stay within the 16-bit band of each other,
-    and the loss falls."""
+    """Three epochs at per-rank batch 1024 (graph-replayed; the epoch tail of 300 samples is below
+    tile_min_batch(), so it runs on the per-sample kernel in both trainings -- the tile kernel's
+    tail path is test_tile_epoch_tail_on_the_tile_kernel): the tile-kernel and per-sample
+    trainings stay within the 16-bit band of each other, and the loss falls."""
     n = 1024 * 5 + 300
     train = synthetic_mnist(n, seed=3)
     test = synthetic_mnist(1000, seed=4, train=False)
@@ -138,3 +139,29 @@ def test_tile_training_epoch_matches_per_sample_and_converges():
     assert torch.isfinite(finals[0][0]).all()
     assert _rel(finals[0][0], finals[1][0]) < 3e-2
     assert abs(finals[0][1] - finals[1][1]) < 0.02 * finals[1][1]
+
+
+def test_tile_epoch_tail_on_the_tile_kernel():
+    """An epoch whose short last batch is itself a large batch (per-rank batch 2048, tail 1500 >=
+    tile_min_batch()): the tail step runs on the tile kernel (its unstaged path: no cursor, no
+    staging rows), and the epoch stays within the 16-bit band of the per-sample kernel's."""
+    from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import tile_grid, tile_min_batch
+
+    B, n = 2048, 2 * 2048 + 1500
+    train = synthetic_mnist(n, seed=5)
+    finals = []
+    for kernel in (0, 1):
+        torch.manual_seed(1)
+        eng = FusedLeNetTrainer(Net().to(DEV), train, lr=0.05, momentum=0.5, global_batch=B)
+        eng.train_kernel = kernel
+        rem = n - 2 * B
+        g = torch.Generator().manual_seed(0)
+        eng.train_epoch(torch.randperm(n, generator=g), steps_per_graph=2)
+        assert eng.tail_size() == rem and rem >= tile_min_batch()
+        if kernel == 0:  # the tail launch (B = rem, grid = min(rem, eng.grid)) takes the tile kernel
+            assert eng.kernel_for(rem, min(rem, eng.grid)) == 0 and tile_grid(rem) == min(rem, eng.grid)
+        torch.cuda.synchronize()
+        assert eng.cursor.item() == 3  # two full steps + the tail
+        finals.append(eng.flat.data.cpu().clone())
+    assert torch.isfinite(finals[0]).all()
+    assert _rel(finals[0], finals[1]) < 3e-2

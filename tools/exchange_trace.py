@@ -77,9 +77,9 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda")
     data = synthetic_mnist(8192, seed=1)
-    print("| B | N | step us (graph) | train | gap train->upd | upd s3 | upd s4 | gap upd s4->next train | "
-          "sum |")
-    print("|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+    print("| B | N | step us (graph) | train | gap train->upd | upd s3 | upd s4 | FC s4 | CONV s4 | "
+          "gap upd s4->next train | sum |")
+    print("|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for B in args.batch:
         for N in args.worlds:
             torch.manual_seed(1)
@@ -104,16 +104,18 @@ def main():
             for i in range(n - 1):
                 t0, t1 = T[i, :, 22].min().item(), T[i, :, 23].max().item()
                 u = U[i]
-                u = u[u[:, 0] > 0]
-                u0 = u[:, 0].min().item()
+                u0 = u[:, 0][u[:, 0] > 0].min().item()
                 s3 = u[:, 3].max().item()
                 s4 = u[:, 4][u[:, 4] > 0].max().item()
+                # blocks 0..87: the FC role (one tile each), 88..171: the CONV role
+                fc4 = u[:88, 4][u[:88, 4] > 0].max().item()
+                cv4 = u[88:172, 4][u[88:172, 4] > 0].max().item()
                 nt0 = T[i + 1, :, 22].min().item()
                 rows.append(((t1 - t0) * 0.01, (u0 - t1) * 0.01, (s3 - u0) * 0.01, (s4 - u0) * 0.01,
-                             (nt0 - s4) * 0.01, (nt0 - t0) * 0.01))
+                             (fc4 - u0) * 0.01, (cv4 - u0) * 0.01, (nt0 - s4) * 0.01, (nt0 - t0) * 0.01))
             med = [statistics.median(c) for c in zip(*rows)]
-            print(f"| {B} | {N} | {t_step:.2f} | {med[0]:.2f} | {med[1]:.2f} | {med[2]:.2f} | {med[3]:.2f} | "
-                  f"{med[4]:.2f} | {med[5]:.2f} |", flush=True)
+            print(f"| {B} | {N} | {t_step:.2f} | " +
+                  " | ".join(f"{m:.2f}" for m in med) + " |", flush=True)
             if os.environ.get("TRACE_DUMP"):
                 torch.save({"T": T, "U": U}, f"{os.environ['TRACE_DUMP']}_B{B}_N{N}.pt")
             print(f"  comm_errors {eng.comm_errors()}", flush=True)
