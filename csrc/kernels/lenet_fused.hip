@@ -1450,6 +1450,31 @@ __device__ __forceinline__ uint64_t ll_word(float v, uint32_t t) {
   return ((uint64_t)t << 32) | (uint64_t)__float_as_uint(v);
 }
 
+// A wave-uniform pointer in SGPRs (the buffer-resource base of sys_store16 / sys_load16 must be:
+// a base the compiler cannot prove uniform becomes a loop over the lanes' descriptors).
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
+}
+// 16-byte system-scope (sc0 sc1: write-through / uncached) store and load of two 8-byte LL words
+// through a raw buffer resource on a wave-uniform base with a per-lane byte offset (gfx9
+// descriptor word 3 = 0x00020000, as CK uses): HIP atomics stop at 64 bits.  Each 8-byte word
+// of the pair is still written by one store and read back untorn.
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void sys_store16(uint64_t* base, int byte_off, u64x2v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), sys_rsrc(base), byte_off, 0, 1 | 16);
+}
+__device__ __forceinline__ u64x2v sys_load16(const uint64_t* base, int byte_off) {
+  return __builtin_bit_cast(u64x2v, __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), byte_off, 0, 1 | 16));
+}
+
 // The exchange's peer addresses, resolved at block entry (the pointer loads from the argument
 // segment issue with the block's first loads instead of as a dependent scalar chain inside the
 // exchange), for slot parity 0: dst[p] = this rank's sender slot in peer p's buffer; src =
@@ -1476,41 +1501,56 @@ __device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t
   return (int64_t)(t & 1u) * comm::kIpcMaxRanks * px.cap;
 }
 
-// v[k] (this rank's value of exchange word w0 + 64 k) := sum over ranks, in rank order (so every
-// rank gets identical bits).  A wave's lanes hold consecutive w0, so each push / poll
-// instruction of a wave moves one contiguous 512-byte run.  live[k]: words whose tags must match
-// (the others are pushed and summed but never waited for).
+// v[k] (this rank's value of exchange word k of the lane, K = 1: w0; K = 4: w0 + {0, 1, 128,
+// 129}) := sum over ranks, in rank order (so every rank gets identical bits).  Every push / poll
+// instruction of a wave moves one contiguous run (512 bytes of 8-byte words, or 1 KB of pairs).  Only the world - 1 peer rows are
+// polled (row q holds peer q < rank ? q : q + 1; this rank's own row is never written).
+// live[k]: words whose tags must match (the others are pushed and summed but never waited for).
 template <int K, int R>
 __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                              const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
                                              bool& timed_out) {
+  static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
   const int64_t so = slot_words(px, t) + w0;
+  const int rank = px.rank, world = px.world;
+  // K = 4: the words are w0 + {0, 1} and w0 + 128 + {0, 1} (w0 = base + 2 lane): two 16-byte
+  // pairs per lane, each wave instruction one contiguous 1-KB run
+  const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));  // (uniform: the pair bases)
   // 1. push (write-through, system scope: see comm::push_word) to every peer
 #pragma unroll
   for (int p = 0; p < R; ++p)
-    if (p < px.world && p != px.rank)
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        __hip_atomic_store(x.dst[p] + so + 64 * k, ll_word(v[k], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (p < world && p != rank) {
+      if constexpr (K == 1) {
+        __hip_atomic_store(x.dst[p] + so, ll_word(v[0], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        uint64_t* b = uniform_ptr(x.dst[p] + sw);
+        sys_store16(b, 8 * w0, u64x2v{ll_word(v[0], t), ll_word(v[1], t)});
+        sys_store16(b, 8 * (w0 + 128), u64x2v{ll_word(v[2], t), ll_word(v[3], t)});
+      }
+    }
   // 2. poll this rank's receive buffer for every peer's words of tag t (all loads issued before
   //    the first wait: one memory round trip per pass)
   const int64_t cap = px.cap;
-  const int wl = px.world - 1;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t w[R][K];
+  uint64_t w[R - 1][K];
   while (true) {
 #pragma unroll
-    for (int p = 0; p < R; ++p)
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        w[p][k] = __hip_atomic_load(x.src + (int64_t)min(p, wl) * cap + so + 64 * k, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int q = 0; q < R - 1; ++q) {
+      const int p = min(q < rank ? q : q + 1, world - 1);  // (rows past the world: clamped, unused)
+      if constexpr (K == 1) {
+        w[q][0] = __hip_atomic_load(x.src + (int64_t)p * cap + so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        const uint64_t* b = uniform_ptr(x.src + sw + (int64_t)p * cap);
+        const u64x2v lo = sys_load16(b, 8 * w0), hi = sys_load16(b, 8 * (w0 + 128));
+        w[q][0] = lo.x; w[q][1] = lo.y; w[q][2] = hi.x; w[q][3] = hi.y;
+      }
+    }
     bool ready = true;
 #pragma unroll
-    for (int p = 0; p < R; ++p)
+    for (int q = 0; q < R - 1; ++q)
 #pragma unroll
       for (int k = 0; k < K; ++k)
-        if (p < px.world && p != px.rank && live[k]) ready = ready && (uint32_t)(w[p][k] >> 32) == t;
+        if (q < world - 1 && live[k]) ready = ready && (uint32_t)(w[q][k] >> 32) == t;
     if (ready || timed_out) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) timed_out = true;
     __builtin_amdgcn_s_sleep(1);
@@ -1519,8 +1559,13 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
   for (int k = 0; k < K; ++k) {
     float s = 0.f;
 #pragma unroll
-    for (int p = 0; p < R; ++p)
-      if (p < px.world) s += p == px.rank ? v[k] : __uint_as_float((uint32_t)w[p][k]);
+    for (int p = 0; p < R; ++p) {
+      if (p < world) {
+        // peer p's row: q = p (p < rank) or p - 1 (p > rank)
+        const uint64_t wp = p < rank ? w[min(p, R - 2)][k] : w[max(p - 1, 0)][k];
+        s += p == rank ? v[k] : __uint_as_float((uint32_t)wp);
+      }
+    }
     v[k] = s;
   }
 }
@@ -1883,11 +1928,12 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         g[r] = v * a.grad_post;
       }
       if (EXCH) {
-        // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + r * 64 + lane
+        // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + 2 lane + {0, 1}
+        // and + 128 + {0, 1} (two 16-byte pairs)
         bool live[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) live[r] = pidx[r] >= 0;
-        ll_allreduce<4, XR>(px, xp, xt, CNP_PAD + tile * 256 + lane, live, g, timeout_ticks, timed_out);
+        ll_allreduce<4, XR>(px, xp, xt, CNP_PAD + tile * 256 + 2 * lane, live, g, timeout_ticks, timed_out);
       }
       if (vec) {
         // MFMA layout (row 4kq + r, column l16) -> row layout through this wave's LDS slot
