@@ -169,6 +169,10 @@ class FusedLeNetTrainer:
         # pixels + labels one step ahead, so lenet_train starts with no dependent index chain
         # (the exact-fp32 kernel, lenet_fused_f32.hip, gathers its samples itself)
         self.fp32 = compute_dtype == torch.float32
+        # split-K fc-gradient scratch (lenet_fused.hip fc_split_slices): per-rank batches > 1024
+        # without the fused exchange form the fc weight gradients as up to 8 batch slices per
+        # tile on all CUs, then a finishing launch (88 tiles x 256 floats per slice)
+        self.fc_part = torch.empty(8 * 88 * 256, dtype=torch.float32, device=dev) if self.B > 1024 else None
         # split step (lenet_fused.hip / lenet_fused_f32.hip KS > 1): split_k workgroups per sample
         # share the backward conv stages; used whenever the whole grid fits one wave of the GPU
         # (split_k * B <= 256 CUs).  CSED_SPLIT=0 keeps one workgroup per sample.  The exact-fp32
@@ -516,13 +520,13 @@ class FusedLeNetTrainer:
                              post)
         elif self.comm:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, self.flat.grad, *common, None, None, False,
-                             self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post)
+                             self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post, self.fc_part)
             dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM)
             ops.lenet_update(self.slab, grid, self.vslab, B, self.flat.grad, None, *common, cursor, self.rng_offset,
                              True, None, 0, None, self.mfma)
         else:
             ops.lenet_update(self.slab, grid, self.vslab, B, None, None, *common, cursor, self.rng_offset, True,
-                             self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post)
+                             self.loss_parts, grid, self.loss_acc, self.mfma, None, -1, 2.0, post, self.fc_part)
 
     def _stages(self, kernel: int) -> bool:
         """Whether a full step launched with ``kernel`` (kernel_for) reads / writes the staging
@@ -557,7 +561,7 @@ class FusedLeNetTrainer:
         ops.lenet_update(self.slab, grid, self.vslab, self.B, None, g, self.flat.data, self.momentum_buf, self.wimg,
                          self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov, self.step_count,
                          self.ticket, None, None, False, self.loss_parts, grid, self.loss_acc, self.mfma, None, -1,
-                         2.0, self._post_scale(1.0 / self.global_batch))
+                         2.0, self._post_scale(1.0 / self.global_batch), self.fc_part)
         return g
 
     def step(self) -> None:
@@ -680,7 +684,7 @@ class FusedLeNetTrainer:
                           self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                           self.step_count, self.ticket, self.cursor, self.rng_offset, self.loss_parts, self.grid,
                           self.loss_acc, self.mfma, exch_id, self.exch_timeout_s if exch_id >= 0 else 2.0,
-                          self._post_scale(self.grad_scale))
+                          self._post_scale(self.grad_scale), self.fc_part)
             self._stepper = (key, st)
         return self._stepper[1]
 

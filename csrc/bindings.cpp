@@ -426,7 +426,7 @@ csed::LenetUpdateArgs update_args(const Tensor& slab, int64_t grid, const Tensor
                                   const optional<Tensor>& cursor, const optional<Tensor>& rng_offset, bool apply_sgd,
                                   const optional<Tensor>& loss_parts, const optional<Tensor>& loss_acc,
                                   int64_t mfma_dtype, const optional<Tensor>& dbg, int64_t exch_id,
-                                  double exch_timeout_s, double grad_post) {
+                                  double exch_timeout_s, double grad_post, const optional<Tensor>& fc_part) {
   dev(slab, "slab"); dev(params, "params"); dev(momentum, "momentum"); dev(wimg, "wimg");
   TORCH_CHECK(params.numel() == csed::lenet_param_count() && momentum.numel() == params.numel(),
               "lenet_update: params / momentum must hold the 21840 flat LeNet parameters");
@@ -447,6 +447,13 @@ csed::LenetUpdateArgs update_args(const Tensor& slab, int64_t grid, const Tensor
   if (dbg.has_value()) {
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 8 * 256, "lenet_update: dbg must be int64[>=2048]");
     a.dbg = (uint64_t*)dbg->data_ptr();
+    a.dbg_blocks = (int)std::min<int64_t>(dbg->numel() / 8, 1 << 20);
+  }
+  if (fc_part.has_value()) {  // split-K fc scratch (the launcher picks the slices that fit)
+    dev(*fc_part, "fc_part");
+    TORCH_CHECK(fc_part->scalar_type() == at::kFloat && fc_part->is_contiguous(), "lenet_update: fc_part must be float32");
+    a.fc_part = fc_part->data_ptr<float>();
+    a.fc_part_n = fc_part->numel();
   }
   // exch_id >= 0: csrc/comm buffer of the fused gradient exchange (checked by the launcher)
   TORCH_CHECK(exch_id < 0 || !a.grad_in, "lenet_update: the fused exchange reduces the slabs itself (no grad_in)");
@@ -459,12 +466,12 @@ void lenet_update(const Tensor& slab, int64_t grid, const Tensor& vslab, int64_t
                   double weight_decay, bool nesterov, Tensor& step, Tensor& ticket, const optional<Tensor>& cursor,
                   const optional<Tensor>& rng_offset, bool apply_sgd, const optional<Tensor>& loss_parts,
                   int64_t nparts, const optional<Tensor>& loss_acc, int64_t mfma_dtype, const optional<Tensor>& dbg,
-                  int64_t exch_id, double exch_timeout_s, double grad_post) {
+                  int64_t exch_id, double exch_timeout_s, double grad_post, const optional<Tensor>& fc_part) {
   const c10::DeviceGuard gd(params.device());
   const csed::LenetUpdateArgs a =
       update_args(slab, grid, vslab, B, grad_in, grad_out, params, momentum, wimg, lr, mom, dampening, weight_decay,
                   nesterov, step, ticket, cursor, rng_offset, apply_sgd, loss_parts, loss_acc, mfma_dtype, dbg,
-                  exch_id, exch_timeout_s, grad_post);
+                  exch_id, exch_timeout_s, grad_post, fc_part);
   CHECK_HIP(csed::launch_lenet_update(a, optpt<float>(loss_parts), (int)nparts, optpt<float>(loss_acc),
                                       cur_stream(params)));
 }
@@ -514,16 +521,18 @@ struct LenetStepper : torch::CustomClassHolder {
   void set_update(Tensor slab, int64_t grid, Tensor vslab, int64_t B, Tensor params, Tensor momentum, Tensor wimg,
                   double lr, double mom, double dampening, double weight_decay, bool nesterov, Tensor step,
                   Tensor ticket, Tensor cursor, Tensor rng_offset, Tensor loss_parts_t, int64_t nparts_,
-                  Tensor loss_acc_t, int64_t mfma_dtype, int64_t exch_id, double exch_timeout_s, double grad_post) {
+                  Tensor loss_acc_t, int64_t mfma_dtype, int64_t exch_id, double exch_timeout_s, double grad_post,
+                  optional<Tensor> fc_part) {
     ua = update_args(slab, grid, vslab, B, c10::nullopt, c10::nullopt, params, momentum, wimg, lr, mom, dampening,
                      weight_decay, nesterov, step, ticket, cursor, rng_offset, true, loss_parts_t, loss_acc_t,
-                     mfma_dtype, c10::nullopt, exch_id, exch_timeout_s, grad_post);
+                     mfma_dtype, c10::nullopt, exch_id, exch_timeout_s, grad_post, fc_part);
     loss_parts = loss_parts_t.data_ptr<float>();
     loss_acc = loss_acc_t.data_ptr<float>();
     nparts = nparts_;
     px = {};
     if (exch_id >= 0) CHECK_HIP(csed::comm::ipc_peers((int)exch_id, &px));  // once, not per launch
     keep_u = {slab, vslab, params, momentum, wimg, step, ticket, cursor, rng_offset, loss_parts_t, loss_acc_t};
+    if (fc_part.has_value()) keep_u.push_back(*fc_part);
   }
 
   void run(int64_t k) {
@@ -558,7 +567,8 @@ TORCH_LIBRARY(csed, m) {
         "Tensor(c!) momentum, Tensor(d!) wimg, float lr, float mom, float dampening, float weight_decay, "
         "bool nesterov, Tensor(e!) step, Tensor(f!) ticket, Tensor(g!)? cursor, Tensor(h!)? rng_offset, "
         "bool apply_sgd, Tensor? loss_parts, int nparts, Tensor(i!)? loss_acc, int mfma_dtype, "
-        "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0, float grad_post=1.0) -> ()");
+        "Tensor(j!)? dbg=None, int exch_id=-1, float exch_timeout_s=2.0, float grad_post=1.0, "
+        "Tensor(k!)? fc_part=None) -> ()");
   m.def("lenet_eval(Tensor images, Tensor labels, Tensor order, int n, Tensor wimg, Tensor params, float mean, "
         "float std, Tensor(a!) out_parts, Tensor(b!)? logp_out, int mfma_dtype, int kernel=0) -> ()");
   m.def("gather_normalize(Tensor src, Tensor idx, Tensor? cursor, int B, float mean, float std, Tensor(a!) out, "

@@ -1516,6 +1516,9 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
   // K = 4: the words are w0 + {0, 1} and w0 + 128 + {0, 1} (w0 = base + 2 lane): two 16-byte
   // pairs per lane, each wave instruction one contiguous 1-KB run
   const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));  // (uniform: the pair bases)
+  // a pair with no live word is never pushed (its lanes are off in the store's EXEC mask): the
+  // fc tiles' padding rows / columns (a quarter of the fc words) never cross a link
+  const bool live01 = K == 1 || live[0] || live[min(1, K - 1)], live23 = K == 4 && (live[min(2, K - 1)] || live[K - 1]);
   // 1. push (write-through, system scope: see comm::push_word) to every peer
 #pragma unroll
   for (int p = 0; p < R; ++p)
@@ -1524,8 +1527,8 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
         __hip_atomic_store(x.dst[p] + so, ll_word(v[0], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
         uint64_t* b = uniform_ptr(x.dst[p] + sw);
-        sys_store16(b, 8 * w0, u64x2v{ll_word(v[0], t), ll_word(v[1], t)});
-        sys_store16(b, 8 * (w0 + 128), u64x2v{ll_word(v[2], t), ll_word(v[3], t)});
+        if (live01) sys_store16(b, 8 * w0, u64x2v{ll_word(v[0], t), ll_word(v[1], t)});
+        if (live23) sys_store16(b, 8 * (w0 + 128), u64x2v{ll_word(v[2], t), ll_word(v[3], t)});
       }
     }
   // 2. poll this rank's receive buffer for every peer's words of tag t (all loads issued before
@@ -1576,8 +1579,10 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
 template <typename T, int XW>
 __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
                             int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
-                            int nblk, int tid, float4* part_, float* part2_, int fc_tpb) {
+                            int nblk, int tid, float4* part_, float* part2_, int fc_tpb, int fc_sl_arg) {
   constexpr int NTH = UP_NT;
+  constexpr bool EXCH = XW > 0;
+  const int fc_sl = EXCH ? 1 : fc_sl_arg;  // (the exchange never splits: folded away there)
   // with zero dampening a zero-initialised momentum buffer reproduces torch's
   // first-step rule exactly (buf = m*0 + g), so step[0] is only read otherwise
   const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
@@ -1585,7 +1590,6 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // through an opaque lane offset, so it is a VGPR nothing waits for before the exchange (a
   // uniform load is an SGPR the block's first address math waits for: one more round trip in
   // front of its slab loads)
-  constexpr bool EXCH = XW > 0;
   constexpr int XR = EXCH ? XW : 2;
   typedef const __attribute__((address_space(1))) int64_t* gcptr64;
   const uint32_t xt = EXCH ? (uint32_t)(((gcptr64)px.counters)[blk + opaque(0)] + 1) : 0u;
@@ -1596,14 +1600,16 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // polls once and never waits -- a dead peer costs one timeout, not one per step
   bool timed_out = EXCH && __hip_atomic_load(px.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 #define USTAMP(k) \
-  if (a.dbg && tid == 0) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+  if (a.dbg && tid == 0 && blk < a.dbg_blocks) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
 
   // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (the exchange's fixed map).
   // Tiles per block and waves per tile are powers of two: shifts, not run-time divisions (a
   // division by a run-time value is a long emulated sequence on every wave's scalar issue)
+  // fc_sl > 1: split-K fc gradients (lenet_fc_finish completes them), one tile per workgroup,
+  // fc_sl batch slices of every tile: workgroup slice * 88 + b (b % 8, its XCD, as unsplit)
   const int tpb_ = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
-  const int nb_fc = (FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_);
+  const int nb_fc = ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl;
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
@@ -1708,7 +1714,10 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // one tile per workgroup: XCD-grouped tiles.  Workgroup b runs on XCD b % 8; the tiles
     // in (fc1 column-block, row-block) order are dealt out 11 per XCD, so an XCD's tiles share
     // their column blocks (B operand rows of the vector slab) and its L2 fetches each line once
-    const int tile_w = tpb == 1 ? fc_tile_of_block(blk) : blk * tpb + (wave >> lw), sub = wave & (wpt - 1);
+    const int fslice = blk / FC_TILES;  // (0 unless split: tpb == 1, blk < 88 fc_sl)
+    const int tile_w = tpb == 1 ? fc_tile_of_block(blk - fslice * FC_TILES) : blk * tpb + (wave >> lw);
+    const int sub = wave & (wpt - 1);
+    const bool fin = fc_sl == 1;  // this block finishes its tile (else: a partial for lenet_fc_finish)
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
     const int tile = min(tile_w, FC_TILES - 1);   // they compute a valid tile, store nothing
     const bool fc1 = tile < FC1_TILES;
@@ -1732,12 +1741,12 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
                     ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
                            : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
                     : -1;
-      if (a.apply_sgd && sub == 0 && !vec) {
+      if (a.apply_sgd && sub == 0 && fin && !vec) {
         pp[r] = a.params[max(pidx[r], 0)];
         pm[r] = a.momentum[max(pidx[r], 0)];
       }
     }
-    if (a.apply_sgd && sub == 0 && vec) {
+    if (a.apply_sgd && sub == 0 && fin && vec) {
       const float4 p4 = *reinterpret_cast<const float4*>(a.params + vidx);
       const float4 m4 = *reinterpret_cast<const float4*>(a.momentum + vidx);
       pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
@@ -1754,8 +1763,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // this wave's samples [k0, k1): a multiple-of-4 (16-bit layout: of-32) share of the batch
     constexpr bool FC16 = !std::is_same<T, float>::value;
     constexpr int KG = FC16 ? 32 : 4;
-    const int kw = (((B + wpt - 1) >> lw) + KG - 1) & ~(KG - 1);
-    const int k0 = min(B, sub * kw), k1 = min(B, k0 + kw);
+    // (split: the block's slice [kb0, kb1) of the batch, a multiple-of-32 share, then the waves'
+    const int ks_len = fin ? B : ((((B + fc_sl - 1) >> __builtin_ctz(fc_sl)) + 31) & ~31);
+    const int kb0 = min(B, fslice * ks_len), kb1 = min(B, kb0 + ks_len);
+    const int kw = (((kb1 - kb0 + wpt - 1) >> lw) + KG - 1) & ~(KG - 1);
+    const int k0 = min(kb1, kb0 + sub * kw), k1 = min(kb1, k0 + kw);
     f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (FC16) {
       // 16-bit vectors in sample quads (kernels/lenet_layout.h): K-step s = samples s .. s+31
@@ -1925,8 +1937,15 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       for (int r = 0; r < 4; ++r) {
         float v = c[r];
         for (int w = 1; w < wpt; ++w) v += pfc[(wave + w) * 256 + r * 64 + lane];
-        g[r] = v * a.grad_post;
+        g[r] = fin ? v * a.grad_post : v;
       }
+      if (!fin) {
+        // split-K: this slice's partial tile in the MFMA layout (lenet_fc_finish sums the slices)
+        if (live_tile) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a.fc_part[((int64_t)fslice * FC_TILES + tile) * 256 + r * 64 + lane] = g[r];
+        }
+      } else {
       if (EXCH) {
         // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + 2 lane + {0, 1}
         // and + 128 + {0, 1} (two 16-byte pairs)
@@ -1950,6 +1969,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         for (int r = 0; r < 4; ++r)
           if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
       }
+      }  // fin
       USTAMP(4);
     }
   }
@@ -1962,18 +1982,21 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   if (a.apply_sgd) {
     // Device counters.  cursor / rng_offset are never read by this kernel, so
     // one thread bumps them directly.  step[0] is read by every block only when
-    // dampening != 0; then the last block to take a ticket bumps it.
-    if (a.dampening != 0.f) {
-      __syncthreads();
-      if (tid == 0) {
-        const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
-        if (t == nblk - 1) {
-          a.ticket[0] = 0;
-          if (a.step) a.step[0] += 1;
+    // dampening != 0; then the last block to take a ticket bumps it.  (Split-K: lenet_fc_finish
+    // reads step[0] after this kernel and bumps it itself.)
+    if (fc_sl == 1) {
+      if (a.dampening != 0.f) {
+        __syncthreads();
+        if (tid == 0) {
+          const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
+          if (t == nblk - 1) {
+            a.ticket[0] = 0;
+            if (a.step) a.step[0] += 1;
+          }
         }
+      } else if (blk == 0 && tid == 0 && a.step) {
+        a.step[0] += 1;
       }
-    } else if (blk == 0 && tid == 0 && a.step) {
-      a.step[0] += 1;
     }
     if (blk == 0 && tid == 0) {
       if (a.cursor) a.cursor[0] += 1;
@@ -1985,18 +2008,101 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
 // lenet_update_kernel's arguments as laid out in its argument segment (then px)
 struct UpdateKargs {
   LenetUpdateArgs a; const float* vslab; int B; float* loss_parts; int nparts; float* loss_acc;
-  uint64_t timeout_ticks; int fc_tpb;
+  uint64_t timeout_ticks; int fc_tpb; int fc_sl;
 };
 template <typename T, int XW>
 __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
                                                              int B, float* loss_parts, int nparts,
                                                              float* loss_acc, uint64_t timeout_ticks, int fc_tpb,
-                                                             comm::IpcPeers px) {
+                                                             int fc_sl, comm::IpcPeers px) {
   prefetch_kernargs<sizeof(UpdateKargs) + sizeof(comm::IpcPeers)>();  // (+ gridDim.x after px)
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
   update_role<T, XW>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
-                       threadIdx.x, &part[0][0], &part2[0][0], fc_tpb);
+                       threadIdx.x, &part[0][0], &part2[0][0], fc_tpb, fc_sl);
+}
+
+// Split-K fc gradients, second launch: tile blockIdx.x (64 lanes, the FC role's MFMA layout:
+// lane (l16, kq) holds rows 4 kq + r, column l16) = the sum of its S slice partials in slice
+// order (fixed: bitwise reproducible), then the FC role's finish: export or SGD + weight images.
+// Bumps step[0] (the update launch before it left it alone).
+template <typename T>
+__global__ void __launch_bounds__(64) lenet_fc_finish_kernel(LenetUpdateArgs a, int S) {
+  __shared__ float tr[256];
+  const int tile = blockIdx.x, lane = threadIdx.x, l16 = lane & 15, kq = lane >> 4;
+  const bool fc1 = tile < FC1_TILES;
+  const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
+  const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
+  const int i = nt * 16 + l16;
+  // every load first (clamped slices, masked in the sum): one round trip
+  float pv[8][4];
+#pragma unroll
+  for (int sl = 0; sl < 8; ++sl)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pv[sl][r] = a.fc_part[((int64_t)min(sl, S - 1) * FC_TILES + tile) * 256 + r * 64 + lane];
+  const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
+  const bool vec = fc1 && nt < 20;
+  const int vrow = mt * 16 + (lane >> 2), vcol = nt * 16 + 4 * (lane & 3);
+  const int vidx = O_F1W + min(vrow, 49) * 320 + vcol;
+  int pidx[4], fd[4];
+  float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int oo = mt * 16 + 4 * kq + r;
+    pidx[r] = (oo < rows && i <= cols) ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
+                                              : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
+                                       : -1;
+    if (a.apply_sgd && !vec) {
+      pp[r] = a.params[max(pidx[r], 0)];
+      pm[r] = a.momentum[max(pidx[r], 0)];
+    }
+    int d1;
+    image_slots(max(pidx[r], 0), fd[r], d1);
+    if (pidx[r] < 0) fd[r] = -1;
+  }
+  if (a.apply_sgd && vec) {
+    const float4 p4 = *reinterpret_cast<const float4*>(a.params + vidx);
+    const float4 m4 = *reinterpret_cast<const float4*>(a.momentum + vidx);
+    pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
+    pm[0] = m4.x; pm[1] = m4.y; pm[2] = m4.z; pm[3] = m4.w;
+  }
+  float g[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = pv[0][r];
+#pragma unroll
+    for (int sl = 1; sl < 8; ++sl)
+      if (sl < S) v += pv[sl][r];
+    g[r] = v * a.grad_post;
+  }
+  if (vec) {
+    // MFMA layout -> row layout (lane = row, 4 columns) through LDS, as the FC role
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tr[(4 * kq + r) * 16 + l16] = g[r];
+    __builtin_amdgcn_wave_barrier();
+    const float4 gv = *reinterpret_cast<const float4*>(tr + (lane >> 2) * 16 + 4 * (lane & 3));
+    if (vrow < 50)
+      finish_param4<T>(a, vidx, gv, first, make_float4(pp[0], pp[1], pp[2], pp[3]),
+                       make_float4(pm[0], pm[1], pm[2], pm[3]), I_F1 + vrow * LD_F1 + vcol);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
+  }
+  if (a.apply_sgd) {
+    if (a.dampening != 0.f) {
+      __syncthreads();
+      if (lane == 0) {
+        const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
+        if (t == (int)gridDim.x - 1) {
+          a.ticket[0] = 0;
+          if (a.step) a.step[0] += 1;
+        }
+      }
+    } else if (tile == 0 && lane == 0 && a.step) {
+      a.step[0] += 1;
+    }
+  }
 }
 
 // SGD from an already-reduced gradient (DDP: after the all-reduce).
@@ -2072,6 +2178,26 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Batch slices of the split-K fc gradients for a launch (1: unsplit).  Large batches only (the
+// FC role's K loop then streams B x 32 features per tile on 88 CUs), no exchange, no grad_in,
+// scratch room for S partials.  Auto: S = B / 1024 rounded down to a power of two, at most 8;
+// CSED_FC_SLICES = 1 / 2 / 4 / 8 forces it (A/B measurements).
+static int fc_split_slices(const LenetUpdateArgs& a) {
+  if (!a.fc_part || a.exch_id >= 0 || a.grad_in || a.B <= 512) return 1;
+  static const int forced = [] {
+    const char* e = std::getenv("CSED_FC_SLICES");
+    return e ? std::atoi(e) : 0;
+  }();
+  int S = 1;
+  if (forced > 0) {
+    while (S * 2 <= std::min(forced, 8)) S *= 2;
+  } else {
+    while (S * 2 <= 8 && S * 2 * 1024 <= a.B) S *= 2;
+  }
+  while (S > 1 && a.fc_part_n < (int64_t)S * FC_TILES * 256) S /= 2;
+  return S;
+}
+
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
                                hipStream_t s, const comm::IpcPeers* px_cached) {
   if (a.apply_sgd && a.grad_in) {
@@ -2100,20 +2226,29 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       if (px.world <= 2)
         hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 2>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                           a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
+                           a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
       else if (px.world <= 4)
         hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 4>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                           a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
+                           a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
       else
         hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 8>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                           a.B, loss_parts, nparts, loss_acc, ticks, 1, px);
+                           a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
+    });
+    return hipGetLastError();
+  }
+  const int S = fc_split_slices(a);
+  if (S > 1) {  // split-K fc gradients: one tile per workgroup x S slices, then the finish
+    CSED_DISPATCH_UPDATE(a.mfma_dtype, {
+      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 0>), dim3(FC_TILES * S + NB_CONV), dim3(UP_NT), 0, s, a,
+                         a.vslab, a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 1, S, px);
+      hipLaunchKernelGGL(lenet_fc_finish_kernel<scalar_t>, dim3(FC_TILES), dim3(64), 0, s, a, S);
     });
     return hipGetLastError();
   }
   const int nblocks = update_blocks(a.B);
   CSED_DISPATCH_UPDATE(a.mfma_dtype, {
     hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 0>), dim3(nblocks), dim3(UP_NT), 0, s, a, a.vslab,
-                       a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 0, px);
+                       a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 0, 1, px);
   });
   return hipGetLastError();
 }

@@ -165,3 +165,46 @@ def test_tile_epoch_tail_on_the_tile_kernel():
         finals.append(eng.flat.data.cpu().clone())
     assert torch.isfinite(finals[0]).all()
     assert _rel(finals[0], finals[1]) < 3e-2
+
+
+# split-K fc gradients (lenet_fused.hip fc_split_slices, lenet_fc_finish_kernel): per-rank batches
+# > 1024 form each fc tile as up to 8 batch slices on all CUs plus a finishing launch; against the
+# single-launch FC role only the summation order of the fc sums differs (the conv role is the same)
+@pytest.mark.parametrize("B,dt", [(4096, torch.float16), (2048, torch.bfloat16), (2048, torch.float32)])
+def test_split_k_fc_gradient_matches_unsplit(B, dt):
+    data = synthetic_mnist(B, seed=5)
+    torch.manual_seed(3)
+    eng = FusedLeNetTrainer(Net().to(DEV), data, global_batch=B, compute_dtype=dt, drop_p=0.0)
+    assert eng.fc_part is not None
+    order = torch.randperm(B, generator=torch.Generator().manual_seed(1))
+    eng.set_epoch_order(order)
+    g_split = eng.gradient().cpu()
+    part, eng.fc_part = eng.fc_part, None
+    g_one = eng.gradient().cpu()
+    eng.fc_part = part
+    conv = 5280  # flat offset of fc1.weight (lenet_layout.h O_F1W)
+    assert torch.equal(g_split[:conv], g_one[:conv])
+    assert _rel(g_split[conv:], g_one[conv:]) < 1e-6
+    assert torch.isfinite(g_split).all()
+
+
+def test_split_k_sgd_steps_and_step_counter():
+    """Two SGD steps with dampening (step[0] decides the first-step momentum rule, so the finishing
+    launch must bump it exactly once per step) through the split-K update vs the single launch."""
+    B = 2048
+    data = synthetic_mnist(2 * B, seed=6)
+    out = []
+    for split in (True, False):
+        torch.manual_seed(4)
+        eng = FusedLeNetTrainer(Net().to(DEV), data, lr=0.05, momentum=0.9, dampening=0.3, global_batch=B,
+                                compute_dtype=torch.float16, drop_p=0.0)
+        if not split:
+            eng.fc_part = None
+        eng.set_epoch_order(torch.arange(2 * B))
+        for _ in range(2):
+            eng.step()
+        torch.cuda.synchronize()
+        out.append((eng.flat.data.cpu().clone(), eng.momentum_buf.cpu().clone(), int(eng.step_count.item())))
+    (p1, m1, s1), (p2, m2, s2) = out
+    assert s1 == s2 == 2
+    assert _rel(p1, p2) < 1e-5 and _rel(m1, m2) < 1e-3

@@ -9,7 +9,11 @@ Per step (medians over the graph's steps, us): train = first train workgroup ent
 train workgroup exit; gap_tu = last train exit -> first update block entry; upd_s3 / upd_s4 =
 first update entry -> last block's gradient final (s3) / exchanged + SGD done (s4); gap_ut =
 last update s4 -> next step's first train entry.  The update kernel's own end (its stores
-drained, the dispatch retired) falls inside gap_ut."""
+drained, the dispatch retired) falls inside gap_ut.
+
+At per-rank batches that take the sample-tile kernel (csrc/kernels/lenet_tile.hip, B >=
+tile_min_batch()) "train" is lenet_tile's span (its realtime stamps 12 / 13) and the update grid
+is fc_blocks(B) + 84 blocks (the FC blocks first): e.g. --batch 1024 8192 --worlds 1."""
 import argparse
 import os
 import statistics
@@ -20,7 +24,8 @@ import torch  # noqa: E402
 
 from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist  # noqa: E402
 from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNIST_MEAN, MNIST_STD  # noqa: E402
-from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer  # noqa: E402
+from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import (  # noqa: E402
+    FusedLeNetTrainer, tile_grid, tile_min_batch)
 from csed_514_project_distributed_training_using_pytorch_amd.models import Net  # noqa: E402
 
 
@@ -40,7 +45,7 @@ def stamped_graph(eng, nsteps, dt, du):
                         eng.xstage if st else None, eng.lstage if st else None, st, kern)
         ops.lenet_update(eng.slab, grid, eng.vslab, B, None, None, *common, eng.cursor, eng.rng_offset, True,
                          eng.loss_parts, grid, eng.loss_acc, eng.mfma, du[i], xid, eng.exch_timeout_s,
-                         eng._post_scale(eng.grad_scale))
+                         eng._post_scale(eng.grad_scale), eng.fc_part)
 
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
@@ -76,7 +81,7 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     args = ap.parse_args()
     dev = torch.device("cuda")
-    data = synthetic_mnist(8192, seed=1)
+    data = synthetic_mnist(max(8192, 4 * max(args.batch)), seed=1)
     print("| B | N | step us (graph) | train | gap train->upd | upd s3 | upd s4 | FC s4 | CONV s4 | "
           "gap upd s4->next train | sum |")
     print("|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
@@ -91,7 +96,21 @@ def main():
             t_step = graph_step_us(eng, args.steps)
             n = args.steps
             dt = torch.zeros(n, eng.grid * 32, dtype=torch.long, device=dev)
-            du = torch.zeros(n, 8 * 256, dtype=torch.long, device=dev)
+            du = torch.zeros(n, 8 * 1024, dtype=torch.long, device=dev)
+            kern = eng.kernel_for(B, eng.grid)
+            tile = B >= tile_min_batch() and kern != 1 and eng.grid == tile_grid(B)
+            i_in, i_out = (12, 13) if tile else (22, 23)
+            # fc_blocks(B) (lenet_fused.hip): 88 FC tiles, 8 / waves-per-tile of them per block
+            wpt = 1 if B <= 128 else 2 if B <= 256 else 4 if B <= 512 else 8
+            nfc = 88 if (N > 1 or wpt == 1) else 88 // (8 // wpt)
+            # split-K fc gradients (B > 1024, no exchange): 88 x S FC blocks, S = B / 1024 as a
+            # power of two <= 8 (lenet_fused.hip fc_split_slices; CSED_FC_SLICES forces it)
+            if N == 1 and B > 1024 and eng.fc_part is not None:
+                forced = int(os.environ.get("CSED_FC_SLICES", "0") or 0)
+                S = 1
+                while S * 2 <= 8 and (S * 2 <= forced if forced > 0 else S * 2 * 1024 <= B):
+                    S *= 2
+                nfc = 88 * S
             g = stamped_graph(eng, n, dt, du)
             for _ in range(3):
                 dt.zero_()
@@ -99,18 +118,18 @@ def main():
                 g.replay()
                 torch.cuda.synchronize()
             T = dt.view(n, eng.grid, 32).double().cpu()
-            U = du.view(n, 256, 8).double().cpu()
+            U = du.view(n, 1024, 8).double().cpu()
             rows = []
             for i in range(n - 1):
-                t0, t1 = T[i, :, 22].min().item(), T[i, :, 23].max().item()
+                t0, t1 = T[i, :, i_in].min().item(), T[i, :, i_out].max().item()
                 u = U[i]
                 u0 = u[:, 0][u[:, 0] > 0].min().item()
                 s3 = u[:, 3].max().item()
                 s4 = u[:, 4][u[:, 4] > 0].max().item()
-                # blocks 0..87: the FC role (one tile each), 88..171: the CONV role
-                fc4 = u[:88, 4][u[:88, 4] > 0].max().item()
-                cv4 = u[88:172, 4][u[88:172, 4] > 0].max().item()
-                nt0 = T[i + 1, :, 22].min().item()
+                # blocks [0, nfc): the FC role, then the 84 CONV blocks
+                fc4 = u[:nfc, 4][u[:nfc, 4] > 0].max().item()
+                cv4 = u[nfc:nfc + 84, 4][u[nfc:nfc + 84, 4] > 0].max().item()
+                nt0 = T[i + 1, :, i_in].min().item()
                 rows.append(((t1 - t0) * 0.01, (u0 - t1) * 0.01, (s3 - u0) * 0.01, (s4 - u0) * 0.01,
                              (fc4 - u0) * 0.01, (cv4 - u0) * 0.01, (nt0 - s4) * 0.01, (nt0 - t0) * 0.01))
             med = [statistics.median(c) for c in zip(*rows)]

@@ -13,6 +13,8 @@
 #   stages    in-kernel stage stamps (train B=64 / 8, tile B=1024, fp32 B=64) + update stamps
 #   exchange  loopback exchange table (tools/exchange_loopback.py) + step breakdown
 #             (tools/exchange_trace.py) + the exchange / fault-injection / comm tests
+#   tiletrace per-step breakdown (tools/exchange_trace.py) of the large-batch step: lenet_tile span,
+#             gaps, lenet_update FC / CONV roles at B = 1024 and 8192
 #   pmc       three rocprofv3 --pmc passes over the train kernel (B=64), one over B=8,
 #             and three over the tile kernel (B=1024)
 #   ab        same-box A/B of ab/A_C.so vs ab/B_C.so (tools/ab_build.sh REV) at global batch
@@ -72,6 +74,10 @@ task_exchange() {
   cd $R && py 300 python -u tools/exchange_loopback.py 8 16 32 64 > $O/${T}_loopback.log 2>&1 && \
   py 300 python -u tools/exchange_trace.py --batch 8 16 32 64 --worlds 1 2 4 8 > $O/${T}_xtrace.log 2>&1 && \
   py 600 python -u -m pytest tests/test_exchange_loopback_gpu.py tests/test_fault_injection_gpu.py tests/test_comm_gpu.py -v --timeout 240 --timeout-method thread > $O/${T}_xtests.log 2>&1
+}
+
+task_tiletrace() {
+  cd $R && py 300 python -u tools/exchange_trace.py --batch 1024 8192 --worlds 1 --steps 16 > $O/${T}_tiletrace.log 2>&1
 }
 
 pmc3() {  # pmc3 <tag> <kernel_counters.py args>
