@@ -52,6 +52,10 @@ def test_scaling_report_prediction_from_loopback_log(tmp_path):
     assert rows[3]["vs_pred"] is None  # no N = 8 record yet: prediction only
     md = sr.markdown(rows, "t")
     assert "predicted epoch s" in md
+    # the pushes' link time adds to every N > 1
+    pw = sr.predict(by_n, steps, hop_us=1.0, wire_us=1.5)
+    assert abs(pw[8]["step_us"] - 19.5) < 1e-9 and abs(pw[1]["step_us"] - 15.0) < 1e-9
+    assert abs(sr.WIRE_BYTES / (153.0 * 1e3) - 1.142) < 1e-3
     # the built-in table covers every N of the strong-scaling curve
     assert all(n in sr.predict({}, sr.LOOPBACK_STEP_US, 1.0) for n in (1, 2, 4, 8))
 

@@ -22,11 +22,14 @@ Prediction (``--predict``, on by default).  At global batch 64 each of N ranks r
 per-rank batch 64/N whose exchange pushes to N-1 peers.  Both parts were measured on one GPU
 with the exchange looped back to N virtual ranks (``tools/exchange_loopback.py``,
 profiles/dp_exchange_r3.md section 2): ``LOOPBACK_STEP_US[(B, N)]`` is that graph-replayed
-step.  The predicted N-GPU step adds one xGMI one-way hop (``--hop-us``, 1 us assumed: the
-loopback push never leaves the device) and the predicted epoch keeps the N=1 record's
-non-step remainder (validation + tail):
+step.  The loopback push never leaves the device, so the predicted N-GPU step adds one xGMI
+one-way hop (``--hop-us``, 1 us assumed) and the time the pushes occupy one link: every rank
+sends each peer its whole live gradient as LL words (21,840 x 8 bytes = 175 KB, one link per
+peer, all links at once), ``wire = 175 KB / --link-gbs`` (153 GB/s per link assumed: 1.14 us;
+no overlap with the update's compute is credited, so this term is an upper bound).  The
+predicted epoch keeps the N=1 record's non-step remainder (validation + tail):
 
-    step_N  = LOOPBACK_STEP_US[(64 / N, N)] + hop          (N > 1; N = 1: no exchange, no hop)
+    step_N  = LOOPBACK_STEP_US[(64 / N, N)] + hop + wire   (N > 1; N = 1: no exchange)
     epoch_N = 938 * step_N + (epoch_s_1 - 938 * ms_per_step_1)
 
 A loopback log (``--loopback-log``, the ``B=.. N=.. ... step X us`` lines of
@@ -68,6 +71,7 @@ LOOPBACK_STEP_US = {
     (32, 1): 14.24, (32, 2): 16.57, (32, 4): 16.80, (32, 8): 17.26,
     (64, 1): 15.05, (64, 2): 17.19, (64, 4): 17.49, (64, 8): 17.98,
 }
+WIRE_BYTES = 21840 * 8  # live exchange words per peer per step (lenet_fused.hip ll_allreduce)
 _LB_LINE = re.compile(r"B=\s*(\d+)\s+N=(\d+).*?step\s+([0-9.]+)\s*us")
 
 
@@ -81,7 +85,8 @@ def load_loopback(path) -> dict[tuple[int, int], float]:
     return out
 
 
-def predict(by_n: dict[int, dict], steps_us: dict, hop_us: float, ns=(1, 2, 4, 8)) -> dict[int, dict]:
+def predict(by_n: dict[int, dict], steps_us: dict, hop_us: float, ns=(1, 2, 4, 8),
+            wire_us: float = 0.0) -> dict[int, dict]:
     """Predicted per-N step (us), images/s and warm epoch (s) at global batch 64."""
     r1 = by_n.get(1) or {}
     rest = None
@@ -92,7 +97,7 @@ def predict(by_n: dict[int, dict], steps_us: dict, hop_us: float, ns=(1, 2, 4, 8
         b = GLOBAL_BATCH // n
         if (b, n) not in steps_us:
             continue
-        step = steps_us[(b, n)] + (hop_us if n > 1 else 0.0)
+        step = steps_us[(b, n)] + (hop_us + wire_us if n > 1 else 0.0)
         out[n] = {"step_us": step, "images_s": GLOBAL_BATCH / (step * 1e-6),
                   "epoch_s": STEPS_PER_EPOCH * step * 1e-6 + rest if rest is not None else None}
     return out
@@ -200,7 +205,8 @@ def markdown(rows: list[dict], title: str) -> str:
     out += ["", "Reference: 1 / 2 / 4 / 8 GCP e2-standard-8 CPU VMs, gloo over TCP (BASELINE.md).  Scaling is "
             "strong (global batch 64 split over the GPUs, ref src/train_dist.py:133), so per-GPU work shrinks "
             "to 8 images per step at N = 8.  Predicted columns: the one-GPU loopback measurement of the "
-            "per-rank step (per-rank batch 64/N, exchange with N-1 virtual peers) + one xGMI hop; predicted "
+            "per-rank step (per-rank batch 64/N, exchange with N-1 virtual peers) + one xGMI hop + the "
+            "pushes' link time (175 KB per peer per step at the assumed link rate); predicted "
             "time_elapsed: N concurrent imports + rendezvous measured on the CPU, the N = 1 GPU bring-up, "
             "the exchange bring-up of a 2-rank rehearsal and epoch 0 at the predicted step; see the "
             "module docstring of tools/scaling_report.py."]
@@ -226,7 +232,7 @@ def plot(rows: list[dict], path: Path, title: str) -> bool:
         ax.plot(*zip(*pts), "^-", color="tab:blue", label="MI355X, warm epoch (938 steps + validation)")
     pts = [(r["n"], r["pred_epoch_s"]) for r in rows if r.get("pred_epoch_s")]
     if pts:
-        ax.plot(*zip(*pts), "^--", color="tab:cyan", label="MI355X, predicted warm epoch (loopback + hop)")
+        ax.plot(*zip(*pts), "^--", color="tab:cyan", label="MI355X, predicted warm epoch (loopback + hop + link)")
     ax.set_xscale("log", base=2)
     ax.set_yscale("log")
     ax.set_xticks(ns)
@@ -250,6 +256,8 @@ def main(argv=None) -> int:
     ap.add_argument("--title", default="Time to train 1 epoch vs number of GPUs (MNIST Net, global batch 64)")
     ap.add_argument("--no-predict", dest="predict", action="store_false")
     ap.add_argument("--hop-us", type=float, default=1.0, help="assumed xGMI one-way hop added for N > 1")
+    ap.add_argument("--link-gbs", type=float, default=153.0,
+                    help="assumed xGMI bandwidth per link and direction (GB/s) for the pushes' wire time")
     ap.add_argument("--loopback-log", help="exchange_loopback.py output replacing the built-in step table")
     ap.add_argument("--cpu-bringup", nargs="*", default=[],
                     help="bench.py --device cpu --gpus N JSON lines (spawn / import / rendezvous at N ranks)")
@@ -261,7 +269,9 @@ def main(argv=None) -> int:
         return 1
     pred = None
     if a.predict:
-        pred = predict(by_n, load_loopback(a.loopback_log) if a.loopback_log else LOOPBACK_STEP_US, a.hop_us)
+        wire_us = WIRE_BYTES / (a.link_gbs * 1e3) if a.link_gbs > 0 else 0.0
+        pred = predict(by_n, load_loopback(a.loopback_log) if a.loopback_log else LOOPBACK_STEP_US, a.hop_us,
+                       wire_us=wire_us)
         reh = load_records([a.rehearsal]).get(2) if a.rehearsal else None
         for n, t in predict_time_elapsed(by_n, pred, load_records(a.cpu_bringup) if a.cpu_bringup else {},
                                          reh).items():
