@@ -1509,7 +1509,7 @@ __device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t
 template <int K, int R>
 __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                              const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
-                                             bool& timed_out) {
+                                             bool& timed_out, uint64_t* stamp) {
   static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
   const int64_t so = slot_words(px, t) + w0;
   const int rank = px.rank, world = px.world;
@@ -1535,6 +1535,8 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
   //    the first wait: one memory round trip per pass)
   const int64_t cap = px.cap;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (stamp) stamp[5] = t0;  // (diagnostics: pushes issued)
+  uint32_t passes = 0;
   uint64_t w[R - 1][K];
   while (true) {
 #pragma unroll
@@ -1554,10 +1556,12 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
 #pragma unroll
       for (int k = 0; k < K; ++k)
         if (q < world - 1 && live[k]) ready = ready && (uint32_t)(w[q][k] >> 32) == t;
+    ++passes;
     if (ready || timed_out) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) timed_out = true;
     __builtin_amdgcn_s_sleep(1);
   }
+  if (stamp) stamp[6] = passes;  // (diagnostics: poll passes, 1 = the first one found every word)
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     float s = 0.f;
@@ -1679,7 +1683,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         // exchange word = the slab slot (contiguous over the lanes: one 512-byte run per wave
         // and peer; the parameter index is 250 apart between neighbouring conv2 slots)
         const bool live[1] = {true};
-        ll_allreduce<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out);
+        ll_allreduce<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
+                            a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
       }
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
@@ -1952,7 +1957,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         bool live[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) live[r] = pidx[r] >= 0;
-        ll_allreduce<4, XR>(px, xp, xt, CNP_PAD + tile * 256 + 2 * lane, live, g, timeout_ticks, timed_out);
+        ll_allreduce<4, XR>(px, xp, xt, CNP_PAD + tile * 256 + 2 * lane, live, g, timeout_ticks, timed_out,
+                            a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
       }
       if (vec) {
         // MFMA layout (row 4kq + r, column l16) -> row layout through this wave's LDS slot

@@ -83,8 +83,8 @@ def main():
     dev = torch.device("cuda")
     data = synthetic_mnist(max(8192, 4 * max(args.batch)), seed=1)
     print("| B | N | step us (graph) | train | gap train->upd | upd s3 | upd s4 | FC s4 | CONV s4 | "
-          "gap upd s4->next train | sum |")
-    print("|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+          "gap upd s4->next train | sum | FC push->done | FC passes | CONV push->done | CONV passes |")
+    print("|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for B in args.batch:
         for N in args.worlds:
             torch.manual_seed(1)
@@ -119,7 +119,7 @@ def main():
                 torch.cuda.synchronize()
             T = dt.view(n, eng.grid, 32).double().cpu()
             U = du.view(n, 1024, 8).double().cpu()
-            rows = []
+            rows, xrows = [], []
             for i in range(n - 1):
                 t0, t1 = T[i, :, i_in].min().item(), T[i, :, i_out].max().item()
                 u = U[i]
@@ -132,9 +132,21 @@ def main():
                 nt0 = T[i + 1, :, i_in].min().item()
                 rows.append(((t1 - t0) * 0.01, (u0 - t1) * 0.01, (s3 - u0) * 0.01, (s4 - u0) * 0.01,
                              (fc4 - u0) * 0.01, (cv4 - u0) * 0.01, (nt0 - s4) * 0.01, (nt0 - t0) * 0.01))
+                # exchange stamps (ll_allreduce): 5 = pushes issued, 6 = poll passes; per role, the
+                # median block's push -> exchange done and its mean pass count
+                x = []
+                for lo, hi in ((0, nfc), (nfc, nfc + 84)):
+                    r = u[lo:hi]
+                    ok = r[:, 5] > 0
+                    if ok.any():
+                        x += [statistics.median(((r[ok, 4] - r[ok, 5]) * 0.01).tolist()), r[ok, 6].mean().item()]
+                    else:
+                        x += [float("nan"), float("nan")]
+                xrows.append(x)
             med = [statistics.median(c) for c in zip(*rows)]
-            print(f"| {B} | {N} | {t_step:.2f} | " +
-                  " | ".join(f"{m:.2f}" for m in med) + " |", flush=True)
+            xmed = [statistics.median(c) for c in zip(*xrows)]
+            print(f"| {B} | {N} | {t_step:.2f} | " + " | ".join(f"{m:.2f}" for m in med) + " | " +
+                  " | ".join("-" if m != m else f"{m:.2f}" for m in xmed) + " |", flush=True)
             if os.environ.get("TRACE_DUMP"):
                 torch.save({"T": T, "U": U}, f"{os.environ['TRACE_DUMP']}_B{B}_N{N}.pt")
             print(f"  comm_errors {eng.comm_errors()}", flush=True)
