@@ -171,8 +171,9 @@ class FusedLeNetTrainer:
         self.fp32 = compute_dtype == torch.float32
         # split-K fc-gradient scratch (lenet_fused.hip fc_split_slices): per-rank batches > 1024
         # without the fused exchange form the fc weight gradients as up to 8 batch slices per
-        # tile on all CUs, then a finishing launch (88 tiles x 256 floats per slice)
-        self.fc_part = torch.empty(8 * 88 * 256, dtype=torch.float32, device=dev) if self.B > 1024 else None
+        # tile on all CUs, the tile's last slice finishing it (8 x 88 tiles x 256 partial sums,
+        # then 88 arrival counters that must start at zero)
+        self.fc_part = torch.zeros(8 * 88 * 256 + 128, dtype=torch.float32, device=dev) if self.B > 1024 else None
         # split step (lenet_fused.hip / lenet_fused_f32.hip KS > 1): split_k workgroups per sample
         # share the backward conv stages; used whenever the whole grid fits one wave of the GPU
         # (split_k * B <= 256 CUs).  CSED_SPLIT=0 keeps one workgroup per sample.  The exact-fp32

@@ -1324,6 +1324,9 @@ __host__ __device__ constexpr bool fc_tile_map_is_bijective() {
 }
 static_assert(FC_TILES % 8 == 0 && fc_tile_map_is_bijective(), "FC tile map");
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
+// split-K fc gradients (fc_split_slices): at most 8 slices of 88 tiles x 256 partial sums, then
+// 88 arrival counters (ints, zero between launches) in the same fp32 scratch
+constexpr int FC_PART_FLOATS = 8 * FC_TILES * 256;
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
@@ -1501,28 +1504,34 @@ __device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t
   return (int64_t)(t & 1u) * comm::kIpcMaxRanks * px.cap;
 }
 
-// v[k] (this rank's value of exchange word k of the lane, K = 1: w0; K = 4: w0 + {0, 1, 128,
-// 129}) := sum over ranks, in rank order (so every rank gets identical bits).  Every push / poll
-// instruction of a wave moves one contiguous run (512 bytes of 8-byte words, or 1 KB of pairs).  Only the world - 1 peer rows are
-// polled (row q holds peer q < rank ? q : q + 1; this rank's own row is never written).
-// live[k]: words whose tags must match (the others are pushed and summed but never waited for).
+// The exchange of a workgroup's values is split over its waves: each of waves 1 .. world - 1
+// pushes every value to ONE peer (ll_push), while wave 0 only polls (ll_poll).  A wave's vector
+// memory operations complete in issue order and its waits count stores too, so a wave that
+// pushed to N - 1 peers and then polled waited for all its write-through stores to be acked
+// before its first poll could count (1.9 us at N = 8 for the fc words, profiles/r4/
+// exchange_trace_r4d.txt); split, the polls wait for nothing but themselves.
+//
+// Words of a lane: K = 1: w0; K = 4: w0 + {0, 1} and w0 + 128 + {0, 1} (w0 = base + 2 lane: two
+// 16-byte pairs per lane, each wave instruction one contiguous 1-KB run).  Row q of this rank's
+// receive buffer holds peer q < rank ? q : q + 1 (its own row is never written).  live[k]: words
+// whose tags must match (the others are pushed and summed but never waited for).
+
+// push this lane's K values, tag t, to peer row q's peer (q < world - 1)
 template <int K, int R>
-__device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
-                                             const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
-                                             bool& timed_out, uint64_t* stamp) {
+__device__ __forceinline__ void ll_push(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
+                                        const bool (&live)[K], const float (&v)[K], int q) {
   static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
+  const int rank = px.rank, target = q < rank ? q : q + 1;
   const int64_t so = slot_words(px, t) + w0;
-  const int rank = px.rank, world = px.world;
-  // K = 4: the words are w0 + {0, 1} and w0 + 128 + {0, 1} (w0 = base + 2 lane): two 16-byte
-  // pairs per lane, each wave instruction one contiguous 1-KB run
   const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));  // (uniform: the pair bases)
   // a pair with no live word is never pushed (its lanes are off in the store's EXEC mask): the
   // fc tiles' padding rows / columns (a quarter of the fc words) never cross a link
   const bool live01 = K == 1 || live[0] || live[min(1, K - 1)], live23 = K == 4 && (live[min(2, K - 1)] || live[K - 1]);
-  // 1. push (write-through, system scope: see comm::push_word) to every peer
+  // write-through, system scope (see comm::push_word); the peer index unrolled (uniform
+  // branches) so that x.dst stays in scalar registers
 #pragma unroll
   for (int p = 0; p < R; ++p)
-    if (p < world && p != rank) {
+    if (p == target) {
       if constexpr (K == 1) {
         __hip_atomic_store(x.dst[p] + so, ll_word(v[0], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
@@ -1531,11 +1540,22 @@ __device__ __forceinline__ void ll_allreduce(const comm::IpcPeers& px, const XPt
         if (live23) sys_store16(b, 8 * (w0 + 128), u64x2v{ll_word(v[2], t), ll_word(v[3], t)});
       }
     }
-  // 2. poll this rank's receive buffer for every peer's words of tag t (all loads issued before
-  //    the first wait: one memory round trip per pass)
+}
+
+// v[k] := sum over ranks of word k, in rank order (so every rank gets identical bits): polls
+// this rank's receive buffer for every peer's words of tag t, all loads issued before the first
+// wait (one memory round trip per pass)
+template <int K, int R>
+__device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
+                                        const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
+                                        bool& timed_out, uint64_t* stamp) {
+  static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
+  const int64_t so = slot_words(px, t) + w0;
+  const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));
+  const int rank = px.rank, world = px.world;
   const int64_t cap = px.cap;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  if (stamp) stamp[5] = t0;  // (diagnostics: pushes issued)
+  if (stamp) stamp[5] = t0;  // (diagnostics: poll start)
   uint32_t passes = 0;
   uint64_t w[R - 1][K];
   while (true) {
@@ -1610,7 +1630,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (the exchange's fixed map).
   // Tiles per block and waves per tile are powers of two: shifts, not run-time divisions (a
   // division by a run-time value is a long emulated sequence on every wave's scalar issue)
-  // fc_sl > 1: split-K fc gradients (lenet_fc_finish completes them), one tile per workgroup,
+  // fc_sl > 1: split-K fc gradients (the last slice of a tile finishes it), one tile per workgroup,
   // fc_sl batch slices of every tile: workgroup slice * 88 + b (b % 8, its XCD, as unsplit)
   const int tpb_ = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
   const int nb_fc = ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl;
@@ -1677,15 +1697,23 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     }
     __syncthreads();
     USTAMP(3);
+    // exchange word = the slab slot (contiguous over the lanes: one 512-byte run per wave and
+    // peer; the parameter index is 250 apart between neighbouring conv2 slots).  Waves 1 ..
+    // world - 1 each push the 64 values to one peer, computed from the LDS sums exactly as wave
+    // 0 computes them (same operands, same order: the same bits); wave 0 polls
+    const bool live[1] = {true};
+    if (EXCH && ht >= 64 && ht < 64 * px.world && live_pb) {
+      const int l = ht & 63;
+      if (slot_param(pbc * (UP_C * 4) + l) >= 0) {
+        const float gl[1] = {((part2[0][l] + part2[1][l]) + (part2[2][l] + part2[3][l])) * a.grad_post};
+        ll_push<1, XR>(px, xp, xt, pbc * (UP_C * 4) + l, live, gl, (ht >> 6) - 1);
+      }
+    }
     if (ht < 64 && live_pb && pi >= 0) {
       float g[1] = {((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post};
-      if (EXCH) {
-        // exchange word = the slab slot (contiguous over the lanes: one 512-byte run per wave
-        // and peer; the parameter index is 250 apart between neighbouring conv2 slots)
-        const bool live[1] = {true};
-        ll_allreduce<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
-                            a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
-      }
+      if (EXCH)
+        ll_poll<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
+                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
     USTAMP(4);
@@ -1722,7 +1750,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     const int fslice = blk / FC_TILES;  // (0 unless split: tpb == 1, blk < 88 fc_sl)
     const int tile_w = tpb == 1 ? fc_tile_of_block(blk - fslice * FC_TILES) : blk * tpb + (wave >> lw);
     const int sub = wave & (wpt - 1);
-    const bool fin = fc_sl == 1;  // this block finishes its tile (else: a partial for lenet_fc_finish)
+    const bool fin = fc_sl == 1;  // this block finishes its tile (else: the tile's last slice does)
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
     const int tile = min(tile_w, FC_TILES - 1);   // they compute a valid tile, store nothing
     const bool fc1 = tile < FC1_TILES;
@@ -1936,30 +1964,93 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       __syncthreads();
     }
     USTAMP(3);
-    if (sub == 0 && live_wave) {  // (idle waves: no exchange polls, no stores)
-      float g[4];
+    const bool own = sub == 0 && live_wave;  // the wave that finishes the tile (idle waves: no stores)
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    if (own) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = c[r];
         for (int w = 1; w < wpt; ++w) v += pfc[(wave + w) * 256 + r * 64 + lane];
         g[r] = fin ? v * a.grad_post : v;
       }
-      if (!fin) {
-        // split-K: this slice's partial tile in the MFMA layout (lenet_fc_finish sums the slices)
-        if (live_tile) {
+    }
+    if constexpr (EXCH) {
+      // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + 2 lane + {0, 1}
+      // and + 128 + {0, 1} (two 16-byte pairs).  One tile per workgroup here, owned by wave 0:
+      // it publishes the values in LDS (part2_, unused by this role), waves 1 .. world - 1 push
+      // them to one peer each, and wave 0 polls
+      float* xg = part2_;
+      if (own) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) a.fc_part[((int64_t)fslice * FC_TILES + tile) * 256 + r * 64 + lane] = g[r];
-        }
-      } else {
-      if (EXCH) {
-        // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + 2 lane + {0, 1}
-        // and + 128 + {0, 1} (two 16-byte pairs)
-        bool live[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) live[r] = pidx[r] >= 0;
-        ll_allreduce<4, XR>(px, xp, xt, CNP_PAD + tile * 256 + 2 * lane, live, g, timeout_ticks, timed_out,
-                            a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+        for (int r = 0; r < 4; ++r) xg[r * 64 + lane] = g[r];
       }
+      __syncthreads();
+      bool live[4];  // (from the tile alone: every wave's view of the owner's pidx >= 0)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) live[r] = mt * 16 + 4 * kq + r < rows && i <= cols;
+      const int w0 = CNP_PAD + tile * 256 + 2 * lane;
+      if (wave >= 1 && wave < px.world) {
+        float gv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gv[r] = xg[r * 64 + lane];
+        ll_push<4, XR>(px, xp, xt, w0, live, gv, wave - 1);
+      }
+      if (own)
+        ll_poll<4, XR>(px, xp, xt, w0, live, g, timeout_ticks, timed_out,
+                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+    }
+    if (own) {
+      bool do_fin = fin;
+      if (!fin) {
+        // split-K: this slice's partial tile (MFMA layout) written through (sc1 stores: the tile's
+        // other slices run on other XCDs), then one counter add per tile: the workgroup whose add
+        // comes last (told by the value it returned; only this wave stored, after its vmcnt(0))
+        // reads every slice with sc1 loads, sums them in slice order (fixed: reproducible) and
+        // finishes the tile.  (MI355X_MICROARCH.md hand-off table, first row.)
+        float* pt = a.fc_part + (int64_t)tile * 256 + lane;  // slice sl at + sl * FC_TILES * 256
+        int* cnt = reinterpret_cast<int*>(a.fc_part + FC_PART_FLOATS) + tile;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __hip_atomic_store(pt + (int64_t)fslice * FC_TILES * 256 + r * 64, g[r], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        do_fin = __builtin_amdgcn_readfirstlane(old) == fc_sl - 1;
+        if (do_fin) {
+          float pv[8][4];
+#pragma unroll
+          for (int sl = 0; sl < 8; ++sl)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              pv[sl][r] = __hip_atomic_load(pt + (int64_t)min(sl, fc_sl - 1) * FC_TILES * 256 + r * 64,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (a.apply_sgd) {  // this tile's p / m (not prefetched: only the last slice needs them)
+            if (vec) {
+              const float4 p4 = *reinterpret_cast<const float4*>(a.params + vidx);
+              const float4 m4 = *reinterpret_cast<const float4*>(a.momentum + vidx);
+              pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
+              pm[0] = m4.x; pm[1] = m4.y; pm[2] = m4.z; pm[3] = m4.w;
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                pp[r] = a.params[max(pidx[r], 0)];
+                pm[r] = a.momentum[max(pidx[r], 0)];
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = pv[0][r];
+#pragma unroll
+            for (int sl = 1; sl < 8; ++sl)
+              if (sl < fc_sl) v += pv[sl][r];
+            g[r] = v * a.grad_post;
+          }
+          if (lane == 0) *cnt = 0;  // (the next launch reads it after the kernel boundary)
+        }
+      }
+      if (do_fin) {
       if (vec) {
         // MFMA layout (row 4kq + r, column l16) -> row layout through this wave's LDS slot
         float* tr = pfc + wave * 256;
@@ -1975,7 +2066,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         for (int r = 0; r < 4; ++r)
           if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
       }
-      }  // fin
+      }  // do_fin
       USTAMP(4);
     }
   }
@@ -1988,21 +2079,18 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   if (a.apply_sgd) {
     // Device counters.  cursor / rng_offset are never read by this kernel, so
     // one thread bumps them directly.  step[0] is read by every block only when
-    // dampening != 0; then the last block to take a ticket bumps it.  (Split-K: lenet_fc_finish
-    // reads step[0] after this kernel and bumps it itself.)
-    if (fc_sl == 1) {
-      if (a.dampening != 0.f) {
-        __syncthreads();
-        if (tid == 0) {
-          const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
-          if (t == nblk - 1) {
-            a.ticket[0] = 0;
-            if (a.step) a.step[0] += 1;
-          }
+    // dampening != 0; then the last block to take a ticket bumps it.
+    if (a.dampening != 0.f) {
+      __syncthreads();
+      if (tid == 0) {
+        const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
+        if (t == nblk - 1) {
+          a.ticket[0] = 0;
+          if (a.step) a.step[0] += 1;
         }
-      } else if (blk == 0 && tid == 0 && a.step) {
-        a.step[0] += 1;
       }
+    } else if (blk == 0 && tid == 0 && a.step) {
+      a.step[0] += 1;
     }
     if (blk == 0 && tid == 0) {
       if (a.cursor) a.cursor[0] += 1;
@@ -2026,89 +2114,6 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   __shared__ float part2[4][UP_C * 4];
   update_role<T, XW>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
                        threadIdx.x, &part[0][0], &part2[0][0], fc_tpb, fc_sl);
-}
-
-// Split-K fc gradients, second launch: tile blockIdx.x (64 lanes, the FC role's MFMA layout:
-// lane (l16, kq) holds rows 4 kq + r, column l16) = the sum of its S slice partials in slice
-// order (fixed: bitwise reproducible), then the FC role's finish: export or SGD + weight images.
-// Bumps step[0] (the update launch before it left it alone).
-template <typename T>
-__global__ void __launch_bounds__(64) lenet_fc_finish_kernel(LenetUpdateArgs a, int S) {
-  __shared__ float tr[256];
-  const int tile = blockIdx.x, lane = threadIdx.x, l16 = lane & 15, kq = lane >> 4;
-  const bool fc1 = tile < FC1_TILES;
-  const int mt = fc1 ? tile / 21 : 0, nt = fc1 ? tile % 21 : tile - FC1_TILES;
-  const int rows = fc1 ? 50 : 10, cols = fc1 ? 320 : 50;
-  const int i = nt * 16 + l16;
-  // every load first (clamped slices, masked in the sum): one round trip
-  float pv[8][4];
-#pragma unroll
-  for (int sl = 0; sl < 8; ++sl)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) pv[sl][r] = a.fc_part[((int64_t)min(sl, S - 1) * FC_TILES + tile) * 256 + r * 64 + lane];
-  const bool first = (a.step && a.dampening != 0.f) ? a.step[0] == 0 : false;
-  const bool vec = fc1 && nt < 20;
-  const int vrow = mt * 16 + (lane >> 2), vcol = nt * 16 + 4 * (lane & 3);
-  const int vidx = O_F1W + min(vrow, 49) * 320 + vcol;
-  int pidx[4], fd[4];
-  float pp[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int oo = mt * 16 + 4 * kq + r;
-    pidx[r] = (oo < rows && i <= cols) ? (fc1 ? (i < cols ? O_F1W + oo * 320 + i : O_F1B + oo)
-                                              : (i < cols ? O_F2W + oo * 50 + i : O_F2B + oo))
-                                       : -1;
-    if (a.apply_sgd && !vec) {
-      pp[r] = a.params[max(pidx[r], 0)];
-      pm[r] = a.momentum[max(pidx[r], 0)];
-    }
-    int d1;
-    image_slots(max(pidx[r], 0), fd[r], d1);
-    if (pidx[r] < 0) fd[r] = -1;
-  }
-  if (a.apply_sgd && vec) {
-    const float4 p4 = *reinterpret_cast<const float4*>(a.params + vidx);
-    const float4 m4 = *reinterpret_cast<const float4*>(a.momentum + vidx);
-    pp[0] = p4.x; pp[1] = p4.y; pp[2] = p4.z; pp[3] = p4.w;
-    pm[0] = m4.x; pm[1] = m4.y; pm[2] = m4.z; pm[3] = m4.w;
-  }
-  float g[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float v = pv[0][r];
-#pragma unroll
-    for (int sl = 1; sl < 8; ++sl)
-      if (sl < S) v += pv[sl][r];
-    g[r] = v * a.grad_post;
-  }
-  if (vec) {
-    // MFMA layout -> row layout (lane = row, 4 columns) through LDS, as the FC role
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tr[(4 * kq + r) * 16 + l16] = g[r];
-    __builtin_amdgcn_wave_barrier();
-    const float4 gv = *reinterpret_cast<const float4*>(tr + (lane >> 2) * 16 + 4 * (lane & 3));
-    if (vrow < 50)
-      finish_param4<T>(a, vidx, gv, first, make_float4(pp[0], pp[1], pp[2], pp[3]),
-                       make_float4(pm[0], pm[1], pm[2], pm[3]), I_F1 + vrow * LD_F1 + vcol);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
-  }
-  if (a.apply_sgd) {
-    if (a.dampening != 0.f) {
-      __syncthreads();
-      if (lane == 0) {
-        const int t = atomicAdd(a.ticket, 1);  // every block read step[0] before this
-        if (t == (int)gridDim.x - 1) {
-          a.ticket[0] = 0;
-          if (a.step) a.step[0] += 1;
-        }
-      }
-    } else if (tile == 0 && lane == 0 && a.step) {
-      a.step[0] += 1;
-    }
-  }
 }
 
 // SGD from an already-reduced gradient (DDP: after the all-reduce).
@@ -2186,7 +2191,7 @@ hipError_t launch_lenet_train(const LenetTrainArgs& a, hipStream_t s) {
 
 // Batch slices of the split-K fc gradients for a launch (1: unsplit).  Large batches only (the
 // FC role's K loop then streams B x 32 features per tile on 88 CUs), no exchange, no grad_in,
-// scratch room for S partials.  Auto: S = B / 1024 rounded down to a power of two, at most 8;
+// scratch of FC_PART_FLOATS + FC_TILES (the partials, then the zeroed per-tile counters).  Auto: S = B / 1024 rounded down to a power of two, at most 8;
 // CSED_FC_SLICES = 1 / 2 / 4 / 8 forces it (A/B measurements).
 static int fc_split_slices(const LenetUpdateArgs& a) {
   if (!a.fc_part || a.exch_id >= 0 || a.grad_in || a.B <= 512) return 1;
@@ -2200,7 +2205,7 @@ static int fc_split_slices(const LenetUpdateArgs& a) {
   } else {
     while (S * 2 <= 8 && S * 2 * 1024 <= a.B) S *= 2;
   }
-  while (S > 1 && a.fc_part_n < (int64_t)S * FC_TILES * 256) S /= 2;
+  if (a.fc_part_n < FC_PART_FLOATS + FC_TILES) return 1;  // partials + the per-tile counters
   return S;
 }
 
@@ -2243,11 +2248,10 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     return hipGetLastError();
   }
   const int S = fc_split_slices(a);
-  if (S > 1) {  // split-K fc gradients: one tile per workgroup x S slices, then the finish
+  if (S > 1) {  // split-K fc gradients: one tile per workgroup x S slices (the last one finishes)
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 0>), dim3(FC_TILES * S + NB_CONV), dim3(UP_NT), 0, s, a,
                          a.vslab, a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 1, S, px);
-      hipLaunchKernelGGL(lenet_fc_finish_kernel<scalar_t>, dim3(FC_TILES), dim3(64), 0, s, a, S);
     });
     return hipGetLastError();
   }

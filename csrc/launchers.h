@@ -204,9 +204,9 @@ struct LenetUpdateArgs {
   int mfma_dtype;
   uint64_t* dbg;      // optional [blocks, 8] s_memrealtime stamps (diagnostics)
   int dbg_blocks;     // rows of dbg (blocks past it record nothing)
-  // Split-K fc gradients (large batches, no exchange): fp32 scratch of fc_part_n floats; with
-  // room for S x 88 tiles x 256 the FC role runs as S batch slices per tile, each storing a
-  // partial tile, and a second launch (lenet_fc_finish) sums the slices and applies SGD
+  // Split-K fc gradients (large batches, no exchange): fp32 scratch of fc_part_n floats (8 x 88
+  // tiles x 256 partial sums, then 88 zeroed arrival counters); the FC role then runs as S batch
+  // slices per tile, each storing a partial tile, and the tile's last slice sums and finishes it
   float* fc_part; int64_t fc_part_n;
   // Fused data-parallel gradient exchange (csrc/comm IPC buffer id, -1 = none):
   // the reduced gradient of this kernel is summed over all ranks in-kernel

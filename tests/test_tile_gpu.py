@@ -167,8 +167,8 @@ def test_tile_epoch_tail_on_the_tile_kernel():
     assert _rel(finals[0], finals[1]) < 3e-2
 
 
-# split-K fc gradients (lenet_fused.hip fc_split_slices, lenet_fc_finish_kernel): per-rank batches
-# > 1024 form each fc tile as up to 8 batch slices on all CUs plus a finishing launch; against the
+# split-K fc gradients (lenet_fused.hip fc_split_slices): per-rank batches > 1024 form each fc
+# tile as up to 8 batch slices on all CUs, the tile's last-arriving slice finishing it; against the
 # single-launch FC role only the summation order of the fc sums differs (the conv role is the same)
 @pytest.mark.parametrize("B,dt", [(4096, torch.float16), (2048, torch.bfloat16), (2048, torch.float32)])
 def test_split_k_fc_gradient_matches_unsplit(B, dt):
@@ -189,10 +189,11 @@ def test_split_k_fc_gradient_matches_unsplit(B, dt):
 
 
 def test_split_k_sgd_steps_and_step_counter():
-    """Two SGD steps with dampening (step[0] decides the first-step momentum rule, so the finishing
-    launch must bump it exactly once per step) through the split-K update vs the single launch."""
+    """Two SGD steps with dampening (step[0] decides the first-step momentum rule: bumped exactly
+    once per step) through the split-K update vs the unsplit one; a third step checks that the
+    per-tile arrival counters were reset."""
     B = 2048
-    data = synthetic_mnist(2 * B, seed=6)
+    data = synthetic_mnist(4 * B, seed=6)
     out = []
     for split in (True, False):
         torch.manual_seed(4)
@@ -200,11 +201,13 @@ def test_split_k_sgd_steps_and_step_counter():
                                 compute_dtype=torch.float16, drop_p=0.0)
         if not split:
             eng.fc_part = None
-        eng.set_epoch_order(torch.arange(2 * B))
-        for _ in range(2):
+        eng.set_epoch_order(torch.arange(4 * B))
+        for _ in range(3):
             eng.step()
         torch.cuda.synchronize()
         out.append((eng.flat.data.cpu().clone(), eng.momentum_buf.cpu().clone(), int(eng.step_count.item())))
+        if split:  # every tile's arrival counter back at zero
+            assert int(eng.fc_part[8 * 88 * 256:8 * 88 * 256 + 88].view(torch.int32).abs().sum().item()) == 0
     (p1, m1, s1), (p2, m2, s2) = out
-    assert s1 == s2 == 2
+    assert s1 == s2 == 3
     assert _rel(p1, p2) < 1e-5 and _rel(m1, m2) < 1e-3
