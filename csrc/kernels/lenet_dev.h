@@ -58,4 +58,17 @@ __device__ __forceinline__ void lds_wait8(uint32_t (&v)[8]) {
                : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
 }
 
+// 16-byte write-through store (sc1): the line leaves this XCD's L2 now instead of in the
+// kernel-end write-back, which the next kernel's start waits for (a dependent boundary costs
+// ~B / 6 TB/s more per B bytes its predecessor left dirty, MI355X_MICROARCH.md "boundary").
+// base: wave-uniform (a buffer resource; a per-lane base becomes a loop over the lanes'
+// descriptors), byte_off per lane.
+__device__ __forceinline__ void store16_wt(const void* base, int byte_off, float4 v) {
+  typedef unsigned int u32x4v_ __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_, v),
+                                         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                                                           0x7fffffff, 0x00020000),
+                                         byte_off, 0, 16);
+}
+
 }  // namespace csed

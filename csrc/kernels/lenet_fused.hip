@@ -1504,12 +1504,13 @@ __device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t
   return (int64_t)(t & 1u) * comm::kIpcMaxRanks * px.cap;
 }
 
-// The exchange of a workgroup's values is split over its waves: each of waves 1 .. world - 1
-// pushes every value to ONE peer (ll_push), while wave 0 only polls (ll_poll).  A wave's vector
+// The exchange of a workgroup's values is split over its waves: wave q < world - 1 pushes every
+// value to ONE peer (peer row q, ll_push), and wave 0 then polls (ll_poll).  A wave's vector
 // memory operations complete in issue order and its waits count stores too, so a wave that
-// pushed to N - 1 peers and then polled waited for all its write-through stores to be acked
-// before its first poll could count (1.9 us at N = 8 for the fc words, profiles/r4/
-// exchange_trace_r4d.txt); split, the polls wait for nothing but themselves.
+// pushed to all N - 1 peers and then polled waited for all those write-through stores to be
+// acked before its first poll could count (1.9 us at N = 8 for the fc words, profiles/r4/
+// exchange_trace_r4d.txt).  Wave 0 keeps one push in front of its poll: with none, the poll
+// races the other waves' pushes and a looped-back exchange needs a second pass (r4e: +0.6 us).
 //
 // Words of a lane: K = 1: w0; K = 4: w0 + {0, 1} and w0 + 128 + {0, 1} (w0 = base + 2 lane: two
 // 16-byte pairs per lane, each wave instruction one contiguous 1-KB run).  Row q of this rank's
@@ -1698,15 +1699,15 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     __syncthreads();
     USTAMP(3);
     // exchange word = the slab slot (contiguous over the lanes: one 512-byte run per wave and
-    // peer; the parameter index is 250 apart between neighbouring conv2 slots).  Waves 1 ..
-    // world - 1 each push the 64 values to one peer, computed from the LDS sums exactly as wave
-    // 0 computes them (same operands, same order: the same bits); wave 0 polls
+    // peer; the parameter index is 250 apart between neighbouring conv2 slots).  Wave q < world
+    // - 1 pushes the 64 values to peer row q, each computing them from the LDS sums exactly as
+    // wave 0 does (same operands, same order: the same bits); then wave 0 polls
     const bool live[1] = {true};
-    if (EXCH && ht >= 64 && ht < 64 * px.world && live_pb) {
+    if (EXCH && ht < 64 * (px.world - 1) && live_pb) {
       const int l = ht & 63;
       if (slot_param(pbc * (UP_C * 4) + l) >= 0) {
         const float gl[1] = {((part2[0][l] + part2[1][l]) + (part2[2][l] + part2[3][l])) * a.grad_post};
-        ll_push<1, XR>(px, xp, xt, pbc * (UP_C * 4) + l, live, gl, (ht >> 6) - 1);
+        ll_push<1, XR>(px, xp, xt, pbc * (UP_C * 4) + l, live, gl, ht >> 6);
       }
     }
     if (ht < 64 && live_pb && pi >= 0) {
@@ -1977,8 +1978,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     if constexpr (EXCH) {
       // exchange words of the lane's four tile entries: CNP_PAD + tile * 256 + 2 lane + {0, 1}
       // and + 128 + {0, 1} (two 16-byte pairs).  One tile per workgroup here, owned by wave 0:
-      // it publishes the values in LDS (part2_, unused by this role), waves 1 .. world - 1 push
-      // them to one peer each, and wave 0 polls
+      // it publishes the values in LDS (part2_, unused by this role), wave q < world - 1 pushes
+      // them to peer row q, and wave 0 then polls
       float* xg = part2_;
       if (own) {
 #pragma unroll
@@ -1989,11 +1990,11 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
 #pragma unroll
       for (int r = 0; r < 4; ++r) live[r] = mt * 16 + 4 * kq + r < rows && i <= cols;
       const int w0 = CNP_PAD + tile * 256 + 2 * lane;
-      if (wave >= 1 && wave < px.world) {
+      if (wave < px.world - 1) {
         float gv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gv[r] = xg[r * 64 + lane];
-        ll_push<4, XR>(px, xp, xt, w0, live, gv, wave - 1);
+        for (int r = 0; r < 4; ++r) gv[r] = own ? g[r] : xg[r * 64 + lane];
+        ll_push<4, XR>(px, xp, xt, w0, live, gv, wave);
       }
       if (own)
         ll_poll<4, XR>(px, xp, xt, w0, live, g, timeout_ticks, timed_out,

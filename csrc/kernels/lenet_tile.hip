@@ -813,8 +813,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         else if (kk == 25) *slab_at(O_C1B + oc) = v;
       }
     } else {
+      // (written through: 5 MB of slab rows over the grid, otherwise dirty in the L2s at the
+      // kernel's end)
       for (int i = tid - 512; i < 251 * 20 / 4; i += 512)
-        *reinterpret_cast<float4*>(a.slab + slab_off(S_C2 + 4 * i, g, G, G)) = reinterpret_cast<const float4*>(SLF)[i];
+        store16_wt(a.slab, 4 * slab_off(S_C2 + 4 * i, g, G, G), reinterpret_cast<const float4*>(SLF)[i]);
     }
   } else {
     __syncthreads();

@@ -10,5 +10,6 @@ timeout -k 10 600 python -u -m pytest tests/test_exchange_loopback_gpu.py tests/
 timeout -k 10 300 python -u tools/exchange_trace.py --batch 8 16 32 64 --worlds 1 2 4 8 > gpurun_out/${T}_trace.log 2>&1 && \
 timeout -k 10 200 python -u tools/exchange_trace.py --batch 1024 2048 8192 --worlds 1 --steps 12 > gpurun_out/${T}_tiletrace.log 2>&1 && \
 CSED_FC_SLICES=1 timeout -k 10 200 python -u tools/exchange_trace.py --batch 2048 8192 --worlds 1 --steps 12 > gpurun_out/${T}_tiletrace_s1.log 2>&1 && \
+CSED_FC_SLICES=2 timeout -k 10 200 python -u tools/exchange_trace.py --batch 1024 --worlds 1 --steps 12 > gpurun_out/${T}_tiletrace_s2.log 2>&1 && \
 timeout -k 10 300 python -u tools/exchange_loopback.py 8 16 32 64 > gpurun_out/${T}_loopback.log 2>&1
 echo rc=$?
