@@ -1505,14 +1505,14 @@ __device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t
 }
 
 // The exchange of a workgroup's values is split over its waves: wave q < world - 1 pushes every
-// value to ONE peer (peer row q's, ll_push), then polls that one row (ll_poll_row) into LDS, and
-// after a barrier the owning wave sums the rows in rank order (ll_rank_sum).  Measured on one
-// wave doing it all (profiles/r4/exchange_trace_r4d.txt): its vector memory operations complete
-// in issue order and its waits count stores too, so its first poll waited for all N - 1 peers'
-// write-through stores to be acked, and the N - 1 rows' uncached loads then returned at ~0.07 us
-// per 1-KB wave instruction -- 1.9 us at N = 8 for the fc words against 0.84 at N = 2.  Each wave
-// keeps its one push in front of its poll: with the polls on a wave of their own (no store
-// ahead), a looped-back poll raced the pushes and needed a second pass (r4e: +0.6 us).
+// value to ONE peer (peer row q, ll_push), and wave 0 then polls (ll_poll).  A wave's vector
+// memory operations complete in issue order and its waits count stores too, so a wave that
+// pushed to all N - 1 peers and then polled waited for all those write-through stores to be
+// acked before its first poll could count (1.9 us at N = 8 for the fc words, profiles/r4/
+// exchange_trace_r4d.txt).  Wave 0 keeps one push in front of its poll: with none, the poll
+// races the other waves' pushes and a looped-back exchange needs a second pass (r4e: +0.6 us).
+// Polling the peers' rows on their pushing waves too (one row each, into LDS, then a rank-order
+// sum) was slower again: 2.6 us for the fc words at N = 8 (r4g).
 //
 // Words of a lane: K = 1: w0; K = 4: w0 + {0, 1} and w0 + 128 + {0, 1} (w0 = base + 2 lane: two
 // 16-byte pairs per lane, each wave instruction one contiguous 1-KB run).  Row q of this rank's
@@ -1545,33 +1545,40 @@ __device__ __forceinline__ void ll_push(const comm::IpcPeers& px, const XPtrs<R>
     }
 }
 
-// Poll row q of this rank's receive buffer (peer q < rank ? q : q + 1) until its live words carry
-// tag t (all of a pass's loads issued before its wait: one memory round trip per pass); out[k]
-// = the peer's value of word k.
-template <int K>
-__device__ __forceinline__ void ll_poll_row(const comm::IpcPeers& px, const uint64_t* src, uint32_t t, int w0,
-                                            const bool (&live)[K], int q, float (&out)[K], uint64_t timeout_ticks,
-                                            bool& timed_out, uint64_t* stamp) {
+// v[k] := sum over ranks of word k, in rank order (so every rank gets identical bits): polls
+// this rank's receive buffer for every peer's words of tag t, all loads issued before the first
+// wait (one memory round trip per pass)
+template <int K, int R>
+__device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
+                                        const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
+                                        bool& timed_out, uint64_t* stamp) {
   static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
-  const int p = q < px.rank ? q : q + 1;
-  const int64_t row = (int64_t)p * px.cap;
-  const int64_t so = slot_words(px, t) + w0 + row;
-  const uint64_t* b = uniform_ptr(src + slot_words(px, __builtin_amdgcn_readfirstlane(t)) + row);
+  const int64_t so = slot_words(px, t) + w0;
+  const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));
+  const int rank = px.rank, world = px.world;
+  const int64_t cap = px.cap;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   if (stamp) stamp[5] = t0;  // (diagnostics: poll start)
   uint32_t passes = 0;
-  uint64_t w[K];
+  uint64_t w[R - 1][K];
   while (true) {
-    if constexpr (K == 1) {
-      w[0] = __hip_atomic_load(src + so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-      const u64x2v lo = sys_load16(b, 8 * w0), hi = sys_load16(b, 8 * (w0 + 128));
-      w[0] = lo.x; w[1] = lo.y; w[2] = hi.x; w[3] = hi.y;
+#pragma unroll
+    for (int q = 0; q < R - 1; ++q) {
+      const int p = min(q < rank ? q : q + 1, world - 1);  // (rows past the world: clamped, unused)
+      if constexpr (K == 1) {
+        w[q][0] = __hip_atomic_load(x.src + (int64_t)p * cap + so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        const uint64_t* b = uniform_ptr(x.src + sw + (int64_t)p * cap);
+        const u64x2v lo = sys_load16(b, 8 * w0), hi = sys_load16(b, 8 * (w0 + 128));
+        w[q][0] = lo.x; w[q][1] = lo.y; w[q][2] = hi.x; w[q][3] = hi.y;
+      }
     }
     bool ready = true;
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (live[k]) ready = ready && (uint32_t)(w[k] >> 32) == t;
+    for (int q = 0; q < R - 1; ++q)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (q < world - 1 && live[k]) ready = ready && (uint32_t)(w[q][k] >> 32) == t;
     ++passes;
     if (ready || timed_out) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) timed_out = true;
@@ -1579,18 +1586,18 @@ __device__ __forceinline__ void ll_poll_row(const comm::IpcPeers& px, const uint
   }
   if (stamp) stamp[6] = passes;  // (diagnostics: poll passes, 1 = the first one found every word)
 #pragma unroll
-  for (int k = 0; k < K; ++k) out[k] = __uint_as_float((uint32_t)w[k]);
-}
-
-// v := the sum over ranks in rank order (so every rank gets identical bits); peer row q's value
-// at in[q * stride] (q = p for peers p < rank, p - 1 above)
-template <int R>
-__device__ __forceinline__ float ll_rank_sum(const comm::IpcPeers& px, float v, const float* in, int stride) {
-  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
 #pragma unroll
-  for (int p = 0; p < R; ++p)
-    if (p < px.world) s += p == px.rank ? v : in[(p < px.rank ? p : p - 1) * stride];
-  return s;
+    for (int p = 0; p < R; ++p) {
+      if (p < world) {
+        // peer p's row: q = p (p < rank) or p - 1 (p > rank)
+        const uint64_t wp = p < rank ? w[min(p, R - 2)][k] : w[max(p - 1, 0)][k];
+        s += p == rank ? v[k] : __uint_as_float((uint32_t)wp);
+      }
+    }
+    v[k] = s;
+  }
 }
 
 // Update workgroup blk of nblk (UP_NT threads).  part: float4[UP_S][UP_C], part2:
@@ -1702,26 +1709,20 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // peer; the parameter index is 250 apart between neighbouring conv2 slots).  Wave q < world
     // - 1 pushes the 64 values to peer row q, each computing them from the LDS sums exactly as
     // wave 0 does (same operands, same order: the same bits); then wave 0 polls
-    // (and polls that row: the peers' rows in parallel, one per wave, into LDS; the slab
-    // partials' LDS is free after the barrier above)
-    float* xin = reinterpret_cast<float*>(part_);
-    if (EXCH) {
-      if (ht < 64 * (px.world - 1) && live_pb) {
-        const int l = ht & 63, q = ht >> 6;
-        const bool live[1] = {slot_param(pbc * (UP_C * 4) + l) >= 0};
+    const bool live[1] = {true};
+    if (EXCH && ht < 64 * (px.world - 1) && live_pb) {
+      const int l = ht & 63;
+      if (slot_param(pbc * (UP_C * 4) + l) >= 0) {
         const float gl[1] = {((part2[0][l] + part2[1][l]) + (part2[2][l] + part2[3][l])) * a.grad_post};
-        if (live[0]) ll_push<1, XR>(px, xp, xt, pbc * (UP_C * 4) + l, live, gl, q);
-        float in[1];
-        ll_poll_row<1>(px, xp.src, xt, pbc * (UP_C * 4) + l, live, q, in, timeout_ticks, timed_out,
-                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
-        xin[q * 64 + l] = in[0];
+        ll_push<1, XR>(px, xp, xt, pbc * (UP_C * 4) + l, live, gl, ht >> 6);
       }
-      __syncthreads();
     }
     if (ht < 64 && live_pb && pi >= 0) {
-      float g = ((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post;
-      if (EXCH) g = ll_rank_sum<XR>(px, g, xin + ht, 64);
-      finish_param<T>(a, pi, g, first, p0, m0, d0, d1);
+      float g[1] = {((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post};
+      if (EXCH)
+        ll_poll<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
+                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+      finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
     USTAMP(4);
     if (pb == 0 && loss_parts && tid < 64) {
@@ -1997,24 +1998,15 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
 #pragma unroll
       for (int r = 0; r < 4; ++r) live[r] = mt * 16 + 4 * kq + r < rows && i <= cols;
       const int w0 = CNP_PAD + tile * 256 + 2 * lane;
-      // (and polls that row, the peers' rows in parallel, one per wave, into LDS: rows 1 .. 7
-      // of pfc, row 0 stays free for the finish's transposition)
       if (wave < px.world - 1) {
         float gv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) gv[r] = own ? g[r] : xg[r * 64 + lane];
         ll_push<4, XR>(px, xp, xt, w0, live, gv, wave);
-        float in[4];
-        ll_poll_row<4>(px, xp.src, xt, w0, live, wave, in, timeout_ticks, timed_out,
+      }
+      if (own)
+        ll_poll<4, XR>(px, xp, xt, w0, live, g, timeout_ticks, timed_out,
                        a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pfc[256 * (wave + 1) + r * 64 + lane] = in[r];
-      }
-      __syncthreads();
-      if (own) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) g[r] = ll_rank_sum<XR>(px, g[r], pfc + 256 + r * 64 + lane, 256);
-      }
     }
     if (own) {
       bool do_fin = fin;
