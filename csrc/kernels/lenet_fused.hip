@@ -1494,8 +1494,10 @@ template <int R>
 __device__ __forceinline__ XPtrs<R> xptrs(const comm::IpcPeers& px) {
   static_assert(R >= 2 && R <= comm::kIpcMaxRanks, "world bound");
   XPtrs<R> x;
+  // (static kernel-argument indices: base[min(p, world - 1)] was a dependent scalar load at
+  // block entry; entries p >= world are never dereferenced, ll_push only pushes to p < world)
 #pragma unroll
-  for (int p = 0; p < R; ++p) x.dst[p] = px.base[min(p, px.world - 1)] + (int64_t)px.rank * px.cap;
+  for (int p = 0; p < R; ++p) x.dst[p] = px.base[p] + (int64_t)px.rank * px.cap;
   x.src = px.base[px.rank];
   return x;
 }
@@ -1619,13 +1621,34 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // front of its slab loads)
   constexpr int XR = EXCH ? XW : 2;
   typedef const __attribute__((address_space(1))) int64_t* gcptr64;
-  const uint32_t xt = EXCH ? (uint32_t)(((gcptr64)px.counters)[blk + opaque(0)] + 1) : 0u;
+  // (its low dword only: a 64-bit load whose high half the compiler then reuses as a scratch
+  // register was waited for right away)
+  typedef const __attribute__((address_space(1))) uint32_t* gcptr32u;
+  const uint32_t xt_raw = EXCH ? ((gcptr32u)px.counters)[2 * blk + opaque(0)] : 0u;
   XPtrs<XR> xp;
   if constexpr (EXCH) xp = xptrs<XR>(px);
   // a wait of this exchange has timed out before (the error word is set): the replicas are
   // already inconsistent and the caller re-runs the epoch on the process group, so this call
   // polls once and never waits -- a dead peer costs one timeout, not one per step
-  bool timed_out = EXCH && __hip_atomic_load(px.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  // (a per-lane load through an opaque offset, like xt: as a wave-uniform atomic load it was
+  // waited for right here, a memory round trip in front of the block's first slab load; it is
+  // set by an earlier launch, so a plain load after the kernel boundary sees it)
+  typedef const __attribute__((address_space(1))) int* gcptr32;
+  const int xerr_raw = EXCH ? ((gcptr32)px.err)[opaque(0)] : 0;
+  // The tag and the error flag, consumed where the exchange needs them: the register passes
+  // through an empty asm there, so hipcc cannot compute them (and wait for their loads) at block
+  // entry, in front of the slab loads
+  auto tag_now = [&]() {
+    uint32_t v = xt_raw;
+    asm volatile("" : "+v"(v));
+    return v + 1u;
+  };
+  auto err_now = [&]() {
+    int v = xerr_raw;
+    asm volatile("" : "+v"(v));
+    return v != 0;
+  };
+  bool timed_out = false;
 #define USTAMP(k) \
   if (a.dbg && tid == 0 && blk < a.dbg_blocks) a.dbg[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   USTAMP(0);
@@ -1633,20 +1656,17 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // fc_tpb > 0: FC tiles per workgroup chosen by the launcher (the exchange's fixed map).
   // Tiles per block and waves per tile are powers of two: shifts, not run-time divisions (a
   // division by a run-time value is a long emulated sequence on every wave's scalar issue)
-  // fc_sl > 1: split-K fc gradients (the last slice of a tile finishes it): the CONV blocks
-  // come first (88 of them, the last 4 idle: with the FC role's hundreds of short workgroups
-  // dispatched ahead of them they became the critical path, 8.7 us at B = 8192), then one tile
-  // per workgroup, fc_sl batch slices of every tile: workgroup 88 + slice * 88 + b (b % 8, its
-  // XCD, as unsplit)
+  // fc_sl > 1: split-K fc gradients (the last slice of a tile finishes it), one tile per workgroup,
+  // fc_sl batch slices of every tile: workgroup slice * 88 + b (b % 8, its XCD, as unsplit).
+  // (The CONV blocks stay last: put first, they made the FC blocks' tail 1.5 us longer at B =
+  // 8192, profiles/r4/tile_trace_r4h_conv_first.txt.)
   const int tpb_ = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
   const int nb_fc = ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl;
-  const bool split = fc_sl > 1;
-  static_assert(NB_CONV <= FC_TILES && FC_TILES % 8 == 0, "split-K block layout");
-  if (split ? blk < FC_TILES : blk >= nb_fc) {
-    // ---------------- role CONV (unsplit: after the FC blocks, which have the longer path, so
+  if (blk >= nb_fc) {
+    // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
     const int half = tid / UP_NT, ht = tid % UP_NT;
-    const int cblk = split ? blk : blk - nb_fc, pb = cblk * (NTH / UP_NT) + half;
+    const int cblk = blk - nb_fc, pb = cblk * (NTH / UP_NT) + half;
     const bool live_pb = pb < NB_CONV;
     const int pbc = min(pb, NB_CONV - 1);  // a dead half reads a valid chunk, stores nothing
     float4 (*part)[UP_C] = reinterpret_cast<float4 (*)[UP_C]>(part_ + half * UP_S * UP_C);
@@ -1714,14 +1734,16 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       const int l = ht & 63;
       if (slot_param(pbc * (UP_C * 4) + l) >= 0) {
         const float gl[1] = {((part2[0][l] + part2[1][l]) + (part2[2][l] + part2[3][l])) * a.grad_post};
-        ll_push<1, XR>(px, xp, xt, pbc * (UP_C * 4) + l, live, gl, ht >> 6);
+        ll_push<1, XR>(px, xp, tag_now(), pbc * (UP_C * 4) + l, live, gl, ht >> 6);
       }
     }
     if (ht < 64 && live_pb && pi >= 0) {
       float g[1] = {((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post};
-      if (EXCH)
-        ll_poll<1, XR>(px, xp, xt, pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
+      if (EXCH) {
+        timed_out = err_now();
+        ll_poll<1, XR>(px, xp, tag_now(), pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
                        a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+      }
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
     USTAMP(4);
@@ -1755,9 +1777,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // one tile per workgroup: XCD-grouped tiles.  Workgroup b runs on XCD b % 8; the tiles
     // in (fc1 column-block, row-block) order are dealt out 11 per XCD, so an XCD's tiles share
     // their column blocks (B operand rows of the vector slab) and its L2 fetches each line once
-    const int fblk = split ? blk - FC_TILES : blk;  // (split: tpb == 1, fblk < 88 fc_sl)
-    const int fslice = fblk / FC_TILES;
-    const int tile_w = tpb == 1 ? fc_tile_of_block(fblk - fslice * FC_TILES) : blk * tpb + (wave >> lw);
+    const int fslice = blk / FC_TILES;  // (0 unless split: tpb == 1, blk < 88 fc_sl)
+    const int tile_w = tpb == 1 ? fc_tile_of_block(blk - fslice * FC_TILES) : blk * tpb + (wave >> lw);
     const int sub = wave & (wpt - 1);
     const bool fin = fc_sl == 1;  // this block finishes its tile (else: the tile's last slice does)
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
@@ -2002,11 +2023,13 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         float gv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) gv[r] = own ? g[r] : xg[r * 64 + lane];
-        ll_push<4, XR>(px, xp, xt, w0, live, gv, wave);
+        ll_push<4, XR>(px, xp, tag_now(), w0, live, gv, wave);
       }
-      if (own)
-        ll_poll<4, XR>(px, xp, xt, w0, live, g, timeout_ticks, timed_out,
+      if (own) {
+        timed_out = err_now();
+        ll_poll<4, XR>(px, xp, tag_now(), w0, live, g, timeout_ticks, timed_out,
                        a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+      }
     }
     if (own) {
       bool do_fin = fin;
@@ -2083,7 +2106,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   if (EXCH) {
     if (timed_out) atomicOr(px.err, 1);
     __syncthreads();  // every wave has read counters[blk]
-    if (tid == 0) px.counters[blk] = xt;
+    if (tid == 0) px.counters[blk] = tag_now();
   }
   if (a.apply_sgd) {
     // Device counters.  cursor / rng_offset are never read by this kernel, so
@@ -2259,7 +2282,7 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
   const int S = fc_split_slices(a);
   if (S > 1) {  // split-K fc gradients: one tile per workgroup x S slices (the last one finishes)
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
-      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 0>), dim3(FC_TILES * (S + 1)), dim3(UP_NT), 0, s, a,
+      hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 0>), dim3(FC_TILES * S + NB_CONV), dim3(UP_NT), 0, s, a,
                          a.vslab, a.B, loss_parts, nparts, loss_acc, (uint64_t)0, 1, S, px);
     });
     return hipGetLastError();

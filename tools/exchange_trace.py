@@ -103,7 +103,6 @@ def main():
             # fc_blocks(B) (lenet_fused.hip): 88 FC tiles, 8 / waves-per-tile of them per block
             wpt = 1 if B <= 128 else 2 if B <= 256 else 4 if B <= 512 else 8
             nfc = 88 if (N > 1 or wpt == 1) else 88 // (8 // wpt)
-            split = False
             # split-K fc gradients (B > 1024, no exchange): 88 x S FC blocks, S = B / 1024 as a
             # power of two <= 8 (lenet_fused.hip fc_split_slices; CSED_FC_SLICES forces it)
             if N == 1 and B > 1024 and eng.fc_part is not None:
@@ -112,7 +111,6 @@ def main():
                 while S * 2 <= 8 and (S * 2 <= forced if forced > 0 else S * 2 * 1024 <= B):
                     S *= 2
                 nfc = 88 * S
-                split = S > 1
             g = stamped_graph(eng, n, dt, du)
             for _ in range(3):
                 dt.zero_()
@@ -128,9 +126,8 @@ def main():
                 u0 = u[:, 0][u[:, 0] > 0].min().item()
                 s3 = u[:, 3].max().item()
                 s4 = u[:, 4][u[:, 4] > 0].max().item()
-                # blocks [0, nfc): the FC role, then the 84 CONV blocks (split-K: 88 CONV slots
-                # first, then the FC blocks)
-                fc_r, cv_r = (slice(88, 88 + nfc), slice(0, 84)) if split else (slice(0, nfc), slice(nfc, nfc + 84))
+                # blocks [0, nfc): the FC role, then the 84 CONV blocks
+                fc_r, cv_r = slice(0, nfc), slice(nfc, nfc + 84)
                 fc4 = u[fc_r, 4][u[fc_r, 4] > 0].max().item()
                 cv4 = u[cv_r, 4][u[cv_r, 4] > 0].max().item()
                 nt0 = T[i + 1, :, i_in].min().item()
