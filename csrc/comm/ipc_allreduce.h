@@ -38,7 +38,7 @@ hipError_t ipc_error(int id, int* err_out, bool reset);
 // slot = tag & 1; each 8-byte word is {fp32 value, 32-bit tag}.  counters[blk]
 // is the last tag used by workgroup blk of the kernel that owns the buffer.
 constexpr int kIpcMaxRanks = 8;
-constexpr int kIpcMaxBlocks = 256;
+constexpr int kIpcMaxBlocks = 512;
 struct IpcPeers {
   uint64_t* base[kIpcMaxRanks];
   int64_t* counters;  // [kIpcMaxBlocks]
