@@ -214,6 +214,7 @@ class FusedLeNetTrainer:
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
         self.bringup_s: dict[str, float] = {}  # exchange bring-up phases (s), for the bench JSON
+        self.loopback_world = 0  # (set below; the exchange bring-up's reports read it)
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"
         if multi and mode in ("auto", "fused"):

@@ -1324,9 +1324,15 @@ __host__ __device__ constexpr bool fc_tile_map_is_bijective() {
 }
 static_assert(FC_TILES % 8 == 0 && fc_tile_map_is_bijective(), "FC tile map");
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
-// the fused exchange: two FC workgroups per tile (each exchanges and finishes half the tile)
-constexpr int FC_XHALVES = 2;
-constexpr int NB_UPDATE_X = NB_CONV + FC_XHALVES * NB_FC;
+// The fused exchange: two FC workgroups per tile, each exchanging and finishing half of it (tile
+// rows 4 kq + r, r >> 1 = the half) -- except the fc1 tiles of rows 48..63, whose second half
+// holds only the padding rows 50, 51, 54, ...: 88 workgroups for the first halves (block b: tile
+// fc_tile_of_block(b)), then 67 for the second halves of tiles 0..62 and 84..87.  239 update
+// workgroups in all: at most one per CU (over 128 VGPRs), so every one is resident at once.
+constexpr int FC_X2 = 3 * 21 + 4;  // tiles with a live second half
+constexpr int NB_FC_X = NB_FC + FC_X2;
+constexpr int NB_UPDATE_X = NB_CONV + NB_FC_X;
+static_assert(NB_UPDATE_X <= 256, "one resident update workgroup per CU");
 // split-K fc gradients (fc_split_slices): at most 8 slices of 88 tiles x 256 partial sums, then
 // 88 arrival counters (ints, zero between launches) in the same fp32 scratch
 constexpr int FC_PART_FLOATS = 8 * FC_TILES * 256;
@@ -1673,7 +1679,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // 8192, profiles/r4/tile_trace_r4h_conv_first.txt.)
   // (exchange: two FC workgroups per tile, one per half of its words, see the FC role)
   const int tpb_ = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
-  const int nb_fc = ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl * (EXCH ? FC_XHALVES : 1);
+  const int nb_fc = EXCH ? NB_FC_X : ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl;
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
@@ -1789,13 +1795,15 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // one tile per workgroup: XCD-grouped tiles.  Workgroup b runs on XCD b % 8; the tiles
     // in (fc1 column-block, row-block) order are dealt out 11 per XCD, so an XCD's tiles share
     // their column blocks (B operand rows of the vector slab) and its L2 fetches each line once
-    // split: slice blk / 88 (tpb == 1, blk < 88 fc_sl); exchange: half blk / 88 of the tile's
-    // words (the workgroup forms the whole tile, exchanges and finishes half of it: a CU's
+    // split: slice blk / 88 (tpb == 1, blk < 88 fc_sl); exchange: half xh of the tile's words
+    // (NB_FC_X: the workgroup forms the whole tile, exchanges and finishes half of it: a CU's
     // uncached pushes and polls cost ~0.04 us per wave instruction, in order -- 28 of them for a
     // whole fc tile at N = 8, profiles/r4/exchange_trace_r4i.txt)
-    const int q88 = blk / FC_TILES;
-    const int fslice = EXCH ? 0 : q88, xh = EXCH ? q88 : 0;
-    const int tile_w = tpb == 1 ? fc_tile_of_block(blk - q88 * FC_TILES) : blk * tpb + (wave >> lw);
+    const int q88 = EXCH ? 0 : blk / FC_TILES;
+    const int fslice = q88, xh = EXCH && blk >= FC_TILES;
+    const int b2 = blk - FC_TILES;  // (exchange, second halves: tiles 0..62, then 84..87)
+    const int tile_w = tpb != 1 ? blk * tpb + (wave >> lw)
+                                : (xh ? (b2 < 3 * 21 ? b2 : FC1_TILES + b2 - 3 * 21) : fc_tile_of_block(blk - q88 * FC_TILES));
     const int sub = wave & (wpt - 1);
     const bool fin = fc_sl == 1;  // this block finishes its tile (else: the tile's last slice does)
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
