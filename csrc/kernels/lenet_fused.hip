@@ -1324,15 +1324,6 @@ __host__ __device__ constexpr bool fc_tile_map_is_bijective() {
 }
 static_assert(FC_TILES % 8 == 0 && fc_tile_map_is_bijective(), "FC tile map");
 constexpr int NB_UPDATE = NB_CONV + NB_FC;
-// The fused exchange: two FC workgroups per tile, each exchanging and finishing half of it (tile
-// rows 4 kq + r, r >> 1 = the half) -- except the fc1 tiles of rows 48..63, whose second half
-// holds only the padding rows 50, 51, 54, ...: 88 workgroups for the first halves (block b: tile
-// fc_tile_of_block(b)), then 67 for the second halves of tiles 0..62 and 84..87.  239 update
-// workgroups in all: at most one per CU (over 128 VGPRs), so every one is resident at once.
-constexpr int FC_X2 = 3 * 21 + 4;  // tiles with a live second half
-constexpr int NB_FC_X = NB_FC + FC_X2;
-constexpr int NB_UPDATE_X = NB_CONV + NB_FC_X;
-static_assert(NB_UPDATE_X <= 256, "one resident update workgroup per CU");
 // split-K fc gradients (fc_split_slices): at most 8 slices of 88 tiles x 256 partial sums, then
 // 88 arrival counters (ints, zero between launches) in the same fp32 scratch
 constexpr int FC_PART_FLOATS = 8 * FC_TILES * 256;
@@ -1534,14 +1525,13 @@ __device__ __forceinline__ int64_t slot_words(const comm::IpcPeers& px, uint32_t
 template <int K, int R>
 __device__ __forceinline__ void ll_push(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                         const bool (&live)[K], const float (&v)[K], int q) {
-  static_assert(K == 1 || K == 2 || K == 4, "one word, or one or two 16-byte pairs per lane");
+  static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
   const int rank = px.rank, target = q < rank ? q : q + 1;
   const int64_t so = slot_words(px, t) + w0;
   const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));  // (uniform: the pair bases)
   // a pair with no live word is never pushed (its lanes are off in the store's EXEC mask): the
   // fc tiles' padding rows / columns (a quarter of the fc words) never cross a link
-  const bool live01 = K == 1 || live[0] || live[min(1, K - 1)];
-  const bool live23 = K == 4 && (live[min(2, K - 1)] || live[K - 1]);
+  const bool live01 = K == 1 || live[0] || live[min(1, K - 1)], live23 = K == 4 && (live[min(2, K - 1)] || live[K - 1]);
   // write-through, system scope (see comm::push_word); the peer index unrolled (uniform
   // branches) so that x.dst stays in scalar registers
 #pragma unroll
@@ -1551,9 +1541,8 @@ __device__ __forceinline__ void ll_push(const comm::IpcPeers& px, const XPtrs<R>
         __hip_atomic_store(x.dst[p] + so, ll_word(v[0], t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
         uint64_t* b = uniform_ptr(x.dst[p] + sw);
-        if (live01) sys_store16(b, 8 * w0, u64x2v{ll_word(v[0], t), ll_word(v[min(1, K - 1)], t)});
-        if (K == 4 && live23)
-          sys_store16(b, 8 * (w0 + 128), u64x2v{ll_word(v[min(2, K - 1)], t), ll_word(v[K - 1], t)});
+        if (live01) sys_store16(b, 8 * w0, u64x2v{ll_word(v[0], t), ll_word(v[1], t)});
+        if (live23) sys_store16(b, 8 * (w0 + 128), u64x2v{ll_word(v[2], t), ll_word(v[3], t)});
       }
     }
 }
@@ -1565,11 +1554,14 @@ template <int K, int R>
 __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                         const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
                                         bool& timed_out, uint64_t* stamp) {
-  static_assert(K == 1 || K == 2 || K == 4, "one word, or one or two 16-byte pairs per lane");
+  static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
   const int64_t so = slot_words(px, t) + w0;
   const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));
   const int rank = px.rank, world = px.world;
   const int64_t cap = px.cap;
+  // (a pair with no live word is not loaded either: its lanes are off in the load's EXEC mask)
+  const bool live01 = K == 1 || live[0] || live[min(1, K - 1)];
+  const bool live23 = K == 4 && (live[min(2, K - 1)] || live[K - 1]);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   if (stamp) stamp[5] = t0;  // (diagnostics: poll start)
   uint32_t passes = 0;
@@ -1582,14 +1574,10 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
         w[q][0] = __hip_atomic_load(x.src + (int64_t)p * cap + so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
         const uint64_t* b = uniform_ptr(x.src + sw + (int64_t)p * cap);
-        const u64x2v lo = sys_load16(b, 8 * w0);
-        w[q][0] = lo.x;
-        w[q][min(1, K - 1)] = lo.y;
-        if constexpr (K == 4) {
-          const u64x2v hi = sys_load16(b, 8 * (w0 + 128));
-          w[q][min(2, K - 1)] = hi.x;
-          w[q][K - 1] = hi.y;
-        }
+        u64x2v lo = u64x2v{0, 0}, hi = u64x2v{0, 0};
+        if (live01) lo = sys_load16(b, 8 * w0);
+        if (live23) hi = sys_load16(b, 8 * (w0 + 128));
+        w[q][0] = lo.x; w[q][1] = lo.y; w[q][2] = hi.x; w[q][3] = hi.y;
       }
     }
     bool ready = true;
@@ -1677,9 +1665,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   // fc_sl batch slices of every tile: workgroup slice * 88 + b (b % 8, its XCD, as unsplit).
   // (The CONV blocks stay last: put first, they made the FC blocks' tail 1.5 us longer at B =
   // 8192, profiles/r4/tile_trace_r4h_conv_first.txt.)
-  // (exchange: two FC workgroups per tile, one per half of its words, see the FC role)
   const int tpb_ = fc_tpb > 0 ? fc_tpb : fc_tiles_per_block(B);
-  const int nb_fc = EXCH ? NB_FC_X : ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl;
+  const int nb_fc = ((FC_TILES + tpb_ - 1) >> __builtin_ctz(tpb_)) * fc_sl;
   if (blk >= nb_fc) {
     // ---------------- role CONV (after the FC blocks: those have the longer path, so
     // they are dispatched first).  Each UP_NT-thread half reduces one 64-parameter block.
@@ -1795,15 +1782,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     // one tile per workgroup: XCD-grouped tiles.  Workgroup b runs on XCD b % 8; the tiles
     // in (fc1 column-block, row-block) order are dealt out 11 per XCD, so an XCD's tiles share
     // their column blocks (B operand rows of the vector slab) and its L2 fetches each line once
-    // split: slice blk / 88 (tpb == 1, blk < 88 fc_sl); exchange: half xh of the tile's words
-    // (NB_FC_X: the workgroup forms the whole tile, exchanges and finishes half of it: a CU's
-    // uncached pushes and polls cost ~0.04 us per wave instruction, in order -- 28 of them for a
-    // whole fc tile at N = 8, profiles/r4/exchange_trace_r4i.txt)
-    const int q88 = EXCH ? 0 : blk / FC_TILES;
-    const int fslice = q88, xh = EXCH && blk >= FC_TILES;
-    const int b2 = blk - FC_TILES;  // (exchange, second halves: tiles 0..62, then 84..87)
-    const int tile_w = tpb != 1 ? blk * tpb + (wave >> lw)
-                                : (xh ? (b2 < 3 * 21 ? b2 : FC1_TILES + b2 - 3 * 21) : fc_tile_of_block(blk - q88 * FC_TILES));
+    const int fslice = blk / FC_TILES;  // (0 unless split: tpb == 1, blk < 88 fc_sl)
+    const int tile_w = tpb == 1 ? fc_tile_of_block(blk - fslice * FC_TILES) : blk * tpb + (wave >> lw);
     const int sub = wave & (wpt - 1);
     const bool fin = fc_sl == 1;  // this block finishes its tile (else: the tile's last slice does)
     const bool live_tile = live_wave && tile_w < FC_TILES;  // the last workgroup may hold dead waves:
@@ -2034,30 +2014,26 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       // and + 128 + {0, 1} (two 16-byte pairs).  One tile per workgroup here, owned by wave 0:
       // it publishes the values in LDS (part2_, unused by this role), wave q < world - 1 pushes
       // them to peer row q, and wave 0 then polls
-      // This workgroup's half xh: entries r = 2 xh, 2 xh + 1 (words w0 + {0, 1}).
       float* xg = part2_;
-      float gh[2] = {xh ? g[2] : g[0], xh ? g[3] : g[1]};
       if (own) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) xg[j * 64 + lane] = gh[j];
+        for (int r = 0; r < 4; ++r) xg[r * 64 + lane] = g[r];
       }
       __syncthreads();
-      bool live[2];  // (from the tile alone: every wave's view of the owner's pidx >= 0)
+      bool live[4];  // (from the tile alone: every wave's view of the owner's pidx >= 0)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) live[j] = mt * 16 + 4 * kq + 2 * xh + j < rows && i <= cols;
-      const int w0 = CNP_PAD + tile * 256 + 128 * xh + 2 * lane;
+      for (int r = 0; r < 4; ++r) live[r] = mt * 16 + 4 * kq + r < rows && i <= cols;
+      const int w0 = CNP_PAD + tile * 256 + 2 * lane;
       if (wave < px.world - 1) {
-        float gv[2];
+        float gv[4];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) gv[j] = own ? gh[j] : xg[j * 64 + lane];
-        ll_push<2, XR>(px, xp, tag_now(), w0, live, gv, wave);
+        for (int r = 0; r < 4; ++r) gv[r] = own ? g[r] : xg[r * 64 + lane];
+        ll_push<4, XR>(px, xp, tag_now(), w0, live, gv, wave);
       }
       if (own) {
         timed_out = err_now();
-        ll_poll<2, XR>(px, xp, tag_now(), w0, live, gh, timeout_ticks, timed_out,
+        ll_poll<4, XR>(px, xp, tag_now(), w0, live, g, timeout_ticks, timed_out,
                        a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
-        g[xh ? 2 : 0] = gh[0];
-        g[xh ? 3 : 1] = gh[1];
       }
     }
     if (own) {
@@ -2119,15 +2095,13 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         for (int r = 0; r < 4; ++r) tr[(4 * kq + r) * 16 + l16] = g[r];
         __builtin_amdgcn_wave_barrier();
         const float4 gv = *reinterpret_cast<const float4*>(tr + (lane >> 2) * 16 + 4 * (lane & 3));
-        // (exchange: the rows of this workgroup's half only, tile row 4 kq + r with r >> 1 == xh)
-        if (vrow < 50 && (!EXCH || (((lane >> 3) & 1) == xh)))
+        if (vrow < 50)
           finish_param4<T>(a, vidx, gv, first, make_float4(pp[0], pp[1], pp[2], pp[3]),
                            make_float4(pm[0], pm[1], pm[2], pm[3]), I_F1 + vrow * LD_F1 + vcol);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (pidx[r] >= 0 && (!EXCH || (r >> 1) == xh))
-            finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
+          if (pidx[r] >= 0) finish_param<T>(a, pidx[r], g[r], first, pp[r], pm[r], fd[r], -1);
       }
       }  // do_fin
       USTAMP(4);
@@ -2288,7 +2262,7 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     // must not depend on the batch: one FC tile per workgroup (NB_UPDATE workgroups) for
     // every B, the full steps' and the epoch tail's alike (a batch-dependent layout let
     // the counters of different words drift apart between steps of different batch sizes).
-    static_assert(NB_UPDATE_X <= comm::kIpcMaxBlocks, "one exchange counter per update workgroup");
+    static_assert(NB_UPDATE <= comm::kIpcMaxBlocks, "one exchange counter per update workgroup");
     if (px_cached) {  // resolved once by the caller (csrc/bindings.cpp LenetStepper)
       px = *px_cached;
     } else {
@@ -2299,13 +2273,13 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
       if (px.world <= 2)
-        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 2>), dim3(NB_UPDATE_X), dim3(UP_NT), 0, s, a, a.vslab,
+        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 2>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
                            a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
       else if (px.world <= 4)
-        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 4>), dim3(NB_UPDATE_X), dim3(UP_NT), 0, s, a, a.vslab,
+        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 4>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
                            a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
       else
-        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 8>), dim3(NB_UPDATE_X), dim3(UP_NT), 0, s, a, a.vslab,
+        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 8>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
                            a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
     });
     return hipGetLastError();

@@ -102,8 +102,7 @@ def main():
             i_in, i_out = (12, 13) if tile else (22, 23)
             # fc_blocks(B) (lenet_fused.hip): 88 FC tiles, 8 / waves-per-tile of them per block
             wpt = 1 if B <= 128 else 2 if B <= 256 else 4 if B <= 512 else 8
-            # (the fused exchange, N > 1: 155 FC blocks, most tiles in two halves)
-            nfc = 155 if N > 1 else 88 if wpt == 1 else 88 // (8 // wpt)
+            nfc = 88 if (N > 1 or wpt == 1) else 88 // (8 // wpt)
             # split-K fc gradients (B > 1024, no exchange): 88 x S FC blocks, S = B / 1024 as a
             # power of two <= 8 (lenet_fused.hip fc_split_slices; CSED_FC_SLICES forces it)
             if N == 1 and B > 1024 and eng.fc_part is not None:
