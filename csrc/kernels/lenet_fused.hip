@@ -1338,22 +1338,26 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
 // no dependent cursor -> perm -> image chain in its preamble.  lenet_train
 // itself stages the NEXT step (each workgroup its own sample, loads issued
 // mid-kernel, stored at its end); this kernel fills the buffer at epoch start.
-// One block; every thread issues all of its loads before its first store.
+// STAGE_ROWS rows per block (one memory round trip each: a single block gathering the tile
+// kernel's 1024 rows took a dozen dependent rounds, ~20 us at every epoch start of a large-batch
+// run); every thread issues all of its loads before its first store.
 // ---------------------------------------------------------------------------
 constexpr int STAGE_MAXB = 1024;  // staging rows (the tile kernel: 256 workgroups x 4 samples)
+constexpr int STAGE_ROWS = 16;    // rows per block
 constexpr int IMG_U4 = 784 / 16;  // 49 16-byte chunks per image
 
 __device__ __forceinline__ void gather_batch(const LenetStageArgs& st, int64_t step, int64_t* rows_sh) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const int nrows = st.rows;  // staging row r holds sample r % B (split step: 4 rows per sample)
+  // staging row r holds sample r % B (split step: 4 rows per sample); this block: rows r0 ..
+  const int r0 = blockIdx.x * STAGE_ROWS, nrows = min(STAGE_ROWS, st.rows - r0);
   for (int b = tid; b < nrows; b += nt) {
-    const int64_t row = st.perm[min(step * st.B + b % st.B, st.perm_len - 1)];
+    const int64_t row = st.perm[min(step * st.B + (r0 + b) % st.B, st.perm_len - 1)];
     rows_sh[b] = row;
-    st.lstage[b] = st.labels[row];
+    st.lstage[r0 + b] = st.labels[row];
   }
   __syncthreads();
   const uint4* __restrict__ src = reinterpret_cast<const uint4*>(st.images);
-  uint4* __restrict__ dst = reinterpret_cast<uint4*>(st.xstage);
+  uint4* __restrict__ dst = reinterpret_cast<uint4*>(st.xstage) + (int64_t)r0 * IMG_U4;
   const int total = nrows * IMG_U4;
   constexpr int U = 8;
   for (int i0 = tid; i0 < total; i0 += nt * U) {
@@ -1371,7 +1375,7 @@ __device__ __forceinline__ void gather_batch(const LenetStageArgs& st, int64_t s
 }
 
 __global__ void __launch_bounds__(512) lenet_stage_kernel(LenetStageArgs st, const int64_t* cursor) {
-  __shared__ int64_t rows_sh[STAGE_MAXB];
+  __shared__ int64_t rows_sh[STAGE_ROWS];
   gather_batch(st, cursor ? cursor[0] : 0, rows_sh);
 }
 
@@ -1559,9 +1563,8 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
   const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));
   const int rank = px.rank, world = px.world;
   const int64_t cap = px.cap;
-  // (a pair with no live word is not loaded either: its lanes are off in the load's EXEC mask)
-  const bool live01 = K == 1 || live[0] || live[min(1, K - 1)];
-  const bool live23 = K == 4 && (live[min(2, K - 1)] || live[K - 1]);
+  // (every pair is loaded, dead ones too: masking the dead pairs' loads off made the fc
+  // exchange slower, 1.76 -> 2.16 us at N = 8, profiles/r4/exchange_trace_r4l_poll_masked.txt)
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   if (stamp) stamp[5] = t0;  // (diagnostics: poll start)
   uint32_t passes = 0;
@@ -1574,9 +1577,7 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
         w[q][0] = __hip_atomic_load(x.src + (int64_t)p * cap + so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
         const uint64_t* b = uniform_ptr(x.src + sw + (int64_t)p * cap);
-        u64x2v lo = u64x2v{0, 0}, hi = u64x2v{0, 0};
-        if (live01) lo = sys_load16(b, 8 * w0);
-        if (live23) hi = sys_load16(b, 8 * (w0 + 128));
+        const u64x2v lo = sys_load16(b, 8 * w0), hi = sys_load16(b, 8 * (w0 + 128));
         w[q][0] = lo.x; w[q][1] = lo.y; w[q][2] = hi.x; w[q][3] = hi.y;
       }
     }
@@ -2309,7 +2310,7 @@ int lenet_split_k() { return SPLIT_K; }
 hipError_t launch_lenet_stage(const LenetStageArgs& a, const int64_t* cursor, hipStream_t s) {
   // rows: the staging rows (row r = sample r % B of the step); any batch size
   if (a.B <= 0 || a.rows <= 0 || a.rows > STAGE_MAXB || !a.xstage || !a.lstage) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lenet_stage_kernel, dim3(1), dim3(512), 0, s, a, cursor);
+  hipLaunchKernelGGL(lenet_stage_kernel, dim3(cdiv(a.rows, STAGE_ROWS)), dim3(512), 0, s, a, cursor);
   return hipGetLastError();
 }
 
