@@ -21,7 +21,7 @@ efficiency value_N / (N * value_1).
 Prediction (``--predict``, on by default).  At global batch 64 each of N ranks runs a step of
 per-rank batch 64/N whose exchange pushes to N-1 peers.  Both parts were measured on one GPU
 with the exchange looped back to N virtual ranks (``tools/exchange_loopback.py``,
-profiles/dp_exchange_r3.md section 2): ``LOOPBACK_STEP_US[(B, N)]`` is that graph-replayed
+profiles/dp_exchange_r4.md): ``LOOPBACK_STEP_US[(B, N)]`` is that graph-replayed
 step.  The loopback push never leaves the device, so the predicted N-GPU step adds one xGMI
 one-way hop (``--hop-us``, 1 us assumed) and the time the pushes occupy one link: every rank
 sends each peer its whole live gradient as LL words (21,840 x 8 bytes = 175 KB, one link per
@@ -63,15 +63,15 @@ REF_EPOCH_S = {1: 17.53, 2: 11.29, 4: 7.60, 8: 5.00}  # BASELINE.md (reference R
 STEPS_PER_EPOCH = 938
 GLOBAL_BATCH = 64
 # graph-replayed lenet_train + lenet_update step (us) at per-rank batch B with the in-kernel
-# exchange looped back to N virtual ranks, one MI355X (gpurun_out/r3y_loopback.log,
-# profiles/dp_exchange_r3.md section 2)
+# exchange looped back to N virtual ranks, one MI355X (profiles/r4/exchange_loopback_r4m.log,
+# profiles/dp_exchange_r4.md)
 LOOPBACK_STEP_US = {
-    (8, 1): 13.77, (8, 2): 16.09, (8, 4): 16.29, (8, 8): 16.73,
-    (16, 1): 14.05, (16, 2): 16.24, (16, 4): 16.48, (16, 8): 17.00,
-    (32, 1): 14.24, (32, 2): 16.57, (32, 4): 16.80, (32, 8): 17.26,
-    (64, 1): 15.05, (64, 2): 17.19, (64, 4): 17.49, (64, 8): 17.98,
+    (8, 1): 12.49, (8, 2): 13.81, (8, 4): 14.11, (8, 8): 14.89,
+    (16, 1): 12.78, (16, 2): 13.95, (16, 4): 14.10, (16, 8): 14.95,
+    (32, 1): 12.92, (32, 2): 14.10, (32, 4): 14.34, (32, 8): 15.23,
+    (64, 1): 14.24, (64, 2): 14.83, (64, 4): 15.10, (64, 8): 15.76,
 }
-WIRE_BYTES = 21840 * 8  # live exchange words per peer per step (lenet_fused.hip ll_allreduce)
+WIRE_BYTES = 21840 * 8  # live exchange words per peer per step (lenet_fused.hip ll_push)
 _LB_LINE = re.compile(r"B=\s*(\d+)\s+N=(\d+).*?step\s+([0-9.]+)\s*us")
 
 
