@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -165,8 +166,14 @@ hipError_t ipc_create(int64_t n, int blocks, int* id_out) {
   c->cap = n;
   c->blocks = blocks;
   const size_t bytes = 2 * (size_t)kMaxRanks * (size_t)n * sizeof(uint64_t);
-  // uncached: peers read it over xGMI mid-kernel, so no cache may hold stale lines
-  hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->buf), bytes, hipDeviceMallocUncached);
+  // uncached: peers read it over xGMI mid-kernel, so no cache may hold stale lines.
+  // (CSED_IPC_MEM=finegrained allocates it fine-grained instead: a measurement switch)
+  static const bool fine = [] {
+    const char* v = std::getenv("CSED_IPC_MEM");
+    return v && std::strcmp(v, "finegrained") == 0;
+  }();
+  hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->buf), bytes,
+                                       fine ? hipDeviceMallocFinegrained : hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c->buf, 0, bytes);
   if (e == hipSuccess) e = hipMalloc(&c->counters, kMaxBlocks * sizeof(int64_t));
   if (e == hipSuccess) e = hipMemset(c->counters, 0, kMaxBlocks * sizeof(int64_t));
