@@ -919,6 +919,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         // column k are one aligned float4 run: one wide store per lane (and one more for
         // channels 16-19 on lanes kq = 0) instead of eight scalar ones -- store issue was
         // what these cost.
+        // (plain stores: written through, lenet_dev.h store16_wt, the B = 8 step was 0.22 us
+        // slower and B = 64 unchanged, profiles/r4/ab_train_slab_writethrough.log)
         if (k <= 250) {
           const int slot0 = S_C2 + k * 20 + 4 * kq;
           float* row = a.slab + (C1_CH * (G - R2) + b0) * 64;  // + chunk * R2 * 64 + slot % 64
@@ -1691,6 +1693,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       image_slots_flat(max(pi, 0), d0, d1);  // (lanes without a parameter store nothing)
     };
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 lossv[4] = {};
     // Loads are unconditional from a clamped address and masked afterwards: a
     // per-element "load or zero" select makes hipcc branch around every load
     // and wait vmcnt(0) each time (dependent round trips instead of one).
@@ -1706,6 +1709,14 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u) v[u] = sp[(int64_t)min(sl + u * UP_S, rows - 1) * UP_C];
       pm_loads();
+      // block 0's wave 0 also folds the step's loss / accuracy partials (after its exchange):
+      // their loads go out now, with the slab's (folded later in a loop of dependent rounds,
+      // 4 of them at grid 256, they ran past the block's last store: +0.3 us per step at B = 64)
+      if (pb == 0 && loss_parts && tid < 64) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          lossv[u] = *reinterpret_cast<const float2*>(loss_parts + 2 * min(tid + 64 * u, max(nparts - 1, 0)));
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u)
@@ -1754,9 +1765,16 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     }
     USTAMP(4);
     if (pb == 0 && loss_parts && tid < 64) {
-      // loss / accuracy partials: lane-strided sums, then a fixed butterfly
+      // loss / accuracy partials: lane-strided sums (the first 256 parts prefetched above, in
+      // the same order), then a fixed butterfly
       float s0 = 0.f, s1 = 0.f;
-      for (int q = tid; q < nparts; q += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tid + 64 * u < nparts) {
+          s0 += lossv[u].x;
+          s1 += lossv[u].y;
+        }
+      for (int q = tid + 256; q < nparts; q += 64) {
         s0 += loss_parts[2 * q];
         s1 += loss_parts[2 * q + 1];
       }
