@@ -1715,7 +1715,8 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       if (pb == 0 && loss_parts && tid < 64) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          lossv[u] = *reinterpret_cast<const float2*>(loss_parts + 2 * min(tid + 64 * u, max(nparts - 1, 0)));
+          if (64 * u < nparts)  // (uniform: only the rounds the grid fills)
+            lossv[u] = *reinterpret_cast<const float2*>(loss_parts + 2 * min(tid + 64 * u, nparts - 1));
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
