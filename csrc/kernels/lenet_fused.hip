@@ -1718,16 +1718,6 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
           if (64 * u < nparts)  // (uniform: only the rounds the grid fills)
             lossv[u] = *reinterpret_cast<const float2*>(loss_parts + 2 * min(tid + 64 * u, nparts - 1));
       }
-      // The device counters: cursor / rng_offset are never read by this kernel, and step[0] only
-      // when dampening != 0 (then the last block to take a ticket bumps it, at the end), so this
-      // CONV block bumps them here, its read-modify-writes queued behind its slab loads (at the
-      // end of FC block 0, on the kernel's tail, they put a memory round trip behind its last
-      // store)
-      if (a.apply_sgd && pb == 0 && tid == 0) {
-        if (a.cursor) a.cursor[0] += 1;
-        if (a.rng_offset) a.rng_offset[0] += 1;
-        if (a.step && a.dampening == 0.f) a.step[0] += 1;
-      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < UP_MAXL; ++u)
@@ -2144,9 +2134,9 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     if (tid == 0) px.counters[blk] = tag_now();
   }
   if (a.apply_sgd) {
-    // Device counters (cursor, rng_offset, and step[0] without dampening: bumped by the first
-    // CONV block after its loads).  step[0] is read by every block when dampening != 0; then
-    // the last block to take a ticket bumps it.
+    // Device counters.  cursor / rng_offset are never read by this kernel, so
+    // one thread bumps them directly.  step[0] is read by every block only when
+    // dampening != 0; then the last block to take a ticket bumps it.
     if (a.dampening != 0.f) {
       __syncthreads();
       if (tid == 0) {
@@ -2156,6 +2146,12 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
           if (a.step) a.step[0] += 1;
         }
       }
+    } else if (blk == 0 && tid == 0 && a.step) {
+      a.step[0] += 1;
+    }
+    if (blk == 0 && tid == 0) {
+      if (a.cursor) a.cursor[0] += 1;
+      if (a.rng_offset) a.rng_offset[0] += 1;
     }
   }
 }
