@@ -1,0 +1,147 @@
+"""Time the modular engine's bucketed reducer (parallel/ddp.py) on one GPU: does the per-bucket
+all-reduce on the comm stream overlap the rest of backward?  (ref src/train_dist.py:83: torch DDP
+fires its all-reduce from backward hooks)
+
+    python tools/ddp_overlap.py [--batch 64] [--steps 200]          # step times per mode
+    python tools/ddp_overlap.py --parse <run_kernel_trace.csv>       # overlap from a kernel trace
+    rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/ddp_overlap.py --trace \
+        --mode overlap --bucket-mb 0.01                             # then --parse its csv
+
+One process with an RCCL process group of world 1.  The reducer is forced into its collective path
+(``world_size`` set to 2 after construction), so every bucket's all-reduce is issued on the comm
+stream from the post-accumulate hooks exactly as at N > 1; the collective is a 1-rank RCCL
+all-reduce (no wire time), i.e. this measures the overlap machinery, not xGMI.  Modes:
+
+* ``nocomm``: the reducer's hooks skip communication (``no_sync``);
+* ``overlap`` / ``serial``: per-bucket launch from the hooks vs every bucket after backward;
+* bucket caps 25 MB (the default: the 87 KB model is one bucket) and 0.01 MB (one bucket per
+  parameter tensor of fc1 / conv2 size, several for the smaller ones).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _modes():
+    return [("nocomm", 25.0, True), ("overlap", 25.0, True), ("serial", 25.0, False),
+            ("overlap", 0.01, True), ("serial", 0.01, False)]
+
+
+def run(batch: int, steps: int, warmup: int, trace: bool, only=None) -> list[dict]:
+    import torch
+    import torch.distributed as dist
+
+    from csed_514_project_distributed_training_using_pytorch_amd import ops
+    from csed_514_project_distributed_training_using_pytorch_amd.models.net import Net
+    from csed_514_project_distributed_training_using_pytorch_amd.optim.sgd import FusedSGD
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ddp import DistributedDataParallel
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.rand(batch, 1, 28, 28, device=dev, generator=g).to(ops.compute_dtype())
+    t = torch.randint(0, 10, (batch,), device=dev, generator=g)
+    rows = []
+    for mode, cap, overlap in _modes():
+        if only is not None and (mode, cap) != only:
+            continue
+        torch.manual_seed(1)
+        net = Net().to(dev).train()
+        ddp = DistributedDataParallel(net, bucket_cap_mb=cap, overlap=overlap)
+        ddp.world_size = 2  # force the collective path (see the module docstring)
+        opt = FusedSGD(list(net.parameters()), lr=0.01, momentum=0.5, flat=ddp.flat)
+        ops.rng.default_state.device_step = opt.step_count
+
+        def step():
+            opt.zero_grad()
+            if mode == "nocomm":
+                with ddp.no_sync():
+                    loss = ops.nll_loss(ddp(x), t)
+                    loss.backward()
+            else:
+                loss = ops.nll_loss(ddp(x), t)
+                loss.backward()
+            opt.step()
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(steps):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps
+        rows.append({"mode": mode, "bucket_mb": cap, "buckets": len(ddp.buckets),
+                     "us_per_step_gpu": round(e0.elapsed_time(e1) * 1000 / steps, 2),
+                     "us_per_step_wall": round(wall * 1e6, 2)})
+        for h in ddp._hooks:
+            h.remove()
+    dist.destroy_process_group()
+    return rows
+
+
+def parse(path: str) -> dict:
+    """Comm (RCCL) kernel time and the part of it that overlaps a compute kernel on another stream."""
+    ks = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]))
+    ks.sort()
+    comm = [k for k in ks if "nccl" in k[3].lower() or "rccl" in k[3].lower()]
+    comp = [k for k in ks if k not in comm and "rocclr" not in k[3]]
+    tot = ov = 0
+    for s, e, st, _ in comm:
+        tot += e - s
+        # union of the other streams' compute intervals intersected with [s, e)
+        segs = sorted((max(s, cs), min(e, ce)) for cs, ce, cst, _ in comp if cst != st and cs < e and ce > s)
+        cur_s = cur_e = None
+        for a, b in segs:
+            if cur_e is None or a > cur_e:
+                if cur_e is not None:
+                    ov += cur_e - cur_s
+                cur_s, cur_e = a, b
+            else:
+                cur_e = max(cur_e, b)
+        if cur_e is not None:
+            ov += cur_e - cur_s
+    names = sorted({k[3] for k in comm})
+    return {"comm_kernels": len(comm), "comm_ns": tot, "overlapped_ns": ov,
+            "overlap_share": round(ov / tot, 3) if tot else None, "comm_kernel_names": names[:4],
+            "streams": sorted({k[2] for k in ks})}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--trace", action="store_true", help="short run of one mode for a kernel trace")
+    ap.add_argument("--mode", default="overlap", help="--trace: nocomm / overlap / serial")
+    ap.add_argument("--bucket-mb", type=float, default=0.01, help="--trace: bucket cap")
+    ap.add_argument("--parse", help="run_kernel_trace.csv of a --trace run")
+    a = ap.parse_args()
+    if a.parse:
+        print(json.dumps(parse(a.parse)))
+        return
+    only = None
+    if a.trace:
+        a.steps, a.warmup, only = 20, 5, (a.mode, a.bucket_mb)
+    for r in run(a.batch, a.steps, a.warmup, a.trace, only):
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -17,6 +17,8 @@
 #             gaps, lenet_update FC / CONV roles at B = 1024 and 8192
 #   pmc       three rocprofv3 --pmc passes over the train kernel (B=64), one over B=8,
 #             and three over the tile kernel (B=1024)
+#   ddp       tools/ddp_overlap.py: the modular engine's bucketed reducer, per-bucket all-reduce on the
+#             comm stream vs after backward, step times + overlap share from kernel traces
 #   ab        same-box A/B of ab/A_C.so vs ab/B_C.so (tools/ab_build.sh REV) at global batch
 #             64 and 8 (+ AB_ARGS), N_AB alternations (default 3)
 #   abenv     same-box A/B of one build under ENV_A vs ENV_B (BENCH_ARGS / AB_ARGS / N_AB)
@@ -78,6 +80,15 @@ task_exchange() {
 
 task_tiletrace() {
   cd $R && py 300 python -u tools/exchange_trace.py --batch 1024 8192 --worlds 1 --steps 16 > $O/${T}_tiletrace.log 2>&1
+}
+
+task_ddp() {  # the modular engine's bucketed reducer: step times per mode + overlap from kernel traces
+  cd $R && py 200 python -u tools/ddp_overlap.py > $O/${T}_ddp.log 2>&1 && \
+  cd /tmp && export TMPDIR=/tmp && \
+  for m in overlap serial; do
+    py 200 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_ddp_$m -o run -- python3 $R/tools/ddp_overlap.py --trace --mode $m --bucket-mb 0.01 > $O/${T}_ddp_$m.log 2>&1 && \
+    python3 $R/tools/ddp_overlap.py --parse $O/${T}_ddp_$m/run_kernel_trace.csv >> $O/${T}_ddp.log 2>&1 || return 1
+  done
 }
 
 pmc3() {  # pmc3 <tag> <kernel_counters.py args>
