@@ -62,6 +62,10 @@ namespace csed {
 namespace lenet {
 // (flat parameter order, slab and vector-slab layouts: kernels/lenet_layout.h)
 constexpr int LD_DC2 = 72, LD_DC1 = 592;
+// P1 / I1 channel pitch: 144 pixels + 4, so the 10 channels of one pixel fall on distinct banks (the
+// conv1 epilogue's writes and the wgrad / dgrad-reduce gathers; 144 put them on 4 banks,
+// tools/lds_bank_model.py: 586 -> 268 extra LDS cycles per workgroup)
+constexpr int LD_P1 = 148;
 constexpr int NT = 1024, NW = 16;  // 16 waves, 4 per SIMD
 
 // LDS carve (bytes); every region 16-B aligned
@@ -71,9 +75,9 @@ constexpr int S_F1 = (I_F1 - I_W2C) * 2;              // u16 51*328  fc1 weight 
 // W2C | W2D | F1 are contiguous here exactly as in the global image: one flat copy
 constexpr int WIMG_LDS_U4 = (I_END - I_W2C) / 8;      // 16-byte vectors to stage
 constexpr int S_X = (I_END - I_W2C) * 2;              // u16 784 (+16 pad)
-constexpr int S_P1 = S_X + 800 * 2;                   // u16 1440   [ic][12][12]
-constexpr int S_I1 = S_P1 + 1440 * 2;                 // u8 1440    argmax in window
-constexpr int S_P2 = S_I1 + 1440;                     // u16 320    [oc][4][4] = fc1 input
+constexpr int S_P1 = S_X + 800 * 2;                   // u16 10*148 [ic][12][12] (pitch LD_P1)
+constexpr int S_I1 = S_P1 + 10 * LD_P1 * 2;           // u8 10*148  argmax in window
+constexpr int S_P2 = S_I1 + (10 * LD_P1 + 15) / 16 * 16;  // u16 320  [oc][4][4] = fc1 input
 constexpr int S_I2 = S_P2 + 320 * 2;                  // u8 320
 constexpr int S_P1H = S_I2 + 320;                     // u16 12*320 P1 again, HWC [12][P1H_RP] (16 of 24 used)
 constexpr int S_DC2 = S_P1H + 12 * P1H_RP * 2;       // u16 32*72  dL/dconv2 [oc][pix]
@@ -150,7 +154,7 @@ __device__ __forceinline__ void dgrad_store(unsigned short* DC1, int ci, int mm,
 template <typename T>
 __device__ __forceinline__ void dgrad_out(unsigned short* DC1, const unsigned short* P1, const uint8_t* I1,
                                           int ci, int mm, float v) {
-  const int pi = ci * 144 + mm;
+  const int pi = ci * LD_P1 + mm;
   dgrad_store<T>(DC1, ci, mm, f16v<T>(P1[pi]) > 0.f ? v : 0.f, I1[pi]);
 }
 
@@ -467,7 +471,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   int kwb[1];
   {
     const int k = min(wave * 16 + l16, 249), ic = k / 25, r = k % 25;
-    kwb[0] = ic * 144 + (r / 5) * 12 + (r % 5);
+    kwb[0] = ic * LD_P1 + (r / 5) * 12 + (r % 5);
   }
   // conv1 wgrad B column k = (wave&1)*16 + l16 = kh*5 + kw: X offset
   const int kc1 = (wave & 1) * 16 + l16;
@@ -604,8 +608,8 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
               if (c[it][r] > best) { best = c[it][r]; bi = r; }
             const int w = (wave + it * NW) * 4 + kq;  // pooled position py*12 + px
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
-            P1[l16 * 144 + w] = hv;
-            I1[l16 * 144 + w] = (uint8_t)bi;
+            P1[l16 * LD_P1 + w] = hv;
+            I1[l16 * LD_P1 + w] = (uint8_t)bi;
             P1H[ho[it] + l16] = hv;
           }
         }
@@ -849,26 +853,24 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           c[tt] = Mfma<T>::mma(dz1, __builtin_bit_cast(frag, __builtin_shufflevector(r[tt][2], r[tt][3], 0, 1, 2, 3, 4, 5, 6, 7)),
                                c[tt]);
         }
-        if (lane < 16) {
+        // Every C row is dP2 (A holds dZ1 in every row), so lane kq*16 + w holds dP2[t][w] as
+        // well as lane w: the four lane groups write the unpool window's four positions (DC2H)
+        // and two of them its two rows (DC2) in one instruction each, instead of lanes 0-15
+        // writing all six (4-way bank conflicts on the DC2H rows, tools/lds_bank_model.py)
 #pragma unroll
-          for (int tt = 0; tt < NTT; ++tt) {
-            const int t = wave + NW * tt;
-            // C row 0: lane w holds dP2[t][w]; unpool window w of channel t
-            const int pi = t * 16 + lane;
-            const float gv = f16v<T>(P2[pi]) > 0.f ? c[tt][0] * D2S[t] : 0.f;
-            const int bi = I2[pi];
-            const int oh0 = 2 * (lane >> 2), ow0 = 2 * (lane & 3);
-            const uint32_t hg = h16<T>(gv);
-#pragma unroll
-            for (int dy = 0; dy < 2; ++dy)  // window rows: aligned 32-bit pairs of DC2
-              reinterpret_cast<uint32_t*>(DC2 + t * LD_DC2 + (oh0 + dy) * 8 + ow0)[0] =
-                  bi == 2 * dy ? hg : (bi == 2 * dy + 1 ? hg << 16 : 0u);
-#pragma unroll
-            for (int pos = 0; pos < 4; ++pos) {
-              const int oh = oh0 + (pos >> 1), ow = ow0 + (pos & 1);
-              DC2H[(oh + 4) * DC2H_RP + (ow + 4) * DG_OCP + t] = pos == bi ? (unsigned short)hg : (unsigned short)0;
-            }
-          }
+        for (int tt = 0; tt < NTT; ++tt) {
+          const int t = wave + NW * tt;
+          // unpool window w = l16 of channel t
+          const int pi = t * 16 + l16;
+          const float gv = f16v<T>(P2[pi]) > 0.f ? c[tt][0] * D2S[t] : 0.f;
+          const int bi = I2[pi];
+          const int oh0 = 2 * (l16 >> 2), ow0 = 2 * (l16 & 3);
+          const uint32_t hg = h16<T>(gv);
+          if (kq < 2)  // window row dy = kq: an aligned 32-bit pair of DC2
+            reinterpret_cast<uint32_t*>(DC2 + t * LD_DC2 + (oh0 + kq) * 8 + ow0)[0] =
+                bi == 2 * kq ? hg : (bi == 2 * kq + 1 ? hg << 16 : 0u);
+          const int oh = oh0 + (kq >> 1), ow = ow0 + (kq & 1);  // window position kq
+          DC2H[(oh + 4) * DC2H_RP + (ow + 4) * DG_OCP + t] = kq == bi ? (unsigned short)hg : (unsigned short)0;
         }
       };
       static_assert(20 - NW == 4, "dP2: 2 channels on waves 0-3, 1 on the rest");
@@ -889,7 +891,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         const int kc = min(k, 249), ic = kc / 25, r = kc - 25 * ic;
         // B fragment of K-step ps, lane group kq: output row 4*ps + kq, pixels 0..7 of it:
         // P1 row (4*ps + kq + kh), columns kw .. kw+7 -> two runs of 8 at immediate offsets
-        const unsigned short* pb = P1 + ic * 144 + (r / 5) * 12 + (r % 5) + kq * 12;
+        const unsigned short* pb = P1 + ic * LD_P1 + (r / 5) * 12 + (r % 5) + kq * 12;
         uint32_t rv0[8], rv1[8];
         rv0[0] = lds_u16<0>(pb); rv0[1] = lds_u16<1>(pb); rv0[2] = lds_u16<2>(pb); rv0[3] = lds_u16<3>(pb);
         rv0[4] = lds_u16<4>(pb); rv0[5] = lds_u16<5>(pb); rv0[6] = lds_u16<6>(pb); rv0[7] = lds_u16<7>(pb);
@@ -988,9 +990,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       STAMP(7);
       if (tid < T3 * 256) {
         // dgrad: fixed-order sum of the K parts, then the relu / pool1 backward into DC1
-        const int ts = tid >> 8, idx = tid & 255, row = idx >> 4, ci = idx & 15;
+        // thread -> partial element e (row 4*((e >> 4) & 3) + (e >> 6), channel e & 15: the MFMA
+        // output layout), so each 32-lane half reads 32 consecutive words (thread -> (row, ch)
+        // read rows 64 words apart on one bank, tools/lds_bank_model.py)
+        const int ts = tid >> 8, e = tid & 255, ci = e & 15, row = 4 * ((e >> 4) & 3) + (e >> 6);
         if (ci < 10) {
-          const int e = (row & 3) * 64 + (row >> 2) * 16 + ci;
           float pv[6];
 #pragma unroll
           for (int q = 0; q < 6; ++q) pv[q] = SCR[(ts * P + q) * 256 + e];  // (q >= P: in bounds, unused)
@@ -1062,7 +1066,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
         uint8_t gi[4];
   #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int pi = ci * 144 + wave * 16 + 4 * kq + r;
+          const int pi = ci * LD_P1 + wave * 16 + 4 * kq + r;
           gp[r] = P1[pi];
           gi[r] = I1[pi];
         }

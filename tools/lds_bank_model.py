@@ -7,7 +7,8 @@ banking rules (MI355X_MICROARCH.md §LDS: lane groups per instruction width, ban
 extra LDS cycles per access site, i.e. what SQ_LDS_BANK_CONFLICT attributes to
 each.  Used to choose layouts without a GPU run.
 
-    python tools/lds_bank_model.py            # per-site report for the kernel's layout
+    python tools/lds_bank_model.py            # per-site report, split step (B <= 64, KS = 4)
+    python tools/lds_bank_model.py --unsplit  # the one-workgroup-per-sample path (older sites)
     python tools/lds_bank_model.py --search   # search a dgrad K-slice order (kDgOrder)
 """
 import os
@@ -18,16 +19,17 @@ from collections import defaultdict
 # ---- layout constants (mirror lenet_fused.hip)
 LD_W2C, LD_F1 = 432, 328
 LD_P1H, DG_OCP, LD_DC2, LD_DC1 = 24, 24, 72, 592
+LD_P1 = 148  # P1 / I1 channel pitch (elements, lenet_fused.hip)
 DC2H_RP = 16 * 24 + 32  # DC2H row pitch (elements)
 P1H_RP = 12 * 24 + 32   # P1H row pitch (elements)
 DG_CH = 77  # dgrad B image is chunk-major [chunk][16 rows][8]
 S_W2C = 0
 S_W2D = 21 * LD_W2C * 2
 S_F1 = S_W2D + DG_CH * 16 * 16
-S_X = 73728
+S_X = 65536  # (I_END - I_W2C) * 2
 S_P1 = S_X + 1600
-S_I1 = S_P1 + 2880
-S_P2 = S_I1 + 1440
+S_I1 = S_P1 + 10 * LD_P1 * 2
+S_P2 = S_I1 + (10 * LD_P1 + 15) // 16 * 16
 S_I2 = S_P2 + 640
 S_P1H = S_I2 + 320
 S_DC2 = S_P1H + 12 * P1H_RP * 2
@@ -212,8 +214,8 @@ def site_conv1_epilogue():
                 continue
             act = [l16 < 10 for lane, l16, kq in lanes()]
             w = [mt * 4 + kq for lane, l16, kq in lanes()]
-            p1 = [S_P1 + 2 * (l16 * 144 + w[lane]) for lane, l16, kq in lanes()]
-            i1 = [S_I1 + (l16 * 144 + w[lane]) for lane, l16, kq in lanes()]
+            p1 = [S_P1 + 2 * (l16 * LD_P1 + w[lane]) for lane, l16, kq in lanes()]
+            i1 = [S_I1 + (l16 * LD_P1 + w[lane]) for lane, l16, kq in lanes()]
             p1h = [S_P1H + 2 * ((w[lane] // 12) * P1H_RP + (w[lane] % 12) * LD_P1H + l16)
                    for lane, l16, kq in lanes()]
             tot += extra_cycles(p1, 2, "write", act) + extra_cycles(i1, 1, "write", act) + \
@@ -230,7 +232,7 @@ def site_conv2_wgrad_gather():
             for lane, l16, kq in lanes():
                 k = min((wave + 8 * jj) * 16 + l16, 249)
                 ic, r = k // 25, k % 25
-                row.append(ic * 144 + (r // 5) * 12 + r % 5)
+                row.append(ic * LD_P1 + (r // 5) * 12 + r % 5)
             kwb.append(row)
         for ps in range(2):
             for jj in range(2):
@@ -292,6 +294,194 @@ def site_dgrad_store():
     return tot
 
 
+# ---------------------------------------------------------------- split step (KS = 4, B <= 64)
+# The headline path: 4 workgroups per sample (part = 0..3), 16 waves each.  Sites per workgroup,
+# averaged over the 4 parts (lenet_fused.hip stages 1-8, split branch).
+DG_KS = 19
+LD_DC2_ = LD_DC2
+S_COFF = S_DC1 + 16 * LD_DC1 * 2
+S_DOFF = S_COFF + 4 * 16 * 2
+S_DZ1B = S_DOFF + 4 * 24 * 2
+S_F = S_DZ1B + 64 * 2
+S_W1C = S_F + 2816 * 4
+S_LABEL = S_W1C + 16 * 32 * 2
+S_DBG = S_LABEL + 16
+S_C1T = S_DBG + 32 * 8
+S_C1H = S_C1T + 1024 * 8
+S_XC = S_C1H + 1024 * 8
+XC_LD = 800
+S_CONSTB = S_XC + 3 * XC_LD * 2
+S_I2 = S_P2 + 640
+
+
+def split_conv1_gather():  # stage 1: 36 tiles, 8 ds_read_u16 each
+    koff = [(k // 5) * 28 + (k % 5) if k < 25 else 0 for k in range(32)]
+    tot = 0
+    for mt in range(36):
+        for j in range(8):
+            addrs = []
+            for lane, l16, kq in lanes():
+                m = mt * 16 + l16
+                p, q = m >> 2, m & 3
+                pb = (2 * (p // 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1)
+                # r1 = pb + 28 kq + {0..4}; r2 = pb + 112 + (kq == 1 ? 2 : 0) + {0..2}
+                off = pb + 28 * kq + j if j < 5 else pb + 112 + (2 if kq == 1 else 0) + (j - 5)
+                addrs.append(S_X + 2 * off)
+            tot += extra_cycles(addrs, 2)
+    return tot
+
+
+def split_conv1_epilogue():
+    tot = 0
+    for mt in range(36):
+        act = [l16 < 10 for lane, l16, kq in lanes()]
+        w = [mt * 4 + kq for lane, l16, kq in lanes()]
+        p1 = [S_P1 + 2 * (l16 * LD_P1 + w[lane]) for lane, l16, kq in lanes()]
+        i1 = [S_I1 + (l16 * LD_P1 + w[lane]) for lane, l16, kq in lanes()]
+        p1h = [S_P1H + 2 * ((w[lane] // 12) * P1H_RP + (w[lane] % 12) * LD_P1H + l16) for lane, l16, kq in lanes()]
+        tot += extra_cycles(p1, 2, "write", act) + extra_cycles(i1, 1, "write", act) + \
+            extra_cycles(p1h, 2, "write", act)
+    return tot
+
+
+def split_conv2_epilogue():  # stage 2: P2 / I2 writes
+    tot = 0
+    for wave in range(8):
+        mt, nt = wave & 3, wave >> 2
+        act = [nt * 16 + l16 < 20 for lane, l16, kq in lanes()]
+        p2 = [S_P2 + 2 * ((nt * 16 + l16) * 16 + mt * 4 + kq) for lane, l16, kq in lanes()]
+        i2 = [S_I2 + ((nt * 16 + l16) * 16 + mt * 4 + kq) for lane, l16, kq in lanes()]
+        tot += extra_cycles(p2, 2, "write", act) + extra_cycles(i2, 1, "write", act)
+    return tot
+
+
+def split_fc1():  # stage 3: waves 0-3, 10 K-steps (A = P2 broadcast row)
+    tot = 0
+    for wave in range(4):
+        for ks in range(10):
+            pa = [S_P2 + 2 * (ks * 32 + 8 * kq) for lane, l16, kq in lanes()]
+            fb = [S_F1 + 2 * (min(wave * 16 + l16, 50) * LD_F1 + 8 * kq + ks * 32) for lane, l16, kq in lanes()]
+            tot += extra_cycles(pa, 16) + extra_cycles(fb, 16)
+    return tot
+
+
+def split_stage5_tr():  # dP2: transposed fc1 reads (ds_read_b64_tr_b16), 20 channel tiles
+    tot = 0
+    for t in range(20):
+        for base in (0, 4, 32, 36):
+            addrs = [S_F1 + 2 * (min(base + 8 * kq + (l16 >> 2), 50) * LD_F1 + 4 * (l16 & 3) + t * 16)
+                     for lane, l16, kq in lanes()]
+            tot += extra_cycles(addrs, 8)
+    return tot
+
+
+def split_stage5_writes():  # lane group kq writes window position kq (DC2H) / row kq < 2 (DC2)
+    tot = 0
+    for t in range(20):
+        act = [(lane >> 4) < 2 for lane in range(64)]
+        dc2, dc2h = [], []
+        for lane, l16, kq in lanes():
+            oh0, ow0 = 2 * (l16 >> 2), 2 * (l16 & 3)
+            dc2.append(S_DC2 + 2 * (t * LD_DC2 + (oh0 + (kq & 1)) * 8 + ow0))
+            dc2h.append(S_DC2H + 2 * ((oh0 + (kq >> 1) + 4) * DC2H_RP + (ow0 + (kq & 1) + 4) * DG_OCP + t))
+        tot += extra_cycles(dc2, 4, "write", act) + extra_cycles(dc2h, 2, "write")
+    return tot
+
+
+def split_conv2_wgrad(part):  # stage 6, waves 12-15: one N-tile each
+    tot = 0
+    for w in range(4):
+        kk = [min((4 * part + w) * 16 + l16, 249) for lane, l16, kq in lanes()]
+        for j in list(range(8)) + list(range(48, 56)):
+            addrs = [S_P1 + 2 * ((kk[lane] // 25) * LD_P1 + ((kk[lane] % 25) // 5) * 12 + (kk[lane] % 25) % 5 + kq * 12 + j)
+                     for lane, l16, kq in lanes()]
+            tot += extra_cycles(addrs, 2)
+        for row0, col in ((0, 0), (16, 0), (0, 32), (16, 32)):
+            addrs = [S_DC2 + 2 * ((row0 + l16) * LD_DC2 + col + 8 * kq) for lane, l16, kq in lanes()]
+            tot += extra_cycles(addrs, 16)
+    return tot
+
+
+def split_dgrad(part):  # stage 6, waves 0-11: T3 tiles x P K-parts, <= 5 K-steps each
+    tab = dgrad_offsets()
+    T3 = 3 if part == 0 else 2
+    P = 4 if T3 == 3 else 6
+    tot = 0
+    for wave in range(12):
+        ts, pp = wave % T3, wave // T3
+        ks0, ks1 = pp * DG_KS // P, (pp + 1) * DG_KS // P
+        for u in range(5):
+            ks = ks0 + u
+            a_ = []
+            b_ = []
+            for lane, l16, kq in lanes():
+                mw = (part + 4 * ts) * 16 + l16
+                a_.append(S_DC2H + 2 * ((mw // 12) * DC2H_RP + (mw % 12) * DG_OCP + tab[kq, min(ks, DG_KS - 1)]))
+                b_.append(S_W2D + 2 * ((((4 * ks + kq) * 16 + l16) * 8) if ks < ks1 else ((DG_CH - 1) * 16 + l16) * 8))
+            tot += extra_cycles(a_, 16) + extra_cycles(b_, 16)
+        for r in range(4):
+            tot += extra_cycles([S_C1T + 4 * ((ts * P + pp) * 256 + r * 64 + lane) for lane in range(64)], 4, "write")
+    return tot
+
+
+def split_dgrad_reduce(part):  # stage 7: sum of the K parts + relu / pool1 backward into DC1
+    T3 = 3 if part == 0 else 2
+    P = 4 if T3 == 3 else 6
+    tot = 0
+    for wv in range(T3 * 4):
+        tids = range(wv * 64, wv * 64 + 64)
+        ts = [t >> 8 for t in tids]
+        e = [t & 255 for t in tids]  # thread -> partial element (MFMA output layout)
+        row = [4 * ((x >> 4) & 3) + (x >> 6) for x in e]
+        ci = [x & 15 for x in e]
+        act = [c < 10 for c in ci]
+        for q in range(6):
+            tot += extra_cycles([S_C1T + 4 * ((ts[i] * P + q) * 256 + e[i]) for i in range(64)], 4, "read", act)
+        mm = [(part + 4 * ts[i]) * 16 + row[i] for i in range(64)]
+        tot += extra_cycles([S_P1 + 2 * (ci[i] * LD_P1 + mm[i]) for i in range(64)], 2, "read", act)
+        tot += extra_cycles([S_I1 + (ci[i] * LD_P1 + mm[i]) for i in range(64)], 1, "read", act)
+        for d in (0, 24):
+            tot += extra_cycles([S_DC1 + 2 * (ci[i] * LD_DC1 + 2 * (mm[i] // 12) * 24 + 2 * (mm[i] % 12) + d)
+                                 for i in range(64)], 4, "write", act)
+    return tot
+
+
+def split_conv1_wgrad():  # stage 8, waves 0-11: 3 K-steps each (DC1 A fragment + X runs)
+    tot = 0
+    for wave in range(12):
+        for i in range(3):
+            ps = min((wave >> 1) + 6 * i, 17)
+            tot += extra_cycles([S_DC1 + 2 * (l16 * LD_DC1 + ps * 32 + 8 * kq) for lane, l16, kq in lanes()], 16)
+            for half in range(2):
+                addrs = []
+                for lane, l16, kq in lanes():
+                    kc1 = (wave & 1) * 16 + l16
+                    p0 = ps * 32 + 8 * kq
+                    oh, ow0 = p0 // 24, p0 % 24
+                    if kc1 < 25:
+                        ee = oh * 28 + ow0 + (kc1 // 5) * 28 + kc1 % 5
+                        c = ee & 3
+                        base = S_X if c == 0 else S_XC + 2 * (c - 1) * XC_LD
+                        addrs.append(base + 2 * (ee - c) + 8 * half)
+                    else:
+                        addrs.append(S_CONSTB + 2 * (8 if kc1 == 25 else 0) + 8 * half)
+                tot += extra_cycles(addrs, 8)
+    return tot
+
+
+def _avg_parts(fn):
+    return lambda: round(sum(fn(p) for p in range(4)) / 4)
+
+
+SPLIT_SITES = [("conv1 gathers (u16)", split_conv1_gather), ("conv1 epilogue writes", split_conv1_epilogue),
+               ("conv2 A (b128)", site_conv2_A), ("conv2 B (b128)", site_conv2_B),
+               ("conv2 epilogue writes", split_conv2_epilogue), ("fc1 A / B (b128)", split_fc1),
+               ("dP2 transposed reads", split_stage5_tr), ("stage5 DC2/DC2H writes", split_stage5_writes),
+               ("conv2 wgrad (waves 12-15)", _avg_parts(split_conv2_wgrad)),
+               ("dgrad A / B + partial writes", _avg_parts(split_dgrad)),
+               ("dgrad reduce + DC1 scatter", _avg_parts(split_dgrad_reduce)),
+               ("conv1 wgrad DC1 + X runs", split_conv1_wgrad)]
+
 SITES = [("dgrad A (b128)", site_dgrad_A), ("dgrad B (b128)", site_dgrad_B), ("conv2 A (b128)", site_conv2_A),
          ("conv2 B (b128)", site_conv2_B), ("conv1 gathers (u16)", site_conv1_gather),
          ("conv1 epilogue writes", site_conv1_epilogue), ("conv2 wgrad gathers (u16)", site_conv2_wgrad_gather),
@@ -304,6 +494,9 @@ if __name__ == "__main__":
         print(f"dgrad A extra cycles {cost} with order {order}")
         sys.exit(0)
     total = 0
+    if "--unsplit" not in sys.argv:  # default: the split step (B <= 64)
+        SITES = SPLIT_SITES
+        print("split step (KS = 4), per workgroup, averaged over the 4 parts")
     for name, fn in SITES:
         v = fn()
         total += v
