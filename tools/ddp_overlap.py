@@ -84,7 +84,7 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None) -> list[dic
         e1.record()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / steps
-        rows.append({"mode": mode, "bucket_mb": cap, "buckets": len(ddp.buckets),
+        rows.append({"mode": mode, "batch": batch, "bucket_mb": cap, "buckets": len(ddp.buckets),
                      "us_per_step_gpu": round(e0.elapsed_time(e1) * 1000 / steps, 2),
                      "us_per_step_wall": round(wall * 1e6, 2)})
         for h in ddp._hooks:
@@ -100,7 +100,7 @@ def parse(path: str) -> dict:
         for r in csv.DictReader(f):
             ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]))
     ks.sort()
-    comm = [k for k in ks if "nccl" in k[3].lower() or "rccl" in k[3].lower()]
+    comm = [k for k in ks if any(x in k[3].lower() for x in ("nccl", "rccl", "onerankreduce", "allreduce"))]
     comp = [k for k in ks if k not in comm and "rocclr" not in k[3]]
     tot = ov = 0
     for s, e, st, _ in comm:

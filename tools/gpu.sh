@@ -84,9 +84,10 @@ task_tiletrace() {
 
 task_ddp() {  # the modular engine's bucketed reducer: step times per mode + overlap from kernel traces
   cd $R && py 200 python -u tools/ddp_overlap.py > $O/${T}_ddp.log 2>&1 && \
+  py 300 python -u tools/ddp_overlap.py --batch 4096 --steps 50 >> $O/${T}_ddp.log 2>&1 && \
   cd /tmp && export TMPDIR=/tmp && \
   for m in overlap serial; do
-    py 200 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_ddp_$m -o run -- python3 $R/tools/ddp_overlap.py --trace --mode $m --bucket-mb 0.01 > $O/${T}_ddp_$m.log 2>&1 && \
+    py 200 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_ddp_$m -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 4096 --mode $m --bucket-mb 0.01 > $O/${T}_ddp_$m.log 2>&1 && \
     python3 $R/tools/ddp_overlap.py --parse $O/${T}_ddp_$m/run_kernel_trace.csv >> $O/${T}_ddp.log 2>&1 || return 1
   done
 }
