@@ -52,16 +52,25 @@ namespace lenet_tile {
 using namespace csed::lenet;
 constexpr int TS = 4;               // samples per tile
 constexpr int NT = 1024, NW = 16;   // 16 waves, 4 per SIMD
-constexpr int X_LD = 800;           // u16 per sample image (784 + pad)
+constexpr int X_LD = 804;           // u16 per sample image (784 + pad; pitches: see XCP)
 // The normalised images are kept twice, the second copy shifted left by one pixel (X_1[i] =
 // X[i + 1]): any run of pixels X[o ..] is then 4-byte aligned in copy o & 1, so the conv1 A
 // operand (stage 1) and the conv1 wgrad B operand (stage 7), 5 / 3 / 8-pixel runs at every
 // alignment, are read as dwords instead of one ds_read_u16 per pixel.  (Four copies, for 8-byte
-// alignment, do not fit next to the weight images.)  Copy pitch 1602 dwords (== 2 mod 32).
-constexpr int XCP = TS * X_LD + 4;
+// alignment, do not fit next to the weight images.)  Sample pitch 402 dwords and copy pitch 1624
+// dwords: tools/lds_bank_model_tile.py puts the conv1 A reads at no bank conflicts and the conv1
+// wgrad X runs at 1.4k extra LDS cycles per tile (800 / +4: 0.9k and 2.5k).
+constexpr int XCP = TS * X_LD + 32;
 constexpr int P1H_SZ = 12 * P1H_RP; // u16 per sample: pool1 output, HWC [12][P1H_RP] (channels 10-23 zero)
-constexpr int DC2_LD = 72, DC2_SZ = 20 * DC2_LD;  // dL/dconv2 [oc][64 px] (+pad), wgrad A operand
-constexpr int DCH_SZ = 64 * DG_OCP;              // dL/dconv2 HWC interior [64 pos][24 ch], dgrad A operand
+// dL/dconv2 [oc][64 px] (+pad), wgrad A operand, and its HWC interior [64 pos][24 ch], dgrad A
+// operand.  Row pitch 80 and the sample strides' pads (tools/lds_bank_model_tile.py): the wgrad A
+// reads conflict-free (72: 512 extra LDS cycles per tile) and stage 5's DC2 / DCH writes of two
+// samples per 32-lane half on different banks (1200 -> 480)
+constexpr int DC2_LD = 80, DC2_SZ = 20 * DC2_LD + 24;
+constexpr int DCH_SZ = 64 * DG_OCP + 120;
+// pool1 argmax codes [10][144] per sample, channel pitch 148: the conv1 epilogue's writes and the
+// dgrad's reads of 10 channels per lane group on distinct banks (144: 4 banks; 360 extra LDS cycles)
+constexpr int I1_LD = 148, I1_SZ = 10 * I1_LD;
 constexpr int F_D2S = 0, F_D1S = TS * 20, F_H = F_D1S + TS * 52, F_LAB = F_H + TS * 64, F_LOSS = F_LAB + TS,
               F_END = (F_LOSS + 2 * TS + 3) / 4 * 4;
 // dynamic LDS carve (bytes)
@@ -73,8 +82,8 @@ constexpr int D_ONES = D_DGT + 4 * 20 * 4;      // u16 [192] 1.0: the wgrads' bi
 constexpr int D_ZERO = D_ONES + 192 * 2;        // u16 [192] 0: padding columns, out-of-image dgrad taps
 constexpr int D_X = D_ZERO + 192 * 2;           // u16 [2 copies][XCP]: [TS][X_LD] normalised pixels
 constexpr int D_P1H = D_X + (2 * XCP * 2 + 15) / 16 * 16;  // u16 [TS][P1H_SZ]
-constexpr int D_I1 = D_P1H + TS * P1H_SZ * 2;   // u8  [TS][10][144] pool1 argmax
-constexpr int D_P2 = D_I1 + TS * 1440;          // u16 [TS][320] fc1 input
+constexpr int D_I1 = D_P1H + TS * P1H_SZ * 2;   // u8  [TS][10][I1_LD] pool1 argmax
+constexpr int D_P2 = D_I1 + TS * I1_SZ;         // u16 [TS][320] fc1 input
 constexpr int D_I2 = D_P2 + TS * 320 * 2;       // u8  [TS][320] pool2 argmax
 constexpr int D_F = D_I2 + TS * 320;            // f32 [F_END] masks, fc1 output, labels, loss
 constexpr int D_DZ1B = D_F + F_END * 4;         // u16 [TS][64] dZ1 (dP2's A rows)
@@ -351,7 +360,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       const unsigned short* xe1 = X + o1 + 4;
       const uint32_t* xr2 = reinterpret_cast<const uint32_t*>(X + (o2 & 1) * XCP + (o2 & ~1));
       const unsigned short* xe2 = X + o2 + 2;
-      const int pl = kq * LD_P1H + min(l16, 9), il = min(l16, 9) * 144 + kq;  // P1H / I1 lane parts
+      const int pl = kq * LD_P1H + min(l16, 9), il = min(l16, 9) * I1_LD + kq;  // P1H / I1 lane parts
 #pragma unroll
       for (int grp = 0; grp < 3; ++grp) {
         uint32_t r0[3], r1[3], e4[3], r2[3], e2[3];
@@ -378,7 +387,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
             const unsigned short hv = h16<T>(fmaxf(best + cb, 0.f));
             P1H[wsmp * P1H_SZ + mt3 * P1H_RP + (4 * mtr) * LD_P1H + pl] = hv;
             // argmax of the window, or 4 where the relu gate (stored pool1 output > 0) is shut
-            I1[wsmp * 1440 + 4 * (3 * mt3 + mtr) + il] = (uint8_t)((hv & 0x7fff) ? bi : 4);
+            I1[wsmp * I1_SZ + 4 * (3 * mt3 + mtr) + il] = (uint8_t)((hv & 0x7fff) ? bi : 4);
           }
         }
       }
@@ -711,7 +720,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
         uint32_t bis[NTL];
 #pragma unroll
         for (int i = 0; i < NTL; ++i)
-          bis[i] = *reinterpret_cast<const uint32_t*>(I1 + si[i] * 1440 + ic * 144 + p0[i]);
+          bis[i] = *reinterpret_cast<const uint32_t*>(I1 + si[i] * I1_SZ + ic * I1_LD + p0[i]);
         lds_barrier();
         // pool1 backward: each pooled pixel's gradient goes to its window's argmax position of
         // dL/dconv1 (dense [ic][24 x 24]); this lane's 4 pooled pixels are 8 consecutive conv1

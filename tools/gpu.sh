@@ -21,6 +21,8 @@
 #             comm stream vs after backward, step times + overlap share from kernel traces
 #   ab        same-box A/B of ab/A_C.so vs ab/B_C.so (tools/ab_build.sh REV) at global batch
 #             64 and 8 (+ AB_ARGS), N_AB alternations (default 3)
+#   abtile    same-box A/B of ab/A_C.so vs ab/B_C.so at global batch 1024 / 8192 fp16 (lenet_tile)
+#   pmctile   the three PMC passes over the tile kernel only (B = 1024)
 #   abenv     same-box A/B of one build under ENV_A vs ENV_B (BENCH_ARGS / AB_ARGS / N_AB)
 TASKS=${1:?task list}
 T=${2:-run}
@@ -110,6 +112,18 @@ task_ab() {
   for i in $(seq ${N_AB:-3}); do for b in 64 8; do for v in A B; do
     echo "$v B=$b $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py --global-batch $b --steps 3000 --warmup 300 --no-epoch $AB_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_ab.log || return 1
   done; done; done
+}
+
+task_abtile() {  # same-box A/B of ab/A_C.so vs ab/B_C.so on the large-batch step (B = 1024 / 8192 fp16)
+  cd $R && rm -f $O/${T}_abtile.log && \
+  for i in $(seq ${N_AB:-3}); do for v in A B; do
+    echo "$v B=1024 $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py --global-batch 1024 --dtype fp16 --steps 400 --warmup 40 --no-epoch 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abtile.log || return 1
+    echo "$v B=8192 $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py --global-batch 8192 --dtype fp16 --steps 60 --warmup 6 --no-epoch 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abtile.log || return 1
+  done; done
+}
+
+task_pmctile() {
+  pmc3 ${T}_pmc1024 1024 100
 }
 
 task_abenv() {
