@@ -356,6 +356,8 @@ csed::LenetTrainArgs train_args(const Tensor& images, const Tensor& labels, cons
   if (dbg.has_value()) {
     TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= 32 * grid, "dbg: int64 [grid*32]");
     a.dbg = (uint64_t*)dbg->data_ptr<int64_t>();
+    // a buffer of >= 48 x grid words also takes every wave's entry stamp (after the 32 x grid)
+    if (dbg->numel() >= 48 * grid) a.dbg_entry = a.dbg + 32 * grid;
   }
   TORCH_CHECK(xstage.has_value() == lstage.has_value(), "lenet_train: xstage and lstage go together");
   if (xstage.has_value()) {

@@ -218,6 +218,7 @@ __device__ constexpr SplitNeed kSplitNeed = split_need_table();
 template <typename T, bool TRAIN, bool STAGED, int KS = 1>
 __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, int write_logp, float* logp_out) {
   static_assert(KS == 1 || (KS == SPLIT_K && STAGED && TRAIN), "split step: staged training only");
+  const uint64_t t_entry = __builtin_amdgcn_s_memtime();  // (diagnostics: a.dbg_entry)
   struct TrainKargs { LenetTrainArgs a; int write_logp; float* logp_out; };
   prefetch_kernargs<(int)sizeof(TrainKargs)>();
   // Two LDS objects: the weight images (static, filled by LDS-DMA) and the
@@ -292,7 +293,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   // (a global-space load: a flat load would also count in lgkmcnt, and the next wait for the
   // argument loads would wait for it)
   typedef const __attribute__((address_space(1))) int64_t* gptr64;
-  const uint64_t rng_ctr = (uint64_t)((gptr64)rngp)[opaque(0)];
+  // (staged: loaded by waves 8-15, the only ones that use it, in their role branch: a load at the
+  // top left its registers pending in waves 4-7, which reused them and waited, vmcnt, for the
+  // top loads before issuing their own operand loads -- one memory round trip more in front of
+  // the preamble's barrier)
+  uint64_t rng_ctr = STAGED ? 0 : (uint64_t)((gptr64)rngp)[opaque(0)];
   // Stage 0's LDS work (the preamble's, for a staged sample): zero the HWC conv1 image (thread
   // i of 512) -- conv1 writes channels 0-9 of each position at stage 1; channels 10-15 meet zero
   // conv2 weights in the K sum, so they must hold finite values (zero), not whatever the LDS
@@ -317,7 +322,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   const int nsamp = STAGED ? 1 : (g < a.B ? (a.B - g + G - 1) / G : 0);
   // (staged: a deferred per-lane load, only the next-step row needs it; the multi-sample path
   // reads every sample's row through it, as scalars)
-  const int64_t pbase = (a.cursor ? (STAGED ? a.cursor[opaque(0)] : a.cursor[0]) : 0) * (int64_t)a.B + b0;
+  // (staged: the cursor is a deferred per-lane load in the role branch of the waves that stage the
+  // next step's row, unconditional from a zero word when there is none; the multi-sample path
+  // reads every sample's row through pbase, as scalars)
+  const int64_t* curp = a.cursor ? a.cursor : &kZeroWord;
+  int64_t pbase = STAGED ? (int64_t)b0 : (a.cursor ? a.cursor[0] : 0) * (int64_t)a.B + b0;
   auto perm_at = [&](int s) { return a.perm[min(pbase + (int64_t)s * G, a.perm_len - 1)]; };
 
   if (a.dbg && tid == 0) {
@@ -406,7 +415,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     }
     // the next step's row (batch staging); an opaque lane offset keeps it a VGPR (a
     // uniform load is moved to an SGPR right away, i.e. waited for here)
-    if (KS == 1 && stage_next) nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
+    if (KS == 1 && stage_next) {
+      pbase = ((gptr64)curp)[opaque(0)] * (int64_t)a.B + b0;
+      nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
+    }
     lds_barrier();
     if (t < 64) {
       // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
@@ -440,6 +452,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     asm volatile("" ::"v"(pv[0]), "v"(pv[1]), "v"(pv[2]), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(px0),
                  "v"(lab0), "v"(kg));
   } else {
+    // staged: the dropout counter and (split step) the cursor, issued ahead of the barrier like
+    // waves 4-7's loads (after it they would queue behind the weight DMA)
+    int64_t cur = 0;
+    if (STAGED) {
+      rng_ctr = (uint64_t)((gptr64)rngp)[opaque(0)];
+      if (KS > 1) cur = ((gptr64)curp)[opaque(0)];
+    }
     lds_barrier();
     // waves 8-15 (otherwise idle here): conv1's address tables of all 1024 threads
     // (non-staged; the staged path reads kC1Tab)
@@ -452,9 +471,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       // the staged sample's stage 0, on these otherwise idle waves while waves 0-7 wait for
       // the preamble's loads: its dropout masks and the zero HWC conv1 image (see stage 0),
       // so the sample starts at conv1 with one barrier fewer
+      if (KS > 1) pbase = cur * (int64_t)a.B + b0;
       const int tz = tid - 512;
       zero_p1h(tz);
       if (tz < 70) dropout_scales(tz, b0);
+      asm volatile("" ::"v"(rng_ctr), "v"(pbase));  // retired in this branch (see waves 4-7)
     }
   }
   // non-staged batches: the first sample (cursor -> row -> pixels, label: scalar
@@ -1191,6 +1212,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     if (tid == 0) DBGS[23] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (tid < DBG_W) a.dbg[g * DBG_W + tid] = DBGS[tid];
+    if (a.dbg_entry && lane == 0) a.dbg_entry[g * NW + wave] = t_entry;
   }
 }
 

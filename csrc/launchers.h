@@ -151,6 +151,7 @@ struct LenetTrainArgs {
   int grid;
   int mfma_dtype;
   uint64_t* dbg;             // optional [grid, 16] stage stamps (diagnostics)
+  uint64_t* dbg_entry;       // optional [grid, 16]: each wave's s_memtime at kernel entry (split step)
   uint8_t* xstage;           // optional staged batch [B, 784] (grid == B): sample b = workgroup b
   int64_t* lstage;           // its labels [B]
   int stage_next;            // with xstage: also stage step cursor+1 (perm / cursor are read for it)

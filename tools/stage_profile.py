@@ -30,11 +30,12 @@ def main():
     eng = FusedLeNetTrainer(Net().to(dev), data, global_batch=B, grid=grid)
     grid = eng.grid
     eng.set_epoch_order(torch.randperm(n))
-    dbg = torch.zeros(grid * 32, dtype=torch.long, device=dev)
+    dbg = torch.zeros(grid * 48, dtype=torch.long, device=dev)  # 32 stamp slots + 16 wave entries
     for _ in range(20):
         eng.gradient(grid, dbg)
     torch.cuda.synchronize()
-    st = dbg.view(grid, 32).cpu().double()
+    st = dbg[:grid * 32].view(grid, 32).cpu().double()
+    ent = dbg[grid * 32:].view(grid, 16).cpu().double()
     # Stamps (thread 0): 12 kernel start, 10 LDS-DMA issued, 17 / 16 wave 4 start / small loads consumed,
     # 13 preamble end, 0..8 stage starts of the stamped sample (9 = dgrad inside stage 6),
     # 14 end of the stamped sample, 11 after all samples.  The stamped sample is sample 1
@@ -52,6 +53,11 @@ def main():
     dma = [(st[:, 17 + w] - st[:, 12]).median().item() for w in (1, 2, 3)]
     arr = [(st[:, 24 + w] - st[:, 12]).median().item() for w in range(8)]
     print(f"  DMA issued by waves 1-3: {dma}; waves 0-7 reach the first barrier: {arr}")
+    if ent.abs().sum() > 0:  # every wave's first instruction (s_memtime), relative to the earliest wave
+        e0 = ent.min(1, keepdim=True).values
+        rel = (ent - e0).median(0).values.tolist()
+        print("  wave entry (cycles after the workgroup's first wave): " + " ".join(f"{v:.0f}" for v in rel))
+        print(f"  kernel-start stamp (12) after the first wave's entry: {(st[:, 12] - e0[:, 0]).median().item():.0f}")
     span = (st[:, 14] - st[:, 13]).median().item()
     for name, v in zip(NAMES, med.tolist()):
         print(f"  {name:24s} {v:8.0f}  {100 * v / span:5.1f}%")
