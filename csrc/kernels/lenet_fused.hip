@@ -262,6 +262,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   };
   // normalised pixels X[4q .. 4q+3] (the shifted copies are made at stage 3)
   auto put_x = [&](int q, const u16x4& o) { *reinterpret_cast<u16x4*>(Xs + 4 * q) = o; };
+
   float* D2S = Fs + F_D2S;
   float* D1S = Fs + F_D1S;
   float* Hs = Fs + F_H;
@@ -392,20 +393,20 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
   } else if (wave < 8) {
     const int t = tid - 256;
     if (a.dbg && t == 0) DBGS[17] = __builtin_amdgcn_s_memtime();
-    // K-slice orders (constant memory) for the conv2 / dgrad A-offset tables; first, so the
-    // index math does not reuse a register of an in-flight load (a vmcnt(0) wait for all
-    // of them before this load was issued: one more serial round trip)
-    const int tq = t < 64 ? t >> 4 : (t - 64) / 24;
-    const int tks = t < 64 ? t & 15 : (t - 64) - 24 * tq;
-    const int kg = t < 64 ? (int)kC2Order.fwd[min(4 * tks + tq, 49)] : (int)kDgOrder.fwd[min(4 * tks + tq, 74)];
-    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread)
-    auto par_index = [](int q) {
-      return q < 10 ? O_C1B + q : q < 30 ? O_C2B + q - 10 : q < 80 ? O_F1B + q - 30 : q < 90 ? O_F2B + q - 80
-                                                                                          : O_F2W + q - 90;
-    };
+    // (the conv2 / dgrad A-offset tables are built by waves 8-15: with their K-order table loads
+    // and index math here, these waves reached the barrier ~700 cycles after their start,
+    // holding the operand loads below -- the preamble's critical path -- that long)
+    // fp32 params: c1b, c2b, f1b, f2b, f2w (590 floats, up to 3 per thread); only the first
+    // 256 cross segment borders, and their offset is a branch-free select chain
+    int off0 = O_F2W - 90;
+    off0 = t < 90 ? O_F2B - 80 : off0;
+    off0 = t < 80 ? O_F1B - 30 : off0;
+    off0 = t < 30 ? O_C2B - 10 : off0;
+    off0 = t < 10 ? O_C1B : off0;
     float pv[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) pv[j] = a.params[par_index(min(t + j * 256, 589))];
+    pv[0] = a.params[off0 + t];
+    pv[1] = a.params[O_F2W - 90 + 256 + t];
+    pv[2] = a.params[O_F2W - 90 + min(512 + t, 589)];
     const uint4 w1 = reinterpret_cast<const uint4*>(a.wimg + I_W1C)[t & 63];
     uint32_t px0 = 0;
     int lab0 = 0;
@@ -419,19 +420,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       pbase = ((gptr64)curp)[opaque(0)] * (int64_t)a.B + b0;
       nrow = a.perm[min(pbase + a.B, a.perm_len - 1) + opaque(0)];
     }
+    const uint64_t t_bar4 = __builtin_amdgcn_s_memtime();  // (diagnostics: slot 15, written below)
     lds_barrier();
-    if (t < 64) {
-      // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
-      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
-      const int tap = kg >> 1;
-      COFF[t] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
-      reinterpret_cast<uint4*>(W1Cs)[t] = w1;
-    } else if (t < 160) {
-      // dgrad: K slice 4*ks + q is channels 8*ocg .. +7 of tap (kDgOrder; slice 75 and the
-      // clamped steps >= DG_KS meet zero weights, their A offset only has to be in bounds)
-      const int tap = kg / 3, ocg = kg - 3 * tap;
-      DOFF[t - 64] = (short)((tap / 5) * DC2H_RP + (tap % 5) * DG_OCP + ocg * 8);
-    }
+    if (t < 64) reinterpret_cast<uint4*>(W1Cs)[t] = w1;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       if (t + j * 256 < 590) PAR[t + j * 256] = pv[j];
@@ -445,12 +436,15 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       }
       if (t == 0) LABEL[0] = lab0;
     }
-    if (a.dbg && t == 0) DBGS[16] = __builtin_amdgcn_s_memtime();
+    if (a.dbg && t == 0) {
+      DBGS[16] = __builtin_amdgcn_s_memtime();
+      DBGS[15] = t_bar4;  // wave 4 at the barrier
+    }
     // Retire every load of this branch here, in every lane (an empty asm reading the
     // registers): the merge below would otherwise inherit them as pending, and the
     // first reuse of their registers would make waves 0-3 wait vmcnt(0) -- for the DMA.
     asm volatile("" ::"v"(pv[0]), "v"(pv[1]), "v"(pv[2]), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w), "v"(px0),
-                 "v"(lab0), "v"(kg));
+                 "v"(lab0));
   } else {
     // staged: the dropout counter and (split step) the cursor, issued ahead of the barrier like
     // waves 4-7's loads (after it they would queue behind the weight DMA)
@@ -459,7 +453,24 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       rng_ctr = (uint64_t)((gptr64)rngp)[opaque(0)];
       if (KS > 1) cur = ((gptr64)curp)[opaque(0)];
     }
+    // K-slice orders (constant memory) for the conv2 / dgrad A-offset tables (threads t8 < 160;
+    // needed from conv2 on)
+    const int t8 = tid - 512;
+    const int tq = t8 < 64 ? t8 >> 4 : min(t8 - 64, 95) / 24;
+    const int tks = t8 < 64 ? t8 & 15 : min(t8 - 64, 95) - 24 * tq;
+    const int kg = t8 < 64 ? (int)kC2Order.fwd[min(4 * tks + tq, 49)] : (int)kDgOrder.fwd[min(4 * tks + tq, 74)];
     lds_barrier();
+    if (t8 < 64) {
+      // conv2 A-fragment offset of K-step ks for lane group q: K slice kC2Order[4*ks + q]
+      // covers channels 8*(kg&1) .. +7 of tap kg>>1 (clamped: slices >= 50 meet zero weights)
+      const int tap = kg >> 1;
+      COFF[t8] = (short)((tap / 5) * P1H_RP + (tap % 5) * LD_P1H + (kg & 1) * 8);
+    } else if (t8 < 160) {
+      // dgrad: K slice 4*ks + q is channels 8*ocg .. +7 of tap (kDgOrder; slice 75 and the
+      // clamped steps >= DG_KS meet zero weights, their A offset only has to be in bounds)
+      const int tap = kg / 3, ocg = kg - 3 * tap;
+      DOFF[t8 - 64] = (short)((tap / 5) * DC2H_RP + (tap % 5) * DG_OCP + ocg * 8);
+    }
     // waves 8-15 (otherwise idle here): conv1's address tables of all 1024 threads
     // (non-staged; the staged path reads kC1Tab)
     if (!STAGED) {
@@ -587,7 +598,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
       // reads).  All fragments are gathered first, the independent MFMAs issued back to
       // back, then one epilogue region for all tiles (per-tile branches serialised each
       // tile's MFMA latency and epilogue chain behind the previous one's)
-      // per-thread tables (kC1Tab row / preamble, waves 8-15)
+      // per-thread tables (kC1Tab row / preamble, waves 8-15).  (Aligned 8-byte runs from shifted
+      // copies of X written with X, two ds_read_b64 + one ds_read_u16 per tile instead of eight
+      // ds_read_u16, measured 0.12-0.16 us slower: profiles/r4/ab_conv1_aligned_runs.log)
       const u16x4 xo = STAGED ? __builtin_bit_cast(u16x4, make_uint2(c1row.x, c1row.y)) : C1T[tid];
       const u16x4 ho = STAGED ? __builtin_bit_cast(u16x4, make_uint2(c1row.z, c1row.w)) : C1H[tid];
       auto tiles = [&](auto nti) {
@@ -642,7 +655,10 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
     // the weight DMA (waves 0-3, preamble) is in LDS before conv2 reads W2C.  Every barrier of the
     // sample loop is LDS-only: __syncthreads() also waits vmcnt(0) in every wave, i.e. for the
     // next step's perm row / pixels loaded for the epilogue and for the vector-slab stores
+    // (waiting for W2C alone here and the rest at conv2's epilogue measured 0.1 us slower,
+    // profiles/r4/ab_split_dma_wait.log)
     if (wave < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.dbg && tid == 0 && s == 0) DBGS[21] = __builtin_amdgcn_s_memtime();  // weight DMA landed (wave 0)
     lds_barrier();
 
     // ---------------- stage 2: conv2 + bias + Dropout2d + maxpool + relu -> P2, I2

@@ -314,6 +314,27 @@ S_CONSTB = S_XC + 3 * XC_LD * 2
 S_I2 = S_P2 + 640
 
 
+def xrun(e):  # the aligned 4-pixel run X[e .. e+3] (lenet_fused.hip: X or a shifted copy)
+    c = e & 3
+    return (S_X if c == 0 else S_XC + 2 * (c - 1) * XC_LD) + 2 * (e - c)
+
+
+def split_conv1_reads():  # (tried in round 4: aligned runs from shifted copies; slower, not kept)
+    tot = 0
+    for mt in range(36):
+        A, B, C = [], [], []
+        for lane, l16, kq in lanes():
+            m = mt * 16 + l16
+            p, q = m >> 2, m & 3
+            pb = (2 * (p // 12) + (q >> 1)) * 28 + 2 * (p % 12) + (q & 1)
+            e1, e2 = pb + 28 * kq, pb + 112 + (2 if kq == 1 else 0)
+            A.append(xrun(e1))
+            B.append(S_X + 2 * (e1 + 4))
+            C.append(xrun(e2))
+        tot += extra_cycles(A, 8) + extra_cycles(B, 2) + extra_cycles(C, 8)
+    return tot
+
+
 def split_conv1_gather():  # stage 1: 36 tiles, 8 ds_read_u16 each
     koff = [(k // 5) * 28 + (k % 5) if k < 25 else 0 for k in range(32)]
     tot = 0
@@ -461,8 +482,7 @@ def split_conv1_wgrad():  # stage 8, waves 0-11: 3 K-steps each (DC1 A fragment 
                     if kc1 < 25:
                         ee = oh * 28 + ow0 + (kc1 // 5) * 28 + kc1 % 5
                         c = ee & 3
-                        base = S_X if c == 0 else S_XC + 2 * (c - 1) * XC_LD
-                        addrs.append(base + 2 * (ee - c) + 8 * half)
+                        addrs.append(xrun(ee) + 8 * half)
                     else:
                         addrs.append(S_CONSTB + 2 * (8 if kc1 == 25 else 0) + 8 * half)
                 tot += extra_cycles(addrs, 8)

@@ -50,6 +50,9 @@ def main():
     ld = [(st[:, 17] - st[:, 12]).median().item(), (st[:, 16] - st[:, 12]).median().item()]
     print(f"  preamble (from kernel start): DMA issued {pre[0]:.0f}, wave 4 starts {ld[0]:.0f}, small loads "
           f"consumed {ld[1]:.0f}; wave 0 done {pre[1]:.0f}")
+    bar = [(st[:, k] - st[:, 12]).median().item() for k in (15, 21, 1, 2)]
+    print(f"  wave 4 at the preamble barrier {bar[0]:.0f}; weight DMA landed (wave 0, end of conv1) {bar[1]:.0f}; "
+          f"conv1 start {bar[2]:.0f}, conv2 start {bar[3]:.0f}")
     dma = [(st[:, 17 + w] - st[:, 12]).median().item() for w in (1, 2, 3)]
     arr = [(st[:, 24 + w] - st[:, 12]).median().item() for w in range(8)]
     print(f"  DMA issued by waves 1-3: {dma}; waves 0-7 reach the first barrier: {arr}")
