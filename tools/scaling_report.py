@@ -63,13 +63,13 @@ REF_EPOCH_S = {1: 17.53, 2: 11.29, 4: 7.60, 8: 5.00}  # BASELINE.md (reference R
 STEPS_PER_EPOCH = 938
 GLOBAL_BATCH = 64
 # graph-replayed lenet_train + lenet_update step (us) at per-rank batch B with the in-kernel
-# exchange looped back to N virtual ranks, one MI355X (profiles/r4/exchange_loopback_r4m.log,
+# exchange looped back to N virtual ranks, one MI355X (profiles/r4/exchange_loopback_r4f2.log,
 # profiles/dp_exchange_r4.md)
 LOOPBACK_STEP_US = {
-    (8, 1): 12.49, (8, 2): 13.81, (8, 4): 14.11, (8, 8): 14.89,
-    (16, 1): 12.78, (16, 2): 13.95, (16, 4): 14.10, (16, 8): 14.95,
-    (32, 1): 12.92, (32, 2): 14.10, (32, 4): 14.34, (32, 8): 15.23,
-    (64, 1): 14.24, (64, 2): 14.83, (64, 4): 15.10, (64, 8): 15.76,
+    (8, 1): 12.51, (8, 2): 13.62, (8, 4): 14.05, (8, 8): 14.75,
+    (16, 1): 12.58, (16, 2): 13.82, (16, 4): 14.10, (16, 8): 14.91,
+    (32, 1): 12.70, (32, 2): 13.94, (32, 4): 14.20, (32, 8): 15.08,
+    (64, 1): 13.58, (64, 2): 14.69, (64, 4): 15.06, (64, 8): 15.60,
 }
 WIRE_BYTES = 21840 * 8  # live exchange words per peer per step (lenet_fused.hip ll_push)
 _LB_LINE = re.compile(r"B=\s*(\d+)\s+N=(\d+).*?step\s+([0-9.]+)\s*us")
