@@ -361,22 +361,24 @@ class FusedLeNetTrainer:
                   self.weight_decay, self.nesterov, self.step_count, self.ticket, None, None, False, None, 0, None,
                   self.mfma)
         ok = True
-        for _ in range(rounds):
+        # every round's local and exchanged gradients first, then ONE process-group all-reduce of
+        # all the local ones (a collective round trip per round was most of the self-test's time)
+        local = torch.empty(rounds, N_PARAMS, dtype=torch.float32, device=self.device)
+        fused = torch.empty_like(local)
+        for r in range(rounds):
             self.slab.copy_(torch.randint(-8, 9, self.slab.shape, generator=gen, dtype=torch.float32,
                                           device=self.device))
             self.set_fc_vectors(torch.randint(-4, 5, (self.B, N_VEC), generator=gen, dtype=torch.float32,
                                               device=self.device))
-            local = torch.empty(N_PARAMS, dtype=torch.float32, device=self.device)
-            fused = torch.empty_like(local)
-            ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, local, *common)
-            ref = local.to(pg_dev, copy=True)
-            dist.all_reduce(ref)
+            ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, local[r], *common)
             try:
-                ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, fused, *common, None,
+                ops.lenet_update(self.slab, self.grid, self.vslab, self.B, None, fused[r], *common, None,
                                  self.exch.id, self.exch_timeout_s)
-                ok &= bool(torch.equal(fused, ref.to(self.device)))
             except Exception:
                 ok = False
+        ref = local.to(pg_dev, copy=True)
+        dist.all_reduce(ref)
+        ok &= bool(torch.equal(fused, ref.to(self.device)))
         torch.cuda.synchronize(self.device)
         try:
             ok &= self.exch.error(reset=True) == 0
