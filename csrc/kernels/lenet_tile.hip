@@ -498,6 +498,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
                                                                    false));
       zp += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, zp), 0x4E, 0xf, 0xf,
                                                                    false));
+      // the label's fc2 row (the one-hot term of dZ1), read once t has long arrived: its round
+      // trip hides under the softmax
+      const float w2t = PAR[P_F2W + t * 50 + o];
       float lg[10];
 #pragma unroll
       for (int c = 0; c < 10; ++c)
@@ -514,12 +517,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       for (int c = 1; c < 10; ++c) mx = fmaxf(mx, lg[c]);
       // first index attaining the max (torch argmax)
       const int amax = __builtin_ctzll(__ballot(lane < 10 && zl == mx));
-      float ex[10], se = 0.f;
+      // (the sum as a fixed tree: 4 dependent adds instead of 10)
+      float ex[10];
 #pragma unroll
-      for (int c = 0; c < 10; ++c) {
-        ex[c] = __expf(lg[c] - mx);
-        se += ex[c];
-      }
+      for (int c = 0; c < 10; ++c) ex[c] = __expf(lg[c] - mx);
+      const float se = (((ex[0] + ex[1]) + (ex[2] + ex[3])) + ((ex[4] + ex[5]) + (ex[6] + ex[7]))) + (ex[8] + ex[9]);
       // (t stays a VGPR: a wave-uniform copy in an SGPR made hipcc wait for the label's LDS read
       // ahead of every other read of the stage)
       const float lt = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(4 * t, __builtin_bit_cast(int, zl)));
@@ -535,9 +537,11 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
       }
       if (TRAIN) {
         const float gs = a.grad_scale * __builtin_amdgcn_rcpf(se);
+        // dZ1 = gate * (sum_c softmax_c W2[c][o] - W2[t][o]) / batch: the one-hot term as one read
+        // weight (w2t), not a compare / select per logit
         float dl[10];
 #pragma unroll
-        for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs - (c == t ? a.grad_scale : 0.f);
+        for (int c = 0; c < 10; ++c) dl[c] = ex[c] * gs;
         unsigned short* vs = VH + vec16_index(0, b);
         constexpr int vld = 4;
         float dh0 = 0.f, dh1 = 0.f;
@@ -546,7 +550,7 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
           if (c & 1) dh1 = fmaf(dl[c], w2c[c], dh1);
           else dh0 = fmaf(dl[c], w2c[c], dh0);
         }
-        const float dz = (valid && lane < 50 && ho > 0.f) ? (dh0 + dh1) * d1 : 0.f;
+        const float dz = (valid && lane < 50 && ho > 0.f) ? fmaf(-a.grad_scale, w2t, dh0 + dh1) * d1 : 0.f;
         const unsigned short dzh = h16<T>(dz);
         DZ1B[s * 64 + lane] = dzh;
         if (valid && lane < 50) vs[(V_DZ1 + lane) * vld] = dzh;
