@@ -886,6 +886,19 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           r[tt][2] = lds_read_tr16(fc2 + t * 16);
           r[tt][3] = lds_read_tr16(fc3 + t * 16);
         }
+        // the epilogue's operands (pool2 output and argmax, Dropout2d scale) read with the
+        // transposed reads, not after the MFMAs: hipcc put them behind the MFMAs in branches,
+        // two to three more LDS round trips per tile on the stage's chain
+        float p2f[NTT], d2s[NTT];
+        int i2v[NTT];
+#pragma unroll
+        for (int tt = 0; tt < NTT; ++tt) {
+          const int t = wave + NW * tt, pi = t * 16 + l16;
+          p2f[tt] = f16v<T>(P2[pi]);
+          d2s[tt] = D2S[t];
+          i2v[tt] = I2[pi];
+          asm volatile("" ::"v"(p2f[tt]), "v"(d2s[tt]), "v"(i2v[tt]));  // (issued here, retired with the reads above)
+        }
         f32x4 c[NTT];
 #pragma unroll
         for (int tt = 0; tt < NTT; ++tt) {
@@ -903,8 +916,9 @@ __global__ void __launch_bounds__(NT, 1) lenet_train_kernel(LenetTrainArgs a, in
           const int t = wave + NW * tt;
           // unpool window w = l16 of channel t
           const int pi = t * 16 + l16;
-          const float gv = f16v<T>(P2[pi]) > 0.f ? c[tt][0] * D2S[t] : 0.f;
-          const int bi = I2[pi];
+          (void)pi;
+          const float gv = p2f[tt] > 0.f ? c[tt][0] * d2s[tt] : 0.f;
+          const int bi = i2v[tt];
           const int oh0 = 2 * (l16 >> 2), ow0 = 2 * (l16 & 3);
           const uint32_t hg = h16<T>(gv);
           if (kq < 2)  // window row dy = kq: an aligned 32-bit pair of DC2
