@@ -63,13 +63,13 @@ REF_EPOCH_S = {1: 17.53, 2: 11.29, 4: 7.60, 8: 5.00}  # BASELINE.md (reference R
 STEPS_PER_EPOCH = 938
 GLOBAL_BATCH = 64
 # graph-replayed lenet_train + lenet_update step (us) at per-rank batch B with the in-kernel
-# exchange looped back to N virtual ranks, one MI355X (profiles/r4/exchange_loopback_r4f2.log,
+# exchange looped back to N virtual ranks, one MI355X (profiles/r4/exchange_loopback_r4f7.log,
 # profiles/dp_exchange_r4.md)
 LOOPBACK_STEP_US = {
-    (8, 1): 12.51, (8, 2): 13.62, (8, 4): 14.05, (8, 8): 14.75,
-    (16, 1): 12.58, (16, 2): 13.82, (16, 4): 14.10, (16, 8): 14.91,
-    (32, 1): 12.70, (32, 2): 13.94, (32, 4): 14.20, (32, 8): 15.08,
-    (64, 1): 13.58, (64, 2): 14.69, (64, 4): 15.06, (64, 8): 15.60,
+    (8, 1): 12.42, (8, 2): 13.41, (8, 4): 13.84, (8, 8): 14.70,
+    (16, 1): 12.52, (16, 2): 13.61, (16, 4): 14.00, (16, 8): 14.87,
+    (32, 1): 12.71, (32, 2): 13.87, (32, 4): 14.12, (32, 8): 14.94,
+    (64, 1): 13.39, (64, 2): 14.56, (64, 4): 14.94, (64, 8): 15.61,
 }
 WIRE_BYTES = 21840 * 8  # live exchange words per peer per step (lenet_fused.hip ll_push)
 _LB_LINE = re.compile(r"B=\s*(\d+)\s+N=(\d+).*?step\s+([0-9.]+)\s*us")
