@@ -685,9 +685,13 @@ __global__ void __launch_bounds__(NT, 1) lenet_tile_kernel(LenetTrainArgs a, int
 #pragma unroll
         for (int i = 0; i < NTL; ++i) {
           const int RT = wave + NW * i, ss = RT / 9;  // wave-uniform
-          const int p = (RT - 9 * ss) * 16 + l16, y = p / 12, x = p - 12 * y;
+          // M-tile tl = a 4 x 4 block of pool1 pixels (A row l16 = pixel (y0 + l16/4, x0 + l16%4),
+          // C rows 4 kq + r = pixels (y0 + kq, x0 + r)): its dL/dconv2 reads spread over more banks
+          // than 16 raster pixels across two rows (tools/lds_bank_model_tile.py: 1455 -> 1312)
+          const int tl = RT - 9 * ss, y0 = (tl / 3) * 4, x0 = (tl - 3 * (tl / 3)) * 4;
+          const int y = y0 + (l16 >> 2), x = x0 + (l16 & 3);
           si[i] = ss;
-          p0[i] = (RT - 9 * ss) * 16 + 4 * kq;
+          p0[i] = (y0 + kq) * 12 + x0;
           ab[i] = DCH + ss * DCH_SZ + ((y - 4) * 8 + (x - 4)) * DG_OCP;
           // taps (ty, tx) with 0 <= y + ty - 4 < 8 and 0 <= x + tx - 4 < 8
           const uint32_t rb = ((1u << min(5, 12 - y)) - 1u) & ~((1u << max(0, 4 - y)) - 1u);

@@ -131,9 +131,9 @@ def dgrad():
             RT = wave + 16 * i
             ss = RT // 9
             info = []
+            tl = RT - 9 * ss  # 4 x 4 pixel block tl (lenet_tile.hip dgrad)
             for lane, l16, kq in lanes():
-                p = (RT - 9 * ss) * 16 + l16
-                info.append((p // 12, p % 12))
+                info.append(((tl // 3) * 4 + (l16 >> 2), (tl % 3) * 4 + (l16 & 3)))
             for ks in range(DG_KS):
                 A = []
                 for lane, l16, kq in lanes():
@@ -147,7 +147,7 @@ def dgrad():
                 ra += extra_cycles(A, 16)
                 if i == 0:
                     rb += extra_cycles([S_W2D + 2 * ((kq * 16 + l16) * 8 + ks * 512) for lane, l16, kq in lanes()], 16)
-            p0 = [(RT - 9 * ss) * 16 + 4 * kq for lane, l16, kq in lanes()]
+            p0 = [((tl // 3) * 4 + kq) * 12 + (tl % 3) * 4 for lane, l16, kq in lanes()]
             ri += extra_cycles([D_I1 + ss * I1_SZ + min(l16, 9) * I1_LD + p0[lane] for lane, l16, kq in lanes()], 4)
             act = [l16 < 10 for lane, l16, kq in lanes()]
             for dy in range(2):
