@@ -18,16 +18,25 @@ Order of work on every rank (one process per GPU, RCCL process group for N > 1):
 1. setup: process group, synthetic data, engine, HIP-graph capture of every step
    graph the run will replay (capture is never inside a timed region);
 2. epoch 0, the reference's own quantity: all 938 steps (incl. the short last
-   batch) + the 10k-image validation pass.  ``time_elapsed_s`` = process start ->
-   end of epoch-0 validation (ref src/train_dist.py:119 t0, :112 print), the
-   whole-job cold number; ``epoch0_s`` = the epoch itself;
+   batch) + the 10k-image validation pass.  ``time_elapsed_s`` = the reference's
+   span: t0 taken right after ``import torch`` and the package imports (ref
+   src/train_dist.py:1-11 imports, :119 t0), to the end of epoch-0 validation
+   (:112 print); everything the reference does after its t0 (rendezvous, data set,
+   model) is inside it, and no job work starts before it.  ``process_elapsed_s``
+   = process start -> the same point (imports included); ``epoch0_s`` = the
+   epoch itself;
 3. W warm-up steps, then one untimed rehearsal of exactly the graph sequence
    the timed region replays (so every graph it uses has been replayed before);
 4. exactly K timed steps (each = full forward, backward, gradient all-reduce for
    N > 1, SGD update) from the start of an epoch, bracketed by barrier + device
    synchronisation; the time reported is the max over ranks -> ``value`` =
    whole-job images/s, ``ms_per_step``;
-5. ``epoch_s``: one more full epoch + validation, warm (steady-state epoch time).
+5. ``epoch_s``: one more full epoch + validation, warm (steady-state epoch time);
+6. N > 1: a bitwise replica check of the parameters and momentum over all ranks
+   (``replicas_identical``); a run whose replicas differ reports no value;
+7. unless the run itself is fp32 (or ``--no-fp32-record``): the same K-step
+   window and warm epoch again on the exact-fp32 kernels, the reference's own
+   precision, as the ``fp32`` sub-record.
 
 Rank 0 prints one JSON line.
 """
@@ -35,7 +44,7 @@ from __future__ import annotations
 
 import time
 
-T_START = time.time()  # process start: the reference's t0 (src/train_dist.py:119)
+T_PROC = time.time()  # process start (process_elapsed_s); the reference's t0 comes after the imports
 
 import argparse  # noqa: E402
 import json  # noqa: E402
@@ -70,6 +79,8 @@ def parse(argv=None) -> argparse.Namespace:
                          "time; use with --global-batch 64/N")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: plumbing only (launch/rendezvous/JSON contract), stock PyTorch ops")
+    ap.add_argument("--no-fp32-record", action="store_true",
+                    help="skip the exact-fp32 sub-record (step 7) of a 16-bit run")
     ap.add_argument("--inject-exchange-fault", action="store_true",
                     help="fault-injection test hook: the last rank's exchange pushes go to a dead-end buffer "
                          "(in loopback mode: every virtual peer is dead), so peer waits time out; the bench "
@@ -103,7 +114,7 @@ def spawn(args: argparse.Namespace, argv: list[str]) -> int:
     launch = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(launch)
     return launch.launch(args.gpus, [sys.executable, os.path.abspath(__file__), *argv],
-                         env_extra={"CSED_BENCH_T0": repr(T_START)})
+                         env_extra={"CSED_BENCH_PROC_T0": repr(T_PROC)})
 
 
 def epoch_chunks(k: int, pos: int, full: int) -> list[int]:
@@ -119,7 +130,7 @@ def epoch_chunks(k: int, pos: int, full: int) -> list[int]:
     return out
 
 
-def run_cpu(args, ctx, t_start: float) -> dict:
+def run_cpu(args, ctx, t_start: float, t_proc: float) -> dict:
     """CPU plumbing run (no GPU on this machine): the same launch / rendezvous / timing /
     JSON contract on stock PyTorch ops through the modular trainer.  Not a performance
     number: the JSON says so in ``config.engine``."""
@@ -128,7 +139,8 @@ def run_cpu(args, ctx, t_start: float) -> dict:
     from csed_514_project_distributed_training_using_pytorch_amd.data import DeviceLoader, synthetic_mnist
     from csed_514_project_distributed_training_using_pytorch_amd.engine.modular import ModularTrainer
     from csed_514_project_distributed_training_using_pytorch_amd.models import Net
-    from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import all_reduce_max, barrier
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import (all_reduce_max, barrier,
+                                                                                     replica_checksum)
     from csed_514_project_distributed_training_using_pytorch_amd.parallel.sampler import ShardSampler
 
     n = ctx.world_size
@@ -146,9 +158,12 @@ def run_cpu(args, ctx, t_start: float) -> dict:
         tr.train_batch(*next(it))
     barrier(ctx)
     elapsed = all_reduce_max(ctx, time.perf_counter() - t0)
+    now = time.time()
+    same, _, _ = replica_checksum(ctx, torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]))
     return {"elapsed": elapsed, "engine": "CPU plumbing (stock PyTorch ops, modular trainer): not a GPU number",
             "allreduce": f"process group ({ctx.backend})" if ctx.is_distributed else "none",
-            "time_elapsed_s": all_reduce_max(ctx, time.time() - t_start)}
+            "time_elapsed_s": all_reduce_max(ctx, now - t_start), "process_elapsed_s": all_reduce_max(ctx, now - t_proc),
+            "replicas": same}
 
 
 def start_native_data():
@@ -166,12 +181,12 @@ def start_native_data():
     return ns.Job(60000, 10000, seed=0)
 
 
-def start_gpu_context():
-    """This rank's HIP context, created in a thread while ``import torch`` runs (~0.13 s of
-    ``time_elapsed`` on one GPU, ~0.5 s with two ranks sharing one).  ctypes loads the HIP
-    runtime that torch itself links (torch/lib/libamdhip64.so, found without importing torch),
-    so torch later finds this process's primary context already up.  None when there is no
-    such library (CPU-only torch) or no GPU."""
+def start_gpu_context(phases: dict | None = None):
+    """This rank's HIP context, created in a thread started at t0 that runs while the data set
+    is generated and the process group comes up.  ctypes loads the HIP runtime that torch
+    itself links (torch/lib/libamdhip64.so), so torch later finds this process's primary
+    context already up.  The thread's own wall time goes to ``phases["hip_ctx_thread"]``.
+    None when there is no such library (CPU-only torch) or no GPU."""
     import ctypes
     import importlib.util
     import threading
@@ -187,15 +202,51 @@ def start_gpu_context():
     dev = int(os.environ.get("LOCAL_RANK", "0"))
 
     def run():
+        t = time.time()
         n = ctypes.c_int(0)
         if hip.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value <= 0:
             return
         if hip.hipSetDevice(dev % n.value) == 0:
             hip.hipFree(ctypes.c_void_p(0))  # (the context's creation)
+        if phases is not None:
+            phases["hip_ctx_thread"] = time.time() - t
 
     t = threading.Thread(target=run, name="csed-hip-context", daemon=True)
     t.start()
     return t
+
+
+# the order of bring-up events on this rank, for tests/test_bench_contract_cpu.py: (name, time)
+BRINGUP_EVENTS: list[tuple[str, float]] = []
+
+
+def bringup(args, phases: dict):
+    """Imports, then the reference's t0, then the job's first work (ref src/train_dist.py:1-11
+    imports torch / torchvision / matplotlib / tqdm, :119 takes t0, :146 rendezvous, :148 data):
+    ``import torch`` and the package are timed apart (``import_torch``, ``import_pkg``) and
+    fall outside ``time_elapsed_s``; the synthetic-data generator and the HIP-context thread
+    start only after t0.  Returns (t0, native data job, HIP-context thread)."""
+    t_mark = time.time()
+    import torch  # noqa: F401
+    phases["import_torch"] = time.time() - t_mark
+    t_mark = time.time()
+    import torch.distributed  # noqa: F401
+
+    import csed_514_project_distributed_training_using_pytorch_amd.parallel.comm  # noqa: F401
+    import csed_514_project_distributed_training_using_pytorch_amd.utils.prof  # noqa: F401
+    if args.device == "cuda":
+        import csed_514_project_distributed_training_using_pytorch_amd.engine.fused  # noqa: F401
+    phases["import_pkg"] = time.time() - t_mark
+    t_start = time.time()  # the reference's t0 (src/train_dist.py:119)
+    BRINGUP_EVENTS.append(("t0", t_start))
+    native_job = ctx_job = None
+    if args.device == "cuda" and not os.environ.get("CSED_TORCH_DATA"):
+        BRINGUP_EVENTS.append(("native_data", time.time()))
+        native_job = start_native_data()
+    if args.device == "cuda":
+        BRINGUP_EVENTS.append(("hip_ctx_thread", time.time()))
+        ctx_job = start_gpu_context(phases)
+    return t_start, native_job, ctx_job
 
 
 def main(argv=None) -> int:
@@ -203,21 +254,16 @@ def main(argv=None) -> int:
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn(args, argv)
-    t_start = float(os.environ.get("CSED_BENCH_T0", T_START))
+    t_proc = float(os.environ.get("CSED_BENCH_PROC_T0", T_PROC))
     # bring-up phases (s) on this rank; the JSON reports the max over ranks of each
-    # (the reference's time_elapsed runs from process start, ref src/train_dist.py:119)
-    phases = {"spawn": T_START - t_start}
-    native_job = start_native_data() if args.device == "cuda" and not os.environ.get("CSED_TORCH_DATA") else None
-    ctx_job = start_gpu_context() if args.device == "cuda" else None
-
-    t_mark = time.time()
+    phases = {"spawn": T_PROC - t_proc}
+    t_start, native_job, ctx_job = bringup(args, phases)
     import torch
     import torch.distributed as dist
 
     from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import (
-        all_reduce_max, barrier, init_distributed)
+        all_reduce_max, barrier, init_distributed, replica_checksum)
     from csed_514_project_distributed_training_using_pytorch_amd.utils import prof
-    phases["import"] = time.time() - t_mark
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
@@ -244,11 +290,12 @@ def main(argv=None) -> int:
         raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     if args.device == "cpu":
-        r = run_cpu(args, ctx, t_start)
+        r = run_cpu(args, ctx, t_start, t_proc)
         elapsed, extra = r["elapsed"], {}
         cfg_engine, allreduce, step_kind, hip_graph = r["engine"], r["allreduce"], "eager", False
         time_elapsed, epoch0_s, epoch_s, val, loss_avg, comm_err, comm_retry = r["time_elapsed_s"], None, None, \
             None, None, 0, None
+        process_elapsed, replicas, fp32_rec = r["process_elapsed_s"], r["replicas"], None
         data_src = None
     else:
         from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
@@ -277,7 +324,7 @@ def main(argv=None) -> int:
                 barrier(ctx)
                 torch.cuda.synchronize(ctx.device)
 
-        def run_once(loopback_world: int, inject: bool, ph: dict):
+        def run_once(loopback_world: int, inject: bool, ph: dict, dt=dt):
             t_mark = time.time()
             torch.manual_seed(1)
             net = Net().to(ctx.device)
@@ -329,7 +376,9 @@ def main(argv=None) -> int:
             sync_barrier()
             ph["epoch0"] = time.perf_counter() - te
             epoch0 = all_reduce_max(ctx, ph["epoch0"])
-            t_el = all_reduce_max(ctx, time.time() - t_start)
+            now = time.time()
+            t_el = all_reduce_max(ctx, now - t_start)  # the reference's span (t0 after the imports)
+            p_el = all_reduce_max(ctx, now - t_proc)  # from process start
             # 3. warm-up, then a rehearsal of the timed sequence (same graphs, same order)
             with prof.range("bench:warmup"):
                 new_epoch()
@@ -374,19 +423,27 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(ctx.device)
             # every rank must agree: one rank's timed-out peer wait invalidates the whole run
             err = int(all_reduce_max(ctx, float(eng.comm_errors())))
+            # bitwise replica check: a silently wrong exchange cannot pass as a result
+            same_p, _, _ = replica_checksum(ctx, eng.flat.data)
+            same_m, _, _ = replica_checksum(ctx, eng.momentum_buf)
             return dict(eng=eng, elapsed=elapsed, dev_ms=dev_ms, loss_sum=loss_sum, epoch0=epoch0, t_el=t_el,
-                        epoch_s=epoch_s, val=val, err=err)
+                        p_el=p_el,
+                        epoch_s=epoch_s, val=val, err=err, replicas=same_p and same_m,
+                        diag=eng.comm_diag() if err else None)
 
         from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc
 
         r = run_once(args.loopback_world, args.inject_exchange_fault, phases)
         comm_retry = None
-        if r["err"] and os.environ.get("CSED_ALLREDUCE", "auto").lower() != "rccl":
-            # a peer wait of the IPC exchange timed out somewhere: release the IPC buffers on
-            # every rank (collective) and measure again on the process group's all-reduce
-            # (RCCL on GPUs; loopback mode: the plain one-GPU step), so the reported number is
-            # a valid training run
+        first_fault = None
+        if ((r["err"] or not r["replicas"]) and r["eng"].exch is not None
+                and os.environ.get("CSED_ALLREDUCE", "auto").lower() != "rccl"):
+            # a peer wait of the IPC exchange timed out somewhere (or a replica differs): release
+            # the IPC buffers on every rank (collective) and measure again on the process group's
+            # all-reduce (RCCL on GPUs; loopback mode: the plain one-GPU step), so the reported
+            # number is a valid training run
             comm_retry = r["eng"].allreduce_kind
+            first_fault = {"error_word": r["err"], "replicas_identical": r["replicas"], "first_mismatch": r["diag"]}
             r["eng"].close()
             del r
             import gc
@@ -399,7 +456,8 @@ def main(argv=None) -> int:
             phases.update({f"retry.{k}": v for k, v in retry_phases.items()})
         eng = r["eng"]
         elapsed, time_elapsed, epoch0_s, epoch_s, val = r["elapsed"], r["t_el"], r["epoch0"], r["epoch_s"], r["val"]
-        comm_err = r["err"]
+        process_elapsed = r["p_el"]
+        comm_err, replicas = r["err"], r["replicas"]
         loss_avg = r["loss_sum"] / max(1, args.steps * eng.B)
         engine_kernels = {"fused-ipc": " with in-kernel xGMI gradient exchange", "none": ""}.get(
             eng.allreduce_kind, " + gradient all-reduce")
@@ -420,15 +478,38 @@ def main(argv=None) -> int:
             extra["exchange"] = eng.exchange_note
         if _ipc.LAST_NOTE:
             extra["allreduce_note"] = _ipc.LAST_NOTE
+        if first_fault:
+            extra["first_run_fault"] = first_fault
+        # 7. the reference's precision (src/model.py: fp32 defaults) on the same window + warm epoch
+        fp32_rec = None
+        if args.dtype != "fp32" and not args.no_fp32_record and not args.inject_exchange_fault:
+            eng.close()
+            del r, eng
+            import gc
+            gc.collect()
+            sync_barrier()
+            f = run_once(args.loopback_world, False, {}, dt=torch.float32)
+            fe = f["eng"]
+            fp32_rec = {"ms_per_step": round(1e3 * f["elapsed"] / args.steps, 5),
+                        "value": round(args.steps * args.global_batch / f["elapsed"], 1),
+                        "device_ms_per_step": round(f["dev_ms"] / args.steps, 5),
+                        "epoch_s": round(f["epoch_s"], 4) if f["epoch_s"] is not None else None,
+                        "epoch0_s": round(f["epoch0"], 4),
+                        "engine": f"fused HIP ({fe.kernel_names}), allreduce {fe.allreduce_kind}",
+                        "replicas_identical": f["replicas"], "comm_error_word": f["err"]}
+            if f["val"]:
+                fp32_rec.update({k: round(v, 4) for k, v in f["val"].items()})
+            fe.close()
 
-    bringup = {k: round(v, 4) for k, v in reduce_max(ctx, phases).items()}
+    bringup_rec = {k: round(v, 4) for k, v in reduce_max(ctx, phases).items()}
     value = args.steps * args.global_batch / elapsed
+    valid = not comm_err and replicas
     base = BASELINE_EPOCH_S.get(n)
     base_ips = 60000.0 / base if base else None
     if ctx.is_main:
         rec = {
             "metric": METRIC,
-            "value": round(value, 1),
+            "value": round(value, 1) if valid else None,
             "unit": "images/s",
             "n_gpus": n,
             "steps": args.steps,
@@ -448,27 +529,40 @@ def main(argv=None) -> int:
                        "process_group": {"backend": ctx.backend, "ranks": n} if ctx.is_distributed else None,
                        **extra},
             "time_elapsed_s": round(time_elapsed, 4) if time_elapsed is not None else None,
+            "process_elapsed_s": round(process_elapsed, 4) if process_elapsed is not None else None,
             "epoch0_s": round(epoch0_s, 4) if epoch0_s is not None else None,
             "epoch_s": round(epoch_s, 4) if epoch_s is not None else None,
             "baseline_epoch_s": base,
             "vs_baseline_time_elapsed": round(base / time_elapsed, 2) if base and time_elapsed else None,
             "vs_baseline_epoch": round(base / epoch_s, 1) if base and epoch_s else None,
             "vs_baseline_note": ("vs_baseline = warm timed-window images/s / the reference's images/s over its "
-                                 "whole 1-epoch run (process start to the epoch-0 print, incl. data loading and "
-                                 "validation); the like-for-like ratios are vs_baseline_time_elapsed (the same "
-                                 "cold whole-job span here) and vs_baseline_epoch (a warm epoch + validation)"),
+                                 "whole 1-epoch run (its t0, right after its imports, to the epoch-0 print, incl. "
+                                 "rendezvous, data loading and validation); the like-for-like ratios are "
+                                 "vs_baseline_time_elapsed (the same span here: t0 after import torch and the "
+                                 "package) and vs_baseline_epoch (a warm epoch + validation); process_elapsed_s "
+                                 "adds the imports (process start -> the same point)"),
+            "replicas_identical": replicas if n > 1 else None,
             "train_loss_timed_rank0": round(loss_avg, 4) if loss_avg is not None else None,
-            # where time_elapsed_s goes, max over ranks of each phase (s): spawn (launcher ->
-            # this process), import (torch + package), process_group (rendezvous, RCCL
-            # communicator), data_wait (the generator overlapped with import; what is left),
-            # engine (incl. engine.ipc_open / engine.self_test of the fused exchange), capture
-            # (HIP graphs), test_upload, epoch0 (938 steps + validation)
-            "bringup_s": bringup,
+            # where the time goes, max over ranks of each phase (s).  Before t0 (process_elapsed_s
+            # only): spawn (launcher -> this process), import_torch, import_pkg.  After t0
+            # (time_elapsed_s): process_group (rendezvous, RCCL communicator; includes the wait
+            # for the HIP-context thread, hip_ctx_thread = that thread's own time), data_wait
+            # (what is left of the native generator), engine (incl. engine.ipc_open /
+            # engine.self_test of the fused exchange), capture (HIP graphs), test_upload, epoch0
+            # (938 steps + validation)
+            "bringup_s": bringup_rec,
         }
         if comm_retry:
             rec["config"]["comm_retry"] = f"{comm_retry} path timed out; re-measured on the process-group all-reduce"
         if comm_err:
-            rec["comm_error"] = "IPC all-reduce timed out waiting for a peer: results invalid"
+            rec["comm_error"] = (f"IPC exchange error word {comm_err} (1: a peer wait timed out, 2: a received "
+                                 "word differed from the value pushed): results invalid")
+        if not replicas:
+            rec["replica_error"] = "parameters / momentum differ between ranks after the run: results invalid"
+        if fp32_rec:
+            rec["fp32"] = fp32_rec
+            if base and fp32_rec.get("epoch_s"):
+                fp32_rec["vs_baseline_epoch"] = round(base / fp32_rec["epoch_s"], 1)
         if val:
             rec.update({k: round(v, 4) for k, v in val.items()})
         print(json.dumps(rec), flush=True)

@@ -84,16 +84,27 @@ def _headers_digest() -> str:
     return h.hexdigest()[:12]
 
 
-def _needs(obj: Path, src: Path, stamp: str) -> bool:
+def _src_stamp(src: Path, common: str, cmd: list[str]) -> str:
+    """Content stamp of one object: the source's bytes, every header's bytes (``common``) and
+    the compile command (flags, arch).  Modification times play no part, so a source whose
+    content changed is rebuilt even when its mtime is older than its object (a checkout, a
+    copy with preserved times), and an untouched source is not rebuilt after a ``touch``."""
+    h = hashlib.sha1()
+    h.update(src.read_bytes())
+    h.update(common.encode())
+    h.update("\0".join(c for c in cmd if c not in (str(src),)).encode())
+    return h.hexdigest()
+
+
+def _needs(obj: Path, stamp: str) -> bool:
     tag = obj.with_suffix(".tag")
     if not obj.exists() or not tag.exists():
         return True
-    if tag.read_text() != stamp:
-        return True
-    return obj.stat().st_mtime < src.stat().st_mtime
+    return tag.read_text() != stamp
 
 
 def _compile(cmd: list[str], obj: Path, stamp: str) -> str:
+    obj.with_suffix(".tag").unlink(missing_ok=True)  # (a failed compile leaves no valid stamp)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -107,30 +118,34 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
     tflags, tlibs = _torch_flags()
     kernels, hosts = _sources()
-    stamp = _headers_digest() + ARCH
+    common = _headers_digest() + ARCH
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
     cmds = []
     objs = []
-    for src in kernels:
+    stamps = []
+    for src in kernels + hosts:
         obj = BUILD_DIR / (src.stem + ".o")
         objs.append(obj)
-        if force or _needs(obj, src, stamp):
-            cmds.append(([hipcc, *COMMON, f"-I{CSRC}", "-c", str(src), "-o", str(obj)], obj))
-    for src in hosts:
-        obj = BUILD_DIR / (src.stem + ".o")
-        objs.append(obj)
-        if force or _needs(obj, src, stamp):
-            cmds.append(([hipcc, *COMMON, *tflags, f"-I{CSRC}", "-x", "hip", "-c", str(src),
-                          "-o", str(obj)], obj))
+        if src in kernels:
+            cmd = [hipcc, *COMMON, f"-I{CSRC}", "-c", str(src), "-o", str(obj)]
+        else:
+            cmd = [hipcc, *COMMON, *tflags, f"-I{CSRC}", "-x", "hip", "-c", str(src), "-o", str(obj)]
+        stamp = _src_stamp(src, common, cmd)
+        stamps.append(stamp)
+        if force or _needs(obj, stamp):
+            cmds.append((cmd, obj, stamp))
+    # the shared object's own stamp: every object's stamp, so a relink follows any rebuilt object
+    so_stamp = hashlib.sha1("".join(stamps).encode()).hexdigest()
+    so_tag = SO_PATH.with_suffix(".tag")
     if cmds:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = [ex.submit(_compile, c, o, stamp) for c, o in cmds]
+            futs = [ex.submit(_compile, c, o, st) for c, o, st in cmds]
             for f in cf.as_completed(futs):
                 name = f.result()
                 if verbose:
                     print(f"[csed build] compiled {name}", flush=True)
-    link_needed = force or bool(cmds) or not SO_PATH.exists() or any(
-        o.stat().st_mtime > SO_PATH.stat().st_mtime for o in objs)
+    link_needed = (force or bool(cmds) or not SO_PATH.exists() or not so_tag.exists()
+                   or so_tag.read_text() != so_stamp)
     if link_needed:
         tmp = SO_PATH.with_suffix(".so.tmp")
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), *tlibs,
@@ -139,6 +154,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, SO_PATH)
+        so_tag.write_text(so_stamp)
         if verbose:
             print(f"[csed build] linked {SO_PATH}", flush=True)
     return SO_PATH
@@ -151,17 +167,20 @@ def build_data_lib(force: bool = False, verbose: bool = True) -> Path:
     """Host-only native data generator (``csrc/data/synth_mnist.cpp`` -> ``_csed_data.so``):
     plain g++, no torch and no HIP, so it loads before ``import torch``."""
     src = CSRC / "data" / "synth_mnist.cpp"
-    if not force and DATA_SO.exists() and DATA_SO.stat().st_mtime >= src.stat().st_mtime:
-        return DATA_SO
     cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++")
     if not cxx:
         raise RuntimeError("no host C++ compiler for the data generator")
     tmp = DATA_SO.with_suffix(".so.tmp")
     cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-ffp-contract=off", "-march=x86-64-v2", str(src), "-o", str(tmp)]
+    stamp = _src_stamp(src, "", cmd)
+    tag = DATA_SO.with_suffix(".tag")
+    if not force and DATA_SO.exists() and tag.exists() and tag.read_text() == stamp:
+        return DATA_SO
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, DATA_SO)
+    tag.write_text(stamp)
     if verbose:
         print(f"[csed build] built {DATA_SO}", flush=True)
     return DATA_SO

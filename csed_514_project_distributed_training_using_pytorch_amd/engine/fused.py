@@ -17,8 +17,12 @@ enabled after a collective bring-up and an exact self-test; if either fails, or
 
     lenet_update (reduce only) -> RCCL all-reduce -> SGD kernel
 
-(``CSED_TIME_PATHS=1`` additionally times both in ``auto`` mode and keeps the
-faster; off by default, since it costs three graph captures at bring-up.)
+In ``auto`` mode with one rank per GPU (a real node, pushes over xGMI) both
+steps are then timed at bring-up -- one 16-step graph each -- and the faster is
+kept, so a fused exchange slower than RCCL is never locked in (SURVEY §7.3 step
+6).  ``CSED_TIME_PATHS``: ``auto`` (default: time exactly then), ``1`` (always
+time, also on ranks sharing a GPU, and also time an exchange-free step), ``0``
+(never: a passing self-test keeps the fused path).
 
 All per-step state (batch cursor into this rank's epoch permutation, Philox
 offset, optimizer step) lives on the device, so a sequence of steps is
@@ -287,11 +291,9 @@ class FusedLeNetTrainer:
     # ------------------------------------------------- fused gradient exchange
     def _enable_exchange(self, required: bool) -> None:
         """Bring up lenet_update's in-kernel exchange (collective on every rank): open the IPC
-        buffers and self-test them with the update kernel itself.  With ``CSED_TIME_PATHS=1``
-        (auto mode, RCCL) the fused, fallback and exchange-free steps are also timed and the
-        faster of the first two is kept; by default a passing self-test keeps the fused path
-        (three graph captures and timings less inside the job's bring-up, i.e. inside the
-        reference's time_elapsed)."""
+        buffers and self-test them with the update kernel itself.  Then (auto mode, RCCL, see
+        the module docstring for ``CSED_TIME_PATHS``) the fused and fallback steps are timed
+        and the faster is kept."""
         import time
 
         t0 = time.perf_counter()
@@ -317,16 +319,26 @@ class FusedLeNetTrainer:
                 raise RuntimeError(f"CSED_ALLREDUCE=fused but the fused exchange is unusable ({why})")
             return
         self.exchange_note = "fused exchange on (self-test passed)"
-        if not required and self.ctx.backend == "nccl" and os.environ.get("CSED_TIME_PATHS", "0") == "1":
+        tp = os.environ.get("CSED_TIME_PATHS", "auto").strip().lower()
+        if not required and self.ctx.backend == "nccl" and tp != "0":
+            from ..parallel.ipc import ranks_per_gpu
+
+            # (collective: every rank takes the same branch)
+            do_time = tp == "1" or ranks_per_gpu(self.ctx) == 1
+        else:
+            do_time = False
+        if do_time:
             t2 = time.perf_counter()
             t_fused = self._time_steps()
             saved, self.exch = self.exch, None
             t_fallback = self._time_steps()
-            # the same step with no exchange at all (each rank updates on its own gradient; the
-            # state is restored): fused - local = what the exchange costs per step
-            self.comm = False
-            t_local = self._time_steps()
-            self.comm = True
+            t_local = float("inf")
+            if tp == "1":
+                # the same step with no exchange at all (each rank updates on its own gradient;
+                # the state is restored): fused - local = what the exchange costs per step
+                self.comm = False
+                t_local = self._time_steps()
+                self.comm = True
             # a path whose graph could not be captured times as inf; ties keep the fused path
             self.exch = saved if t_fused <= t_fallback else None
             if self.exch is None:
@@ -339,7 +351,7 @@ class FusedLeNetTrainer:
                                    "local_step_us": fin(t_local),
                                    "exchange_us": fin(t_fused - t_local) if max(t_fused, t_local) != float("inf")
                                    else None,
-                                   "fallback": "rccl"}
+                                   "fallback": "rccl", "kept": "fused" if self.exch is not None else "rccl"}
             self.bringup_s["path_timing"] = time.perf_counter() - t2
 
     def _vote(self, ok: bool) -> bool:
@@ -387,7 +399,7 @@ class FusedLeNetTrainer:
         self.vslab.zero_()
         return ok
 
-    def _time_steps(self, nsteps: int = 16, reps: int = 5) -> float:
+    def _time_steps(self, nsteps: int = 16, reps: int = 3) -> float:
         """us per training step of a captured graph (max over ranks); engine state is restored."""
         state = self._state()
         saved = [t.clone() for t in state]
@@ -437,8 +449,14 @@ class FusedLeNetTrainer:
         self.exch = None
 
     def comm_errors(self) -> int:
-        """Nonzero if the IPC exchange ever timed out waiting for a peer (synchronous)."""
+        """Nonzero if the IPC exchange ever timed out waiting for a peer (bit 0) or, looped back,
+        received a word whose value was not the one pushed (bit 1; see ``comm_diag``).
+        Synchronous."""
         return self.exch.error() if self.exch is not None else 0
+
+    def comm_diag(self) -> dict | None:
+        """The first in-kernel loopback mismatch record (block, peer row, word, tag, got, want)."""
+        return self.exch.diag() if self.exch is not None else None
 
     def inject_exchange_fault(self, on: bool = True) -> None:
         """Fault injection (tests, ``--inject-exchange-fault``): this rank's exchange pushes go

@@ -113,8 +113,24 @@ class IpcAllReduce:
             out.copy_(self._pad_out[: self.n])
         return out
 
+    # error-word bits (csrc/comm/ipc_allreduce.h)
+    ERR_TIMEOUT = 1
+    ERR_MISMATCH = 2
+
     def error(self, reset: bool = False) -> int:
+        """Error bits: ``ERR_TIMEOUT`` (a peer wait ran out), ``ERR_MISMATCH`` (loopback only:
+        a received word carried the current tag but not the value its sender pushed)."""
         return int(torch.ops.csed.ipc_error(self.id, reset))
+
+    def diag(self) -> dict | None:
+        """The first loopback mismatch, as recorded in-kernel (None if there was none)."""
+        d = list(torch.ops.csed.ipc_diag(self.id))
+        if not d[0]:
+            return None
+        got = (d[5] & 0xFFFFFFFF) | ((d[6] & 0xFFFFFFFF) << 32)
+        return {"block": d[1], "peer_row": d[2], "word": d[3], "tag": d[4] & 0xFFFFFFFF,
+                "got_word": hex(got), "got_tag": d[6] & 0xFFFFFFFF, "want_bits": hex(d[7] & 0xFFFFFFFF),
+                "poll_passes": d[8]}
 
     def mute(self, on: bool = True) -> None:
         """Fault injection: while on, this rank's pushes go to a dead-end buffer (csrc/comm

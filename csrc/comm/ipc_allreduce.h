@@ -28,9 +28,18 @@ hipError_t ipc_destroy(int id);
 // peers see a dead rank (their waits time out).  Takes effect for launches resolved after the
 // call (kernel arguments captured in a graph keep the mapping they were captured with).
 hipError_t ipc_set_mute(int id, bool mute);
-// Error word: nonzero if a wait ever timed out (synchronous read).  Once set, the exchange
-// kernels stop waiting (one poll per call) until it is reset.
+// Error word (synchronous read): bit 0 (kErrTimeout) = a wait timed out; once set, the exchange
+// kernels stop waiting (one poll per call) until it is reset.  Bit 1 (kErrMismatch, loopback
+// only) = a received word carried the current tag but not the value its sender pushed.
 hipError_t ipc_error(int id, int* err_out, bool reset);
+// The first mismatch's record (kDiagWords ints, all zero if none): claimed flag, workgroup,
+// peer row, exchange word, tag, received word (low, high dword), the value pushed, poll passes.
+constexpr int kErrTimeout = 1, kErrMismatch = 2;
+constexpr int kDiagWords = 9;
+hipError_t ipc_diag(int id, int* out);
+// Test hook: fill every word of this rank's receive slot (tag & 1) with {value_bits, tag}, i.e. a
+// word that carries a current tag but a value nobody pushed (synchronous).
+hipError_t ipc_poison(int id, uint32_t tag, uint32_t value_bits);
 
 // Device view of an opened exchange buffer, for kernels that carry their own
 // LL exchange (lenet_update's fused gradient all-reduce).  Layout of rank r's
@@ -42,9 +51,10 @@ constexpr int kIpcMaxBlocks = 512;
 struct IpcPeers {
   uint64_t* base[kIpcMaxRanks];
   int64_t* counters;  // [kIpcMaxBlocks]
-  int* err;
+  int* err;           // [1 + kDiagWords]: error bits, then the first mismatch's record
   int64_t cap;        // words per sender per slot
   int world, rank;
+  int loopback, pad_; // loopback: every received word must bit-equal this rank's own value
 };
 hipError_t ipc_peers(int id, IpcPeers* out);
 

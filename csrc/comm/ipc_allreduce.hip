@@ -33,6 +33,7 @@ namespace comm {
 constexpr int kMaxRanks = kIpcMaxRanks;
 constexpr int kMaxBlocks = kIpcMaxBlocks;
 constexpr int kThreads = 256;
+constexpr int kErrInts = 1 + kDiagWords;  // error bits + the first mismatch's record
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
@@ -62,7 +63,7 @@ __global__ void __launch_bounds__(kThreads) ipc_allreduce_kernel(const float* __
   // once any wait of this buffer has timed out the replicas are already inconsistent (the
   // caller re-runs on the process group): later calls poll once and never wait again, so a
   // dead peer costs one timeout, not one per call
-  const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const bool failed = (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kErrTimeout) != 0;
   __shared__ int64_t t_sh;
   if (tid == 0) t_sh = counters[blk] + 1;
   __syncthreads();
@@ -123,7 +124,7 @@ __global__ void __launch_bounds__(kThreads) ipc_allreduce_kernel(const float* __
     }
     reinterpret_cast<float2*>(out)[i] = s;
   }
-  if (timed_out) atomicOr(err, 1);
+  if (timed_out) atomicOr(err, kErrTimeout);
   if (tid == 0) counters[blk] = t;
 }
 
@@ -177,8 +178,8 @@ hipError_t ipc_create(int64_t n, int blocks, int* id_out) {
   if (e == hipSuccess) e = hipMemset(c->buf, 0, bytes);
   if (e == hipSuccess) e = hipMalloc(&c->counters, kMaxBlocks * sizeof(int64_t));
   if (e == hipSuccess) e = hipMemset(c->counters, 0, kMaxBlocks * sizeof(int64_t));
-  if (e == hipSuccess) e = hipMalloc(&c->err, sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->err, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&c->err, kErrInts * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->err, 0, kErrInts * sizeof(int));
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     delete c;  // buffers of a failed create are left to process teardown
@@ -244,13 +245,20 @@ hipError_t ipc_allreduce(int id, const float* in, float* out, int64_t n, double 
   if (!c || c->world < 1 || n > c->cap || n % 4) return hipErrorInvalidValue;
   const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
   PeerBufs p = c->peers;
-  if (c->muted)  // (ipc_set_mute: pushes go to the dead-end buffer)
+  if (c->muted)  // (ipc_set_mute: pushes go to the dead-end buffer; see ipc_set_mute)
     for (int r = 0; r < c->world; ++r)
-      if (r != c->rank) p.base[r] = c->sink + (int64_t)r * c->cap;
+      if (r != c->rank) p.base[r] = c->sink;
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(c->blocks), dim3(kThreads), 0, s, in, out, n / 2, c->cap,
                      c->world, c->rank, p, c->counters, c->err, ticks);
   return hipGetLastError();
 }
+
+// Every muted peer is pointed at the sink's base itself: a kernel adds at most slot (1 x
+// kMaxRanks x cap) + sender row (rank <= kMaxRanks - 1, x cap) + word (< cap), i.e. < 2 x kMaxRanks
+// x cap words -- exactly the sink's size, for any world and rank.  (Offsetting the base by the
+// peer index as well overran the sink from world 6 up.)  Peers sharing one sink only ever
+// collide in a buffer nobody reads.
+static_assert(1 * kMaxRanks + (kMaxRanks - 1) + 1 <= 2 * kMaxRanks, "sink bound");
 
 hipError_t ipc_set_mute(int id, bool mute) {
   IpcComm* c = get(id);
@@ -270,12 +278,13 @@ hipError_t ipc_peers(int id, IpcPeers* out) {
   IpcComm* c = get(id);
   if (!c || c->world < 1) return hipErrorInvalidValue;
   for (int r = 0; r < kMaxRanks; ++r)
-    out->base[r] = (c->muted && r != c->rank && r < c->world) ? c->sink + (int64_t)r * c->cap : c->peers.base[r];
+    out->base[r] = (c->muted && r != c->rank && r < c->world) ? c->sink : c->peers.base[r];
   out->counters = c->counters;
   out->err = c->err;
   out->cap = c->cap;
   out->world = c->world;
   out->rank = c->rank;
+  out->loopback = c->loopback ? 1 : 0;
   return hipSuccess;
 }
 
@@ -304,8 +313,25 @@ hipError_t ipc_error(int id, int* err_out, bool reset) {
   IpcComm* c = get(id);
   if (!c) return hipErrorInvalidValue;
   hipError_t e = hipMemcpy(err_out, c->err, sizeof(int), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && reset) e = hipMemset(c->err, 0, sizeof(int));
+  if (e == hipSuccess && reset) e = hipMemset(c->err, 0, kErrInts * sizeof(int));
   return e;
+}
+
+hipError_t ipc_poison(int id, uint32_t tag, uint32_t value_bits) {
+  IpcComm* c = get(id);
+  if (!c) return hipErrorInvalidValue;
+  const size_t words = (size_t)kMaxRanks * (size_t)c->cap;
+  std::vector<uint64_t> host(words, ((uint64_t)tag << 32) | value_bits);
+  hipError_t e = hipMemcpy(c->buf + (size_t)(tag & 1u) * words, host.data(), words * sizeof(uint64_t),
+                           hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return e;
+}
+
+hipError_t ipc_diag(int id, int* out) {
+  IpcComm* c = get(id);
+  if (!c) return hipErrorInvalidValue;
+  return hipMemcpy(out, c->err + 1, kDiagWords * sizeof(int), hipMemcpyDeviceToHost);
 }
 
 }  // namespace comm

@@ -6,6 +6,8 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <vector>
+
 #include "comm/ipc_allreduce.h"
 
 namespace {
@@ -62,6 +64,17 @@ int64_t ipc_error(int64_t id, bool reset) {
   return e;
 }
 
+// the first loopback mismatch's record (ipc_allreduce.h ipc_diag), synchronous
+std::vector<int64_t> ipc_diag(int64_t id) {
+  int d[csed::comm::kDiagWords] = {};
+  COMM_CHECK(csed::comm::ipc_diag((int)id, d));
+  return std::vector<int64_t>(d, d + csed::comm::kDiagWords);
+}
+
+void ipc_poison(int64_t id, int64_t tag, int64_t value_bits) {
+  COMM_CHECK(csed::comm::ipc_poison((int)id, (uint32_t)tag, (uint32_t)value_bits));
+}
+
 void ipc_set_mute(int64_t id, bool mute) { COMM_CHECK(csed::comm::ipc_set_mute((int)id, mute)); }
 
 void ipc_destroy(int64_t id) { COMM_CHECK(csed::comm::ipc_destroy((int)id)); }
@@ -76,5 +89,7 @@ TORCH_LIBRARY_FRAGMENT(csed, m) {
   m.def("ipc_allreduce(int id, Tensor input, Tensor(a!) out, float timeout_s=2.0) -> ()", &ipc_allreduce);
   m.def("ipc_error(int id, bool reset=False) -> int", &ipc_error);
   m.def("ipc_destroy(int id) -> ()", &ipc_destroy);
+  m.def("ipc_diag(int id) -> int[]", &ipc_diag);
+  m.def("ipc_poison(int id, int tag, int value_bits) -> ()", &ipc_poison);
   m.def("ipc_set_mute(int id, bool mute) -> ()", &ipc_set_mute);
 }

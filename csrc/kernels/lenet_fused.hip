@@ -1619,7 +1619,7 @@ __device__ __forceinline__ void ll_push(const comm::IpcPeers& px, const XPtrs<R>
 template <int K, int R>
 __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                         const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
-                                        bool& timed_out, uint64_t* stamp) {
+                                        bool& timed_out, uint64_t* stamp, int blk) {
   static_assert(K == 1 || K == 4, "one word, or two 16-byte pairs per lane");
   const int64_t so = slot_words(px, t) + w0;
   const int64_t sw = slot_words(px, __builtin_amdgcn_readfirstlane(t));
@@ -1655,6 +1655,30 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
     __builtin_amdgcn_s_sleep(1);
   }
   if (stamp) stamp[6] = passes;  // (diagnostics: poll passes, 1 = the first one found every word)
+  // Loopback invariant: every virtual peer returns this lane's own pushed value, so a live word
+  // that carries the current tag must bit-equal v[k].  A mismatch (a torn or stale word under a
+  // current tag) raises kErrMismatch and records the first one (ipc_diag), so a silently wrong
+  // sum cannot pass as a clean exchange.
+  if (px.loopback && !timed_out) {
+#pragma unroll
+    for (int q = 0; q < R - 1; ++q)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (q < world - 1 && live[k] && (uint32_t)w[q][k] != __float_as_uint(v[k])) {
+          atomicOr(px.err, comm::kErrMismatch);
+          if (atomicCAS(px.err + 1, 0, 1) == 0) {
+            int* d = px.err + 1;
+            d[1] = blk;
+            d[2] = q;
+            d[3] = K == 1 ? w0 : w0 + (k & 1) + 128 * (k >> 1);
+            d[4] = (int)t;
+            d[5] = (int)(uint32_t)w[q][k];
+            d[6] = (int)(uint32_t)(w[q][k] >> 32);
+            d[7] = (int)__float_as_uint(v[k]);
+            d[8] = (int)passes;
+          }
+        }
+  }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     float s = 0.f;
@@ -1714,7 +1738,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   auto err_now = [&]() {
     int v = xerr_raw;
     asm volatile("" : "+v"(v));
-    return v != 0;
+    return (v & comm::kErrTimeout) != 0;  // (a loopback mismatch is reported, never waited on)
   };
   bool timed_out = false;
 #define USTAMP(k) \
@@ -1820,7 +1844,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       if (EXCH) {
         timed_out = err_now();
         ll_poll<1, XR>(px, xp, tag_now(), pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
-                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr, blk);
       }
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
     }
@@ -2113,28 +2137,32 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       if (own) {
         timed_out = err_now();
         ll_poll<4, XR>(px, xp, tag_now(), w0, live, g, timeout_ticks, timed_out,
-                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr);
+                       a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr, blk);
       }
     }
     if (own) {
       bool do_fin = fin;
       if (!fin) {
-        // split-K: this slice's partial tile (MFMA layout) written through (sc1 stores: the tile's
-        // other slices run on other XCDs), then one counter add per tile: the workgroup whose add
-        // comes last (told by the value it returned; only this wave stored, after its vmcnt(0))
-        // reads every slice with sc1 loads, sums them in slice order (fixed: reproducible) and
-        // finishes the tile.  (MI355X_MICROARCH.md hand-off table, first row.)
+        // split-K: this slice's partial tile (MFMA layout) stored at agent scope (the tile's other
+        // slices run on other XCDs), then one counter add per tile: the workgroup whose add comes
+        // last (told by the value it returned) reads every slice, sums them in slice order (fixed:
+        // reproducible) and finishes the tile.  (MI355X_MICROARCH.md hand-off table, first row.)
+        // Ordering is the memory model's, not a hand-placed wait: every lane's agent-scope release
+        // fence orders its partial stores before the counter add (which only lane 0 issues, after
+        // the fences of the whole wave), and the finishing wave's acquire fence orders the add
+        // before its partial loads.
         float* pt = a.fc_part + (int64_t)tile * 256 + lane;  // slice sl at + sl * FC_TILES * 256
         int* cnt = reinterpret_cast<int*>(a.fc_part + FC_PART_FLOATS) + tile;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           __hip_atomic_store(pt + (int64_t)fslice * FC_TILES * 256 + r * 64, g[r], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         int old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         do_fin = __builtin_amdgcn_readfirstlane(old) == fc_sl - 1;
         if (do_fin) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           float pv[8][4];
 #pragma unroll
           for (int sl = 0; sl < 8; ++sl)
@@ -2189,7 +2217,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
   }
 
   if (EXCH) {
-    if (timed_out) atomicOr(px.err, 1);
+    if (timed_out) atomicOr(px.err, comm::kErrTimeout);
     __syncthreads();  // every wave has read counters[blk]
     if (tid == 0) px.counters[blk] = tag_now();
   }

@@ -175,10 +175,14 @@ def test_bench_eight_ranks_bringup_phases_cpu():
     rec = json.loads(js[0])
     assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
     ph = rec["bringup_s"]
-    assert {"spawn", "import", "process_group"} <= set(ph), ph
+    assert {"spawn", "import_torch", "import_pkg", "process_group"} <= set(ph), ph
     assert all(v >= 0 for v in ph.values()), ph
-    # every phase is a part of the span it is measured in
-    assert ph["spawn"] + ph["import"] + ph["process_group"] <= rec["time_elapsed_s"] + 1e-3, rec
+    # every phase is a part of the span it is measured in: the imports (and the spawn) come
+    # before the reference's t0, the rendezvous after it
+    assert ph["process_group"] <= rec["time_elapsed_s"] + 1e-3, rec
+    assert ph["spawn"] + ph["import_torch"] + ph["import_pkg"] + ph["process_group"] \
+        <= rec["process_elapsed_s"] + 1e-3, rec
+    assert rec["replicas_identical"] is True, rec
 
 
 def test_bench_rejects_world_size_mismatch_cpu():

@@ -82,18 +82,57 @@ def test_loopback_training_is_local_training():
     assert torch.equal(finals[0], finals[1])
 
 
+def _train16(world: int) -> torch.Tensor:
+    eng = _engine(8, loopback_world=world, dtype=torch.float32)
+    eng.set_epoch_order(torch.randperm(2048, generator=torch.Generator().manual_seed(1)))
+    eng.run_steps(16, steps_per_graph=8)
+    torch.cuda.synchronize()
+    err, diag = eng.comm_errors(), eng.comm_diag()
+    out = eng.flat.data.clone()
+    eng.close()
+    assert err == 0, f"world {world}: exchange error word {err}, first mismatch {diag}"
+    return out
+
+
 def test_loopback_world8_trains_close_to_local():
     """World 8 sums eight copies in rank order (not exactly 8x in fp32): close to world 1.
     Exact-fp32 kernels (with bf16 weight images a last-bit difference re-rounds an image
-    element and the trajectories drift apart by ~5e-3 in 16 steps, argmax flips included)."""
-    finals = []
-    for world in (0, 8):
-        eng = _engine(8, loopback_world=world, dtype=torch.float32)
-        eng.set_epoch_order(torch.randperm(2048, generator=torch.Generator().manual_seed(1)))
-        eng.run_steps(16, steps_per_graph=8)
-        torch.cuda.synchronize()
-        assert eng.comm_errors() == 0
-        finals.append(eng.flat.data.clone())
-        eng.close()
-    rel = (finals[1] - finals[0]).norm() / finals[0].norm()
-    assert rel < 1e-3, rel.item()
+    element and the trajectories drift apart by ~5e-3 in 16 steps, argmax flips included).
+
+    Three runs, so a divergence names its side: two world-1 runs must be bitwise equal (the
+    step is deterministic: a difference there is the training kernel, not the exchange), and
+    the world-8 run must be close to both, with the in-kernel loopback invariant clean (every
+    received word bit-equal to the value pushed; a failure prints the first mismatch)."""
+    local_a = _train16(0)
+    world8 = _train16(8)
+    local_b = _train16(0)
+    assert torch.equal(local_a, local_b), "the world-1 fp32 step is not deterministic (training kernel side)"
+    rel = ((world8 - local_a).norm() / local_a.norm()).item()
+    assert rel < 1e-3, f"world-8 looped-back run diverged from world 1 (exchange side): rel {rel}"
+
+
+def test_loopback_mismatch_is_detected():
+    """The loopback invariant itself: a receive slot pre-filled with words that carry the
+    next call's tag but a value nobody pushed (csrc/comm ipc_poison), with this rank's pushes
+    muted, must raise the mismatch bit (not the timeout bit) and record the first bad word."""
+    eng = _engine(8, loopback_world=4)
+    ops = torch.ops.csed
+    common = (eng.flat.data, eng.momentum_buf, eng.wimg, eng.lr, eng.momentum, eng.dampening, eng.weight_decay,
+              eng.nesterov, eng.step_count, eng.ticket, None, None, False, None, 0, None, eng.mfma)
+    eng.slab.fill_(1.0)
+    eng.set_fc_vectors(torch.ones(eng.B, 464))
+    poison = 0x7FC0BEEF  # a NaN no gradient produces
+    ops.ipc_poison(eng.exch.id, 1, poison)  # fresh buffer: every workgroup's first tag is 1
+    eng.exch.mute(True)
+    out = torch.empty(N_PARAMS, device=eng.device)
+    ops.lenet_update(eng.slab, eng.grid, eng.vslab, eng.B, None, out, *common, None, eng.exch.id,
+                     eng.exch_timeout_s)
+    torch.cuda.synchronize()
+    err, diag = eng.comm_errors(), eng.comm_diag()
+    assert err == eng.exch.ERR_MISMATCH, err
+    assert diag is not None and diag["tag"] == 1 and diag["got_tag"] == 1
+    assert int(diag["got_word"], 16) & 0xFFFFFFFF == poison
+    assert 0 <= diag["peer_row"] < 3
+    eng.exch.error(reset=True)
+    assert eng.comm_diag() is None
+    eng.close()
