@@ -14,10 +14,11 @@ from .functional import (
     max_pool2d_relu,
     nll_loss,
     set_compute_dtype,
+    set_grad_destination,
 )
 
 __all__ = [
     "accuracy_count", "compute_dtype", "conv2d", "conv2d_pool_relu", "cross_entropy", "dropout",
     "dropout2d", "dropout2d_scale", "linear", "log_softmax", "max_pool2d_relu", "nll_loss",
-    "set_compute_dtype", "rng", "_native",
+    "set_compute_dtype", "set_grad_destination", "rng", "_native",
 ]

@@ -57,6 +57,36 @@ def _act_dtype(x: torch.Tensor) -> torch.dtype:
     return x.dtype if x.dtype in (torch.bfloat16, torch.float16) else _compute_dtype
 
 
+# Weight-gradient destinations (engine/modular.py): a parameter registered here whose ``.grad``
+# is None when its backward runs gets its gradient written straight into the registered buffer
+# (a view of the flat gradient), which autograd's AccumulateGrad then adopts as ``.grad`` without
+# a copy or an add kernel.  A parameter that already holds a gradient gets a fresh buffer, so
+# accumulation (no zero_grad between two backwards) keeps its usual semantics.
+import weakref  # noqa: E402
+
+# id(param) -> (weak reference to param, buffer); keyed by identity (tensors compare elementwise)
+_grad_dest: dict[int, tuple[weakref.ref, torch.Tensor]] = {}
+
+
+def set_grad_destination(param: torch.Tensor, buf: torch.Tensor | None) -> None:
+    """Register (or with None, drop) the fp32 buffer ``param``'s gradient is written into."""
+    if buf is None:
+        _grad_dest.pop(id(param), None)
+        return
+    if buf.shape != param.shape or buf.dtype != torch.float32 or buf.device != param.device:
+        raise ValueError("gradient destination must be an fp32 tensor of the parameter's shape and device")
+    for k in [k for k, (r, _) in _grad_dest.items() if r() is None]:  # (drop dead entries)
+        del _grad_dest[k]
+    _grad_dest[id(param)] = (weakref.ref(param), buf)
+
+
+def _grad_buffer(param: torch.Tensor | None, shape, device) -> torch.Tensor:
+    hit = _grad_dest.get(id(param)) if param is not None else None
+    if hit is not None and hit[0]() is param and param.grad is None:
+        return hit[1].view(hit[1].shape)  # (a fresh view: AccumulateGrad steals only a sole reference)
+    return torch.empty(shape, device=device, dtype=torch.float32)
+
+
 def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
     return max(1, min(N, 256)) * OC * (IC * KH * KW + 1)
 
@@ -81,6 +111,7 @@ class _Conv2d(torch.autograd.Function):
             _ops().conv2d_fwd(x, w, b, y, pad, None, None, 0, mf)
             ctx.save_for_backward(x, w)
         ctx.pad, ctx.pool, ctx.mf, ctx.has_bias = pad, pool, mf, b is not None
+        ctx.bias_param = b
         ctx.conv_shape = (N, OC, OH, OW)
         return y
 
@@ -98,8 +129,8 @@ class _Conv2d(torch.autograd.Function):
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             N, IC = x.shape[:2]
             OC, _, KH, KW = w.shape
-            dw = torch.empty_like(w, dtype=torch.float32)
-            db = torch.empty((OC,), device=w.device, dtype=torch.float32) if ctx.has_bias else None
+            dw = _grad_buffer(w, w.shape, w.device)
+            db = _grad_buffer(ctx.bias_param, (OC,), w.device) if ctx.has_bias else None
             ws = torch.empty(wgrad_workspace_elems(N, IC, KH, KW, OC), device=w.device, dtype=torch.float32)
             _ops().conv2d_wgrad(x, dconv, dw, db, ws, ctx.pad, ctx.mf, 0.0)
         if ctx.needs_input_grad[0]:
@@ -226,6 +257,7 @@ class _Linear(torch.autograd.Function):
         _ops().gemm(x2, w.t(), y, b, 1.0, 0.0, act, p, seed, offset, offset_dev, None, 1.0, _mfma())
         ctx.save_for_backward(x2, w, y if act else None)
         ctx.act, ctx.p, ctx.has_bias, ctx.lead = act, p, b is not None, lead
+        ctx.bias_param = b
         return y.view(*lead, w.shape[0])
 
     @staticmethod
@@ -244,10 +276,10 @@ class _Linear(torch.autograd.Function):
             dx = dx.view(*ctx.lead, x2.shape[1])
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         if want_db:
-            db = torch.empty((w.shape[0],), device=w.device, dtype=torch.float32)
+            db = _grad_buffer(ctx.bias_param, (w.shape[0],), w.device)
         if ctx.needs_input_grad[1]:
             # dW = gate(dY)^T X; the bias gradient rides along as the GEMM's ones column
-            dw = torch.empty(w.shape, device=w.device, dtype=torch.float32)
+            dw = _grad_buffer(w, w.shape, w.device)
             _ops().gemm(dy2.t(), x2, dw, None, 1.0, 0.0, 0, 0.0, 0, 0, None,
                         gate.t() if gate is not None else None, gs, mf, db if want_db else None)
         elif want_db:

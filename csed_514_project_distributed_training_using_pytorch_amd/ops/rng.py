@@ -32,6 +32,13 @@ class PhiloxState:
             self._seed = int(seed) & 0xFFFFFFFFFFFF
             self._offset = 0
 
+    def reset_offset(self) -> None:
+        """Restart the host offsets (engine/modular.py calls it at every step start: with the
+        device step counter in the high bits, masks are then a pure function of (seed, step,
+        call index), identical between an eager step and a graph replay of it)."""
+        with self._lock:
+            self._offset = 0
+
     def next(self) -> tuple[int, int, torch.Tensor | None]:
         with self._lock:
             off = self._offset

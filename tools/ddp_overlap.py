@@ -34,14 +34,18 @@ def _modes():
             ("overlap", 0.01, True), ("serial", 0.01, False)]
 
 
-def run(batch: int, steps: int, warmup: int, trace: bool, only=None) -> list[dict]:
+def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(False, True)) -> list[dict]:
+    """Step times of the modular engine (engine/modular.py ModularTrainer: its DDP reducer, fused
+    SGD, and -- graph=True -- one HIP-graph replay per step) per reducer mode."""
+    import contextlib
+    import types
+
     import torch
     import torch.distributed as dist
 
     from csed_514_project_distributed_training_using_pytorch_amd import ops
+    from csed_514_project_distributed_training_using_pytorch_amd.engine.modular import ModularTrainer
     from csed_514_project_distributed_training_using_pytorch_amd.models.net import Net
-    from csed_514_project_distributed_training_using_pytorch_amd.optim.sgd import FusedSGD
-    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ddp import DistributedDataParallel
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
@@ -51,44 +55,40 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None) -> list[dic
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand(batch, 1, 28, 28, device=dev, generator=g).to(ops.compute_dtype())
     t = torch.randint(0, 10, (batch,), device=dev, generator=g)
+    ctx = types.SimpleNamespace(is_distributed=True, backend="nccl")  # (the reducer's collective path)
     rows = []
-    for mode, cap, overlap in _modes():
-        if only is not None and (mode, cap) != only:
-            continue
-        torch.manual_seed(1)
-        net = Net().to(dev).train()
-        ddp = DistributedDataParallel(net, bucket_cap_mb=cap, overlap=overlap)
-        ddp.world_size = 2  # force the collective path (see the module docstring)
-        opt = FusedSGD(list(net.parameters()), lr=0.01, momentum=0.5, flat=ddp.flat)
-        ops.rng.default_state.device_step = opt.step_count
+    for graph in graphs:
+        for mode, cap, overlap in _modes():
+            if only is not None and (mode, cap) != only:
+                continue
+            torch.manual_seed(1)
+            net = Net().to(dev).train()
+            tr = ModularTrainer(net, lr=0.01, momentum=0.5, ctx=ctx, bucket_cap_mb=cap, graph=graph,
+                                overlap=overlap)
+            tr.ddp.world_size = 2  # force the collective path (see the module docstring)
 
-        def step():
-            opt.zero_grad()
-            if mode == "nocomm":
-                with ddp.no_sync():
-                    loss = ops.nll_loss(ddp(x), t)
-                    loss.backward()
-            else:
-                loss = ops.nll_loss(ddp(x), t)
-                loss.backward()
-            opt.step()
+            def step():
+                with tr.ddp.no_sync() if mode == "nocomm" else contextlib.nullcontext():
+                    tr.train_batch(x, t, clone_loss=False)
 
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        e0.record()
-        for _ in range(steps):
-            step()
-        e1.record()
-        torch.cuda.synchronize()
-        wall = (time.perf_counter() - t0) / steps
-        rows.append({"mode": mode, "batch": batch, "bucket_mb": cap, "buckets": len(ddp.buckets),
-                     "us_per_step_gpu": round(e0.elapsed_time(e1) * 1000 / steps, 2),
-                     "us_per_step_wall": round(wall * 1e6, 2)})
-        for h in ddp._hooks:
-            h.remove()
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            for _ in range(steps):
+                step()
+            e1.record()
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) / steps
+            rows.append({"mode": mode, "graph": graph and tr.use_graph, "batch": batch, "bucket_mb": cap,
+                         "buckets": len(tr.ddp.buckets),
+                         "us_per_step_gpu": round(e0.elapsed_time(e1) * 1000 / steps, 2),
+                         "us_per_step_wall": round(wall * 1e6, 2)})
+            for h in tr.ddp._hooks:
+                h.remove()
+            del tr
     dist.destroy_process_group()
     return rows
 
@@ -132,6 +132,7 @@ def main() -> None:
     ap.add_argument("--mode", default="overlap", help="--trace: nocomm / overlap / serial")
     ap.add_argument("--bucket-mb", type=float, default=0.01, help="--trace: bucket cap")
     ap.add_argument("--parse", help="run_kernel_trace.csv of a --trace run")
+    ap.add_argument("--graph", choices=["both", "eager", "graph"], default="both")
     a = ap.parse_args()
     if a.parse:
         print(json.dumps(parse(a.parse)))
@@ -139,7 +140,8 @@ def main() -> None:
     only = None
     if a.trace:
         a.steps, a.warmup, only = 20, 5, (a.mode, a.bucket_mb)
-    for r in run(a.batch, a.steps, a.warmup, a.trace, only):
+    graphs = {"both": (False, True), "eager": (False,), "graph": (True,)}[a.graph]
+    for r in run(a.batch, a.steps, a.warmup, a.trace, only, graphs):
         print(json.dumps(r), flush=True)
 
 
