@@ -36,17 +36,22 @@ A loopback log (``--loopback-log``, the ``B=.. N=.. ... step X us`` lines of
 exchange_loopback.py) replaces the built-in table.  The driver's SCALE record is then checked
 against the prediction in the ``measured / predicted`` column.
 
-Predicted ``time_elapsed`` (the reference's own quantity: process start -> end of epoch-0
-validation, ref src/train_dist.py:119,112).  bench.py's ``bringup_s`` splits it into phases
-(max over ranks).  For N ranks:
+Predicted ``time_elapsed`` (the reference's own quantity: its t0, taken right after its imports,
+-> end of epoch-0 validation, ref src/train_dist.py:1-11,119,112; bench.py takes t0 after
+``import torch`` and the package, so the imports are outside it and inside
+``process_elapsed_s``).  bench.py's ``bringup_s`` splits it into phases (max over ranks).  For
+N ranks:
 
-    time_elapsed_N = spawn_N + import_N + process_group_N      (--cpu-bringup: bench.py --gpus N
-                                                                 --device cpu on the GPU box: N
-                                                                 concurrent imports + rendezvous)
+    time_elapsed_N = process_group_N                           (--cpu-bringup: bench.py --gpus N
+                                                                 --device cpu on the GPU box: an
+                                                                 N-rank rendezvous)
                    + data_wait_1 + engine_1 + capture_1 + test_upload_1     (the N = 1 GPU record)
-                   + exchange bring-up (engine.ipc_open + engine.self_test of --rehearsal, a
-                     2-rank gloo run sharing the GPU; 0 at N = 1)
+                   + exchange bring-up (engine.ipc_open + engine.self_test + engine.path_timing of
+                     --rehearsal, a 2-rank gloo run sharing the GPU; 0 at N = 1)
                    + epoch0_1 + 938 * (step_N - step_1)        (the epoch at the predicted step)
+
+Records from before round 5 (an ``import`` phase, no ``import_torch``) measured time_elapsed_s
+from process start; for those the prediction keeps spawn + import in the span.
 
 What it leaves out: RCCL's communicator set-up over N GPUs (the CPU rehearsal's rendezvous is
 gloo) and xGMI peer mapping (the rehearsal maps one GPU's memory).
@@ -114,13 +119,15 @@ def predict_time_elapsed(by_n: dict[int, dict], pred: dict[int, dict], cpu_by_n:
     xb = 0.0
     if rehearsal:
         rph = rehearsal.get("bringup_s") or {}
-        xb = rph.get("engine.ipc_open", 0.0) + rph.get("engine.self_test", 0.0)
+        xb = sum(rph.get(k, 0.0) for k in ("engine.ipc_open", "engine.self_test", "engine.path_timing"))
     out = {}
     for n, p in pred.items():
         c = (cpu_by_n.get(n) or {}).get("bringup_s") if n > 1 else ph1
         if not c:
             continue
-        launch = sum(c.get(k, 0.0) for k in ("spawn", "import", "process_group"))
+        # round 5+: t0 after the imports (import_torch / import_pkg are outside the span)
+        keys = ("process_group",) if "import_torch" in c else ("spawn", "import", "process_group")
+        launch = sum(c.get(k, 0.0) for k in keys)
         ep0 = r1["epoch0_s"] + STEPS_PER_EPOCH * (p["step_us"] - pred[1]["step_us"]) * 1e-6
         out[n] = launch + base + (xb if n > 1 else 0.0) + ep0
     return out
@@ -207,7 +214,8 @@ def markdown(rows: list[dict], title: str) -> str:
             "to 8 images per step at N = 8.  Predicted columns: the one-GPU loopback measurement of the "
             "per-rank step (per-rank batch 64/N, exchange with N-1 virtual peers) + one xGMI hop + the "
             "pushes' link time (175 KB per peer per step at the assumed link rate); predicted "
-            "time_elapsed: N concurrent imports + rendezvous measured on the CPU, the N = 1 GPU bring-up, "
+            "time_elapsed (the reference's span: t0 after the imports): an N-rank rendezvous measured on the "
+            "CPU, the N = 1 GPU bring-up, "
             "the exchange bring-up of a 2-rank rehearsal and epoch 0 at the predicted step; see the "
             "module docstring of tools/scaling_report.py."]
     return "\n".join(out) + "\n"
@@ -226,7 +234,7 @@ def plot(rows: list[dict], path: Path, title: str) -> bool:
     ax.plot(ns, [REF_EPOCH_S[n] for n in ns], "o-", color="gray", label="reference (CPU VMs, gloo)")
     pts = [(r["n"], r["time_elapsed_s"]) for r in rows if r["time_elapsed_s"]]
     if pts:
-        ax.plot(*zip(*pts), "s-", color="tab:orange", label="MI355X, process start -> epoch 0 done")
+        ax.plot(*zip(*pts), "s-", color="tab:orange", label="MI355X, t0 (after imports) -> epoch 0 done")
     pts = [(r["n"], r["epoch_s"]) for r in rows if r["epoch_s"]]
     if pts:
         ax.plot(*zip(*pts), "^-", color="tab:blue", label="MI355X, warm epoch (938 steps + validation)")
