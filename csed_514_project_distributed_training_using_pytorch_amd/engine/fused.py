@@ -644,7 +644,12 @@ class FusedLeNetTrainer:
         for t, v in zip(state, saved):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g, stream=s):
+        # thread_local: only this thread's unsafe calls invalidate the capture.  The process
+        # group's watchdog thread keeps querying the events of earlier collectives while a step
+        # that contains an RCCL all-reduce is captured; in the default (global) mode that query
+        # invalidates the capture and the watchdog then aborts the process (seen on the GPU box,
+        # profiles/round5.md)
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for _ in range(nsteps):
                 step()
         torch.cuda.synchronize(self.device)

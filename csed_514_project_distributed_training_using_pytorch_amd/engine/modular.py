@@ -125,7 +125,9 @@ class ModularTrainer:
                 t.copy_(v)
             torch.cuda.synchronize(dev)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=s):
+            # thread_local: the process group's watchdog thread may query earlier collectives'
+            # events during the capture (see engine/fused.py _capture)
+            with torch.cuda.graph(graph, stream=s, capture_error_mode="thread_local"):
                 sloss = self._step(sx, st)
             torch.cuda.synchronize(dev)
         except Exception as e:  # an op or collective that cannot be captured: eager steps

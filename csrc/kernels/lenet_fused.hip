@@ -2143,26 +2143,26 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
     if (own) {
       bool do_fin = fin;
       if (!fin) {
-        // split-K: this slice's partial tile (MFMA layout) stored at agent scope (the tile's other
-        // slices run on other XCDs), then one counter add per tile: the workgroup whose add comes
-        // last (told by the value it returned) reads every slice, sums them in slice order (fixed:
-        // reproducible) and finishes the tile.  (MI355X_MICROARCH.md hand-off table, first row.)
-        // Ordering is the memory model's, not a hand-placed wait: every lane's agent-scope release
-        // fence orders its partial stores before the counter add (which only lane 0 issues, after
-        // the fences of the whole wave), and the finishing wave's acquire fence orders the add
-        // before its partial loads.
+        // split-K: this slice's partial tile (MFMA layout) written through (sc1 stores: the tile's
+        // other slices run on other XCDs), drained (vmcnt(0)), then one counter add per tile: the
+        // workgroup whose add comes last (told by the value it returned) reads every slice with
+        // sc1 loads, sums them in slice order (fixed: reproducible) and finishes the tile.  This is
+        // the write-through hand-off form of MI355X_MICROARCH.md's inter-workgroup visibility row
+        // ("EVERY store of the handed-off bytes sc1 and drained ... before the flag/counter and
+        // EVERY load of them ... sc1"), which stands in for the release / acquire pair: an
+        // agent-scope release fence is an L2 write-back and the acquire an L2 invalidate on this
+        // multi-XCD part, and with them the B = 8192 step measured 145 -> 172 us (profiles/round5.md).
         float* pt = a.fc_part + (int64_t)tile * 256 + lane;  // slice sl at + sl * FC_TILES * 256
         int* cnt = reinterpret_cast<int*>(a.fc_part + FC_PART_FLOATS) + tile;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           __hip_atomic_store(pt + (int64_t)fslice * FC_TILES * 256 + r * 64, g[r], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         do_fin = __builtin_amdgcn_readfirstlane(old) == fc_sl - 1;
         if (do_fin) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           float pv[8][4];
 #pragma unroll
           for (int sl = 0; sl < 8; ++sl)

@@ -26,7 +26,7 @@ def timed_graph(fn, dev, calls=200, reps=5):
             fn()
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
+    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):  # (see engine/fused.py _capture)
         for _ in range(calls):
             fn()
     ts = []

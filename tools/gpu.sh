@@ -24,6 +24,7 @@
 #   abtile    same-box A/B of ab/A_C.so vs ab/B_C.so at global batch 1024 / 8192 fp16 (lenet_tile)
 #   pmctile   the three PMC passes over the tile kernel only (B = 1024)
 #   abenv     same-box A/B of one build under ENV_A vs ENV_B (BENCH_ARGS / AB_ARGS / N_AB)
+#   abcfg     same-box A/B of ab/A_C.so vs ab/B_C.so over several bench configs (AB_CFGS, N_AB)
 TASKS=${1:?task list}
 T=${2:-run}
 R=$GRAFT_REPO_ROOT
@@ -120,6 +121,14 @@ task_abtile() {  # same-box A/B of ab/A_C.so vs ab/B_C.so on the large-batch ste
     echo "$v B=1024 $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py --global-batch 1024 --dtype fp16 --steps 400 --warmup 40 --no-epoch 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abtile.log || return 1
     echo "$v B=8192 $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py --global-batch 8192 --dtype fp16 --steps 60 --warmup 6 --no-epoch 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abtile.log || return 1
   done; done
+}
+
+task_abcfg() {  # same-box A/B of ab/A_C.so vs ab/B_C.so over AB_CFGS (';'-separated bench argument sets)
+  cd $R && rm -f $O/${T}_abcfg.log && \
+  IFS=';' read -ra CFGS <<< "${AB_CFGS:---global-batch 64 --steps 3000 --warmup 300;--global-batch 8 --loopback-world 8 --steps 3000 --warmup 300;--global-batch 1024 --dtype fp16 --steps 400 --warmup 40;--global-batch 8192 --dtype fp16 --steps 60 --warmup 6}" && \
+  for i in $(seq ${N_AB:-3}); do for c in "${CFGS[@]}"; do for v in A B; do
+    echo "$v [$c] $(CSED_NATIVE_SO=$R/ab/${v}_C.so py 100 python bench.py $c --no-epoch --no-fp32-record 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abcfg.log || return 1
+  done; done; done
 }
 
 task_pmctile() {
