@@ -328,6 +328,7 @@ def main(argv=None) -> int:
             t_mark = time.time()
             torch.manual_seed(1)
             net = Net().to(ctx.device)
+            ph["engine.net"] = time.time() - t_mark
             eng = FusedLeNetTrainer(net, train, lr=0.02, momentum=0.5, global_batch=args.global_batch, ctx=ctx,
                                     compute_dtype=dt, grid=args.grid or None, loopback_world=loopback_world)
             ph["engine"] = time.time() - t_mark

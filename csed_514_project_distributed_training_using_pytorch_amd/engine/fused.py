@@ -116,7 +116,11 @@ class FusedLeNetTrainer:
                  compute_dtype: torch.dtype = torch.bfloat16, drop_p: float = 0.5, seed: int = 1,
                  grid: int | None = None, broadcast_init: bool = True, comm: bool | None = None,
                  split: bool | None = None, loopback_world: int = 0):
+        import time
+
         _native.require()
+        t_init = time.perf_counter()
+        self.bringup_s: dict[str, float] = {}  # bring-up phases (s), for the bench JSON
         self.ctx = ctx or DistContext(device=next(model.parameters()).device)
         self.device = self.ctx.device
         if self.device.type != "cuda":
@@ -141,6 +145,7 @@ class FusedLeNetTrainer:
         self.seed = int(seed)  # masks decorrelate across ranks through the rank id in the element index
         self.train_data = train.to(self.device)
         dev = self.device
+        self.bringup_s["data_to_device"] = time.perf_counter() - t_init
 
         self.flat = FlatParams(list(model.parameters()))
         if self.flat.numel != N_PARAMS:
@@ -200,7 +205,9 @@ class FusedLeNetTrainer:
         srows = self.grid if self.staged else (self.grid * tile_samples() if self.tile_staged else 0)
         self.xstage = torch.zeros((srows, 784), dtype=torch.uint8, device=dev) if srows else None
         self.lstage = torch.zeros(srows, dtype=torch.long, device=dev) if srows else None
-        self.repack()
+        t_mark = time.perf_counter()
+        self.repack()  # (the extension's first kernel launch: its code object loads here)
+        self.bringup_s["first_kernel"] = time.perf_counter() - t_mark
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._stepper: tuple | None = None  # (key, csed.LenetStepper), see stepper()
         self.native_max = native_max_steps()
@@ -217,7 +224,6 @@ class FusedLeNetTrainer:
         self.exchange_note: str | None = None  # why the data-parallel step runs as it does (reports)
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
-        self.bringup_s: dict[str, float] = {}  # exchange bring-up phases (s), for the bench JSON
         self.loopback_world = 0  # (set below; the exchange bring-up's reports read it)
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"

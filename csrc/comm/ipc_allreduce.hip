@@ -284,7 +284,13 @@ hipError_t ipc_peers(int id, IpcPeers* out) {
   out->cap = c->cap;
   out->world = c->world;
   out->rank = c->rank;
-  out->loopback = c->loopback ? 1 : 0;
+  // CSED_LOOPBACK_CHECK=0 switches the loopback invariant off (a measurement switch: the looped-back
+  // step without the check's per-word compare, i.e. the code path a real world-N step runs)
+  static const bool check = [] {
+    const char* e = std::getenv("CSED_LOOPBACK_CHECK");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  out->loopback = (c->loopback && check) ? 1 : 0;
   return hipSuccess;
 }
 

@@ -75,33 +75,66 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   const int npix = rows * g.OW;
   const int tid = threadIdx.x;
 
-  // ---- stage weights (fp32 -> 16 bit) and the k -> patch offset table
-  for (int i = tid; i < g.Cop * g.Kp; i += 256) {
-    const int oc = i / g.Kp, k = i % g.Kp;
-    float v = 0.f;
-    if (oc < g.Co && k < g.K) {
-      const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
-      v = weff(a.w, a.mode, g.Ci, g.Co, g.KH, g.KW, oc, ic, r / g.KW, r % g.KW);
-    }
-    Ws[oc * LDW + k] = Stor<T>::of(v);
-  }
+  // ---- stage weights (fp32 -> 16 bit) and the k -> patch offset table.  A thread keeps its K
+  // columns for every oc: the k -> (ic, kh, kw) split (integer divisions) is done once per column,
+  // not once per element (per-element divisions were most of a small-batch launch)
+  const int KHW = g.KH * g.KW;
   for (int k = tid; k < g.Kp; k += 256) {
-    int o = 0;
-    if (k < g.K) {
-      const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
-      o = (ic * g.PR + r / g.KW) * g.PW + r % g.KW;
+    const bool kv = k < g.K;
+    const int ic = kv ? k / KHW : 0, r = k - ic * KHW, kh = r / g.KW, kw = r - kh * g.KW;
+    koff[k] = kv ? (ic * g.PR + kh) * g.PW + kw : 0;
+    // effective weight (oc, ic, kh, kw) = w[base + oc * step] (see weff)
+    const int64_t base = a.mode == 0 ? k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
+    const int64_t step = a.mode == 0 ? g.K : KHW;
+    // eight loads in flight, then eight LDS stores (a load -> convert -> store chain per element
+    // waited for every load in turn: ~1 us of memory latency each)
+    for (int oc0 = 0; oc0 < g.Cop; oc0 += 8) {  // (Cop: a multiple of 16)
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = kv && oc0 + j < g.Co ? a.w[base + (oc0 + j) * step] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(v[j]);
     }
-    koff[k] = o;
   }
-  // ---- stage the zero-padded input patch
+  // ---- stage the zero-padded input patch: a thread owns one patch column, rows step by
+  // 256 / PW (no per-element divisions)
   const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
-  const int pe = g.Ci * g.PR * g.PW;
-  for (int i = tid; i < pe; i += 256) {
-    const int pc = i % g.PW, pr = (i / g.PW) % g.PR, ic = i / (g.PW * g.PR);
-    const int ih = oh0 - g.pad + pr, iw = pc - g.pad;
-    float v = 0.f;
-    if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) v = ldf(a.x, a.x_dtype, xbase + ((int64_t)ic * g.H + ih) * g.W + iw);
-    patch[i] = Stor<T>::of(v);
+  {
+    const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+    int rr = tid / g.PW;
+    if (rr < rpi) {
+      int ic = rr / g.PR, pr = rr - ic * g.PR;
+      const int iw = pc - g.pad;
+      const bool colv = iw >= 0 && iw < g.W;
+      // (the input dtype dispatched once, outside the loop: a per-load switch kept the loads apart)
+      auto rows = [&](auto tag) {
+        typedef decltype(tag) X;
+        const X* xs = static_cast<const X*>(a.x);
+        while (rr < nrows) {  // eight rows' loads in flight, then their LDS stores
+          float v[8];
+          int at[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ih = oh0 - g.pad + pr;
+            at[j] = rr < nrows ? rr : -1;
+            v[j] = (rr < nrows && colv && ih >= 0 && ih < g.H) ? (float)xs[xbase + ((int64_t)ic * g.H + ih) * g.W + iw]
+                                                               : 0.f;
+            rr += rpi;
+            pr += rpi;
+            while (pr >= g.PR) {
+              pr -= g.PR;
+              ++ic;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(v[j]);
+        }
+      };
+      if (a.x_dtype == kF32) rows(float{});
+      else if (a.x_dtype == kBF16) rows(__bf16{});
+      else rows(_Float16{});
+    }
   }
   __syncthreads();
 
@@ -237,21 +270,60 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
   for (int n = n_begin; n < n_end; ++n) {
     __syncthreads();  // previous image's LDS reads are done
     const int64_t xb = (int64_t)n * g.Ci * g.H * g.W;
-    for (int i = tid; i < pe + 1; i += 256) {
-      float v = 1.f;  // slot pe holds 1.0 -> db column
-      if (i < pe) {
-        const int pc = i % g.PW, pr = (i / g.PW) % g.PR, ic = i / (g.PW * g.PR);
-        const int ih = pr - g.pad, iw = pc - g.pad;
-        v = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? ldf(x, xdt, xb + ((int64_t)ic * g.H + ih) * g.W + iw) : 0.f;
+    {  // the zero-padded input patch: one patch column per thread, rows stepping by 256 / PW
+      const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+      int rr = tid / g.PW;
+      if (rr < rpi) {
+        int ic = rr / g.PR, pr = rr - ic * g.PR;
+        const int iw = pc - g.pad;
+        const bool colv = iw >= 0 && iw < g.W;
+        auto rows = [&](auto tag) {  // (dtype dispatched once, see conv_fwd_kernel)
+          typedef decltype(tag) X;
+          const X* xs = static_cast<const X*>(x);
+          while (rr < nrows) {  // eight rows' loads in flight, then their LDS stores
+            float v[8];
+            int at[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int ih = pr - g.pad;
+              at[j] = rr < nrows ? rr : -1;
+              v[j] = (rr < nrows && colv && ih >= 0 && ih < g.H) ? (float)xs[xb + ((int64_t)ic * g.H + ih) * g.W + iw]
+                                                                 : 0.f;
+              rr += rpi;
+              pr += rpi;
+              while (pr >= g.PR) {
+                pr -= g.PR;
+                ++ic;
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(v[j]);
+          }
+        };
+        if (xdt == kF32) rows(float{});
+        else if (xdt == kBF16) rows(__bf16{});
+        else rows(_Float16{});
       }
-      patch[i] = Stor<T>::of(v);
+      if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
     }
     const int64_t yb = (int64_t)n * g.Co * g.npix;
-    for (int i = tid; i < g.Cop * g.npp; i += 256) {
-      const int oc = i / g.npp, p = i % g.npp;
-      const float v = (oc < g.Co && p < g.npix) ? ldf(dy, dydt, yb + (int64_t)oc * g.npix + p) : 0.f;
-      dys[oc * LDY + p] = Stor<T>::of(v);
-    }
+    auto dyrows = [&](auto tag) {  // a thread keeps its pixel for every oc, 8 loads in flight
+      typedef decltype(tag) X;
+      const X* ys = static_cast<const X*>(dy);
+      for (int p = tid; p < g.npp; p += 256)
+        for (int oc0 = 0; oc0 < g.Cop; oc0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = (oc0 + j < g.Co && p < g.npix) ? (float)ys[yb + (int64_t)(oc0 + j) * g.npix + p] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(v[j]);
+        }
+    };
+    if (dydt == kF32) dyrows(float{});
+    else if (dydt == kBF16) dyrows(__bf16{});
+    else dyrows(_Float16{});
     __syncthreads();
     if (my_nt0 >= NT) continue;
     for (int ps = my_s; ps * 32 < g.npp; ps += psplit) {
@@ -321,19 +393,41 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
   }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int nblocks, int Co, int K,
-                                    float* __restrict__ dw, float* __restrict__ db, float beta) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
+// 4 slices of the partials each (every lane's loads issued together, 8 in flight), then the
+// slices combine in slice order through LDS.  One thread per output walking all nblocks partials
+// in a dependent add chain was latency-bound: 15.8 us for 64 partials (profiles/round5.md).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nblocks, int Co,
+                                                           int K, float* __restrict__ dw, float* __restrict__ db,
+                                                           float beta) {
+  __shared__ float part[4][64];
   const int L = Co * (K + 1);
-  if (i >= L) return;
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int b = 0; b < nblocks; ++b) s += slab[(int64_t)b * L + i];
-  const int oc = i / (K + 1), col = i % (K + 1);
-  if (col < K) {
-    float* d = dw + (int64_t)oc * K + col;
-    *d = beta != 0.f ? fmaf(beta, *d, s) : s;
-  } else if (db) {
-    db[oc] = beta != 0.f ? fmaf(beta, db[oc], s) : s;
+  if (i < L) {
+    const int per = (nblocks + 3) >> 2, b0 = sl * per, b1 = min(nblocks, b0 + per);
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(b + u) * L + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += slab[(int64_t)b * L + i];
+  }
+  part[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && i < L) {
+    const float t = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
+    const int oc = i / (K + 1), col = i % (K + 1);
+    if (col < K) {
+      float* d = dw + (int64_t)oc * K + col;
+      *d = beta != 0.f ? fmaf(beta, *d, t) : t;
+    } else if (db) {
+      db[oc] = beta != 0.f ? fmaf(beta, db[oc], t) : t;
+    }
   }
 }
 
@@ -429,8 +523,8 @@ hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int d
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int L = OC * (g.K + 1);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 256)), dim3(256), 0, s, ws, g.nblocks, OC, g.K, dw,
-                     db, beta);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, ws, g.nblocks, OC, g.K, dw, db,
+                     beta);
   return hipGetLastError();
 }
 

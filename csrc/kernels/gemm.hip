@@ -89,19 +89,30 @@ __device__ __forceinline__ void load_raw(Raw& raw, const void* X, int dt, int mo
       return;
     }
   }
-  // scalar path (any layout / dtype, and the ragged edges of the vector modes)
+  // scalar path (any layout / dtype, and the ragged edges of the vector modes).  The dtype is
+  // dispatched once around the eight loads: a per-load switch kept them from issuing together
   float f[8];
+  auto gather = [&](auto tag) {
+    typedef decltype(tag) X_t;
+    const X_t* xp = static_cast<const X_t*>(X);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    int gr, gk;
-    if (mode == kRContig) {
-      gr = r0 + (t & 7) * 8 + j;
-      gk = k0 + (t >> 3);
-    } else {
-      gr = r0 + (t >> 2);
-      gk = k0 + (t & 3) * 8 + j;
+    for (int j = 0; j < 8; ++j) {
+      int gr, gk;
+      if (mode == kRContig) {
+        gr = r0 + (t & 7) * 8 + j;
+        gk = k0 + (t >> 3);
+      } else {
+        gr = r0 + (t >> 2);
+        gk = k0 + (t & 3) * 8 + j;
+      }
+      f[j] = (gr < R && gk < K) ? (float)xp[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
     }
-    f[j] = (gr < R && gk < K) ? ld_any(X, dt, (int64_t)gr * s_r + (int64_t)gk * s_k) : 0.f;
+  };
+  switch (dt) {
+    case kF32: gather(float{}); break;
+    case kBF16: gather(__bf16{}); break;
+    case kF16: gather(_Float16{}); break;
+    default: gather(uint8_t{}); break;
   }
   if constexpr (!__is_same(T, float)) {
     if (pk) {

@@ -1613,6 +1613,41 @@ __device__ __forceinline__ void ll_push(const comm::IpcPeers& px, const XPtrs<R>
     }
 }
 
+// The first loopback mismatch's record (ll_poll's invariant).  The slow path, off the poll loop:
+// it re-reads the lane's words from the receive buffer itself (they stay put until the next call
+// of the same parity) and takes only scalars, so the hot loop's word array never has to be
+// addressable (an array passed by reference, or indexed by a run-time bound, lives in scratch
+// memory: +3.5 us per looped-back step, profiles/round5.md).
+__device__ __attribute__((noinline)) void loopback_mismatch(int* err, const uint64_t* src, int64_t cap,
+                                                            int64_t slot, int w0, int k_words, int nrows,
+                                                            uint32_t live_bits, float v0, float v1, float v2,
+                                                            float v3, uint32_t t, uint32_t passes, int rank,
+                                                            int blk) {
+  atomicOr(err, comm::kErrMismatch);
+  for (int q = 0; q < nrows; ++q)
+    for (int k = 0; k < k_words; ++k) {
+      if (!((live_bits >> k) & 1u)) continue;
+      const int word = k_words == 1 ? w0 : w0 + (k & 1) + 128 * (k >> 1);
+      const int p = q < rank ? q : q + 1;  // row q holds sender p (ll_poll)
+      const uint64_t got =
+          __hip_atomic_load(src + (int64_t)p * cap + slot + word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const float want = k == 0 ? v0 : (k == 1 ? v1 : (k == 2 ? v2 : v3));
+      if ((uint32_t)got == __float_as_uint(want)) continue;
+      if (atomicCAS(err + 1, 0, 1) == 0) {
+        int* d = err + 1;
+        d[1] = blk;
+        d[2] = q;
+        d[3] = word;
+        d[4] = (int)t;
+        d[5] = (int)(uint32_t)got;
+        d[6] = (int)(uint32_t)(got >> 32);
+        d[7] = (int)__float_as_uint(want);
+        d[8] = (int)passes;
+      }
+      return;
+    }
+}
+
 // v[k] := sum over ranks of word k, in rank order (so every rank gets identical bits): polls
 // this rank's receive buffer for every peer's words of tag t, all loads issued before the first
 // wait (one memory round trip per pass)
@@ -1658,29 +1693,15 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
   // Loopback invariant: every virtual peer returns this lane's own pushed value, so a live word
   // that carries the current tag must bit-equal v[k].  A mismatch (a torn or stale word under a
   // current tag) raises kErrMismatch and records the first one (ipc_diag), so a silently wrong
-  // sum cannot pass as a clean exchange.
-  if (px.loopback && !timed_out) {
-#pragma unroll
-    for (int q = 0; q < R - 1; ++q)
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (q < world - 1 && live[k] && (uint32_t)w[q][k] != __float_as_uint(v[k])) {
-          atomicOr(px.err, comm::kErrMismatch);
-          if (atomicCAS(px.err + 1, 0, 1) == 0) {
-            int* d = px.err + 1;
-            d[1] = blk;
-            d[2] = q;
-            d[3] = K == 1 ? w0 : w0 + (k & 1) + 128 * (k >> 1);
-            d[4] = (int)t;
-            d[5] = (int)(uint32_t)w[q][k];
-            d[6] = (int)(uint32_t)(w[q][k] >> 32);
-            d[7] = (int)__float_as_uint(v[k]);
-            d[8] = (int)passes;
-          }
-        }
-  }
+  // sum cannot pass as a clean exchange.  The check rides in the rank-order sum below (one XOR /
+  // OR per word, static indices only); the recording runs only on a mismatch (loopback_mismatch).
+  const uint32_t lbm = (px.loopback && !timed_out) ? 0xffffffffu : 0u;
+  uint32_t diff = 0;
+  float own[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    own[k] = v[k];
+    const uint32_t vb = __float_as_uint(v[k]);
     float s = 0.f;
 #pragma unroll
     for (int p = 0; p < R; ++p) {
@@ -1688,9 +1709,17 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
         // peer p's row: q = p (p < rank) or p - 1 (p > rank)
         const uint64_t wp = p < rank ? w[min(p, R - 2)][k] : w[max(p - 1, 0)][k];
         s += p == rank ? v[k] : __uint_as_float((uint32_t)wp);
+        if (p != rank && live[k]) diff |= (uint32_t)wp ^ vb;
       }
     }
     v[k] = s;
+  }
+  if (__builtin_expect((diff & lbm) != 0, 0)) {
+    uint32_t lb = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) lb |= live[k] ? (1u << k) : 0u;
+    loopback_mismatch(px.err, x.src, cap, slot_words(px, t), w0, K, world - 1, lb, own[0], own[min(1, K - 1)],
+                      own[min(2, K - 1)], own[K - 1], t, passes, rank, blk);
   }
 }
 
@@ -2151,7 +2180,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
         // ("EVERY store of the handed-off bytes sc1 and drained ... before the flag/counter and
         // EVERY load of them ... sc1"), which stands in for the release / acquire pair: an
         // agent-scope release fence is an L2 write-back and the acquire an L2 invalidate on this
-        // multi-XCD part, and with them the B = 8192 step measured 145 -> 172 us (profiles/round5.md).
+        // multi-XCD part (MI355X_MICROARCH.md, the same row), paid by every slice of every tile.
         float* pt = a.fc_part + (int64_t)tile * 256 + lane;  // slice sl at + sl * FC_TILES * 256
         int* cnt = reinterpret_cast<int*>(a.fc_part + FC_PART_FLOATS) + tile;
 #pragma unroll
