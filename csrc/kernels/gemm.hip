@@ -257,6 +257,88 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
       }
 }
 
+// Small GEMMs (the fc layers of a small batch: a few dozen 16 x 16 output tiles, K <= 1024): one
+// wave per 16 x 16 output tile, its operand fragments gathered straight from global memory into
+// registers (two K-steps of loads in flight), no LDS, no barrier, no split-K pass.  The 64 x 64
+// block kernel ran these as a chain of 1-10 dependent K-tiles on 1-6 workgroups plus a split-K
+// reduce launch (7-20 us each in the modular step's kernel trace, profiles/round5.md).
+// Lane (l16, kq) holds A[row l16][k 8kq .. 8kq+7] and B[k 8kq .. 8kq+7][col l16] (Mfma<T> layout).
+template <typename T>
+__device__ __forceinline__ void gather8(float (&f)[8], const void* X, int dt, int64_t off, int64_t sk, int nk) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) X_t;
+    const X_t* p = static_cast<const X_t*>(X) + off;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = j < nk ? (float)p[j * sk] : 0.f;
+  };
+  switch (dt) {
+    case kF32: run(float{}); break;
+    case kBF16: run(__bf16{}); break;
+    case kF16: run(_Float16{}); break;
+    default: run(uint8_t{}); break;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag to_frag(const float (&f)[8]) {
+  typedef typename Mfma<T>::frag frag;
+  if constexpr (__is_same(T, float)) {
+    return frag{f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7]};
+  } else {
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bits_of<T>((T)f[j]);
+    return __builtin_bit_cast(frag, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  const int tn = (Np + 15) >> 4, tiles = ((a.M + 15) >> 4) * tn;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= tiles) return;  // (no barrier in this kernel)
+  const int mt = tile / tn, nt = tile - mt * tn;
+  const int m = mt * 16 + l16, n = nt * 16 + l16;
+  const bool mv = m < a.M;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < a.K; k0 += 64) {
+    float fa[2][8], fb[2][8], fg[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kb = k0 + 32 * u + 8 * kq;
+      const int nk = min(8, max(0, a.K - kb));
+      gather8<T>(fa[u], a.A, a.a_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)min(kb, a.K - 1) * a.sak, a.sak,
+                 mv ? nk : 0);
+      if (a.G)
+        gather8<T>(fg[u], a.G, a.g_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)min(kb, a.K - 1) * a.sak, a.sak,
+                   mv ? nk : 0);
+      if (n < a.N) {
+        gather8<T>(fb[u], a.B, a.b_dtype, (int64_t)min(kb, a.K - 1) * a.sbk + (int64_t)n * a.sbn, a.sbk, nk);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fb[u][j] = (n == a.N && j < nk) ? 1.f : 0.f;  // the ones column / padding
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (a.G) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fa[u][j] = fg[u][j] > 0.f ? fa[u][j] * a.gate_scale : 0.f;
+      }
+      acc = Mfma<T>::mma(to_frag<T>(fa[u]), to_frag<T>(fb[u]), acc);
+    }
+  }
+  const uint64_t off = rng_offset(a.offset, a.offset_dev);
+  const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mm = mt * 16 + 4 * kq + r;
+    if (mm < a.M && n < Np) epilogue<T>(a, mm, n, acc[r], off, dscale);
+  }
+}
+
 // Fixed-order sum of the split-K partials + the epilogue.
 template <typename T>
 __global__ void gemm_splitk_reduce(GemmArgs a, int splits) {
@@ -311,7 +393,14 @@ int pick_mode(const void* X, int dt, int64_t s_r, int64_t s_k, int mfma) {
 }
 }  // namespace
 
+// the small-GEMM path (gemm_small_kernel): few 16 x 16 output tiles, K <= 1024
+static bool gemm_small(const GemmArgs& a) {
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  return cdiv(a.M, 16) * cdiv(Np, 16) <= 1024 && a.K <= 1024;
+}
+
 int gemm_splits(const GemmArgs& a) {
+  if (gemm_small(a)) return 1;
   const int Np = a.N + (a.rowsum ? 1 : 0);
   const int tiles = cdiv(Np, BN) * cdiv(a.M, BM);
   const int ktiles = cdiv(a.K, BK);
@@ -327,8 +416,15 @@ hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
   a.b_mode = pick_mode(a.B, a.b_dtype, a.sbn, a.sbk, a.mfma_dtype);
   // the gate is loaded with A's mode: it must allow the same vector access
   if (a.G && pick_mode(a.G, a.g_dtype, a.sam, a.sak, a.mfma_dtype) != a.a_mode) a.a_mode = kScalar;
-  const int splits = a.ws ? gemm_splits(a) : 1;
   const int Np = a.N + (a.rowsum ? 1 : 0);
+  if (gemm_small(a)) {
+    CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
+      hipLaunchKernelGGL(gemm_small_kernel<scalar_t>, dim3(cdiv(cdiv(a.M, 16) * cdiv(Np, 16), 4)), dim3(256), 0, s,
+                         a);
+    });
+    return hipGetLastError();
+  }
+  const int splits = a.ws ? gemm_splits(a) : 1;
   dim3 grid(cdiv(Np, BN), cdiv(a.M, BM), splits);
   CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
     hipLaunchKernelGGL(gemm_kernel<scalar_t>, grid, dim3(256), 0, s, a);

@@ -1651,7 +1651,7 @@ __device__ __attribute__((noinline)) void loopback_mismatch(int* err, const uint
 // v[k] := sum over ranks of word k, in rank order (so every rank gets identical bits): polls
 // this rank's receive buffer for every peer's words of tag t, all loads issued before the first
 // wait (one memory round trip per pass)
-template <int K, int R>
+template <int K, int R, bool LBC = false>
 __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>& x, uint32_t t, int w0,
                                         const bool (&live)[K], float (&v)[K], uint64_t timeout_ticks,
                                         bool& timed_out, uint64_t* stamp, int blk) {
@@ -1690,43 +1690,60 @@ __device__ __forceinline__ void ll_poll(const comm::IpcPeers& px, const XPtrs<R>
     __builtin_amdgcn_s_sleep(1);
   }
   if (stamp) stamp[6] = passes;  // (diagnostics: poll passes, 1 = the first one found every word)
-  // Loopback invariant: every virtual peer returns this lane's own pushed value, so a live word
-  // that carries the current tag must bit-equal v[k].  A mismatch (a torn or stale word under a
-  // current tag) raises kErrMismatch and records the first one (ipc_diag), so a silently wrong
-  // sum cannot pass as a clean exchange.  The check rides in the rank-order sum below (one XOR /
-  // OR per word, static indices only); the recording runs only on a mismatch (loopback_mismatch).
-  const uint32_t lbm = (px.loopback && !timed_out) ? 0xffffffffu : 0u;
-  uint32_t diff = 0;
-  float own[K];
+  if constexpr (!LBC) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    own[k] = v[k];
-    const uint32_t vb = __float_as_uint(v[k]);
-    float s = 0.f;
+    for (int k = 0; k < K; ++k) {
+      float s = 0.f;
 #pragma unroll
-    for (int p = 0; p < R; ++p) {
-      if (p < world) {
-        // peer p's row: q = p (p < rank) or p - 1 (p > rank)
-        const uint64_t wp = p < rank ? w[min(p, R - 2)][k] : w[max(p - 1, 0)][k];
-        s += p == rank ? v[k] : __uint_as_float((uint32_t)wp);
-        if (p != rank && live[k]) diff |= (uint32_t)wp ^ vb;
+      for (int p = 0; p < R; ++p) {
+        if (p < world) {
+          // peer p's row: q = p (p < rank) or p - 1 (p > rank)
+          const uint64_t wp = p < rank ? w[min(p, R - 2)][k] : w[max(p - 1, 0)][k];
+          s += p == rank ? v[k] : __uint_as_float((uint32_t)wp);
+        }
       }
+      v[k] = s;
     }
-    v[k] = s;
-  }
-  if (__builtin_expect((diff & lbm) != 0, 0)) {
-    uint32_t lb = 0;
+  } else {
+    // Loopback invariant (LBC: the looped-back exchange with its check on, a kernel of its own so
+    // that the real exchange's code is untouched -- present but idle, the check still cost the
+    // world-8 step 0.6 us, profiles/round5.md): every virtual peer returns this lane's own pushed
+    // value, so a live word that carries the current tag must bit-equal v[k].  A mismatch (a torn
+    // or stale word under a current tag) raises kErrMismatch and records the first one
+    // (ipc_diag), so a silently wrong sum cannot pass as a clean exchange.  The check rides in the
+    // rank-order sum (one XOR / OR per word, static indices only); the recording runs only on a
+    // mismatch (loopback_mismatch).
+    uint32_t diff = 0;
+    float own[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) lb |= live[k] ? (1u << k) : 0u;
-    loopback_mismatch(px.err, x.src, cap, slot_words(px, t), w0, K, world - 1, lb, own[0], own[min(1, K - 1)],
-                      own[min(2, K - 1)], own[K - 1], t, passes, rank, blk);
+    for (int k = 0; k < K; ++k) {
+      own[k] = v[k];
+      const uint32_t vb = __float_as_uint(v[k]);
+      float s = 0.f;
+#pragma unroll
+      for (int p = 0; p < R; ++p) {
+        if (p < world) {
+          const uint64_t wp = p < rank ? w[min(p, R - 2)][k] : w[max(p - 1, 0)][k];
+          s += p == rank ? v[k] : __uint_as_float((uint32_t)wp);
+          if (p != rank && live[k]) diff |= (uint32_t)wp ^ vb;
+        }
+      }
+      v[k] = s;
+    }
+    if (__builtin_expect(diff != 0 && !timed_out, 0)) {
+      uint32_t lb = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) lb |= live[k] ? (1u << k) : 0u;
+      loopback_mismatch(px.err, x.src, cap, slot_words(px, t), w0, K, world - 1, lb, own[0], own[min(1, K - 1)],
+                        own[min(2, K - 1)], own[K - 1], t, passes, rank, blk);
+    }
   }
 }
 
 // Update workgroup blk of nblk (UP_NT threads).  part: float4[UP_S][UP_C], part2:
 // float[4][UP_C*4] in LDS.  XW: 0 = no exchange, else the fused exchange's world bound
 // (2, 4 or 8 >= px.world).
-template <typename T, int XW>
+template <typename T, int XW, bool LBC = false>
 __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ vslab, int B, float* loss_parts,
                             int nparts, float* loss_acc, const comm::IpcPeers& px, uint64_t timeout_ticks, int blk,
                             int nblk, int tid, float4* part_, float* part2_, int fc_tpb, int fc_sl_arg) {
@@ -1872,7 +1889,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       float g[1] = {((part2[0][ht] + part2[1][ht]) + (part2[2][ht] + part2[3][ht])) * a.grad_post};
       if (EXCH) {
         timed_out = err_now();
-        ll_poll<1, XR>(px, xp, tag_now(), pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
+        ll_poll<1, XR, LBC>(px, xp, tag_now(), pbc * (UP_C * 4) + ht, live, g, timeout_ticks, timed_out,
                        a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr, blk);
       }
       finish_param<T>(a, pi, g[0], first, p0, m0, d0, d1);
@@ -2165,7 +2182,7 @@ __device__ void update_role(const LenetUpdateArgs& a, const float* __restrict__ 
       }
       if (own) {
         timed_out = err_now();
-        ll_poll<4, XR>(px, xp, tag_now(), w0, live, g, timeout_ticks, timed_out,
+        ll_poll<4, XR, LBC>(px, xp, tag_now(), w0, live, g, timeout_ticks, timed_out,
                        a.dbg && tid == 0 && blk < a.dbg_blocks ? a.dbg + blk * 8 : nullptr, blk);
       }
     }
@@ -2278,7 +2295,7 @@ struct UpdateKargs {
   LenetUpdateArgs a; const float* vslab; int B; float* loss_parts; int nparts; float* loss_acc;
   uint64_t timeout_ticks; int fc_tpb; int fc_sl;
 };
-template <typename T, int XW>
+template <typename T, int XW, bool LBC = false>
 __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, const float* __restrict__ vslab,
                                                              int B, float* loss_parts, int nparts,
                                                              float* loss_acc, uint64_t timeout_ticks, int fc_tpb,
@@ -2286,7 +2303,7 @@ __global__ void __launch_bounds__(UP_NT) lenet_update_kernel(LenetUpdateArgs a, 
   prefetch_kernargs<sizeof(UpdateKargs) + sizeof(comm::IpcPeers)>();  // (+ gridDim.x after px)
   __shared__ float4 part[UP_S][UP_C];
   __shared__ float part2[4][UP_C * 4];
-  update_role<T, XW>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
+  update_role<T, XW, LBC>(a, vslab, B, loss_parts, nparts, loss_acc, px, timeout_ticks, blockIdx.x, gridDim.x,
                        threadIdx.x, &part[0][0], &part2[0][0], fc_tpb, fc_sl);
 }
 
@@ -2408,17 +2425,22 @@ hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int 
     }
     if (px.cap < EXCH_WORDS || a.exch_timeout_s <= 0.0) return hipErrorInvalidValue;
     const uint64_t ticks = (uint64_t)(a.exch_timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    // (px.loopback: the looped-back exchange with its invariant check, own instantiations)
+#define CSED_UPDATE_X(W, L)                                                                                   \
+  hipLaunchKernelGGL((lenet_update_kernel<scalar_t, W, L>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab, a.B, \
+                     loss_parts, nparts, loss_acc, ticks, 1, 1, px)
     CSED_DISPATCH_UPDATE(a.mfma_dtype, {
-      if (px.world <= 2)
-        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 2>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                           a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
-      else if (px.world <= 4)
-        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 4>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                           a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
-      else
-        hipLaunchKernelGGL((lenet_update_kernel<scalar_t, 8>), dim3(NB_UPDATE), dim3(UP_NT), 0, s, a, a.vslab,
-                           a.B, loss_parts, nparts, loss_acc, ticks, 1, 1, px);
+      if (px.loopback) {
+        if (px.world <= 2) CSED_UPDATE_X(2, true);
+        else if (px.world <= 4) CSED_UPDATE_X(4, true);
+        else CSED_UPDATE_X(8, true);
+      } else {
+        if (px.world <= 2) CSED_UPDATE_X(2, false);
+        else if (px.world <= 4) CSED_UPDATE_X(4, false);
+        else CSED_UPDATE_X(8, false);
+      }
     });
+#undef CSED_UPDATE_X
     return hipGetLastError();
   }
   const int S = fc_split_slices(a);

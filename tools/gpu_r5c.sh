@@ -2,7 +2,7 @@
 # loopback check switched off) at the looped-back world-8 / world-4 steps; then the kernel,
 # exchange and modular tests and the modular engine's step times / kernel trace on the B build
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; T=${1:-r5f}
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; T=${1:-r5g}
 cd $R && rm -f $O/${T}_ab3.log && \
 for i in 1 2 3; do for c in "--global-batch 8 --loopback-world 8" "--global-batch 16 --loopback-world 4"; do
   for v in A B C; do
