@@ -181,7 +181,7 @@ def start_native_data():
     return ns.Job(60000, 10000, seed=0)
 
 
-def start_gpu_context(phases: dict | None = None):
+def start_gpu_context(phases: dict | None = None, torch_too: bool = True):
     """This rank's HIP context, created in a thread started at t0 that runs while the data set
     is generated and the process group comes up.  ctypes loads the HIP runtime that torch
     itself links (torch/lib/libamdhip64.so), so torch later finds this process's primary
@@ -208,6 +208,13 @@ def start_gpu_context(phases: dict | None = None):
             return
         if hip.hipSetDevice(dev % n.value) == 0:
             hip.hipFree(ctypes.c_void_p(0))  # (the context's creation)
+            if torch_too:
+                # torch's own CUDA state (lazy init, caching allocator: ~0.09 s, round-5 bring-up
+                # breakdown engine.net) comes up here too, behind the data generator
+                import torch
+
+                torch.cuda.set_device(dev % n.value)
+                torch.empty(1, device=torch.device("cuda", dev % n.value))
         if phases is not None:
             phases["hip_ctx_thread"] = time.time() - t
 
@@ -464,7 +471,10 @@ def main(argv=None) -> int:
             eng.allreduce_kind, " + gradient all-reduce")
         if eng.loopback_world:
             engine_kernels = f" with the in-kernel exchange looped back to {eng.loopback_world} virtual ranks"
-            extra_lb = {"loopback_world": eng.loopback_world}
+            # the loopback invariant check runs in kernels of its own (CSED_LOOPBACK_CHECK=0: the
+            # real world-N update kernel, as tools/exchange_loopback.py times it)
+            extra_lb = {"loopback_world": eng.loopback_world,
+                        "loopback_check": os.environ.get("CSED_LOOPBACK_CHECK", "1") != "0"}
         else:
             extra_lb = {}
         cfg_engine = f"fused HIP ({eng.kernel_names}{engine_kernels})"

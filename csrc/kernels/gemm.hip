@@ -258,16 +258,32 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 }
 
 // Small GEMMs (the fc layers of a small batch: a few dozen 16 x 16 output tiles, K <= 1024): one
-// wave per 16 x 16 output tile, its operand fragments gathered straight from global memory into
-// registers (two K-steps of loads in flight), no LDS, no barrier, no split-K pass.  The 64 x 64
-// block kernel ran these as a chain of 1-10 dependent K-tiles on 1-6 workgroups plus a split-K
-// reduce launch (7-20 us each in the modular step's kernel trace, profiles/round5.md).
+// workgroup per 16 x 16 output tile, its K split over the 4 waves (each wave's operand fragments
+// gathered straight from global memory into registers, up to 4 K-steps of loads in flight; a
+// 16-byte load per fragment where the operand is K-contiguous), the 4 partial tiles combined in
+// wave order through LDS.  No split-K pass, no LDS staging of operands.  The 64 x 64 block kernel
+// ran these as a chain of 1-10 dependent K-tiles on 1-6 workgroups plus a split-K reduce launch
+// (7-20 us each in the modular step's kernel trace, profiles/round5.md).
 // Lane (l16, kq) holds A[row l16][k 8kq .. 8kq+7] and B[k 8kq .. 8kq+7][col l16] (Mfma<T> layout).
 template <typename T>
-__device__ __forceinline__ void gather8(float (&f)[8], const void* X, int dt, int64_t off, int64_t sk, int nk) {
+__device__ __forceinline__ void gather8(float (&f)[8], const void* X, int dt, int64_t off, int64_t sk, int nk,
+                                        bool vec) {
   auto run = [&](auto tag) {
     typedef decltype(tag) X_t;
     const X_t* p = static_cast<const X_t*>(X) + off;
+    if (vec && nk == 8) {  // K-contiguous, 16-byte aligned (kKContig): one or two vector loads
+      if constexpr (sizeof(X_t) == 2) {
+        typedef X_t v8 __attribute__((ext_vector_type(8)));
+        const v8 q = *reinterpret_cast<const v8*>(p);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (float)q[j];
+        return;
+      } else if constexpr (sizeof(X_t) == 4) {
+        const float4 q0 = *reinterpret_cast<const float4*>(p), q1 = *reinterpret_cast<const float4*>(p + 4);
+        f[0] = q0.x; f[1] = q0.y; f[2] = q0.z; f[3] = q0.w; f[4] = q1.x; f[5] = q1.y; f[6] = q1.z; f[7] = q1.w;
+        return;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = j < nk ? (float)p[j * sk] : 0.f;
   };
@@ -294,35 +310,40 @@ __device__ __forceinline__ typename Mfma<T>::frag to_frag(const float (&f)[8]) {
 
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
+  __shared__ float part[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
   const int Np = a.N + (a.rowsum ? 1 : 0);
-  const int tn = (Np + 15) >> 4, tiles = ((a.M + 15) >> 4) * tn;
-  const int tile = blockIdx.x * 4 + wave;
-  if (tile >= tiles) return;  // (no barrier in this kernel)
-  const int mt = tile / tn, nt = tile - mt * tn;
+  const int tn = (Np + 15) >> 4;
+  const int mt = blockIdx.x / tn, nt = blockIdx.x - mt * tn;
   const int m = mt * 16 + l16, n = nt * 16 + l16;
   const bool mv = m < a.M;
+  const bool avec = a.a_mode == kKContig, bvec = a.b_mode == kKContig;
+  // this wave's K-steps [ks0, ks1) of 32
+  const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
+  const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < a.K; k0 += 64) {
-    float fa[2][8], fb[2][8], fg[2][8];
+  for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
+    float fa[4][8], fb[4][8], fg[4][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int kb = k0 + 32 * u + 8 * kq;
-      const int nk = min(8, max(0, a.K - kb));
-      gather8<T>(fa[u], a.A, a.a_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)min(kb, a.K - 1) * a.sak, a.sak,
-                 mv ? nk : 0);
+    for (int u = 0; u < 4; ++u) {
+      const int kb = (kb0 + u) * 32 + 8 * kq;
+      const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
+      const int kc = min(kb, a.K - 1);
+      gather8<T>(fa[u], a.A, a.a_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak, a.sak, mv ? nk : 0,
+                 avec);
       if (a.G)
-        gather8<T>(fg[u], a.G, a.g_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)min(kb, a.K - 1) * a.sak, a.sak,
-                   mv ? nk : 0);
+        gather8<T>(fg[u], a.G, a.g_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak, a.sak, mv ? nk : 0,
+                   avec);
       if (n < a.N) {
-        gather8<T>(fb[u], a.B, a.b_dtype, (int64_t)min(kb, a.K - 1) * a.sbk + (int64_t)n * a.sbn, a.sbk, nk);
+        gather8<T>(fb[u], a.B, a.b_dtype, (int64_t)kc * a.sbk + (int64_t)n * a.sbn, a.sbk, nk, bvec);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) fb[u][j] = (n == a.N && j < nk) ? 1.f : 0.f;  // the ones column / padding
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 4; ++u) {
+      if (kb0 + u >= ks1) break;
       if (a.G) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) fa[u][j] = fg[u][j] > 0.f ? fa[u][j] * a.gate_scale : 0.f;
@@ -330,12 +351,19 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
       acc = Mfma<T>::mma(to_frag<T>(fa[u]), to_frag<T>(fb[u]), acc);
     }
   }
+  // fixed-order combine of the four K ranges (wave order), then the epilogue on wave 0
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
+  __syncthreads();
+  if (wave != 0) return;
   const uint64_t off = rng_offset(a.offset, a.offset_dev);
   const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
+    const float v = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) +
+                    part[3][r * 64 + lane];
     const int mm = mt * 16 + 4 * kq + r;
-    if (mm < a.M && n < Np) epilogue<T>(a, mm, n, acc[r], off, dscale);
+    if (mm < a.M && n < Np) epilogue<T>(a, mm, n, v, off, dscale);
   }
 }
 
@@ -418,9 +446,11 @@ hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
   if (a.G && pick_mode(a.G, a.g_dtype, a.sam, a.sak, a.mfma_dtype) != a.a_mode) a.a_mode = kScalar;
   const int Np = a.N + (a.rowsum ? 1 : 0);
   if (gemm_small(a)) {
+    // (vector fragment loads where the operand is K-contiguous, aligned, in the compute dtype or fp32)
+    if (a.a_mode != kKContig) a.a_mode = kScalar;
+    if (a.b_mode != kKContig) a.b_mode = kScalar;
     CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
-      hipLaunchKernelGGL(gemm_small_kernel<scalar_t>, dim3(cdiv(cdiv(a.M, 16) * cdiv(Np, 16), 4)), dim3(256), 0, s,
-                         a);
+      hipLaunchKernelGGL(gemm_small_kernel<scalar_t>, dim3(cdiv(a.M, 16) * cdiv(Np, 16)), dim3(256), 0, s, a);
     });
     return hipGetLastError();
   }
