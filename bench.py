@@ -334,7 +334,9 @@ def main(argv=None) -> int:
         def run_once(loopback_world: int, inject: bool, ph: dict, dt=dt):
             t_mark = time.time()
             torch.manual_seed(1)
-            net = Net().to(ctx.device)
+            net = Net()
+            ph["engine.net_cpu"] = time.time() - t_mark
+            net = net.to(ctx.device)
             ph["engine.net"] = time.time() - t_mark
             eng = FusedLeNetTrainer(net, train, lr=0.02, momentum=0.5, global_batch=args.global_batch, ctx=ctx,
                                     compute_dtype=dt, grid=args.grid or None, loopback_world=loopback_world)

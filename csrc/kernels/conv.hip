@@ -161,11 +161,16 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
       f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // the k -> patch offsets of K-step k0 + 32 are read while K-step k0's patch reads are in
+      // flight (one dependent LDS round trip per K-step instead of two)
+      int4 o0 = *reinterpret_cast<const int4*>(koff + 8 * (lane >> 4));
+      int4 o1 = *reinterpret_cast<const int4*>(koff + 8 * (lane >> 4) + 4);
       for (int k0 = 0; k0 < g.Kp; k0 += 32) {
         const int kb = k0 + 8 * (lane >> 4);
-        const int4 o0 = *reinterpret_cast<const int4*>(koff + kb);
-        const int4 o1 = *reinterpret_cast<const int4*>(koff + kb + 4);
         const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+        const int kn = min(kb + 32, g.Kp - 8);  // (clamped past the last step: a valid slot)
+        o0 = *reinterpret_cast<const int4*>(koff + kn);
+        o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
         frag fa;
         typename Stor<T>::V8 raw;
 #pragma unroll
@@ -326,6 +331,14 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
     else dyrows(_Float16{});
     __syncthreads();
     if (my_nt0 >= NT) continue;
+    // this lane's B-column patch offsets, one per N-tile (the same for every pixel step: read once
+    // per image instead of once per MFMA, a dependent LDS round trip less per pixel step)
+    int kos[MAXNTW];
+#pragma unroll
+    for (int jj = 0; jj < MAXNTW; ++jj) {
+      const int nt = (jj == 0 || NT >= 4) ? my_nt0 + jj * 4 : NT;  // (NT < 4: only jj = 0 is used)
+      kos[jj] = nt < NT ? koff[nt * 16 + (lane & 15)] : pe;
+    }
     for (int ps = my_s; ps * 32 < g.npp; ps += psplit) {
       const int p0 = ps * 32 + 8 * (lane >> 4);
       const int4 b0 = *reinterpret_cast<const int4*>(pbase + p0);
@@ -340,7 +353,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
         const int nt = my_nt0 + jj * nt_step;
         if (jj > 0 && NT < 4) break;
         if (nt >= NT) break;
-        const int ko = koff[nt * 16 + (lane & 15)];
+        const int ko = kos[jj];
         typename Stor<T>::V8 raw;
 #pragma unroll
         for (int j = 0; j < 8; ++j) raw[j] = patch[bb[j] * (ko != pe) + ko];
