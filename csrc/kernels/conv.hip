@@ -466,6 +466,7 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   g.Kp = rup(g.K, 32);
   g.Cop = rup(g.Co, 16);
   g.PW = g.W + 2 * g.pad;
+  if (g.PW > 256) return hipErrorInvalidConfiguration;  // (patch staging: one column per thread)
   // ~128 output pixels per block, LDS-limited
   int tr = std::max(1, std::min(g.OH, (128 + g.OW - 1) / g.OW));
   int bands = (g.OH + tr - 1) / tr;
@@ -520,6 +521,7 @@ hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int d
   if (N <= 0) return hipSuccess;
   WgradGeo g = wgrad_geo(N, IC, H, W, OC, KH, KW, pad);
   if (g.OH <= 0 || g.OW <= 0) return hipErrorInvalidValue;
+  if (g.PW > 256) return hipErrorInvalidConfiguration;  // (patch staging: one column per thread)
   if (g.Cop > 64 || (g.Kc / 16) > 32) return hipErrorInvalidConfiguration;  // accumulator budget
   const size_t es = mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
   const size_t lds_main = (size_t)g.Cop * (g.npp + 8) * es + (size_t)g.Kc * 4 + (size_t)g.npp * 4 +

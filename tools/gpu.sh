@@ -59,10 +59,10 @@ task_rehearse() {
 
 task_trace() {
   cd /tmp && export TMPDIR=/tmp && \
-  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt64 -o run -- python3 $R/bench.py --steps 300 --warmup 30 --no-epoch > $O/${T}_kt64.log 2>&1 && \
-  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt8 -o run -- python3 $R/bench.py --global-batch 8 --steps 300 --warmup 30 --no-epoch > $O/${T}_kt8.log 2>&1 && \
-  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt1024 -o run -- python3 $R/bench.py --global-batch 1024 --dtype fp16 --steps 200 --warmup 20 --no-epoch > $O/${T}_kt1024.log 2>&1 && \
-  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt8192 -o run -- python3 $R/bench.py --global-batch 8192 --dtype fp16 --steps 40 --warmup 5 --no-epoch > $O/${T}_kt8192.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt64 -o run -- python3 $R/bench.py --steps 300 --warmup 30 --no-epoch --no-fp32-record > $O/${T}_kt64.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt8 -o run -- python3 $R/bench.py --global-batch 8 --steps 300 --warmup 30 --no-epoch --no-fp32-record > $O/${T}_kt8.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt1024 -o run -- python3 $R/bench.py --global-batch 1024 --dtype fp16 --steps 200 --warmup 20 --no-epoch --no-fp32-record > $O/${T}_kt1024.log 2>&1 && \
+  py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_kt8192 -o run -- python3 $R/bench.py --global-batch 8192 --dtype fp16 --steps 40 --warmup 5 --no-epoch --no-fp32-record > $O/${T}_kt8192.log 2>&1 && \
   py 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_ktf32 -o run -- python3 $R/bench.py --dtype fp32 --steps 300 --warmup 30 --no-epoch > $O/${T}_ktf32.log 2>&1
 }
 
