@@ -33,6 +33,9 @@ class DeviceLoader:
         self.drop_last = drop_last
         self.mean, self.std = float(mean), float(std)
         self.generator = generator
+        # optional (B, dtype) -> (x, target) buffers to gather into (e.g. a captured training
+        # step's static inputs, engine/modular.py bind_loader) or None for fresh tensors
+        self.into = None
 
     def _order(self) -> torch.Tensor:
         if self.sampler is not None:
@@ -52,8 +55,12 @@ class DeviceLoader:
         if self.device.type == "cuda":
             from ..ops import _native
 
-            out = torch.empty((B, 1, 28, 28), device=self.device, dtype=self.dtype)
-            lab = torch.empty((B,), device=self.device, dtype=torch.long)
+            bufs = self.into(B, self.dtype) if self.into is not None else None
+            if bufs is not None:
+                out, lab = bufs
+            else:
+                out = torch.empty((B, 1, 28, 28), device=self.device, dtype=self.dtype)
+                lab = torch.empty((B,), device=self.device, dtype=torch.long)
             _native.ops().gather_normalize(self.data.images, idx, None, B, self.mean, self.std, out, lab,
                                            self.data.labels)
             return out, lab

@@ -169,6 +169,7 @@ def single_main(argv=None) -> int:
                                        os.path.join(results, "optimizer.pth"))
         train_loader = DeviceLoader(train, args.batch_size, shuffle=True, device=dev,
                                     dtype=ops.compute_dtype() if dev.type == "cuda" else torch.float32)
+        tr.bind_loader(train_loader)
 
         def test():
             total, correct, _ = tr.evaluate(test_loader)
@@ -180,7 +181,7 @@ def single_main(argv=None) -> int:
         for epoch in range(1, args.epochs + 1):
             nb = len(train_loader)
             for batch_idx, (x, t) in enumerate(train_loader):
-                loss = tr.train_batch(x, t)
+                loss = tr.train_batch(x, t, clone_loss=batch_idx % args.log_interval == 0)
                 if batch_idx % args.log_interval == 0:
                     lv = loss.item()
                     print(metrics.train_line(epoch, batch_idx * len(x), n_train, 100.0 * batch_idx / nb, lv))
@@ -360,6 +361,7 @@ def dist_main(argv=None) -> int:
                             bucket_cap_mb=25.0 if args.bucket_mb is None else args.bucket_mb)
         loader = DeviceLoader(train, per_rank, sampler=sampler, device=dev,
                               dtype=ops.compute_dtype() if dev.type == "cuda" else torch.float32)
+        tr.bind_loader(loader)
         for i in range(args.epochs):
             sampler.set_epoch(i)
             losses = []

@@ -60,6 +60,7 @@ class ModularTrainer:
             for i, p in enumerate(self.flat.params):  # backward kernels write into the flat gradient
                 ops.set_grad_destination(p, self.flat.grad_view(i))
         self.loss_name = loss
+        self._logits = self.opt.on_gpu and loss in ("nll", "ce") and getattr(model, "returns_logits", False)
         gloo = self.distributed and getattr(ctx, "backend", None) != "nccl"
         self.use_graph = bool(graph) and self.opt.on_gpu and not gloo
         self._graphs: dict[tuple, tuple] = {}  # input shapes -> (graph, static x, static target, static loss)
@@ -70,6 +71,17 @@ class ModularTrainer:
             return ops.cross_entropy(out, target)  # nn.CrossEntropyLoss on log-probs (ref train_dist.py:67)
         return ops.nll_loss(out, target)
 
+    def _forward_loss(self, x, target):
+        """The model's output and the loss.  A model whose forward ends in log_softmax and can
+        return its logits (``returns_logits``, e.g. ``Net``) gets the loss as ONE fused
+        log_softmax + NLL op on the logits: nll(log_softmax(z)) for 'nll', and for 'ce' the same
+        value (CrossEntropyLoss on log-probs re-applies an idempotent log_softmax)."""
+        if self._logits:
+            z = self.forward(x, return_logits=True)
+            return z, ops.log_softmax_nll(z, target)
+        out = self.forward(x)
+        return out, self.loss_fn(out, target)
+
     def zero_grad(self) -> None:
         """set_to_none (torch's default): the next backward writes every gradient in place."""
         for p in self.flat.params:
@@ -78,8 +90,7 @@ class ModularTrainer:
     def _step(self, x: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         ops.rng.default_state.reset_offset()
         self.zero_grad()
-        out = self.forward(x)
-        loss = self.loss_fn(out, target)
+        _, loss = self._forward_loss(x, target)
         if self._one is None or self._one.device != loss.device:
             self._one = torch.ones((), device=loss.device, dtype=loss.dtype)
         loss.backward(self._one)  # (a kept d loss / d loss: no fill kernel per step)
@@ -102,10 +113,21 @@ class ModularTrainer:
             if g is None:
                 return self._step(x, target)
         graph, sx, st, sloss = g
-        sx.copy_(x, non_blocking=True)
-        st.copy_(target, non_blocking=True)
+        if x.data_ptr() != sx.data_ptr():  # (a bound loader gathers straight into sx / st)
+            sx.copy_(x, non_blocking=True)
+        if target.data_ptr() != st.data_ptr():
+            st.copy_(target, non_blocking=True)
         graph.replay()
         return sloss.clone() if clone_loss else sloss
+
+    def bind_loader(self, loader) -> None:
+        """Let ``loader`` (data/loader.py DeviceLoader) gather each batch straight into the captured
+        step's input buffers once a graph exists for its shape: no copy launches per step."""
+        def into(B: int, dtype: torch.dtype):
+            g = self._graphs.get(((B, 1, 28, 28), dtype, (B,))) if self.use_graph else None
+            return (g[1], g[2]) if g is not None else None
+
+        loader.into = into
 
     def _state(self) -> list[torch.Tensor]:
         return [self.flat.data, self.opt.momentum_flat, self.opt.step_count]

@@ -7,8 +7,8 @@ weights and ``state_dict()`` files load into the reference model unchanged).
 
 The GPU forward is five fused HIP kernels instead of ~15 ATen ops:
 
-    conv1 + bias + maxpool2 + relu              (conv2d_pool_relu)
-    conv2 + bias + Dropout2d + maxpool2 + relu  (conv2d_pool_relu with channel scale)
+    conv1 + bias + maxpool2 + relu              (conv2d_pool_relu, fp32 input read directly)
+    conv2 + bias + Dropout2d + maxpool2 + relu  (conv2d_pool_relu, mask drawn in the epilogue)
     fc1 + bias + relu + dropout                 (linear, act='relu_dropout')
     fc2 + bias                                  (linear, fp32 logits)
     log_softmax                                 (log_softmax)
@@ -37,30 +37,33 @@ class Net(nn.Module):
         self.fc1 = nn.Linear(320, 50)
         self.fc2 = nn.Linear(50, 10)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    # the modular engine may ask for the logits and fuse log_softmax into its NLL
+    # (ops.log_softmax_nll: one kernel each way); the module's output stays the log-probs
+    returns_logits = True
+
+    def forward(self, x: torch.Tensor, return_logits: bool = False) -> torch.Tensor:
         if not x.is_cuda:
-            return self.reference_forward(x)
-        n = x.shape[0]
-        x = x.to(ops.compute_dtype())
+            out = self.reference_forward(x, log_probs=not return_logits)
+            return out
+        # (the fp32 input is read and converted by conv1's staging: no cast launch)
         x = ops.conv2d_pool_relu(x, self.conv1.weight, self.conv1.bias)
         p2 = self.conv2_drop.p
-        chscale = ops.dropout2d_scale(n, self.conv2.out_channels, p2, x.device) if (
-            self.training and p2 > 0) else None
-        x = ops.conv2d_pool_relu(x, self.conv2.weight, self.conv2.bias, chscale)
+        x = ops.conv2d_pool_relu(x, self.conv2.weight, self.conv2.bias,
+                                 dropout2d_p=p2 if self.training else 0.0)  # Dropout2d drawn in-kernel
         x = x.view(-1, 320)
         x = ops.linear(x, self.fc1.weight, self.fc1.bias,
                        act="relu_dropout" if self.training else "relu", p=0.5)
         x = ops.linear(x, self.fc2.weight, self.fc2.bias, out_dtype=torch.float32)
-        return ops.log_softmax(x, dim=1)
+        return x if return_logits else ops.log_softmax(x, dim=1)
 
-    def reference_forward(self, x: torch.Tensor) -> torch.Tensor:
+    def reference_forward(self, x: torch.Tensor, log_probs: bool = True) -> torch.Tensor:
         x = F.relu(F.max_pool2d(self.conv1(x), 2))
         x = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(x)), 2))
         x = x.view(-1, 320)
         x = F.relu(self.fc1(x))
         x = F.dropout(x, training=self.training)
         x = self.fc2(x)
-        return F.log_softmax(x, dim=1)
+        return F.log_softmax(x, dim=1) if log_probs else x
 
 
 PARAM_SHAPES = [

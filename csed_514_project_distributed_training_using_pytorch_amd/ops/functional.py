@@ -94,7 +94,7 @@ def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
 # ----------------------------------------------------------------- conv ----
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, pad, pool, chscale):
+    def forward(ctx, x, w, b, pad, pool, chscale, drop):
         x = x.contiguous()
         N, IC, H, W = x.shape
         OC, _, KH, KW = w.shape
@@ -104,7 +104,12 @@ class _Conv2d(torch.autograd.Function):
         if pool:
             y = torch.empty((N, OC, OH // 2, OW // 2), device=x.device, dtype=adt)
             idx = torch.empty(y.shape, device=x.device, dtype=torch.uint8)
-            _ops().conv2d_fwd(x, w, b, y, pad, idx, chscale, 2, mf)
+            if drop is not None:  # Dropout2d drawn in the conv's epilogue; its scales kept for the backward
+                p, seed, off, dev = drop
+                chscale = torch.empty(N * OC, device=x.device, dtype=torch.float32)
+                _ops().conv2d_fwd(x, w, b, y, pad, idx, None, 2, mf, p, seed, off, dev, chscale)
+            else:
+                _ops().conv2d_fwd(x, w, b, y, pad, idx, chscale, 2, mf)
             ctx.save_for_backward(x, w, y, idx, chscale)
         else:
             y = torch.empty((N, OC, OH, OW), device=x.device, dtype=adt)
@@ -120,44 +125,62 @@ class _Conv2d(torch.autograd.Function):
         dy = dy.contiguous()
         if ctx.pool:
             x, w, y, idx, chscale = ctx.saved_tensors
-            dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)
-            _ops().maxpool_relu_bwd(dy.to(y.dtype), y, idx, chscale, dconv, 2)
+            if dy.dtype != y.dtype:
+                dy = dy.to(y.dtype)
+            pooled = (idx, y, chscale)
         else:
             x, w = ctx.saved_tensors
-            dconv = dy
+            pooled = (None, None, None)
         dx = dw = db = None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            # one launch for dW, db and dX (+ the slab reduce); a pooled forward's gradient is
+            # expanded inside the kernels' staging (dL/dconv never materialised)
             N, IC = x.shape[:2]
             OC, _, KH, KW = w.shape
             dw = _grad_buffer(w, w.shape, w.device)
             db = _grad_buffer(ctx.bias_param, (OC,), w.device) if ctx.has_bias else None
             ws = torch.empty(wgrad_workspace_elems(N, IC, KH, KW, OC), device=w.device, dtype=torch.float32)
-            _ops().conv2d_wgrad(x, dconv, dw, db, ws, ctx.pad, ctx.mf, 0.0)
-        if ctx.needs_input_grad[0]:
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+            _ops().conv2d_bwd(x, dy, w, dw, db, ws, dx, ctx.pad, *pooled, ctx.mf)
+        elif ctx.needs_input_grad[0]:
+            if ctx.pool:
+                dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)
+                _ops().maxpool_relu_bwd(dy, y, idx, chscale, dconv, 2)
+            else:
+                dconv = dy
             dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
             _ops().conv2d_dgrad(dconv, w, dx, ctx.pad, ctx.mf)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0):
     """nn.functional.conv2d (stride 1, symmetric padding) on MFMA implicit GEMM."""
     if not x.is_cuda:
         return F.conv2d(x, weight, bias, padding=padding)
-    return _Conv2d.apply(x, weight, bias, int(padding), False, None)
+    return _Conv2d.apply(x, weight, bias, int(padding), False, None, None)
 
 
-def conv2d_pool_relu(x, weight, bias=None, chscale: torch.Tensor | None = None, padding: int = 0):
-    """relu(max_pool2d(conv2d(x) [* chscale], 2)) in one kernel (ref src/model.py:16-17).
+def conv2d_pool_relu(x, weight, bias=None, chscale: torch.Tensor | None = None, padding: int = 0,
+                     dropout2d_p: float = 0.0):
+    """relu(max_pool2d(dropout2d(conv2d(x)), 2)) in one kernel (ref src/model.py:16-17).
 
-    ``chscale`` is an optional fp32 [N*C] per-channel scale (the Dropout2d mask,
-    already divided by 1-p).
+    ``chscale`` is an optional fp32 [N*C] per-channel scale (a Dropout2d mask already divided by
+    1-p); ``dropout2d_p > 0`` instead draws the Dropout2d mask inside the kernel (the same Philox
+    draw as :func:`dropout2d_scale`, one ``default_state`` offset).
     """
     if not x.is_cuda:
         y = F.conv2d(x, weight, bias, padding=padding)
         if chscale is not None:
             y = y * chscale.view(y.shape[0], y.shape[1], 1, 1).to(y.dtype)
+        elif dropout2d_p > 0.0:
+            y = F.dropout2d(y, dropout2d_p, True)
         return F.relu(F.max_pool2d(y, 2))
-    return _Conv2d.apply(x, weight, bias, int(padding), True, chscale)
+    drop = None
+    if chscale is None and dropout2d_p > 0.0:
+        seed, off, dev = default_state.next()
+        drop = (float(dropout2d_p), seed, off, dev)
+    return _Conv2d.apply(x, weight, bias, int(padding), True, chscale, drop)
 
 
 # ----------------------------------------------------------------- pool ----
@@ -268,22 +291,21 @@ class _Linear(torch.autograd.Function):
         if gate is not None and dy2.dtype != gate.dtype:
             dy2 = dy2.to(gate.dtype)
         gs = 1.0 / (1.0 - ctx.p) if ctx.act == 2 else 1.0
-        mf = _mfma()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
-            _ops().gemm(dy2, w, dx, None, 1.0, 0.0, 0, 0.0, 0, 0, None, gate, gs, mf)
-            dx = dx.view(*ctx.lead, x2.shape[1])
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         if want_db:
             db = _grad_buffer(ctx.bias_param, (w.shape[0],), w.device)
         if ctx.needs_input_grad[1]:
-            # dW = gate(dY)^T X; the bias gradient rides along as the GEMM's ones column
             dw = _grad_buffer(w, w.shape, w.device)
-            _ops().gemm(dy2.t(), x2, dw, None, 1.0, 0.0, 0, 0.0, 0, 0, None,
-                        gate.t() if gate is not None else None, gs, mf, db if want_db else None)
         elif want_db:
             _ops().colsum(dy2, gate, gs, db, 0.0)
+        if dx is not None or dw is not None:
+            # dX = gate(dY) W and dW = gate(dY)^T X (+ db as the GEMM's ones column): one launch
+            _ops().linear_bwd(dy2, x2, w, gate, gs, dx, dw, db if dw is not None else None, _mfma())
+        if dx is not None:
+            dx = dx.view(*ctx.lead, x2.shape[1])
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -364,9 +386,39 @@ def nll_loss(logp, target, reduction: str = "mean", size_average: bool | None = 
     return _NLL.apply(logp, target, _RED[reduction])
 
 
+class _LogSoftmaxNLL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, target, reduction):
+        z = z.contiguous()
+        target = target.contiguous().long()
+        logp = torch.empty(z.shape, device=z.device, dtype=torch.float32)
+        out = torch.empty((z.shape[0],) if reduction == 0 else (), device=z.device, dtype=torch.float32)
+        _ops().lsm_nll_fwd(z, target, logp, out, reduction)
+        ctx.save_for_backward(logp, target)
+        ctx.reduction, ctx.zdtype = reduction, z.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        logp, target = ctx.saved_tensors
+        dz = torch.empty(logp.shape, device=logp.device, dtype=ctx.zdtype)
+        _ops().lsm_nll_bwd(gout.contiguous().float(), logp, target, dz, ctx.reduction)
+        return dz, None, None
+
+
+def log_softmax_nll(z, target, reduction: str = "mean"):
+    """nll_loss(log_softmax(z, 1), target): one kernel each way instead of four (the modular step's
+    loss on logits: ref src/model.py:22 + src/train.py:74)."""
+    if not z.is_cuda:
+        return F.nll_loss(F.log_softmax(z, dim=1), target, reduction=reduction)
+    if z.dim() != 2:
+        raise ValueError("log_softmax_nll expects [rows, classes] logits")
+    return _LogSoftmaxNLL.apply(z, target, _RED[reduction])
+
+
 def cross_entropy(x, target, reduction: str = "mean"):
     """nn.CrossEntropyLoss: log_softmax then NLL (idempotent on log-probs, ref src/train_dist.py:67)."""
-    return nll_loss(log_softmax(x), target, reduction)
+    return log_softmax_nll(x, target, reduction)
 
 
 def accuracy_count(logp: torch.Tensor, target: torch.Tensor) -> torch.Tensor:

@@ -131,6 +131,28 @@ void nll_bwd(const Tensor& gout, const Tensor& target, Tensor& dlogp, int64_t re
                                  (int)dlogp.size(0), (int)dlogp.size(1), (int)reduction, cur_stream(dlogp)));
 }
 
+void lsm_nll_fwd(const Tensor& z, const Tensor& target, Tensor& logp, Tensor& out, int64_t reduction) {
+  dev(z, "z"); dev(target, "target"); dev(logp, "logp"); dev(out, "out");
+  TORCH_CHECK(z.dim() == 2 && target.scalar_type() == at::kLong && target.numel() == z.size(0));
+  TORCH_CHECK(logp.scalar_type() == at::kFloat && logp.sizes() == z.sizes());
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() == (reduction == 0 ? z.size(0) : 1));
+  const c10::DeviceGuard gd(z.device());
+  CHECK_HIP(csed::launch_lsm_nll_fwd(z.data_ptr(), dcode(z), target.data_ptr<int64_t>(), logp.data_ptr<float>(),
+                                     out.data_ptr<float>(), (int)z.size(0), (int)z.size(1), (int)reduction,
+                                     cur_stream(z)));
+}
+
+void lsm_nll_bwd(const Tensor& gout, const Tensor& logp, const Tensor& target, Tensor& dz, int64_t reduction) {
+  dev(gout, "gout"); dev(logp, "logp"); dev(target, "target"); dev(dz, "dz");
+  TORCH_CHECK(gout.scalar_type() == at::kFloat && logp.scalar_type() == at::kFloat && logp.dim() == 2);
+  TORCH_CHECK(dz.sizes() == logp.sizes() && target.numel() == logp.size(0));
+  TORCH_CHECK(gout.numel() == (reduction == 0 ? logp.size(0) : 1));
+  const c10::DeviceGuard gd(dz.device());
+  CHECK_HIP(csed::launch_lsm_nll_bwd(gout.data_ptr<float>(), logp.data_ptr<float>(), target.data_ptr<int64_t>(),
+                                     dz.data_ptr(), dcode(dz), (int)logp.size(0), (int)logp.size(1), (int)reduction,
+                                     cur_stream(dz)));
+}
+
 // ------------------------------------------------------------------- pool
 void maxpool_relu_fwd(const Tensor& x, Tensor& out, Tensor& idx, const optional<Tensor>& chscale, int64_t k) {
   dev(x, "x"); dev(out, "out"); dev(idx, "idx");
@@ -184,9 +206,10 @@ void gate_bwd(const Tensor& dout, const Tensor& y, Tensor& dx, double s) {
 // ------------------------------------------------------------------- gemm
 // C = alpha * A(MxK) @ B(KxN) + beta*C (+bias, act).  A/B/C are 2-D views with
 // arbitrary strides (e.g. .t() views); strides are read from the tensors.
-void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, double alpha, double beta,
-          int64_t act, double drop_p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev,
-          const optional<Tensor>& gate, double gate_scale, int64_t mfma_dtype, const optional<Tensor>& rowsum) {
+csed::GemmArgs make_gemm(const Tensor& A, const Tensor& B, const Tensor& C, const optional<Tensor>& bias,
+                         double alpha, double beta, int64_t act, double drop_p, int64_t seed, int64_t offset,
+                         const optional<Tensor>& offset_dev, const optional<Tensor>& gate, double gate_scale,
+                         int64_t mfma_dtype, const optional<Tensor>& rowsum) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2);
   TORCH_CHECK(A.size(1) == B.size(0) && C.size(0) == A.size(0) && C.size(1) == B.size(1), "gemm: shape mismatch");
@@ -196,7 +219,6 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
   if (bias.has_value()) {
     TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == C.size(1) && bias->is_contiguous());
   }
-  const c10::DeviceGuard gd(A.device());
   csed::GemmArgs a{};
   a.A = A.data_ptr(); a.a_dtype = dcode(A); a.sam = A.stride(0); a.sak = A.stride(1);
   a.B = B.data_ptr(); a.b_dtype = dcode(B); a.sbk = B.stride(0); a.sbn = B.stride(1);
@@ -215,6 +237,10 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
                 "gemm: rowsum must be fp32 [M]");
     a.rowsum = rowsum->data_ptr<float>();
   }
+  return a;
+}
+
+void run_gemm(csed::GemmArgs a, const Tensor& A) {
   // split-K workspace (stream-ordered caching allocation: legal inside graph capture)
   Tensor ws;
   const int splits = csed::gemm_splits(a);
@@ -223,6 +249,47 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
     a.ws = ws.data_ptr<float>();
   }
   CHECK_HIP(csed::launch_gemm(a, cur_stream(A)));
+}
+
+// C = alpha * A(MxK) @ B(KxN) + beta*C (+bias, act).  A/B/C are 2-D views with
+// arbitrary strides (e.g. .t() views); strides are read from the tensors.
+void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, double alpha, double beta,
+          int64_t act, double drop_p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev,
+          const optional<Tensor>& gate, double gate_scale, int64_t mfma_dtype, const optional<Tensor>& rowsum) {
+  const c10::DeviceGuard gd(A.device());
+  run_gemm(make_gemm(A, B, C, bias, alpha, beta, act, drop_p, seed, offset, offset_dev, gate, gate_scale, mfma_dtype,
+                     rowsum),
+           A);
+}
+
+// nn.Linear's backward (y = act(x W^T + b), dy [M, O], x [M, I], w [O, I]): dx = gate(dy) W and
+// dw = gate(dy)^T x with db as the ones column, gate(dy) = dy * (y > 0) * gate_scale when the
+// forward had an activation.  One launch when both GEMMs fit the small-GEMM path.
+void linear_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const optional<Tensor>& gate, double gate_scale,
+                const optional<Tensor>& dx, const optional<Tensor>& dw, const optional<Tensor>& db,
+                int64_t mfma_dtype) {
+  dev(dy, "dy"); dev(x, "x"); dev(w, "w");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && w.dim() == 2 && dy.size(0) == x.size(0) && w.size(0) == dy.size(1) &&
+              w.size(1) == x.size(1), "linear_bwd: shape mismatch");
+  if (gate.has_value()) dev(*gate, "gate");
+  TORCH_CHECK(!db.has_value() || dw.has_value(), "linear_bwd: db rides on the dw GEMM");
+  const c10::DeviceGuard gd(dy.device());
+  const optional<Tensor> none;
+  std::vector<csed::GemmArgs> todo;
+  if (dx.has_value()) {
+    dev(*dx, "dx");
+    todo.push_back(make_gemm(dy, w, *dx, none, 1.0, 0.0, 0, 0.0, 0, 0, none, gate, gate_scale, mfma_dtype, none));
+  }
+  if (dw.has_value()) {
+    dev(*dw, "dw");
+    const optional<Tensor> gt = gate.has_value() ? optional<Tensor>(gate->t()) : none;
+    todo.push_back(make_gemm(dy.t(), x, *dw, none, 1.0, 0.0, 0, 0.0, 0, 0, none, gt, gate_scale, mfma_dtype, db));
+  }
+  if (todo.size() == 2 && csed::gemm_pairable(todo[0], todo[1])) {
+    CHECK_HIP(csed::launch_gemm_pair(todo[0], todo[1], cur_stream(dy)));
+    return;
+  }
+  for (const auto& a : todo) run_gemm(a, dy);
 }
 
 void colsum(const Tensor& x, const optional<Tensor>& gate, double gate_scale, Tensor& out, double beta) {
@@ -237,7 +304,9 @@ void colsum(const Tensor& x, const optional<Tensor>& gate, double gate_scale, Te
 
 // ------------------------------------------------------------------- conv
 void conv2d_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, Tensor& y, int64_t pad,
-                const optional<Tensor>& idx, const optional<Tensor>& chscale, int64_t pool_k, int64_t mfma_dtype) {
+                const optional<Tensor>& idx, const optional<Tensor>& chscale, int64_t pool_k, int64_t mfma_dtype,
+                double drop2d_p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev,
+                const optional<Tensor>& chscale_out) {
   dev(x, "x"); dev(w, "w"); dev(y, "y");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.scalar_type() == at::kFloat && x.size(1) == w.size(1));
   const int N = x.size(0), IC = x.size(1), H = x.size(2), W = x.size(3);
@@ -249,6 +318,12 @@ void conv2d_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, 
   } else {
     TORCH_CHECK(y.numel() == (int64_t)N * OC * OH * OW, "conv2d_fwd: y size mismatch");
   }
+  if (chscale_out.has_value()) {
+    dev(*chscale_out, "chscale_out");
+    TORCH_CHECK(pool_k == 2 && !chscale.has_value() && chscale_out->scalar_type() == at::kFloat &&
+                    chscale_out->numel() == (int64_t)N * OC,
+                "conv2d_fwd: chscale_out (in-kernel Dropout2d) needs pool_k 2, no chscale, fp32 [N*OC]");
+  }
   const c10::DeviceGuard gd(x.device());
   csed::ConvArgs a{};
   a.x = x.data_ptr(); a.x_dtype = dcode(x); a.w = w.data_ptr<float>(); a.bias = optpt<float>(bias);
@@ -257,6 +332,9 @@ void conv2d_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, 
   a.chscale = optpt<float>(chscale); a.pool_k = (int)pool_k;
   a.N = N; a.IC = IC; a.H = H; a.W = W; a.OC = OC; a.KH = KH; a.KW = KW; a.pad = (int)pad;
   a.mode = 0; a.mfma_dtype = mcode(mfma_dtype);
+  a.drop_p = (float)drop2d_p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset;
+  a.offset_dev = optpt<int64_t>(offset_dev);
+  a.chscale_out = chscale_out.has_value() ? chscale_out->data_ptr<float>() : nullptr;
   CHECK_HIP(csed::launch_conv2d(a, cur_stream(x)));
 }
 
@@ -288,6 +366,54 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
   CHECK_HIP(csed::launch_conv2d_wgrad(x.data_ptr(), dcode(x), dy.data_ptr(), dcode(dy), dw.data_ptr<float>(),
                                       optpt<float>(db), ws.data_ptr<float>(), N, IC, H, W, OC, KH, KW, (int)pad,
                                       mcode(mfma_dtype), (float)beta, cur_stream(x)));
+}
+
+// Backward of y = conv(x, w, b, pad) [-> maxpool2 + relu (* chscale)]: dw, db (+ dx), one launch
+// + the slab reduce.  With pool_idx, dy is the gradient of the pooled output and pool_idx /
+// pool_out / pool_scale the forward's argmax bytes, pooled output and channel scale.
+void conv2d_bwd(const Tensor& x, const Tensor& dy, const Tensor& w, Tensor& dw, const optional<Tensor>& db,
+                Tensor& ws, const optional<Tensor>& dx, int64_t pad, const optional<Tensor>& pool_idx,
+                const optional<Tensor>& pool_out, const optional<Tensor>& pool_scale, int64_t mfma_dtype) {
+  dev(x, "x"); dev(dy, "dy"); dev(w, "w"); dev(dw, "dw"); dev(ws, "ws");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && dy.dim() == 4 && w.scalar_type() == at::kFloat);
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.sizes() == w.sizes() && ws.scalar_type() == at::kFloat);
+  const int N = x.size(0), IC = x.size(1), H = x.size(2), W = x.size(3);
+  const int OC = w.size(0), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(w.size(1) == IC && dy.size(0) == N && dy.size(1) == OC, "conv2d_bwd: shape mismatch");
+  const int OH = H + 2 * (int)pad - KH + 1, OW = W + 2 * (int)pad - KW + 1;
+  csed::ConvBwdArgs b{};
+  if (pool_idx.has_value()) {
+    TORCH_CHECK(pool_out.has_value(), "conv2d_bwd: pool_out (the ReLU gate) is required with pool_idx");
+    dev(*pool_idx, "pool_idx"); dev(*pool_out, "pool_out");
+    TORCH_CHECK(dy.size(2) == OH / 2 && dy.size(3) == OW / 2 && pool_idx->sizes() == dy.sizes() &&
+                    pool_out->sizes() == dy.sizes() && pool_idx->scalar_type() == at::kByte &&
+                    pool_out->scalar_type() == dy.scalar_type(),
+                "conv2d_bwd: pooled dy / argmax / output must be [N, OC, OH/2, OW/2] (dy and output one dtype)");
+    if (pool_scale.has_value()) {
+      dev(*pool_scale, "pool_scale");
+      TORCH_CHECK(pool_scale->scalar_type() == at::kFloat && pool_scale->numel() == (int64_t)N * OC);
+    }
+    b.pidx = pool_idx->data_ptr<uint8_t>(); b.pout = pool_out->data_ptr(); b.pscale = optpt<float>(pool_scale);
+  } else {
+    TORCH_CHECK(dy.size(2) == OH && dy.size(3) == OW, "conv2d_bwd: dy spatial mismatch");
+  }
+  TORCH_CHECK(ws.numel() >= csed::conv2d_wgrad_workspace(N, IC, KH, KW, OC), "conv2d_bwd: workspace too small");
+  if (db.has_value()) {
+    dev(*db, "db");
+    TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() == OC);
+  }
+  if (dx.has_value()) {
+    dev(*dx, "dx");
+    TORCH_CHECK(dx->sizes() == x.sizes(), "conv2d_bwd: dx must have x's shape");
+    b.dx = dx->data_ptr(); b.dx_dtype = dcode(*dx);
+  }
+  const c10::DeviceGuard gd(x.device());
+  b.x = x.data_ptr(); b.x_dtype = dcode(x); b.dy = dy.data_ptr(); b.dy_dtype = dcode(dy);
+  b.w = w.data_ptr<float>(); b.dw = dw.data_ptr<float>(); b.db = optpt<float>(db); b.ws = ws.data_ptr<float>();
+  b.beta = 0.f;
+  b.N = N; b.IC = IC; b.H = H; b.W = W; b.OC = OC; b.KH = KH; b.KW = KW; b.pad = (int)pad;
+  b.mfma_dtype = mcode(mfma_dtype);
+  CHECK_HIP(csed::launch_conv2d_bwd(b, cur_stream(x)));
 }
 
 // ----------------------------------------------------------- fused lenet
@@ -592,7 +718,14 @@ TORCH_LIBRARY(csed, m) {
         "Tensor(b!)? rowsum=None) -> ()");
   m.def("colsum(Tensor x, Tensor? gate, float gate_scale, Tensor(a!) out, float beta) -> ()");
   m.def("conv2d_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, int pad, Tensor(b!)? idx, Tensor? chscale, "
-        "int pool_k, int mfma_dtype) -> ()");
+        "int pool_k, int mfma_dtype, float drop2d_p=0.0, int seed=0, int offset=0, Tensor? offset_dev=None, "
+        "Tensor(c!)? chscale_out=None) -> ()");
+  m.def("conv2d_bwd(Tensor x, Tensor dy, Tensor w, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, Tensor(d!)? dx, "
+        "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype) -> ()");
+  m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? gate, float gate_scale, Tensor(a!)? dx, Tensor(b!)? dw, "
+        "Tensor(c!)? db, int mfma_dtype) -> ()");
+  m.def("lsm_nll_fwd(Tensor z, Tensor target, Tensor(a!) logp, Tensor(b!) out, int reduction) -> ()");
+  m.def("lsm_nll_bwd(Tensor gout, Tensor logp, Tensor target, Tensor(a!) dz, int reduction) -> ()");
   m.def("conv2d_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int pad, int mfma_dtype) -> ()");
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, int pad, int mfma_dtype, "
         "float beta) -> ()");
@@ -615,6 +748,10 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("conv2d_fwd", &conv2d_fwd);
   m.impl("conv2d_dgrad", &conv2d_dgrad);
   m.impl("conv2d_wgrad", &conv2d_wgrad);
+  m.impl("conv2d_bwd", &conv2d_bwd);
+  m.impl("linear_bwd", &linear_bwd);
+  m.impl("lsm_nll_fwd", &lsm_nll_fwd);
+  m.impl("lsm_nll_bwd", &lsm_nll_bwd);
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);
   m.impl("lenet_update", &lenet_update);

@@ -14,6 +14,11 @@
 // fragments are then gathered from LDS through a k -> offset table, i.e. the
 // im2col matrix is never materialised in memory.
 //
+// Backward of a pool-fused forward without materialising dL/dconv: the data- and weight-gradient
+// stagings take the POOLED gradient plus the forward's argmax bytes, pooled output (the ReLU gate)
+// and channel scale, and expand each 2x2 window on load (one nonzero per window).  The weight and
+// data gradients of one conv run as two block ranges of ONE launch (conv_bwd_kernel).
+//
 // Pool-fused pixel order: m = 4*window + (dy*2 + dx).  With the 16x16x32
 // MFMA C layout (row = 4*(lane>>4) + reg) every lane then holds one complete
 // 2x2 window of one channel in its 4 accumulators, so the max-pool, argmax,
@@ -34,6 +39,7 @@ struct ConvGeo {
   int TR;                // output rows per block
   int PR, PW;            // patch rows / cols in LDS
   int bands;             // blocks per image
+  int Hp, Wp;            // pooled input dims (a.pidx set: the input is given max-pooled)
 };
 
 __device__ __forceinline__ float ldf(const void* p, int dt, int64_t i) {
@@ -59,9 +65,16 @@ __device__ __forceinline__ float weff(const float* w, int mode, int Ci, int Co, 
   return w[(((int64_t)ic * Co + oc) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
 }
 
+// Expanded element of a max-pooled gradient: x(n, c, h, w) of the un-pooled tensor from the pooled
+// value at po (= (n, c, h / 2, w / 2)), its argmax byte (sel = (h & 1) * 2 + (w & 1)), the pooled
+// forward output (ReLU gate) and the channel scale (maxpool_relu_bwd_kernel's rule).
+__device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc, int sel) {
+  return ((int)bi == sel && yo > 0.f) ? v * sc : 0.f;
+}
+
 template <typename T>
-__global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
+                                              unsigned char* __restrict__ smem) {
   typedef typename Mfma<T>::frag frag;
   typedef typename Stor<T>::S S;
   const int LDW = g.Kp + 8;                         // 16-B aligned row pad
@@ -69,7 +82,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   int* koff = (int*)(Ws + g.Cop * LDW);             // [Kp]
   S* patch = (S*)(koff + g.Kp);                     // [Ci][PR][PW]
 
-  const int n = blockIdx.x / g.bands, band = blockIdx.x % g.bands;
+  const int n = blk / g.bands, band = blk % g.bands;
   const int oh0 = band * g.TR;
   const int rows = min(g.TR, g.OH - oh0);
   const int npix = rows * g.OW;
@@ -131,7 +144,45 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
             if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(v[j]);
         }
       };
-      if (a.x_dtype == kF32) rows(float{});
+      // pooled input (the gradient of a pool-fused forward): eight rows' value / argmax / gate /
+      // scale loads in flight, expanded in registers
+      auto prows = [&](auto tag) {
+        typedef decltype(tag) X;
+        const X* xs = static_cast<const X*>(a.x);
+        const X* ys = static_cast<const X*>(a.pout);
+        const int64_t nc0 = (int64_t)n * g.Ci;
+        while (rr < nrows) {
+          float v[8], yo[8], sc[8];
+          uint8_t bi[8];
+          int at[8], sel[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ih = oh0 - g.pad + pr;
+            const bool ok = rr < nrows && colv && ih >= 0 && ih < g.H;
+            at[j] = rr < nrows ? rr : -1;
+            sel[j] = ((ih & 1) << 1) | (iw & 1);
+            const int64_t po = ok ? ((nc0 + ic) * g.Hp + (ih >> 1)) * g.Wp + (iw >> 1) : 0;
+            v[j] = ok ? (float)xs[po] : 0.f;
+            yo[j] = ok ? (float)ys[po] : 0.f;
+            bi[j] = ok ? a.pidx[po] : (uint8_t)255;
+            sc[j] = ok ? (a.pscale ? a.pscale[nc0 + ic] : 1.f) : 0.f;
+            rr += rpi;
+            pr += rpi;
+            while (pr >= g.PR) {
+              pr -= g.PR;
+              ++ic;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], sel[j]));
+        }
+      };
+      if (a.pidx) {
+        if (a.x_dtype == kF32) prows(float{});
+        else if (a.x_dtype == kBF16) prows(__bf16{});
+        else prows(_Float16{});
+      } else if (a.x_dtype == kF32) rows(float{});
       else if (a.x_dtype == kBF16) rows(__bf16{});
       else rows(_Float16{});
     }
@@ -203,7 +254,15 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
           const int p = wbase >> 2;
           const int ph = (oh0 >> 1) + p / PWb, pw = p % PWb;
           const int PH = g.OH >> 1;
-          const float sc = a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
+          float sc = 1.f;
+          if (a.chscale) {
+            sc = a.chscale[(int64_t)n * g.Co + oc];
+          } else if (a.chscale_out) {  // Dropout2d drawn here (channel_mask_kernel's draw: index n*Co+oc)
+            sc = dropout_keep(a.seed, rng_offset(a.offset, a.offset_dev), (uint64_t)n * g.Co + oc, a.drop_p)
+                     ? (a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f)
+                     : 0.f;
+            if (band == 0 && wbase == 0) a.chscale_out[(int64_t)n * g.Co + oc] = sc;  // once per (n, oc)
+          }
           const float v = fmaxf(best + b, 0.f) * sc;
           const int64_t o = (((int64_t)n * g.Co + oc) * PH + ph) * PWb + pw;
           stf(a.y, a.y_dtype, o, v);
@@ -222,7 +281,23 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   }
 }
 
+template <typename T>
+__global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  conv_fwd_body<T>(a, g, blockIdx.x, smem);
+}
+
 // ------------------------------------------------------------- wgrad ----
+// Operands of the weight gradient: the forward input and dL/d(conv output), the latter optionally
+// given max-pooled (pidx set: expanded on load like the data gradient's input).
+struct WgradArgs {
+  const void* x; int xdt;
+  const void* dy; int dydt;
+  const uint8_t* pidx; const void* pout; const float* pscale;
+  int N;
+  float* slab;
+};
+
 struct WgradGeo {
   int Ci, Co, H, W, OH, OW, KH, KW, pad;
   int K, Kc;       // K = Ci*KH*KW ; Kc = roundup(K+1, 16) columns (last real = db)
@@ -234,10 +309,12 @@ struct WgradGeo {
 };
 
 template <typename T>
-__global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict__ x, int xdt,
-                                                         const void* __restrict__ dy, int dydt, int N,
-                                                         float* __restrict__ slab, WgradGeo g) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const WgradGeo& g, const int blk,
+                                                unsigned char* __restrict__ smem) {
+  const void* __restrict__ x = wa.x;
+  const void* __restrict__ dy = wa.dy;
+  const int xdt = wa.xdt, dydt = wa.dydt, N = wa.N;
+  float* __restrict__ slab = wa.slab;
   typedef typename Mfma<T>::frag frag;
   typedef typename Stor<T>::S S;
   const int LDY = g.npp + 8;
@@ -270,7 +347,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
 #pragma unroll
     for (int j = 0; j < MAXNTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int n_begin = blockIdx.x * g.per_block;
+  const int n_begin = blk * g.per_block;
   const int n_end = min(N, n_begin + g.per_block);
   for (int n = n_begin; n < n_end; ++n) {
     __syncthreads();  // previous image's LDS reads are done
@@ -326,7 +403,40 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
           for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(v[j]);
         }
     };
-    if (dydt == kF32) dyrows(float{});
+    // pooled dy: a thread keeps its pixel's window position for every oc; value / argmax / gate /
+    // scale loads of 8 channels in flight, expanded in registers
+    auto pdyrows = [&](auto tag) {
+      typedef decltype(tag) X;
+      const X* ys = static_cast<const X*>(dy);
+      const X* os = static_cast<const X*>(wa.pout);
+      const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
+      const int64_t ybp = (int64_t)n * g.Co * npixp;
+      for (int p = tid; p < g.npp; p += 256) {
+        const bool pv = p < g.npix;
+        const int oh = pv ? p / g.OW : 0, ow = pv ? p - oh * g.OW : 0;
+        const int sel = ((oh & 1) << 1) | (ow & 1), q = (oh >> 1) * PWp + (ow >> 1);
+        for (int oc0 = 0; oc0 < g.Cop; oc0 += 8) {
+          float v[8], yo[8], sc[8];
+          uint8_t bi[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const bool ok = oc0 + j < g.Co && pv;
+            const int64_t po = ok ? ybp + (int64_t)(oc0 + j) * npixp + q : 0;
+            v[j] = ok ? (float)ys[po] : 0.f;
+            yo[j] = ok ? (float)os[po] : 0.f;
+            bi[j] = ok ? wa.pidx[po] : (uint8_t)255;
+            sc[j] = ok ? (wa.pscale ? wa.pscale[(int64_t)n * g.Co + oc0 + j] : 1.f) : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], sel));
+        }
+      }
+    };
+    if (wa.pidx) {
+      if (dydt == kF32) pdyrows(float{});
+      else if (dydt == kBF16) pdyrows(__bf16{});
+      else pdyrows(_Float16{});
+    } else if (dydt == kF32) dyrows(float{});
     else if (dydt == kBF16) dyrows(__bf16{});
     else dyrows(_Float16{});
     __syncthreads();
@@ -366,7 +476,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
   }
 
   // ---- write this block's partial [Co][K+1] slab (fixed-order combine of split waves)
-  float* out = slab + (int64_t)blockIdx.x * g.Co * (g.K + 1);
+  float* out = slab + (int64_t)blk * g.Co * (g.K + 1);
   if (psplit == 1) {
 #pragma unroll
     for (int jj = 0; jj < MAXNTW; ++jj) {
@@ -404,6 +514,23 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(const void* __restrict_
       out[(int64_t)oc * (g.K + 1) + col] = s;
     }
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  conv_wgrad_body<T>(wa, g, blockIdx.x, smem);
+}
+
+// The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
+// partial slabs, the rest compute the data gradient (conv_fwd_body in mode 1); both read the same
+// (possibly pooled) dy.  A second launch for the data gradient was a kernel boundary (~1.4 us in a
+// graph) plus its own ramp.
+template <typename T>
+__global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T>(wa, wg, blockIdx.x, smem);
+  else conv_fwd_body<T>(a, g, blockIdx.x - wg.nblocks, smem);
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
@@ -448,8 +575,9 @@ inline int rup(int a, int b) { return (a + b - 1) / b * b; }
 
 }  // namespace
 
-hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
-  ConvGeo g;
+// Geometry + LDS bytes of a forward / data-gradient launch (hipSuccess with grid 0: nothing to do).
+static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid) {
+  grid = 0;
   g.KH = a.KH; g.KW = a.KW;
   g.H = a.H; g.W = a.W;
   if (a.mode == 0) {
@@ -458,10 +586,13 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
     g.Ci = a.IC; g.Co = a.OC; g.pad = a.KH - 1 - a.pad;
     if (a.KH != a.KW || g.pad < 0) return hipErrorInvalidValue;
   }
+  g.Hp = g.H >> 1; g.Wp = g.W >> 1;
+  if (a.pidx && (a.mode != 1 || (g.H & 1) || (g.W & 1) || !a.pout)) return hipErrorInvalidValue;
   g.OH = g.H + 2 * g.pad - g.KH + 1;
   g.OW = g.W + 2 * g.pad - g.KW + 1;
   if (g.OH <= 0 || g.OW <= 0 || a.N <= 0) return hipSuccess;
   if (a.pool_k != 0 && (a.pool_k != 2 || a.mode != 0 || (g.OH & 1) || (g.OW & 1))) return hipErrorInvalidValue;
+  if (a.chscale_out && (a.pool_k != 2 || a.chscale)) return hipErrorInvalidValue;
   g.K = g.Ci * g.KH * g.KW;
   g.Kp = rup(g.K, 32);
   g.Cop = rup(g.Co, 16);
@@ -482,12 +613,21 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   g.TR = tr;
   g.PR = tr + g.KH - 1;
   g.bands = (g.OH + tr - 1) / tr;
-  const size_t lds = lds_bytes(tr);
-  dim3 grid(a.N * g.bands);
+  lds = lds_bytes(tr);
+  grid = a.N * g.bands;
+  return hipSuccess;
+}
+
+hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
+  ConvGeo g;
+  size_t lds = 0;
+  int grid = 0;
+  hipError_t e = conv_geo(a, g, lds, grid);
+  if (e != hipSuccess || grid == 0) return e;
   CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_fwd_kernel<scalar_t>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv_fwd_kernel<scalar_t>, grid, dim3(256), lds, s, a, g);
+    hipLaunchKernelGGL(conv_fwd_kernel<scalar_t>, dim3(grid), dim3(256), lds, s, a, g);
   });
   return hipGetLastError();
 }
@@ -515,32 +655,64 @@ int64_t conv2d_wgrad_workspace(int N, int IC, int KH, int KW, int OC) {
   return (int64_t)nb * OC * (IC * KH * KW + 1);
 }
 
-hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw,
-                               float* db, float* ws, int N, int IC, int H, int W, int OC, int KH,
-                               int KW, int pad, int mfma_dtype, float beta, hipStream_t s) {
-  if (N <= 0) return hipSuccess;
-  WgradGeo g = wgrad_geo(N, IC, H, W, OC, KH, KW, pad);
-  if (g.OH <= 0 || g.OW <= 0) return hipErrorInvalidValue;
-  if (g.PW > 256) return hipErrorInvalidConfiguration;  // (patch staging: one column per thread)
-  if (g.Cop > 64 || (g.Kc / 16) > 32) return hipErrorInvalidConfiguration;  // accumulator budget
-  const size_t es = mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
-  const size_t lds_main = (size_t)g.Cop * (g.npp + 8) * es + (size_t)g.Kc * 4 + (size_t)g.npp * 4 +
-                          ((size_t)g.Ci * g.PR * g.PW + 1) * es + 16;
+hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
+  if (b.N <= 0) return hipSuccess;
+  WgradGeo wg = wgrad_geo(b.N, b.IC, b.H, b.W, b.OC, b.KH, b.KW, b.pad);
+  if (wg.OH <= 0 || wg.OW <= 0) return hipErrorInvalidValue;
+  if (wg.PW > 256) return hipErrorInvalidConfiguration;  // (patch staging: one column per thread)
+  if (wg.Cop > 64 || (wg.Kc / 16) > 32) return hipErrorInvalidConfiguration;  // accumulator budget
+  if (b.pidx && (!b.pout || (wg.OH & 1) || (wg.OW & 1))) return hipErrorInvalidValue;
+  const size_t es = b.mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
+  const size_t lds_main = (size_t)wg.Cop * (wg.npp + 8) * es + (size_t)wg.Kc * 4 + (size_t)wg.npp * 4 +
+                          ((size_t)wg.Ci * wg.PR * wg.PW + 1) * es + 16;
   const size_t lds_red = (size_t)4 * 4 * 16 * 16 * 4;
-  const size_t lds = std::max(lds_main, lds_red);
+  size_t lds = std::max(lds_main, lds_red);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  CSED_DISPATCH_COMPUTE(mfma_dtype, {
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_wgrad_kernel<scalar_t>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv_wgrad_kernel<scalar_t>, dim3(g.nblocks), dim3(256), lds, s, x, x_dtype, dy,
-                       dy_dtype, N, ws, g);
+  WgradArgs wa{b.x, b.x_dtype, b.dy, b.dy_dtype, b.pidx, b.pout, b.pscale, b.N, b.ws};
+  // the data gradient (optional): conv of dy (un-pooled on load) with the flipped weights
+  ConvArgs a{};
+  ConvGeo g{};
+  int dgrid = 0;
+  if (b.dx) {
+    a.x = b.dy; a.x_dtype = b.dy_dtype; a.w = b.w; a.bias = nullptr;
+    a.y = b.dx; a.y_dtype = b.dx_dtype;
+    a.N = b.N; a.IC = b.OC; a.H = wg.OH; a.W = wg.OW; a.OC = b.IC; a.KH = b.KH; a.KW = b.KW; a.pad = b.pad;
+    a.mode = 1; a.mfma_dtype = b.mfma_dtype;
+    a.pidx = b.pidx; a.pout = b.pout; a.pscale = b.pscale;
+    size_t dl = 0;
+    hipError_t e = conv_geo(a, g, dl, dgrid);
+    if (e != hipSuccess) return e;
+    if (g.OH != b.H || g.OW != b.W) return hipErrorInvalidValue;
+    lds = std::max(lds, dl);
+  }
+  CSED_DISPATCH_COMPUTE(b.mfma_dtype, {
+    if (dgrid > 0) {
+      if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_bwd_kernel<scalar_t>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(conv_bwd_kernel<scalar_t>, dim3(wg.nblocks + dgrid), dim3(256), lds, s, wa, wg, a, g);
+    } else {
+      if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_wgrad_kernel<scalar_t>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(conv_wgrad_kernel<scalar_t>, dim3(wg.nblocks), dim3(256), lds, s, wa, wg);
+    }
   });
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int L = OC * (g.K + 1);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, ws, g.nblocks, OC, g.K, dw, db,
-                     beta);
+  const int L = b.OC * (wg.K + 1);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, b.ws, wg.nblocks, b.OC, wg.K, b.dw,
+                     b.db, b.beta);
   return hipGetLastError();
+}
+
+hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw,
+                               float* db, float* ws, int N, int IC, int H, int W, int OC, int KH,
+                               int KW, int pad, int mfma_dtype, float beta, hipStream_t s) {
+  ConvBwdArgs b{};
+  b.x = x; b.x_dtype = x_dtype; b.dy = dy; b.dy_dtype = dy_dtype;
+  b.dw = dw; b.db = db; b.ws = ws; b.beta = beta;
+  b.N = N; b.IC = IC; b.H = H; b.W = W; b.OC = OC; b.KH = KH; b.KW = KW; b.pad = pad;
+  b.mfma_dtype = mfma_dtype;
+  return launch_conv2d_bwd(b, s);
 }
 
 }  // namespace csed

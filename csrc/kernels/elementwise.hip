@@ -223,6 +223,82 @@ hipError_t launch_nll_bwd(const float* gout, const int64_t* target, float* dlogp
 }
 
 // ---------------------------------------------------------------------------
+// log_softmax + NLL in one launch each way (the modular step's loss: nll(log_softmax(z)), ref
+// src/model.py:22 + src/train.py:74 / train_dist.py:67,82 -- four launches as separate ops).
+// Forward: one block, a thread per row (rows strided over the block), log-probs kept for the
+// backward, the mean / sum reduced in a fixed order (bitwise reproducible).  Backward: one
+// thread per element, dz = g_r * (exp(logp) - onehot).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) lsm_nll_fwd_kernel(const T* __restrict__ z, const int64_t* __restrict__ target,
+                                                          float* __restrict__ logp, float* __restrict__ out, int rows,
+                                                          int C, int reduction) {
+  __shared__ float ssum[256];
+  float acc = 0.f;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    const T* zr = z + (int64_t)r * C;
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, to_f32(zr[c]));
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += __expf(to_f32(zr[c]) - mx);
+    const float lse = mx + __logf(s);
+    const int64_t t = target[r];
+    float* lr = logp + (int64_t)r * C;
+    float v = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float q = to_f32(zr[c]) - lse;
+      lr[c] = q;
+      if (c == t) v = -q;
+    }
+    if (reduction == 0) out[r] = v;
+    acc += v;
+  }
+  ssum[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) ssum[threadIdx.x] += ssum[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (reduction == 1) out[0] = ssum[0] / (float)rows;
+    else if (reduction == 2) out[0] = ssum[0];
+  }
+}
+
+hipError_t launch_lsm_nll_fwd(const void* z, int z_dtype, const int64_t* target, float* logp, float* out, int rows,
+                              int C, int reduction, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  CSED_DISPATCH_FLOAT(z_dtype, {
+    hipLaunchKernelGGL(lsm_nll_fwd_kernel<scalar_t>, dim3(1), dim3(256), 0, s, (const scalar_t*)z, target, logp,
+                       out, rows, C, reduction);
+  });
+  return hipGetLastError();
+}
+
+template <typename T>
+__global__ void lsm_nll_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ logp,
+                                   const int64_t* __restrict__ target, T* __restrict__ dz, int rows, int C,
+                                   int reduction) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * C) return;
+  const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+  float g = reduction == 0 ? gout[r] : gout[0];
+  if (reduction == 1) g /= (float)rows;
+  dz[i] = from_f32<T>(g * (__expf(logp[i]) - (c == target[r] ? 1.f : 0.f)));
+}
+
+hipError_t launch_lsm_nll_bwd(const float* gout, const float* logp, const int64_t* target, void* dz, int dz_dtype,
+                              int rows, int C, int reduction, hipStream_t s) {
+  const int64_t n = (int64_t)rows * C;
+  if (n == 0) return hipSuccess;
+  CSED_DISPATCH_FLOAT(dz_dtype, {
+    hipLaunchKernelGGL(lsm_nll_bwd_kernel<scalar_t>, dim3(cdiv(n, 256)), dim3(256), 0, s, gout, logp, target,
+                       (scalar_t*)dz, rows, C, reduction);
+  });
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // max-pool (k x k, stride k) + ReLU (+ per-channel scale) forward / backward
 // One thread per pooled output.
 // ---------------------------------------------------------------------------

@@ -309,12 +309,11 @@ __device__ __forceinline__ typename Mfma<T>::frag to_frag(const float (&f)[8]) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
-  __shared__ float part[4][256];
+__device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk, float (*part)[256]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
   const int Np = a.N + (a.rowsum ? 1 : 0);
   const int tn = (Np + 15) >> 4;
-  const int mt = blockIdx.x / tn, nt = blockIdx.x - mt * tn;
+  const int mt = blk / tn, nt = blk - mt * tn;
   const int m = mt * 16 + l16, n = nt * 16 + l16;
   const bool mv = m < a.M;
   const bool avec = a.a_mode == kKContig, bvec = a.b_mode == kKContig;
@@ -365,6 +364,21 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
     const int mm = mt * 16 + 4 * kq + r;
     if (mm < a.M && n < Np) epilogue<T>(a, mm, n, v, off, dscale);
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
+  __shared__ float part[4][256];
+  gemm_small_body<T>(a, blockIdx.x, part);
+}
+
+// Two independent small GEMMs in one launch (nn.Linear's backward: dX = dY.W and dW = dY^T.X + the
+// bias gradient read the same dY; as two launches they were two kernel boundaries in a graph)
+template <typename T>
+__global__ void __launch_bounds__(256) gemm_small_pair_kernel(GemmArgs a, GemmArgs b, int tiles_a) {
+  __shared__ float part[4][256];
+  if ((int)blockIdx.x < tiles_a) gemm_small_body<T>(a, blockIdx.x, part);
+  else gemm_small_body<T>(b, blockIdx.x - tiles_a, part);
 }
 
 // Fixed-order sum of the split-K partials + the epilogue.
@@ -437,18 +451,42 @@ int gemm_splits(const GemmArgs& a) {
   return std::max(1, std::min(s, 64));
 }
 
-hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
-  if (in.M <= 0 || in.N <= 0) return hipSuccess;
+static GemmArgs with_modes(const GemmArgs& in) {
   GemmArgs a = in;
   a.a_mode = pick_mode(a.A, a.a_dtype, a.sam, a.sak, a.mfma_dtype);
   a.b_mode = pick_mode(a.B, a.b_dtype, a.sbn, a.sbk, a.mfma_dtype);
   // the gate is loaded with A's mode: it must allow the same vector access
   if (a.G && pick_mode(a.G, a.g_dtype, a.sam, a.sak, a.mfma_dtype) != a.a_mode) a.a_mode = kScalar;
-  const int Np = a.N + (a.rowsum ? 1 : 0);
   if (gemm_small(a)) {
     // (vector fragment loads where the operand is K-contiguous, aligned, in the compute dtype or fp32)
     if (a.a_mode != kKContig) a.a_mode = kScalar;
     if (a.b_mode != kKContig) a.b_mode = kScalar;
+  }
+  return a;
+}
+
+static int small_tiles(const GemmArgs& a) { return cdiv(a.M, 16) * cdiv(a.N + (a.rowsum ? 1 : 0), 16); }
+
+bool gemm_pairable(const GemmArgs& a, const GemmArgs& b) {
+  return a.M > 0 && a.N > 0 && b.M > 0 && b.N > 0 && gemm_small(a) && gemm_small(b) &&
+         a.mfma_dtype == b.mfma_dtype && small_tiles(a) + small_tiles(b) <= 2048;
+}
+
+hipError_t launch_gemm_pair(const GemmArgs& in_a, const GemmArgs& in_b, hipStream_t s) {
+  if (!gemm_pairable(in_a, in_b)) return hipErrorInvalidValue;
+  const GemmArgs a = with_modes(in_a), b = with_modes(in_b);
+  const int ta = small_tiles(a);
+  CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
+    hipLaunchKernelGGL(gemm_small_pair_kernel<scalar_t>, dim3(ta + small_tiles(b)), dim3(256), 0, s, a, b, ta);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
+  if (in.M <= 0 || in.N <= 0) return hipSuccess;
+  const GemmArgs a = with_modes(in);
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  if (gemm_small(a)) {
     CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
       hipLaunchKernelGGL(gemm_small_kernel<scalar_t>, dim3(cdiv(a.M, 16) * cdiv(Np, 16)), dim3(256), 0, s, a);
     });

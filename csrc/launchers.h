@@ -45,6 +45,12 @@ hipError_t launch_nll_fwd(const float* logp, const int64_t* target, float* out, 
                           int reduction, int64_t* correct, hipStream_t s);
 hipError_t launch_nll_bwd(const float* gout, const int64_t* target, float* dlogp, int rows, int C,
                           int reduction, hipStream_t s);
+// nll(log_softmax(z)) in one launch: logp[rows, C] (fp32, kept for the backward) and out ([rows]
+// or [1]); backward dz = g * (exp(logp) - onehot(target)) (g / rows for the mean).
+hipError_t launch_lsm_nll_fwd(const void* z, int z_dtype, const int64_t* target, float* logp, float* out, int rows,
+                              int C, int reduction, hipStream_t s);
+hipError_t launch_lsm_nll_bwd(const float* gout, const float* logp, const int64_t* target, void* dz, int dz_dtype,
+                              int rows, int C, int reduction, hipStream_t s);
 
 // ----------------------------------------------------------------- pool ----
 // 2-D max pool (kernel == stride == k) fused with ReLU and an optional
@@ -94,6 +100,10 @@ struct GemmArgs {
 // Number of K splits launch_gemm will use for these shapes (1 = no workspace needed).
 int gemm_splits(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
+// Two independent GEMMs of the small-GEMM path in one launch (nn.Linear's backward); pairable ==
+// both fit that path (few 16 x 16 tiles, K <= 1024) with the same compute dtype.
+bool gemm_pairable(const GemmArgs& a, const GemmArgs& b);
+hipError_t launch_gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s);
 
 // Column sums of a (gated) [rows, cols] matrix -> fp32 out[cols] (fixed order).
 hipError_t launch_colsum(const void* x, int x_dtype, const void* gate, int g_dtype, float gate_scale,
@@ -107,6 +117,12 @@ hipError_t launch_colsum(const void* x, int x_dtype, const void* gate, int g_dty
 //         padding KH-1-p), no bias.
 // pool_k > 0 fuses maxpool(k)+relu(+chscale) into the epilogue (mode 0 only):
 //   y becomes the pooled output and idx the argmax within each window.
+// chscale_out (mode 0 with pool_k, no chscale): Dropout2d drawn in the epilogue -- per-(n, oc)
+//   scale keep(seed, offset(+offset_dev), n*OC + oc, drop_p) / (1 - drop_p), the draw of
+//   launch_channel_mask -- applied and written to chscale_out[N*OC] for the backward.
+// pidx / pout / pscale (mode 1): x is given max-pooled ([N, IC, H/2, W/2]: the gradient of a
+//   pool-fused forward) and is expanded on load with the forward's argmax bytes, pooled output
+//   (ReLU gate) and channel scale -- maxpool_relu_bwd fused into the staging.
 struct ConvArgs {
   const void* x; int x_dtype;
   const float* w; const float* bias;
@@ -115,8 +131,26 @@ struct ConvArgs {
   int N, IC, H, W, OC, KH, KW, pad;
   int mode;
   int mfma_dtype;
+  float drop_p; uint64_t seed, offset; const int64_t* offset_dev; float* chscale_out;
+  const uint8_t* pidx; const void* pout; const float* pscale;
 };
 hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s);
+// Backward of y = conv(x, w, b, pad) [+ maxpool2 + relu + channel scale]: the weight / bias
+// gradient (partials + fixed-order reduce, as launch_conv2d_wgrad) and, with dx set, the data
+// gradient, in one launch (+ the reduce).  With pidx set, dy is the gradient of the POOLED output
+// [N, OC, OH/2, OW/2] and pidx / pout / pscale are the forward's argmax bytes, pooled output and
+// channel scale (dL/dconv is never materialised).
+struct ConvBwdArgs {
+  const void* x; int x_dtype;
+  const void* dy; int dy_dtype;
+  const uint8_t* pidx; const void* pout; const float* pscale;
+  const float* w;
+  float* dw; float* db; float* ws; float beta;
+  void* dx; int dx_dtype;
+  int N, IC, H, W, OC, KH, KW, pad;
+  int mfma_dtype;
+};
+hipError_t launch_conv2d_bwd(const ConvBwdArgs& a, hipStream_t s);
 // Weight gradient: dW[OC, IC*KH*KW] (fp32) and db[OC] (fp32, optional) of a
 // stride-1 conv; dY may be given gated (dY *= (G > 0) * gs is NOT applied
 // here -- pass the already-unpooled gradient).  `ws` is a workspace of at

@@ -1,0 +1,157 @@
+"""The modular step's fused launches against their unfused equivalents (bitwise where the same
+arithmetic runs) and against a plain PyTorch fp32 reference:
+
+* conv2d_bwd: dW, db and dX of a pool-fused conv in ONE launch, the pooled gradient expanded in
+  the kernels' staging == maxpool_relu_bwd + conv2d_wgrad + conv2d_dgrad (bitwise);
+* conv2d_fwd with the Dropout2d mask drawn in its epilogue == channel_mask + conv2d_fwd (bitwise);
+* linear_bwd: dX and dW (+ db) in one launch == the two gemm launches (bitwise);
+* log_softmax_nll: one kernel each way == torch's log_softmax + nll_loss in fp32.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from csed_514_project_distributed_training_using_pytorch_amd import ops
+from csed_514_project_distributed_training_using_pytorch_amd.ops import _native
+from csed_514_project_distributed_training_using_pytorch_amd.ops.functional import wgrad_workspace_elems
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MF = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_loaded():
+    _native.require()
+    yield
+
+
+def _pooled_fwd(x, w, b, dt, scale):
+    N, OC = x.shape[0], w.shape[0]
+    OH, OW = x.shape[2] - w.shape[2] + 1, x.shape[3] - w.shape[3] + 1
+    y = torch.empty(N, OC, OH // 2, OW // 2, device=DEV, dtype=dt)
+    idx = torch.empty(y.shape, device=DEV, dtype=torch.uint8)
+    _native.ops().conv2d_fwd(x, w, b, y, 0, idx, scale, 2, MF[dt])
+    return y, idx
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("shape,with_dx", [((64, 10, 12, 12, 20), True), ((5, 1, 28, 28, 10), False),
+                                           ((3, 4, 10, 14, 16), True)])
+def test_conv_bwd_pooled_matches_unfused_bitwise(dt, shape, with_dx):
+    N, C, H, W, OC = shape
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g).to(dt)
+    w = torch.randn(OC, C, 5, 5, device=DEV, generator=g) * 0.2
+    b = torch.randn(OC, device=DEV, generator=g) * 0.1
+    scale = (torch.rand(N * OC, device=DEV, generator=g) > 0.5).float() * 2.0
+    y, idx = _pooled_fwd(x, w, b, dt, scale)
+    dy = torch.randn(y.shape, device=DEV, generator=g).to(dt)
+    ws = torch.empty(wgrad_workspace_elems(N, C, 5, 5, OC), device=DEV)
+    o = _native.ops()
+    # fused: one launch (+ reduce), pooled dy expanded on load
+    dw1, db1 = torch.empty_like(w), torch.empty_like(b)
+    dx1 = torch.empty_like(x) if with_dx else None
+    o.conv2d_bwd(x, dy, w, dw1, db1, ws, dx1, 0, idx, y, scale, MF[dt])
+    # unfused: dL/dconv materialised, then the weight and data gradients
+    dconv = torch.empty(N, OC, H - 4, W - 4, device=DEV, dtype=dt)
+    o.maxpool_relu_bwd(dy, y, idx, scale, dconv, 2)
+    dw2, db2 = torch.empty_like(w), torch.empty_like(b)
+    o.conv2d_wgrad(x, dconv, dw2, db2, ws, 0, MF[dt], 0.0)
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    if with_dx:
+        dx2 = torch.empty_like(x)
+        o.conv2d_dgrad(dconv, w, dx2, 0, MF[dt])
+        assert torch.equal(dx1, dx2)
+    # and the fp32 reference of the whole thing
+    xr, wr, br = (t.detach().float().cpu().requires_grad_(True) for t in (x, w, b))
+    c = F.conv2d(xr, wr, br) * scale.cpu().view(N, OC, 1, 1)
+    yr = F.relu(F.max_pool2d(c, 2))
+    yr.backward(dy.float().cpu())
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    for got, ref, name in ((dw1, wr.grad, "dw"), (db1, br.grad, "db")) + (((dx1, xr.grad, "dx"),) if with_dx else ()):
+        err = (got.float().cpu() - ref).abs().max().item()
+        assert err <= tol * max(ref.abs().max().item(), 1e-6), f"{name}: {err:.3e}"
+
+
+def test_conv_fwd_in_kernel_dropout2d_matches_channel_mask():
+    N, C, OC = 64, 10, 20
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(N, C, 12, 12, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(OC, C, 5, 5, device=DEV, generator=g) * 0.2
+    b = torch.randn(OC, device=DEV, generator=g) * 0.1
+    off_dev = torch.tensor([5], device=DEV, dtype=torch.long)
+    o = _native.ops()
+    sc_ref = torch.empty(N * OC, device=DEV)
+    o.channel_mask(sc_ref, 0.5, 1234, 7, off_dev)
+    y_ref, idx_ref = _pooled_fwd(x, w, b, torch.bfloat16, sc_ref)
+    y = torch.empty_like(y_ref)
+    idx = torch.empty_like(idx_ref)
+    sc = torch.full((N * OC,), -1.0, device=DEV)
+    o.conv2d_fwd(x, w, b, y, 0, idx, None, 2, 1, 0.5, 1234, 7, off_dev, sc)
+    assert torch.equal(sc, sc_ref)
+    assert torch.equal(y, y_ref) and torch.equal(idx, idx_ref)
+    assert 0.3 < (sc_ref == 0).float().mean().item() < 0.7
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("act,mio", [(2, (64, 50, 320)), (0, (64, 10, 50)), (1, (37, 70, 45)), (0, (512, 10, 50))])
+def test_linear_bwd_pair_matches_two_gemms(dt, act, mio):
+    M, O, I = mio
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(M, I, device=DEV, generator=g).to(dt)
+    w = torch.randn(O, I, device=DEV, generator=g) * 0.1
+    dy = torch.randn(M, O, device=DEV, generator=g).to(dt if act else torch.float32)
+    gate = torch.randn(M, O, device=DEV, generator=g).to(dt) if act else None
+    gs = 2.0 if act == 2 else 1.0
+    o = _native.ops()
+    dx1, dw1, db1 = torch.empty_like(x), torch.empty_like(w), torch.empty(O, device=DEV)
+    o.linear_bwd(dy, x, w, gate, gs, dx1, dw1, db1, MF[dt])
+    dx2, dw2, db2 = torch.empty_like(x), torch.empty_like(w), torch.empty(O, device=DEV)
+    o.gemm(dy, w, dx2, None, 1.0, 0.0, 0, 0.0, 0, 0, None, gate, gs, MF[dt])
+    o.gemm(dy.t(), x, dw2, None, 1.0, 0.0, 0, 0.0, 0, 0, None, gate.t() if gate is not None else None, gs, MF[dt], db2)
+    assert torch.equal(dx1, dx2) and torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    # fp32 reference
+    d = dy.float() if gate is None else torch.where(gate.float() > 0, dy.float() * gs, torch.zeros_like(dy.float()))
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    for got, ref in ((dx1, d @ w.to(dt).float()), (dw1, d.t() @ x.float()), (db1, d.sum(0))):
+        assert (got.float() - ref).abs().max().item() <= tol * max(ref.abs().max().item(), 1e-6)
+
+
+@pytest.mark.parametrize("red", ["mean", "sum", "none"])
+@pytest.mark.parametrize("rows", [64, 8, 1000])
+def test_log_softmax_nll_matches_torch(red, rows):
+    g = torch.Generator(device=DEV).manual_seed(6)
+    z = (torch.randn(rows, 10, device=DEV, generator=g) * 3).requires_grad_(True)
+    t = torch.randint(0, 10, (rows,), device=DEV, generator=g)
+    loss = ops.log_softmax_nll(z, t, red)
+    zr = z.detach().cpu().double().requires_grad_(True)
+    lr = F.nll_loss(F.log_softmax(zr, 1), t.cpu(), reduction=red)
+    assert torch.allclose(loss.detach().cpu().double(), lr.detach(), rtol=2e-6, atol=1e-6)
+    gout = torch.randn(loss.shape, device=DEV, generator=g)
+    loss.backward(gout)
+    lr.backward(gout.cpu().double())
+    assert torch.allclose(z.grad.cpu().double(), zr.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_net_logits_path_matches_log_probs_path():
+    """The modular engine's fused loss on Net's logits == nll_loss on Net's log-probs (same masks)."""
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+    ops.rng.default_state.reset_offset()
+    torch.manual_seed(1)
+    net = Net().to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.rand(64, 1, 28, 28, device=DEV, generator=g)
+    t = torch.randint(0, 10, (64,), device=DEV, generator=g)
+    grads = []
+    for fused in (True, False):
+        ops.rng.default_state.reset_offset()
+        net.zero_grad(set_to_none=True)
+        loss = ops.log_softmax_nll(net(x, return_logits=True), t) if fused else ops.nll_loss(net(x), t)
+        loss.backward()
+        grads.append((loss.detach(), [p.grad.clone() for p in net.parameters()]))
+    (l1, g1), (l2, g2) = grads
+    assert torch.allclose(l1, l2, rtol=1e-6, atol=1e-6)
+    for a, b in zip(g1, g2):
+        assert (a - b).abs().max().item() <= 1e-2 * max(b.abs().max().item(), 1e-6)

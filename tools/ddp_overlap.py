@@ -34,9 +34,12 @@ def _modes():
             ("overlap", 0.01, True), ("serial", 0.01, False)]
 
 
-def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(False, True)) -> list[dict]:
+def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(False, True),
+        loader: bool = False) -> list[dict]:
     """Step times of the modular engine (engine/modular.py ModularTrainer: its DDP reducer, fused
-    SGD, and -- graph=True -- one HIP-graph replay per step) per reducer mode."""
+    SGD, and -- graph=True -- one HIP-graph replay per step) per reducer mode.  ``loader``: each
+    step also gathers a new shuffled batch (data/loader.py DeviceLoader bound to the trainer, i.e.
+    the CLI's loop) instead of replaying one fixed batch."""
     import contextlib
     import types
 
@@ -67,9 +70,25 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(Fal
                                 overlap=overlap)
             tr.ddp.world_size = 2  # force the collective path (see the module docstring)
 
+            batches = None
+            if loader:
+                from csed_514_project_distributed_training_using_pytorch_amd.data import synthetic_mnist
+                from csed_514_project_distributed_training_using_pytorch_amd.data.loader import DeviceLoader
+
+                dl = DeviceLoader(synthetic_mnist(max(64 * batch, 8192), seed=0), batch, shuffle=True, device=dev,
+                                  dtype=ops.compute_dtype(), drop_last=True)
+                tr.bind_loader(dl)
+
+                def batches_forever():
+                    while True:
+                        yield from dl
+
+                batches = batches_forever()
+
             def step():
+                xb, tb = next(batches) if batches is not None else (x, t)
                 with tr.ddp.no_sync() if mode == "nocomm" else contextlib.nullcontext():
-                    tr.train_batch(x, t, clone_loss=False)
+                    tr.train_batch(xb, tb, clone_loss=False)
 
             for _ in range(warmup):
                 step()
@@ -82,7 +101,7 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(Fal
             e1.record()
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / steps
-            rows.append({"mode": mode, "graph": graph and tr.use_graph, "batch": batch, "bucket_mb": cap,
+            rows.append({"mode": mode, "graph": graph and tr.use_graph, "batch": batch, "loader": loader, "bucket_mb": cap,
                          "buckets": len(tr.ddp.buckets),
                          "us_per_step_gpu": round(e0.elapsed_time(e1) * 1000 / steps, 2),
                          "us_per_step_wall": round(wall * 1e6, 2)})
@@ -133,6 +152,7 @@ def main() -> None:
     ap.add_argument("--bucket-mb", type=float, default=0.01, help="--trace: bucket cap")
     ap.add_argument("--parse", help="run_kernel_trace.csv of a --trace run")
     ap.add_argument("--graph", choices=["both", "eager", "graph"], default="both")
+    ap.add_argument("--loader", action="store_true", help="gather a new batch per step (bound DeviceLoader)")
     a = ap.parse_args()
     if a.parse:
         print(json.dumps(parse(a.parse)))
@@ -141,7 +161,7 @@ def main() -> None:
     if a.trace:
         a.steps, a.warmup, only = 20, 5, (a.mode, a.bucket_mb)
     graphs = {"both": (False, True), "eager": (False,), "graph": (True,)}[a.graph]
-    for r in run(a.batch, a.steps, a.warmup, a.trace, only, graphs):
+    for r in run(a.batch, a.steps, a.warmup, a.trace, only, graphs, a.loader):
         print(json.dumps(r), flush=True)
 
 

@@ -17,6 +17,7 @@
 #             gaps, lenet_update FC / CONV roles at B = 1024 and 8192
 #   pmc       three rocprofv3 --pmc passes over the train kernel (B=64), one over B=8,
 #             and three over the tile kernel (B=1024)
+#   modular   the modular engine: fusion + op tests, graph step times (B = 64), a kernel trace
 #   ddp       tools/ddp_overlap.py: the modular engine's bucketed reducer, per-bucket all-reduce on the
 #             comm stream vs after backward, step times + overlap share from kernel traces
 #   ab        same-box A/B of ab/A_C.so vs ab/B_C.so (tools/ab_build.sh REV) at global batch
@@ -83,6 +84,16 @@ task_exchange() {
 
 task_tiletrace() {
   cd $R && py 300 python -u tools/exchange_trace.py --batch 1024 8192 --worlds 1 --steps 16 > $O/${T}_tiletrace.log 2>&1
+}
+
+task_modular() {  # the modular (per-op) engine: fusion / op tests, graph step times at B = 64, a kernel trace
+  cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_kernels_gpu.py tests/test_modular_graph_gpu.py \
+    tests/test_dropout_pin_gpu.py tests/test_fused_gpu.py tests/test_kernels_f32_gpu.py tests/test_engine_gpu.py \
+    -x -v --timeout 200 --timeout-method thread > $O/${T}_modtests.log 2>&1 && \
+  py 200 python -u tools/ddp_overlap.py --graph graph --steps 500 > $O/${T}_modddp.log 2>&1 && \
+  py 200 python -u tools/ddp_overlap.py --graph graph --steps 500 --loader >> $O/${T}_modddp.log 2>&1 && \
+  cd /tmp && export TMPDIR=/tmp && \
+  py 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_modkt -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt.log 2>&1
 }
 
 task_ddp() {  # the modular engine's bucketed reducer: step times per mode + overlap from kernel traces
