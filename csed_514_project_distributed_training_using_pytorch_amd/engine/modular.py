@@ -60,7 +60,7 @@ class ModularTrainer:
             for i, p in enumerate(self.flat.params):  # backward kernels write into the flat gradient
                 ops.set_grad_destination(p, self.flat.grad_view(i))
         self.loss_name = loss
-        self._logits = self.opt.on_gpu and loss in ("nll", "ce") and getattr(model, "returns_logits", False)
+        self._fused_head = self.opt.on_gpu and loss in ("nll", "ce") and getattr(model, "fused_loss_head", False)
         gloo = self.distributed and getattr(ctx, "backend", None) != "nccl"
         self.use_graph = bool(graph) and self.opt.on_gpu and not gloo
         self._graphs: dict[tuple, tuple] = {}  # input shapes -> (graph, static x, static target, static loss)
@@ -72,13 +72,12 @@ class ModularTrainer:
         return ops.nll_loss(out, target)
 
     def _forward_loss(self, x, target):
-        """The model's output and the loss.  A model whose forward ends in log_softmax and can
-        return its logits (``returns_logits``, e.g. ``Net``) gets the loss as ONE fused
-        log_softmax + NLL op on the logits: nll(log_softmax(z)) for 'nll', and for 'ce' the same
-        value (CrossEntropyLoss on log-probs re-applies an idempotent log_softmax)."""
-        if self._logits:
-            z = self.forward(x, return_logits=True)
-            return z, ops.log_softmax_nll(z, target)
+        """The model's output and the loss.  A model whose forward ends in log_softmax and takes
+        the targets (``fused_loss_head``, e.g. ``Net``) returns the mean NLL itself, computed by its
+        fused classifier-head + loss op: nll(log_softmax(z)) for 'nll', and for 'ce' the same value
+        (CrossEntropyLoss on log-probs re-applies an idempotent log_softmax)."""
+        if self._fused_head:
+            return None, self.forward(x, target=target)
         out = self.forward(x)
         return out, self.loss_fn(out, target)
 

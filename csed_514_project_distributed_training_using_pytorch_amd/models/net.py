@@ -13,6 +13,8 @@ The GPU forward is five fused HIP kernels instead of ~15 ATen ops:
     fc2 + bias                                  (linear, fp32 logits)
     log_softmax                                 (log_softmax)
 
+(with targets: fc2 + log_softmax + NLL as ops.linear_log_softmax_nll, the loss returned)
+
 The CPU forward is the reference forward verbatim in stock PyTorch (the fp32
 oracle used by the tests).
 """
@@ -37,14 +39,15 @@ class Net(nn.Module):
         self.fc1 = nn.Linear(320, 50)
         self.fc2 = nn.Linear(50, 10)
 
-    # the modular engine may ask for the logits and fuse log_softmax into its NLL
-    # (ops.log_softmax_nll: one kernel each way); the module's output stays the log-probs
-    returns_logits = True
+    # the modular engine may hand the targets to forward and get the mean NLL back: the classifier
+    # head + log_softmax + NLL then run as ops.linear_log_softmax_nll (one backward launch for fc2
+    # and the loss); without targets the module's output stays the log-probs
+    fused_loss_head = True
 
-    def forward(self, x: torch.Tensor, return_logits: bool = False) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, target: torch.Tensor | None = None) -> torch.Tensor:
         if not x.is_cuda:
-            out = self.reference_forward(x, log_probs=not return_logits)
-            return out
+            out = self.reference_forward(x)
+            return out if target is None else F.nll_loss(out, target)
         # (the fp32 input is read and converted by conv1's staging: no cast launch)
         x = ops.conv2d_pool_relu(x, self.conv1.weight, self.conv1.bias)
         p2 = self.conv2_drop.p
@@ -53,17 +56,19 @@ class Net(nn.Module):
         x = x.view(-1, 320)
         x = ops.linear(x, self.fc1.weight, self.fc1.bias,
                        act="relu_dropout" if self.training else "relu", p=0.5)
+        if target is not None:
+            return ops.linear_log_softmax_nll(x, self.fc2.weight, self.fc2.bias, target)
         x = ops.linear(x, self.fc2.weight, self.fc2.bias, out_dtype=torch.float32)
-        return x if return_logits else ops.log_softmax(x, dim=1)
+        return ops.log_softmax(x, dim=1)
 
-    def reference_forward(self, x: torch.Tensor, log_probs: bool = True) -> torch.Tensor:
+    def reference_forward(self, x: torch.Tensor) -> torch.Tensor:
         x = F.relu(F.max_pool2d(self.conv1(x), 2))
         x = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(x)), 2))
         x = x.view(-1, 320)
         x = F.relu(self.fc1(x))
         x = F.dropout(x, training=self.training)
         x = self.fc2(x)
-        return F.log_softmax(x, dim=1) if log_probs else x
+        return F.log_softmax(x, dim=1)
 
 
 PARAM_SHAPES = [

@@ -416,6 +416,50 @@ def log_softmax_nll(z, target, reduction: str = "mean"):
     return _LogSoftmaxNLL.apply(z, target, _RED[reduction])
 
 
+class _LinearLogSoftmaxNLL(torch.autograd.Function):
+    """nll(log_softmax(x W^T + b)): the GEMM, then one log_softmax + NLL kernel; the backward is ONE
+    paired launch whose GEMMs read dz = g * (exp(logp) - onehot) straight from the kept log-probs
+    (no dz tensor, no separate loss-backward kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, target, reduction):
+        x2 = x.contiguous()
+        z = torch.empty((x2.shape[0], w.shape[0]), device=x.device, dtype=torch.float32)
+        _ops().gemm(x2, w.t(), z, b, 1.0, 0.0, 0, 0.0, 0, 0, None, None, 1.0, _mfma())
+        target = target.contiguous().long()
+        logp = torch.empty(z.shape, device=z.device, dtype=torch.float32)
+        out = torch.empty((), device=z.device, dtype=torch.float32)
+        _ops().lsm_nll_fwd(z, target, logp, out, reduction)
+        ctx.save_for_backward(x2, w, logp, target)
+        ctx.reduction, ctx.has_bias, ctx.bias_param = reduction, b is not None, b
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x2, w, logp, target = ctx.saved_tensors
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw = _grad_buffer(w, w.shape, w.device)
+            if ctx.has_bias:
+                db = _grad_buffer(ctx.bias_param, (w.shape[0],), w.device)
+        div = float(logp.shape[0]) if ctx.reduction == 1 else 1.0
+        _ops().linear_bwd(logp, x2, w, None, 1.0, dx, dw, db, _mfma(), target, gout.contiguous().float(), div)
+        return dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None, None, None
+
+
+def linear_log_softmax_nll(x, weight, bias, target, reduction: str = "mean"):
+    """nll_loss(log_softmax(linear(x, weight, bias), 1), target) -- a classifier head and its loss
+    (ref src/model.py:21-22 + src/train.py:74) as one forward GEMM + one loss kernel and ONE backward
+    launch.  reduction: 'mean' or 'sum'."""
+    if not x.is_cuda:
+        return F.nll_loss(F.log_softmax(F.linear(x, weight, bias), dim=1), target, reduction=reduction)
+    if reduction not in ("mean", "sum"):
+        raise ValueError("linear_log_softmax_nll supports reduction 'mean' or 'sum'")
+    return _LinearLogSoftmaxNLL.apply(x, weight, bias, target, _RED[reduction])
+
+
 def cross_entropy(x, target, reduction: str = "mean"):
     """nn.CrossEntropyLoss: log_softmax then NLL (idempotent on log-probs, ref src/train_dist.py:67)."""
     return log_softmax_nll(x, target, reduction)

@@ -267,7 +267,8 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
 // forward had an activation.  One launch when both GEMMs fit the small-GEMM path.
 void linear_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const optional<Tensor>& gate, double gate_scale,
                 const optional<Tensor>& dx, const optional<Tensor>& dw, const optional<Tensor>& db,
-                int64_t mfma_dtype) {
+                int64_t mfma_dtype, const optional<Tensor>& lsm_target, const optional<Tensor>& lsm_gout,
+                double lsm_div) {
   dev(dy, "dy"); dev(x, "x"); dev(w, "w");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && w.dim() == 2 && dy.size(0) == x.size(0) && w.size(0) == dy.size(1) &&
               w.size(1) == x.size(1), "linear_bwd: shape mismatch");
@@ -284,6 +285,18 @@ void linear_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const option
     dev(*dw, "dw");
     const optional<Tensor> gt = gate.has_value() ? optional<Tensor>(gate->t()) : none;
     todo.push_back(make_gemm(dy.t(), x, *dw, none, 1.0, 0.0, 0, 0.0, 0, 0, none, gt, gate_scale, mfma_dtype, db));
+  }
+  if (lsm_target.has_value()) {  // dy holds the head's log-probs: the GEMMs read d nll(log_softmax) / dz
+    TORCH_CHECK(lsm_gout.has_value() && lsm_gout->numel() == 1 && lsm_gout->scalar_type() == at::kFloat &&
+                    dy.scalar_type() == at::kFloat && !gate.has_value() && lsm_target->scalar_type() == at::kLong &&
+                    lsm_target->numel() == dy.size(0) && lsm_target->is_contiguous(),
+                "linear_bwd: the loss-head form needs fp32 log-probs, int64 targets, a scalar gout, no gate");
+    for (size_t i = 0; i < todo.size(); ++i) {
+      todo[i].lsm_target = lsm_target->data_ptr<int64_t>();
+      todo[i].lsm_gout = lsm_gout->data_ptr<float>();
+      todo[i].lsm_div = (float)lsm_div;
+      todo[i].lsm_rows_are_m = (dx.has_value() && i == 0) ? 1 : 0;
+    }
   }
   if (todo.size() == 2 && csed::gemm_pairable(todo[0], todo[1])) {
     CHECK_HIP(csed::launch_gemm_pair(todo[0], todo[1], cur_stream(dy)));
@@ -723,7 +736,7 @@ TORCH_LIBRARY(csed, m) {
   m.def("conv2d_bwd(Tensor x, Tensor dy, Tensor w, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, Tensor(d!)? dx, "
         "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype) -> ()");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? gate, float gate_scale, Tensor(a!)? dx, Tensor(b!)? dw, "
-        "Tensor(c!)? db, int mfma_dtype) -> ()");
+        "Tensor(c!)? db, int mfma_dtype, Tensor? lsm_target=None, Tensor? lsm_gout=None, float lsm_div=1.0) -> ()");
   m.def("lsm_nll_fwd(Tensor z, Tensor target, Tensor(a!) logp, Tensor(b!) out, int reduction) -> ()");
   m.def("lsm_nll_bwd(Tensor gout, Tensor logp, Tensor target, Tensor(a!) dz, int reduction) -> ()");
   m.def("conv2d_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int pad, int mfma_dtype) -> ()");

@@ -87,6 +87,24 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   const int rows = min(g.TR, g.OH - oh0);
   const int npix = rows * g.OW;
   const int tid = threadIdx.x;
+  const int NT = g.Cop >> 4;
+
+  // ---- epilogue operands of this lane's channels (N-tiles 0..3), loaded / drawn first so their
+  // latency hides under the staging (they were one more dependent round trip at the end)
+  float eb[4], es[4];
+  {
+    const uint64_t off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
+    const float keep_sc = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oc = j * 16 + (tid & 15);
+      const bool ok = j < NT && oc < g.Co;
+      eb[j] = ok && a.bias ? a.bias[oc] : 0.f;
+      es[j] = ok && a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
+      if (a.chscale_out)  // Dropout2d drawn here (channel_mask_kernel's draw: index n*Co+oc)
+        es[j] = ok && dropout_keep(a.seed, off, (uint64_t)n * g.Co + oc, a.drop_p) ? keep_sc : 0.f;
+    }
+  }
 
   // ---- stage weights (fp32 -> 16 bit) and the k -> patch offset table.  A thread keeps its K
   // columns for every oc: the k -> (ic, kh, kw) split (integer divisions) is done once per column,
@@ -99,14 +117,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     // effective weight (oc, ic, kh, kw) = w[base + oc * step] (see weff)
     const int64_t base = a.mode == 0 ? k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
     const int64_t step = a.mode == 0 ? g.K : KHW;
-    // eight loads in flight, then eight LDS stores (a load -> convert -> store chain per element
-    // waited for every load in turn: ~1 us of memory latency each)
-    for (int oc0 = 0; oc0 < g.Cop; oc0 += 8) {  // (Cop: a multiple of 16)
-      float v[8];
+    // up to 32 loads in flight, then their LDS stores (a load -> convert -> store chain per element
+    // waited for every load in turn: ~1 us of memory latency each; batches of 8 were 2-4 rounds)
+    for (int oc0 = 0; oc0 < g.Cop; oc0 += 32) {  // (Cop: a multiple of 16)
+      float v[32];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = kv && oc0 + j < g.Co ? a.w[base + (oc0 + j) * step] : 0.f;
+      for (int j = 0; j < 32; ++j) v[j] = kv && oc0 + j < g.Co ? a.w[base + (oc0 + j) * step] : 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(v[j]);
+      for (int j = 0; j < 32; ++j)
+        if (oc0 + j < g.Cop) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(v[j]);
     }
   }
   // ---- stage the zero-padded input patch: a thread owns one patch column, rows step by
@@ -123,11 +142,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       auto rows = [&](auto tag) {
         typedef decltype(tag) X;
         const X* xs = static_cast<const X*>(a.x);
-        while (rr < nrows) {  // eight rows' loads in flight, then their LDS stores
-          float v[8];
-          int at[8];
+        while (rr < nrows) {  // sixteen rows' loads in flight, then their LDS stores
+          float v[16];
+          int at[16];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
+          for (int j = 0; j < 16; ++j) {
             const int ih = oh0 - g.pad + pr;
             at[j] = rr < nrows ? rr : -1;
             v[j] = (rr < nrows && colv && ih >= 0 && ih < g.H) ? (float)xs[xbase + ((int64_t)ic * g.H + ih) * g.W + iw]
@@ -140,11 +159,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
             }
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
+          for (int j = 0; j < 16; ++j)
             if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(v[j]);
         }
       };
-      // pooled input (the gradient of a pool-fused forward): eight rows' value / argmax / gate /
+      // pooled input (the gradient of a pool-fused forward): sixteen rows' value / argmax / gate /
       // scale loads in flight, expanded in registers
       auto prows = [&](auto tag) {
         typedef decltype(tag) X;
@@ -152,11 +171,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
         const X* ys = static_cast<const X*>(a.pout);
         const int64_t nc0 = (int64_t)n * g.Ci;
         while (rr < nrows) {
-          float v[8], yo[8], sc[8];
-          uint8_t bi[8];
-          int at[8], sel[8];
+          float v[16], yo[16], sc[16];
+          uint8_t bi[16];
+          int at[16], sel[16];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
+          for (int j = 0; j < 16; ++j) {
             const int ih = oh0 - g.pad + pr;
             const bool ok = rr < nrows && colv && ih >= 0 && ih < g.H;
             at[j] = rr < nrows ? rr : -1;
@@ -174,7 +193,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
             }
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
+          for (int j = 0; j < 16; ++j)
             if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], sel[j]));
         }
       };
@@ -193,7 +212,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   const int mtiles = (npix + 15) >> 4;
   const int pooled = a.pool_k == 2;
   const int PWb = g.OW >> 1;
-  const int NT = g.Cop >> 4;
   for (int mt = wave; mt < mtiles; mt += 4) {
     // pixel owned by this lane as an A row
     const int m = mt * 16 + (lane & 15);
@@ -242,7 +260,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
         if (nc + j >= NT) continue;
         const int oc = (nc + j) * 16 + (lane & 15);
         if (oc >= g.Co) continue;
-        const float b = a.bias ? a.bias[oc] : 0.f;
+        const float b = nc == 0 ? eb[j] : (a.bias ? a.bias[oc] : 0.f);
         if (pooled) {
           const int wbase = mt * 16 + 4 * (lane >> 4);  // first pixel of this lane's window
           if (wbase >= npix) continue;
@@ -254,15 +272,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
           const int p = wbase >> 2;
           const int ph = (oh0 >> 1) + p / PWb, pw = p % PWb;
           const int PH = g.OH >> 1;
-          float sc = 1.f;
-          if (a.chscale) {
-            sc = a.chscale[(int64_t)n * g.Co + oc];
-          } else if (a.chscale_out) {  // Dropout2d drawn here (channel_mask_kernel's draw: index n*Co+oc)
-            sc = dropout_keep(a.seed, rng_offset(a.offset, a.offset_dev), (uint64_t)n * g.Co + oc, a.drop_p)
-                     ? (a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f)
-                     : 0.f;
-            if (band == 0 && wbase == 0) a.chscale_out[(int64_t)n * g.Co + oc] = sc;  // once per (n, oc)
+          float sc = es[j];
+          if (nc != 0) {  // (channels past the first 64: operands not preloaded)
+            sc = a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
+            if (a.chscale_out)
+              sc = dropout_keep(a.seed, rng_offset(a.offset, a.offset_dev), (uint64_t)n * g.Co + oc, a.drop_p)
+                       ? (a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f)
+                       : 0.f;
           }
+          if (a.chscale_out && band == 0 && wbase == 0) a.chscale_out[(int64_t)n * g.Co + oc] = sc;  // once per (n, oc)
           const float v = fmaxf(best + b, 0.f) * sc;
           const int64_t o = (((int64_t)n * g.Co + oc) * PH + ph) * PWb + pw;
           stf(a.y, a.y_dtype, o, v);
@@ -390,11 +408,16 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
     }
     const int64_t yb = (int64_t)n * g.Co * g.npix;
-    auto dyrows = [&](auto tag) {  // a thread keeps its pixel for every oc, 8 loads in flight
+    // dy staging spread over the whole block: pst threads per pixel row, 256 / pst channel groups
+    // of 8 side by side (a small image's 64 pixels kept 3/4 of the block idle and ran its channels
+    // as 4 serial rounds of loads)
+    const int pst = min(g.npp, 256), ocg = 256 / pst, p0 = tid % pst, og = tid / pst;
+    auto dyrows = [&](auto tag) {  // a thread keeps its pixel for its channel groups, 8 loads in flight
       typedef decltype(tag) X;
       const X* ys = static_cast<const X*>(dy);
-      for (int p = tid; p < g.npp; p += 256)
-        for (int oc0 = 0; oc0 < g.Cop; oc0 += 8) {
+      if (og >= ocg) return;
+      for (int p = p0; p < g.npp; p += pst)
+        for (int oc0 = og * 8; oc0 < g.Cop; oc0 += ocg * 8) {
           float v[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j)
@@ -403,19 +426,20 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
           for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(v[j]);
         }
     };
-    // pooled dy: a thread keeps its pixel's window position for every oc; value / argmax / gate /
-    // scale loads of 8 channels in flight, expanded in registers
+    // pooled dy: a thread keeps its pixel's window position for its channel groups; value / argmax
+    // / gate / scale loads of 8 channels in flight, expanded in registers
     auto pdyrows = [&](auto tag) {
       typedef decltype(tag) X;
       const X* ys = static_cast<const X*>(dy);
       const X* os = static_cast<const X*>(wa.pout);
       const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
       const int64_t ybp = (int64_t)n * g.Co * npixp;
-      for (int p = tid; p < g.npp; p += 256) {
+      if (og >= ocg) return;
+      for (int p = p0; p < g.npp; p += pst) {
         const bool pv = p < g.npix;
         const int oh = pv ? p / g.OW : 0, ow = pv ? p - oh * g.OW : 0;
         const int sel = ((oh & 1) << 1) | (ow & 1), q = (oh >> 1) * PWp + (ow >> 1);
-        for (int oc0 = 0; oc0 < g.Cop; oc0 += 8) {
+        for (int oc0 = og * 8; oc0 < g.Cop; oc0 += ocg * 8) {
           float v[8], yo[8], sc[8];
           uint8_t bi[8];
 #pragma unroll

@@ -321,12 +321,16 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
   const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the loss head's dz (a.lsm_target): the scalar upstream gradient, loaded once
+  const float lsm_g = a.lsm_target ? a.lsm_gout[0] / a.lsm_div : 0.f;
   for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
     float fa[4][8], fb[4][8], fg[4][8];
+    int nku[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int kb = (kb0 + u) * 32 + 8 * kq;
       const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
+      nku[u] = nk;
       const int kc = min(kb, a.K - 1);
       gather8<T>(fa[u], a.A, a.a_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak, a.sak, mv ? nk : 0,
                  avec);
@@ -338,6 +342,19 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) fb[u][j] = (n == a.N && j < nk) ? 1.f : 0.f;  // the ones column / padding
+      }
+    }
+    if (a.lsm_target) {  // log-probs -> dz = g * (exp(logp) - onehot(target)) (lsm_nll_bwd_kernel's rule)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kb = (kb0 + u) * 32 + 8 * kq;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool in = mv && j < nku[u];
+          const int r = a.lsm_rows_are_m ? m : kb + j, c = a.lsm_rows_are_m ? kb + j : m;
+          const int64_t t = in ? a.lsm_target[r] : -1;
+          fa[u][j] = in ? lsm_g * (__expf(fa[u][j]) - (c == t ? 1.f : 0.f)) : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -474,6 +491,8 @@ bool gemm_pairable(const GemmArgs& a, const GemmArgs& b) {
 
 hipError_t launch_gemm_pair(const GemmArgs& in_a, const GemmArgs& in_b, hipStream_t s) {
   if (!gemm_pairable(in_a, in_b)) return hipErrorInvalidValue;
+  for (const GemmArgs* g : {&in_a, &in_b})
+    if (g->lsm_target && (g->a_dtype != kF32 || g->G)) return hipErrorInvalidValue;
   const GemmArgs a = with_modes(in_a), b = with_modes(in_b);
   const int ta = small_tiles(a);
   CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
@@ -484,6 +503,7 @@ hipError_t launch_gemm_pair(const GemmArgs& in_a, const GemmArgs& in_b, hipStrea
 
 hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
   if (in.M <= 0 || in.N <= 0) return hipSuccess;
+  if (in.lsm_target && (!gemm_small(in) || in.a_dtype != kF32 || in.G)) return hipErrorInvalidValue;
   const GemmArgs a = with_modes(in);
   const int Np = a.N + (a.rowsum ? 1 : 0);
   if (gemm_small(a)) {

@@ -96,6 +96,10 @@ struct GemmArgs {
   float* rowsum;      // optional [M]: alpha * sum_k A(m,k) (bias gradient via a ones column of B)
   float* ws;          // optional split-K workspace, >= gemm_splits(a) * M * (N + (rowsum != 0)) floats
   int a_mode, b_mode; // set by launch_gemm (operand staging modes)
+  // optional (small-GEMM path): A holds fp32 log-probs logp[rows, C] and the GEMM reads the gradient
+  // of nll(log_softmax(z)) instead, dz[r][c] = (gout[0] / lsm_div) * (exp(logp[r][c]) - (c == target[r]))
+  // -- lsm_rows_are_m: A(m, k) = dz[m][k] (dX of the head), else A(m, k) = dz[k][m] (its dW)
+  const int64_t* lsm_target; const float* lsm_gout; float lsm_div; int lsm_rows_are_m;
 };
 // Number of K splits launch_gemm will use for these shapes (1 = no workspace needed).
 int gemm_splits(const GemmArgs& a);

@@ -5,7 +5,9 @@ arithmetic runs) and against a plain PyTorch fp32 reference:
   the kernels' staging == maxpool_relu_bwd + conv2d_wgrad + conv2d_dgrad (bitwise);
 * conv2d_fwd with the Dropout2d mask drawn in its epilogue == channel_mask + conv2d_fwd (bitwise);
 * linear_bwd: dX and dW (+ db) in one launch == the two gemm launches (bitwise);
-* log_softmax_nll: one kernel each way == torch's log_softmax + nll_loss in fp32.
+* log_softmax_nll: one kernel each way == torch's log_softmax + nll_loss in fp32;
+* the classifier head + loss (linear_log_softmax_nll): its backward GEMMs read dz from the kept
+  log-probs == lsm_nll_bwd + linear_bwd (bitwise), and Net's fused head == its log-probs + nll_loss.
 """
 import pytest
 import torch
@@ -134,11 +136,31 @@ def test_log_softmax_nll_matches_torch(red, rows):
     assert torch.allclose(z.grad.cpu().double(), zr.grad, rtol=1e-5, atol=1e-7)
 
 
-def test_net_logits_path_matches_log_probs_path():
-    """The modular engine's fused loss on Net's logits == nll_loss on Net's log-probs (same masks)."""
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("red", [1, 2])
+def test_loss_head_backward_matches_unfused_bitwise(dt, red):
+    """linear_bwd reading dz from the log-probs == lsm_nll_bwd's dz fed to linear_bwd."""
+    B, C, I = 64, 10, 50
+    g = torch.Generator(device=DEV).manual_seed(8)
+    h = torch.randn(B, I, device=DEV, generator=g).to(dt)
+    w = torch.randn(C, I, device=DEV, generator=g) * 0.1
+    logp = torch.log_softmax(torch.randn(B, C, device=DEV, generator=g) * 2, 1)
+    t = torch.randint(0, C, (B,), device=DEV, generator=g)
+    gout = torch.tensor(1.7, device=DEV)
+    o = _native.ops()
+    dx1, dw1, db1 = torch.empty_like(h), torch.empty_like(w), torch.empty(C, device=DEV)
+    o.linear_bwd(logp, h, w, None, 1.0, dx1, dw1, db1, MF[dt], t, gout, float(B) if red == 1 else 1.0)
+    dz = torch.empty(B, C, device=DEV)
+    o.lsm_nll_bwd(gout, logp, t, dz, red)
+    dx2, dw2, db2 = torch.empty_like(h), torch.empty_like(w), torch.empty(C, device=DEV)
+    o.linear_bwd(dz, h, w, None, 1.0, dx2, dw2, db2, MF[dt])
+    assert torch.equal(dx1, dx2) and torch.equal(dw1, dw2) and torch.equal(db1, db2)
+
+
+def test_net_fused_head_matches_log_probs_path():
+    """Net's fused classifier head + loss (what the modular engine runs) == nll_loss on its log-probs."""
     from csed_514_project_distributed_training_using_pytorch_amd.models import Net
 
-    ops.rng.default_state.reset_offset()
     torch.manual_seed(1)
     net = Net().to(DEV).train()
     g = torch.Generator(device=DEV).manual_seed(7)
@@ -146,9 +168,9 @@ def test_net_logits_path_matches_log_probs_path():
     t = torch.randint(0, 10, (64,), device=DEV, generator=g)
     grads = []
     for fused in (True, False):
-        ops.rng.default_state.reset_offset()
+        ops.rng.default_state.reset_offset()  # (the same dropout masks in both passes)
         net.zero_grad(set_to_none=True)
-        loss = ops.log_softmax_nll(net(x, return_logits=True), t) if fused else ops.nll_loss(net(x), t)
+        loss = net(x, target=t) if fused else ops.nll_loss(net(x), t)
         loss.backward()
         grads.append((loss.detach(), [p.grad.clone() for p in net.parameters()]))
     (l1, g1), (l2, g2) = grads
