@@ -426,34 +426,45 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
           for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(v[j]);
         }
     };
-    // pooled dy: a thread keeps its pixel's window position for its channel groups; value / argmax
-    // / gate / scale loads of 8 channels in flight, expanded in registers
+    // pooled dy: a thread owns one pooling window of 16 channels (value / argmax / gate / scale
+    // loads of all 16 in flight) and writes the window's 4 pixels, one of them nonzero; the padding
+    // pixels past npix are zeroed separately
     auto pdyrows = [&](auto tag) {
       typedef decltype(tag) X;
       const X* ys = static_cast<const X*>(dy);
       const X* os = static_cast<const X*>(wa.pout);
       const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
       const int64_t ybp = (int64_t)n * g.Co * npixp;
-      if (og >= ocg) return;
-      for (int p = p0; p < g.npp; p += pst) {
-        const bool pv = p < g.npix;
-        const int oh = pv ? p / g.OW : 0, ow = pv ? p - oh * g.OW : 0;
-        const int sel = ((oh & 1) << 1) | (ow & 1), q = (oh >> 1) * PWp + (ow >> 1);
-        for (int oc0 = og * 8; oc0 < g.Cop; oc0 += ocg * 8) {
-          float v[8], yo[8], sc[8];
-          uint8_t bi[8];
+      const int wst = min(npixp, 256), wg = 256 / wst, q0 = tid % wst, gq = tid / wst;
+      if (gq < wg) {
+        for (int q = q0; q < npixp; q += wst) {
+          const int ph = q / PWp, pw = q - ph * PWp;
+          const int pbase = 2 * ph * g.OW + 2 * pw;
+          for (int oc0 = gq * 16; oc0 < g.Cop; oc0 += wg * 16) {
+            float v[16], yo[16], sc[16];
+            uint8_t bi[16];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const bool ok = oc0 + j < g.Co && pv;
-            const int64_t po = ok ? ybp + (int64_t)(oc0 + j) * npixp + q : 0;
-            v[j] = ok ? (float)ys[po] : 0.f;
-            yo[j] = ok ? (float)os[po] : 0.f;
-            bi[j] = ok ? wa.pidx[po] : (uint8_t)255;
-            sc[j] = ok ? (wa.pscale ? wa.pscale[(int64_t)n * g.Co + oc0 + j] : 1.f) : 0.f;
+            for (int j = 0; j < 16; ++j) {
+              const bool ok = oc0 + j < g.Co;
+              const int64_t po = ok ? ybp + (int64_t)(oc0 + j) * npixp + q : 0;
+              v[j] = ok ? (float)ys[po] : 0.f;
+              yo[j] = ok ? (float)os[po] : 0.f;
+              bi[j] = ok ? wa.pidx[po] : (uint8_t)255;
+              sc[j] = ok ? (wa.pscale ? wa.pscale[(int64_t)n * g.Co + oc0 + j] : 1.f) : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              if (oc0 + j >= g.Cop) break;
+              S* d = dys + (oc0 + j) * LDY + pbase;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], e));
+            }
           }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], sel));
         }
+      }
+      for (int i = tid; i < g.Cop * (g.npp - g.npix); i += 256) {  // (the MFMA K padding)
+        const int oc = i / (g.npp - g.npix), pp = g.npix + i % (g.npp - g.npix);
+        dys[oc * LDY + pp] = Stor<T>::of(0.f);
       }
     };
     if (wa.pidx) {
