@@ -65,15 +65,27 @@ def test_conv_bwd_pooled_matches_unfused_bitwise(dt, shape, with_dx):
         dx2 = torch.empty_like(x)
         o.conv2d_dgrad(dconv, w, dx2, 0, MF[dt])
         assert torch.equal(dx1, dx2)
-    # and the fp32 reference of the whole thing
-    xr, wr, br = (t.detach().float().cpu().requires_grad_(True) for t in (x, w, b))
-    c = F.conv2d(xr, wr, br) * scale.cpu().view(N, OC, 1, 1)
-    yr = F.relu(F.max_pool2d(c, 2))
-    yr.backward(dy.float().cpu())
+    # and the fp32 reference of the backward, from the kernel forward's own argmax / gate (a
+    # reference forward in fp32 would pick other maxima at near-ties of the 16-bit one)
+    dconv_ref = _unpool_ref(dy, idx, y, scale)
+    xf, wf = x.float().cpu(), w.to(dt).float().cpu()
+    refs = [(dw1, torch.nn.grad.conv2d_weight(xf, w.shape, dconv_ref), "dw"), (db1, dconv_ref.sum((0, 2, 3)), "db")]
+    if with_dx:
+        refs.append((dx1, torch.nn.grad.conv2d_input(x.shape, wf, dconv_ref), "dx"))
     tol = 1e-4 if dt == torch.float32 else 3e-2
-    for got, ref, name in ((dw1, wr.grad, "dw"), (db1, br.grad, "db")) + (((dx1, xr.grad, "dx"),) if with_dx else ()):
+    for got, ref, name in refs:
         err = (got.float().cpu() - ref).abs().max().item()
         assert err <= tol * max(ref.abs().max().item(), 1e-6), f"{name}: {err:.3e}"
+
+
+def _unpool_ref(dy, idx, y, scale):
+    """dL/dconv of relu(maxpool2(conv) * scale) from the pooled gradient, the argmax bytes and the
+    pooled output (maxpool_relu_bwd's rule) in fp32 on the CPU."""
+    N, OC, PH, PW = dy.shape
+    sel = torch.arange(4).view(1, 1, 1, 1, 4)
+    keep = (idx.long().cpu().unsqueeze(-1) == sel) & (y.float().cpu() > 0).unsqueeze(-1)
+    val = (dy.float().cpu() * scale.cpu().view(N, OC, 1, 1)).unsqueeze(-1) * keep
+    return val.view(N, OC, PH, PW, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(N, OC, 2 * PH, 2 * PW)
 
 
 def test_conv_fwd_in_kernel_dropout2d_matches_channel_mask():
