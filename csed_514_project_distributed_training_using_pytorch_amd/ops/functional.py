@@ -416,20 +416,40 @@ def log_softmax_nll(z, target, reduction: str = "mean"):
     return _LogSoftmaxNLL.apply(z, target, _RED[reduction])
 
 
+# arrival counters of the fused head's tile hand-off, one per head weight (zero between launches;
+# launches of one head are stream-ordered)
+_head_cnt: dict[int, tuple[weakref.ref, torch.Tensor]] = {}
+
+
+def _head_counter(w: torch.Tensor) -> torch.Tensor:
+    hit = _head_cnt.get(id(w))
+    if hit is None or hit[0]() is not w or hit[1].device != w.device:
+        for k in [k for k, (r, _) in _head_cnt.items() if r() is None]:
+            del _head_cnt[k]
+        hit = (weakref.ref(w), torch.zeros(1, device=w.device, dtype=torch.int32))
+        _head_cnt[id(w)] = hit
+    return hit[1]
+
+
 class _LinearLogSoftmaxNLL(torch.autograd.Function):
-    """nll(log_softmax(x W^T + b)): the GEMM, then one log_softmax + NLL kernel; the backward is ONE
-    paired launch whose GEMMs read dz = g * (exp(logp) - onehot) straight from the kept log-probs
-    (no dz tensor, no separate loss-backward kernel)."""
+    """nll(log_softmax(x W^T + b)): ONE forward launch (the GEMM's epilogue computes the row-wise
+    log_softmax and the NLL, the per-tile sums handed to the last tile) and ONE backward launch whose
+    paired GEMMs read dz = g * (exp(logp) - onehot) straight from the kept log-probs (no logits or
+    dz tensors, no separate loss kernels)."""
 
     @staticmethod
     def forward(ctx, x, w, b, target, reduction):
         x2 = x.contiguous()
-        z = torch.empty((x2.shape[0], w.shape[0]), device=x.device, dtype=torch.float32)
-        _ops().gemm(x2, w.t(), z, b, 1.0, 0.0, 0, 0.0, 0, 0, None, None, 1.0, _mfma())
         target = target.contiguous().long()
-        logp = torch.empty(z.shape, device=z.device, dtype=torch.float32)
-        out = torch.empty((), device=z.device, dtype=torch.float32)
-        _ops().lsm_nll_fwd(z, target, logp, out, reduction)
+        logp = torch.empty((x2.shape[0], w.shape[0]), device=x.device, dtype=torch.float32)
+        out = torch.empty((), device=x.device, dtype=torch.float32)
+        if _ops().linear_lsm_nll_ok(x2, w):  # GEMM + log_softmax + NLL in one launch
+            part = torch.empty((x2.shape[0] + 15) // 16, device=x.device, dtype=torch.float32)
+            _ops().linear_lsm_nll_fwd(x2, w, b, target, logp, out, part, _head_counter(w), reduction, _mfma())
+        else:
+            z = torch.empty(logp.shape, device=x.device, dtype=torch.float32)
+            _ops().gemm(x2, w.t(), z, b, 1.0, 0.0, 0, 0.0, 0, 0, None, None, 1.0, _mfma())
+            _ops().lsm_nll_fwd(z, target, logp, out, reduction)
         ctx.save_for_backward(x2, w, logp, target)
         ctx.reduction, ctx.has_bias, ctx.bias_param = reduction, b is not None, b
         return out
@@ -451,8 +471,8 @@ class _LinearLogSoftmaxNLL(torch.autograd.Function):
 
 def linear_log_softmax_nll(x, weight, bias, target, reduction: str = "mean"):
     """nll_loss(log_softmax(linear(x, weight, bias), 1), target) -- a classifier head and its loss
-    (ref src/model.py:21-22 + src/train.py:74) as one forward GEMM + one loss kernel and ONE backward
-    launch.  reduction: 'mean' or 'sum'."""
+    (ref src/model.py:21-22 + src/train.py:74) as one forward and one backward launch.  reduction:
+    'mean' or 'sum'."""
     if not x.is_cuda:
         return F.nll_loss(F.log_softmax(F.linear(x, weight, bias), dim=1), target, reduction=reduction)
     if reduction not in ("mean", "sum"):

@@ -262,6 +262,33 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
            A);
 }
 
+// The classifier head + loss forward: logp = log_softmax(x W^T + b) (fp32 [M, C]) and
+// out = nll(logp, target) (mean or sum) in ONE launch; part [cdiv(M, 16)] fp32 scratch and cnt a
+// zero int32 counter that the launch leaves zero.
+void linear_lsm_nll_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& b, const Tensor& target,
+                        Tensor& logp, Tensor& out, Tensor& part, Tensor& cnt, int64_t reduction, int64_t mfma_dtype) {
+  dev(x, "x"); dev(w, "w"); dev(target, "target"); dev(logp, "logp"); dev(out, "out"); dev(part, "part");
+  dev(cnt, "cnt");
+  TORCH_CHECK(reduction == 1 || reduction == 2, "linear_lsm_nll_fwd: reduction mean (1) or sum (2)");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == x.size(0) && out.numel() == 1 &&
+                  out.scalar_type() == at::kFloat && cnt.scalar_type() == at::kInt && part.scalar_type() == at::kFloat &&
+                  part.numel() >= (x.size(0) + 15) / 16,
+              "linear_lsm_nll_fwd: bad target / out / scratch");
+  const optional<Tensor> none;
+  const c10::DeviceGuard gd(x.device());
+  csed::GemmArgs a = make_gemm(x, w.t(), logp, b, 1.0, 0.0, 0, 0.0, 0, 0, none, none, 1.0, mfma_dtype, none);
+  a.head_target = target.data_ptr<int64_t>(); a.head_part = part.data_ptr<float>(); a.head_cnt = cnt.data_ptr<int>();
+  a.head_out = out.data_ptr<float>(); a.head_mean = reduction == 1;
+  TORCH_CHECK(csed::gemm_head_ok(a), "linear_lsm_nll_fwd: shapes outside the fused head (C <= 16, small GEMM)");
+  CHECK_HIP(csed::launch_gemm(a, cur_stream(x)));
+}
+
+bool linear_lsm_nll_ok(const Tensor& x, const Tensor& w) {
+  csed::GemmArgs a{};
+  a.M = x.size(0); a.N = w.size(0); a.K = x.size(1); a.c_dtype = csed::kF32;
+  return csed::gemm_head_ok(a);
+}
+
 // nn.Linear's backward (y = act(x W^T + b), dy [M, O], x [M, I], w [O, I]): dx = gate(dy) W and
 // dw = gate(dy)^T x with db as the ones column, gate(dy) = dy * (y > 0) * gate_scale when the
 // forward had an activation.  One launch when both GEMMs fit the small-GEMM path.
@@ -738,6 +765,9 @@ TORCH_LIBRARY(csed, m) {
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? gate, float gate_scale, Tensor(a!)? dx, Tensor(b!)? dw, "
         "Tensor(c!)? db, int mfma_dtype, Tensor? lsm_target=None, Tensor? lsm_gout=None, float lsm_div=1.0) -> ()");
   m.def("lsm_nll_fwd(Tensor z, Tensor target, Tensor(a!) logp, Tensor(b!) out, int reduction) -> ()");
+  m.def("linear_lsm_nll_fwd(Tensor x, Tensor w, Tensor? b, Tensor target, Tensor(a!) logp, Tensor(b!) out, "
+        "Tensor(c!) part, Tensor(d!) cnt, int reduction, int mfma_dtype) -> ()");
+  m.def("linear_lsm_nll_ok(Tensor x, Tensor w) -> bool", &linear_lsm_nll_ok);
   m.def("lsm_nll_bwd(Tensor gout, Tensor logp, Tensor target, Tensor(a!) dz, int reduction) -> ()");
   m.def("conv2d_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int pad, int mfma_dtype) -> ()");
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, int pad, int mfma_dtype, "
@@ -764,6 +794,7 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("conv2d_bwd", &conv2d_bwd);
   m.impl("linear_bwd", &linear_bwd);
   m.impl("lsm_nll_fwd", &lsm_nll_fwd);
+  m.impl("linear_lsm_nll_fwd", &linear_lsm_nll_fwd);
   m.impl("lsm_nll_bwd", &lsm_nll_bwd);
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);

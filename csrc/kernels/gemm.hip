@@ -308,6 +308,47 @@ __device__ __forceinline__ typename Mfma<T>::frag to_frag(const float (&f)[8]) {
   }
 }
 
+// Classifier-head epilogue (a.head_part): row-wise log_softmax over the tile's 16 columns (the
+// lanes of one kq group hold one row's columns: xor-shuffles within 16 lanes), the NLL of each row's
+// target, the tile's sum (fixed xor tree), then the write-through hand-off of the per-tile sums:
+// sc1 store + vmcnt(0) + one relaxed counter add, the last tile reads every partial with sc1 loads
+// and sums them in tile order (reproducible), as lenet_update's split-K hand-off.
+__device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, int kq, const float (&v)[4], int lane,
+                                              const int64_t (&tgt)[4]) {
+  const float b = n < a.N && a.bias ? a.bias[n] : 0.f;
+  float nll = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mm = mt * 16 + 4 * kq + r;
+    const float z = n < a.N ? a.alpha * v[r] + b : -INFINITY;
+    float mx = z;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float e = n < a.N ? __expf(z - mx) : 0.f;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) e += __shfl_xor(e, o);
+    const float lp = z - (mx + __logf(e));
+    if (mm < a.M) {
+      if (n < a.N) ((float*)a.C)[(int64_t)mm * a.scm + (int64_t)n * a.scn] = lp;
+      if ((int64_t)n == tgt[r]) nll -= lp;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nll += __shfl_xor(nll, o);
+  if (lane == 0) {
+    const int ntiles = (a.M + 15) >> 4;
+    __hip_atomic_store(a.head_part + mt, nll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(a.head_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == ntiles - 1) {
+      float t = 0.f;
+      for (int i = 0; i < ntiles; ++i) t += __hip_atomic_load(a.head_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *a.head_out = a.head_mean ? t / (float)a.M : t;
+      *a.head_cnt = 0;  // (the next launch reads it after the kernel boundary)
+    }
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk, float (*part)[256]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
@@ -321,6 +362,15 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
   const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the head's targets of this lane's 4 rows (loaded ahead of the K loop)
+  int64_t tgt[4] = {-1, -1, -1, -1};
+  if (a.head_part && wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int mm = mt * 16 + 4 * kq + r;
+      tgt[r] = mm < a.M ? a.head_target[mm] : -1;
+    }
+  }
   // the loss head's dz (a.lsm_target): the scalar upstream gradient, loaded once
   const float lsm_g = a.lsm_target ? a.lsm_gout[0] / a.lsm_div : 0.f;
   for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
@@ -372,6 +422,14 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
   __syncthreads();
   if (wave != 0) return;
+  if (a.head_part) {  // classifier head: log_softmax rows + NLL (one 16-column tile holds a row)
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      v[r] = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) + part[3][r * 64 + lane];
+    head_epilogue(a, mt, n, kq, v, lane, tgt);
+    return;
+  }
   const uint64_t off = rng_offset(a.offset, a.offset_dev);
   const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
 #pragma unroll
@@ -501,8 +559,14 @@ hipError_t launch_gemm_pair(const GemmArgs& in_a, const GemmArgs& in_b, hipStrea
   return hipGetLastError();
 }
 
+bool gemm_head_ok(const GemmArgs& a) {
+  return a.M > 0 && a.N > 0 && a.N <= 16 && !a.rowsum && a.act == 0 && !a.G && !a.lsm_target && a.beta == 0.f &&
+         a.c_dtype == kF32 && gemm_small(a);
+}
+
 hipError_t launch_gemm(const GemmArgs& in, hipStream_t s) {
   if (in.M <= 0 || in.N <= 0) return hipSuccess;
+  if (in.head_part && !gemm_head_ok(in)) return hipErrorInvalidValue;
   if (in.lsm_target && (!gemm_small(in) || in.a_dtype != kF32 || in.G)) return hipErrorInvalidValue;
   const GemmArgs a = with_modes(in);
   const int Np = a.N + (a.rowsum ? 1 : 0);

@@ -100,7 +100,15 @@ struct GemmArgs {
   // of nll(log_softmax(z)) instead, dz[r][c] = (gout[0] / lsm_div) * (exp(logp[r][c]) - (c == target[r]))
   // -- lsm_rows_are_m: A(m, k) = dz[m][k] (dX of the head), else A(m, k) = dz[k][m] (its dW)
   const int64_t* lsm_target; const float* lsm_gout; float lsm_div; int lsm_rows_are_m;
+  // optional (small-GEMM path, N <= 16, no activation / rowsum): the classifier head's forward --
+  // the epilogue turns each row of z = A B + bias into fp32 log-probs (written to C) and the NLL of
+  // head_target; each 16-row tile's NLL sum goes to head_part[tile] (write-through) and the tile
+  // whose arrival (head_cnt, re-armed to 0) comes last sums them in tile order into head_out
+  // (/ M for the mean)
+  const int64_t* head_target; float* head_part; int* head_cnt; float* head_out; int head_mean;
 };
+// The classifier head + NLL forward above; false if the shapes do not fit it.
+bool gemm_head_ok(const GemmArgs& a);
 // Number of K splits launch_gemm will use for these shapes (1 = no workspace needed).
 int gemm_splits(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);

@@ -189,3 +189,30 @@ def test_net_fused_head_matches_log_probs_path():
     assert torch.allclose(l1, l2, rtol=1e-6, atol=1e-6)
     for a, b in zip(g1, g2):
         assert (a - b).abs().max().item() <= 1e-2 * max(b.abs().max().item(), 1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,red", [(64, 1), (37, 2), (1000, 1)])
+def test_head_forward_matches_gemm_then_loss(dt, rows, red):
+    """The classifier head's one-launch forward (log_softmax + NLL in the GEMM epilogue, per-tile
+    sums handed to the last tile) == gemm + lsm_nll_fwd, over repeated launches (the arrival
+    counter re-arms itself)."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(rows, 50, device=DEV, generator=g).to(dt)
+    w = torch.randn(10, 50, device=DEV, generator=g) * 0.3
+    b = torch.randn(10, device=DEV, generator=g)
+    t = torch.randint(0, 10, (rows,), device=DEV, generator=g)
+    o = _native.ops()
+    assert o.linear_lsm_nll_ok(x, w)
+    z = torch.empty(rows, 10, device=DEV)
+    o.gemm(x, w.t(), z, b, 1.0, 0.0, 0, 0.0, 0, 0, None, None, 1.0, MF[dt])
+    lp_ref, out_ref = torch.empty_like(z), torch.empty((), device=DEV)
+    o.lsm_nll_fwd(z, t, lp_ref, out_ref, red)
+    cnt = torch.zeros(1, device=DEV, dtype=torch.int32)
+    part = torch.empty((rows + 15) // 16, device=DEV)
+    for _ in range(3):
+        lp, out = torch.full_like(z, 7.0), torch.full((), 7.0, device=DEV)
+        o.linear_lsm_nll_fwd(x, w, b, t, lp, out, part, cnt, red, MF[dt])
+        torch.testing.assert_close(lp, lp_ref, rtol=0, atol=2e-6)
+        torch.testing.assert_close(out, out_ref, rtol=2e-6, atol=2e-6)
+        assert int(cnt.item()) == 0
