@@ -145,7 +145,7 @@ def test_log_softmax_nll_matches_torch(red, rows):
     gout = torch.randn(loss.shape, device=DEV, generator=g)
     loss.backward(gout)
     lr.backward(gout.cpu().double())
-    assert torch.allclose(z.grad.cpu().double(), zr.grad, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(z.grad.cpu().double(), zr.grad, rtol=1e-4, atol=1e-6)  # (__expf / __logf, fp32)
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
