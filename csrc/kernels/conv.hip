@@ -89,122 +89,152 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   const int tid = threadIdx.x;
   const int NT = g.Cop >> 4;
 
-  // ---- epilogue operands of this lane's channels (N-tiles 0..3), loaded / drawn first so their
-  // latency hides under the staging (they were one more dependent round trip at the end)
+  // ---- staging in ONE memory round trip: every global load of the weights (up to 32 per thread),
+  // the first 16 patch rows and the epilogue operands is issued before any LDS store, the Dropout2d
+  // draw runs while they are in flight; further rows / columns (large shapes) follow in rounds.
+  // (Weights, patch and epilogue operands as three dependent rounds cost ~2 us each: the per-op
+  // step's conv launches were latency chains, profiles/round5.md.)
+  const int KHW = g.KH * g.KW;
+  const int64_t wstep = a.mode == 0 ? g.K : KHW;
+  // effective weight (oc, ic, kh, kw) of column k = w[wbase(k) + oc * wstep] (see weff); koff(k) its patch offset
+  auto wcol = [&](int k, int64_t& base, int& ko) {
+    const bool kv = k < g.K;
+    const int ic = kv ? k / KHW : 0, r = k - ic * KHW, kh = r / g.KW, kw = r - kh * g.KW;
+    ko = kv ? (ic * g.PR + kh) * g.PW + kw : 0;
+    base = !kv ? -1 : a.mode == 0 ? (int64_t)k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
+  };
+  // single-round weight form: a thread's columns k = tid + 256 i (i < 32 / COP) x all COP channels
+  const int wcols = 32 / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
+  const bool wfast = g.Cop <= 32 && g.Kp <= 256 * wcols;
+  int64_t wb[2] = {-1, -1};
+  int wko[2] = {0, 0};
+  float wv[32];
+  if (wfast) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (i < wcols && tid + 256 * i < g.Kp) wcol(tid + 256 * i, wb[i], wko[i]);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
+      wv[j] = wb[i] >= 0 && oc < g.Co ? a.w[wb[i] + oc * wstep] : 0.f;
+    }
+  }
+  // epilogue operands of this lane's channels (N-tiles 0..3)
   float eb[4], es[4];
-  {
-    const uint64_t off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int oc = j * 16 + (tid & 15);
+    const bool ok = j < NT && oc < g.Co;
+    eb[j] = ok && a.bias ? a.bias[oc] : 0.f;
+    es[j] = ok && a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
+  }
+  const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
+
+  // the zero-padded input patch: a thread owns one patch column, rows step by 256 / PW
+  const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
+  const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+  int rr = tid / g.PW;
+  const bool prow = rr < rpi;
+  int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
+  const int iw = pc - g.pad;
+  const bool colv = iw >= 0 && iw < g.W;
+  const int64_t nc0 = (int64_t)n * g.Ci;
+  float pv[16], yo[16], sc[16];
+  uint8_t bi[16];
+  int at[16], sel[16];
+  // (the input dtype dispatched once around each batch: a per-load switch kept the loads apart)
+  auto load_rows = [&](auto tag) {  // 16 rows' loads (pooled input: value / argmax / gate / scale)
+    typedef decltype(tag) X;
+    const X* xs = static_cast<const X*>(a.x);
+    const X* ys = static_cast<const X*>(a.pout);
+    if (!a.pidx) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int ih = oh0 - g.pad + pr;
+        const bool in = prow && rr < nrows;
+        at[j] = in ? rr : -1;
+        pv[j] = (in && colv && ih >= 0 && ih < g.H) ? (float)xs[xbase + ((int64_t)ic * g.H + ih) * g.W + iw] : 0.f;
+        rr += rpi;
+        pr += rpi;
+        while (pr >= g.PR) {
+          pr -= g.PR;
+          ++ic;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int ih = oh0 - g.pad + pr;
+        const bool in = prow && rr < nrows;
+        const bool ok = in && colv && ih >= 0 && ih < g.H;
+        at[j] = in ? rr : -1;
+        sel[j] = ((ih & 1) << 1) | (iw & 1);
+        const int64_t po = ok ? ((nc0 + ic) * g.Hp + (ih >> 1)) * g.Wp + (iw >> 1) : 0;
+        pv[j] = ok ? (float)xs[po] : 0.f;
+        yo[j] = ok ? (float)ys[po] : 0.f;
+        bi[j] = ok ? a.pidx[po] : (uint8_t)255;
+        sc[j] = ok ? (a.pscale ? a.pscale[nc0 + ic] : 1.f) : 0.f;
+        rr += rpi;
+        pr += rpi;
+        while (pr >= g.PR) {
+          pr -= g.PR;
+          ++ic;
+        }
+      }
+    }
+  };
+  auto rows_round = [&]() {
+    if (a.x_dtype == kF32) load_rows(float{});
+    else if (a.x_dtype == kBF16) load_rows(__bf16{});
+    else load_rows(_Float16{});
+  };
+  auto store_rows = [&]() {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(a.pidx ? unpool(pv[j], bi[j], yo[j], sc[j], sel[j]) : pv[j]);
+  };
+  rows_round();  // (first batch: in flight with the weight loads)
+
+  // ---- while the loads fly: the Dropout2d draw (channel_mask_kernel's draw, index n*Co + oc)
+  if (a.chscale_out) {
     const float keep_sc = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int oc = j * 16 + (tid & 15);
-      const bool ok = j < NT && oc < g.Co;
-      eb[j] = ok && a.bias ? a.bias[oc] : 0.f;
-      es[j] = ok && a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
-      if (a.chscale_out)  // Dropout2d drawn here (channel_mask_kernel's draw: index n*Co+oc)
-        es[j] = ok && dropout_keep(a.seed, off, (uint64_t)n * g.Co + oc, a.drop_p) ? keep_sc : 0.f;
+      es[j] = j < NT && oc < g.Co && dropout_keep(a.seed, drop_off, (uint64_t)n * g.Co + oc, a.drop_p) ? keep_sc : 0.f;
     }
   }
 
-  // ---- stage weights (fp32 -> 16 bit) and the k -> patch offset table.  A thread keeps its K
-  // columns for every oc: the k -> (ic, kh, kw) split (integer divisions) is done once per column,
-  // not once per element (per-element divisions were most of a small-batch launch)
-  const int KHW = g.KH * g.KW;
-  for (int k = tid; k < g.Kp; k += 256) {
-    const bool kv = k < g.K;
-    const int ic = kv ? k / KHW : 0, r = k - ic * KHW, kh = r / g.KW, kw = r - kh * g.KW;
-    koff[k] = kv ? (ic * g.PR + kh) * g.PW + kw : 0;
-    // effective weight (oc, ic, kh, kw) = w[base + oc * step] (see weff)
-    const int64_t base = a.mode == 0 ? k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
-    const int64_t step = a.mode == 0 ? g.K : KHW;
-    // up to 32 loads in flight, then their LDS stores (a load -> convert -> store chain per element
-    // waited for every load in turn: ~1 us of memory latency each; batches of 8 were 2-4 rounds)
-    for (int oc0 = 0; oc0 < g.Cop; oc0 += 32) {  // (Cop: a multiple of 16)
-      float v[32];
+  // ---- LDS stores of the first round, then any further rounds
+  if (wfast) {
 #pragma unroll
-      for (int j = 0; j < 32; ++j) v[j] = kv && oc0 + j < g.Co ? a.w[base + (oc0 + j) * step] : 0.f;
+    for (int i = 0; i < 2; ++i)
+      if (i < wcols && tid + 256 * i < g.Kp) koff[tid + 256 * i] = wko[i];
 #pragma unroll
-      for (int j = 0; j < 32; ++j)
-        if (oc0 + j < g.Cop) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(v[j]);
+    for (int j = 0; j < 32; ++j) {
+      const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
+      const int k = tid + 256 * i;
+      if (i < wcols && k < g.Kp) Ws[oc * LDW + k] = Stor<T>::of(wv[j]);
+    }
+  } else {
+    for (int k = tid; k < g.Kp; k += 256) {
+      int64_t base;
+      int ko;
+      wcol(k, base, ko);
+      koff[k] = ko;
+      for (int oc0 = 0; oc0 < g.Cop; oc0 += 32) {  // (Cop: a multiple of 16)
+#pragma unroll
+        for (int j = 0; j < 32; ++j) wv[j] = base >= 0 && oc0 + j < g.Co ? a.w[base + (oc0 + j) * wstep] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (oc0 + j < g.Cop) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(wv[j]);
+      }
     }
   }
-  // ---- stage the zero-padded input patch: a thread owns one patch column, rows step by
-  // 256 / PW (no per-element divisions)
-  const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
-  {
-    const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
-    int rr = tid / g.PW;
-    if (rr < rpi) {
-      int ic = rr / g.PR, pr = rr - ic * g.PR;
-      const int iw = pc - g.pad;
-      const bool colv = iw >= 0 && iw < g.W;
-      // (the input dtype dispatched once, outside the loop: a per-load switch kept the loads apart)
-      auto rows = [&](auto tag) {
-        typedef decltype(tag) X;
-        const X* xs = static_cast<const X*>(a.x);
-        while (rr < nrows) {  // sixteen rows' loads in flight, then their LDS stores
-          float v[16];
-          int at[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int ih = oh0 - g.pad + pr;
-            at[j] = rr < nrows ? rr : -1;
-            v[j] = (rr < nrows && colv && ih >= 0 && ih < g.H) ? (float)xs[xbase + ((int64_t)ic * g.H + ih) * g.W + iw]
-                                                               : 0.f;
-            rr += rpi;
-            pr += rpi;
-            while (pr >= g.PR) {
-              pr -= g.PR;
-              ++ic;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 16; ++j)
-            if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(v[j]);
-        }
-      };
-      // pooled input (the gradient of a pool-fused forward): sixteen rows' value / argmax / gate /
-      // scale loads in flight, expanded in registers
-      auto prows = [&](auto tag) {
-        typedef decltype(tag) X;
-        const X* xs = static_cast<const X*>(a.x);
-        const X* ys = static_cast<const X*>(a.pout);
-        const int64_t nc0 = (int64_t)n * g.Ci;
-        while (rr < nrows) {
-          float v[16], yo[16], sc[16];
-          uint8_t bi[16];
-          int at[16], sel[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int ih = oh0 - g.pad + pr;
-            const bool ok = rr < nrows && colv && ih >= 0 && ih < g.H;
-            at[j] = rr < nrows ? rr : -1;
-            sel[j] = ((ih & 1) << 1) | (iw & 1);
-            const int64_t po = ok ? ((nc0 + ic) * g.Hp + (ih >> 1)) * g.Wp + (iw >> 1) : 0;
-            v[j] = ok ? (float)xs[po] : 0.f;
-            yo[j] = ok ? (float)ys[po] : 0.f;
-            bi[j] = ok ? a.pidx[po] : (uint8_t)255;
-            sc[j] = ok ? (a.pscale ? a.pscale[nc0 + ic] : 1.f) : 0.f;
-            rr += rpi;
-            pr += rpi;
-            while (pr >= g.PR) {
-              pr -= g.PR;
-              ++ic;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 16; ++j)
-            if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], sel[j]));
-        }
-      };
-      if (a.pidx) {
-        if (a.x_dtype == kF32) prows(float{});
-        else if (a.x_dtype == kBF16) prows(__bf16{});
-        else prows(_Float16{});
-      } else if (a.x_dtype == kF32) rows(float{});
-      else if (a.x_dtype == kBF16) rows(__bf16{});
-      else rows(_Float16{});
-    }
+  store_rows();
+  while (prow && rr < nrows) {
+    rows_round();
+    store_rows();
   }
   __syncthreads();
 
@@ -369,111 +399,131 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   const int n_end = min(N, n_begin + g.per_block);
   for (int n = n_begin; n < n_end; ++n) {
     __syncthreads();  // previous image's LDS reads are done
+    // ---- this image's staging in ONE memory round trip where it fits: the first 16 patch rows and
+    // the first dy chunk are loaded before any LDS store (two serial rounds were ~2 us each)
     const int64_t xb = (int64_t)n * g.Ci * g.H * g.W;
-    {  // the zero-padded input patch: one patch column per thread, rows stepping by 256 / PW
-      const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
-      int rr = tid / g.PW;
-      if (rr < rpi) {
-        int ic = rr / g.PR, pr = rr - ic * g.PR;
-        const int iw = pc - g.pad;
-        const bool colv = iw >= 0 && iw < g.W;
-        auto rows = [&](auto tag) {  // (dtype dispatched once, see conv_fwd_kernel)
-          typedef decltype(tag) X;
-          const X* xs = static_cast<const X*>(x);
-          while (rr < nrows) {  // eight rows' loads in flight, then their LDS stores
-            float v[8];
-            int at[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int ih = pr - g.pad;
-              at[j] = rr < nrows ? rr : -1;
-              v[j] = (rr < nrows && colv && ih >= 0 && ih < g.H) ? (float)xs[xb + ((int64_t)ic * g.H + ih) * g.W + iw]
-                                                                 : 0.f;
-              rr += rpi;
-              pr += rpi;
-              while (pr >= g.PR) {
-                pr -= g.PR;
-                ++ic;
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(v[j]);
-          }
-        };
-        if (xdt == kF32) rows(float{});
-        else if (xdt == kBF16) rows(__bf16{});
-        else rows(_Float16{});
-      }
-      if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
-    }
-    const int64_t yb = (int64_t)n * g.Co * g.npix;
-    // dy staging spread over the whole block: pst threads per pixel row, 256 / pst channel groups
-    // of 8 side by side (a small image's 64 pixels kept 3/4 of the block idle and ran its channels
-    // as 4 serial rounds of loads)
-    const int pst = min(g.npp, 256), ocg = 256 / pst, p0 = tid % pst, og = tid / pst;
-    auto dyrows = [&](auto tag) {  // a thread keeps its pixel for its channel groups, 8 loads in flight
+    // the zero-padded input patch: one patch column per thread, rows stepping by 256 / PW
+    const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+    int rr = tid / g.PW;
+    const bool prow = rr < rpi;
+    int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
+    const int iw = pc - g.pad;
+    const bool colv = iw >= 0 && iw < g.W;
+    float xv[16];
+    int at[16];
+    auto load_rows = [&](auto tag) {  // (dtype dispatched once per batch, see conv_fwd_body)
       typedef decltype(tag) X;
-      const X* ys = static_cast<const X*>(dy);
-      if (og >= ocg) return;
-      for (int p = p0; p < g.npp; p += pst)
-        for (int oc0 = og * 8; oc0 < g.Cop; oc0 += ocg * 8) {
-          float v[8];
+      const X* xs = static_cast<const X*>(x);
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = (oc0 + j < g.Co && p < g.npix) ? (float)ys[yb + (int64_t)(oc0 + j) * g.npix + p] : 0.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dys[(oc0 + j) * LDY + p] = Stor<T>::of(v[j]);
+      for (int j = 0; j < 16; ++j) {
+        const int ih = pr - g.pad;
+        const bool in = prow && rr < nrows;
+        at[j] = in ? rr : -1;
+        xv[j] = (in && colv && ih >= 0 && ih < g.H) ? (float)xs[xb + ((int64_t)ic * g.H + ih) * g.W + iw] : 0.f;
+        rr += rpi;
+        pr += rpi;
+        while (pr >= g.PR) {
+          pr -= g.PR;
+          ++ic;
         }
+      }
     };
-    // pooled dy: a thread owns one pooling window of 16 channels (value / argmax / gate / scale
-    // loads of all 16 in flight) and writes the window's 4 pixels, one of them nonzero; the padding
-    // pixels past npix are zeroed separately
-    auto pdyrows = [&](auto tag) {
+    auto rows_round = [&]() {
+      if (xdt == kF32) load_rows(float{});
+      else if (xdt == kBF16) load_rows(__bf16{});
+      else load_rows(_Float16{});
+    };
+    auto store_rows = [&]() {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(xv[j]);
+    };
+
+    // dy: plain (pst threads per pixel row, 256 / pst channel groups of 8 side by side) or pooled (a
+    // thread owns one pooling window x 16 channels and writes the window's 4 pixels, one nonzero)
+    const int64_t yb = (int64_t)n * g.Co * g.npix;
+    const int pst = min(g.npp, 256), ocg = 256 / pst, p0 = tid % pst, og = tid / pst;
+    const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
+    const int64_t ybp = (int64_t)n * g.Co * npixp;
+    const int wst = max(1, min(npixp, 256)), wgr = 256 / wst, q0 = tid % wst, gq = tid / wst;
+    float dv[16], yo[16], sc[16];
+    uint8_t bi[16];
+    int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
+    bool d_more = wa.pidx ? (gq < wgr && q0 < npixp && gq * 16 < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
+    auto load_dy = [&](auto tag) {  // one chunk's loads
       typedef decltype(tag) X;
       const X* ys = static_cast<const X*>(dy);
-      const X* os = static_cast<const X*>(wa.pout);
-      const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
-      const int64_t ybp = (int64_t)n * g.Co * npixp;
-      const int wst = min(npixp, 256), wg = 256 / wst, q0 = tid % wst, gq = tid / wst;
-      if (gq < wg) {
-        for (int q = q0; q < npixp; q += wst) {
-          const int ph = q / PWp, pw = q - ph * PWp;
-          const int pbase = 2 * ph * g.OW + 2 * pw;
-          for (int oc0 = gq * 16; oc0 < g.Cop; oc0 += wg * 16) {
-            float v[16], yo[16], sc[16];
-            uint8_t bi[16];
+      if (!wa.pidx) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              const bool ok = oc0 + j < g.Co;
-              const int64_t po = ok ? ybp + (int64_t)(oc0 + j) * npixp + q : 0;
-              v[j] = ok ? (float)ys[po] : 0.f;
-              yo[j] = ok ? (float)os[po] : 0.f;
-              bi[j] = ok ? wa.pidx[po] : (uint8_t)255;
-              sc[j] = ok ? (wa.pscale ? wa.pscale[(int64_t)n * g.Co + oc0 + j] : 1.f) : 0.f;
-            }
+        for (int j = 0; j < 8; ++j)
+          dv[j] = (d_oc0 + j < g.Co && d_p < g.npix) ? (float)ys[yb + (int64_t)(d_oc0 + j) * g.npix + d_p] : 0.f;
+      } else {
+        const X* os = static_cast<const X*>(wa.pout);
+        const int ph = d_q / PWp, pw = d_q - ph * PWp;
+        d_pb = 2 * ph * g.OW + 2 * pw;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              if (oc0 + j >= g.Cop) break;
-              S* d = dys + (oc0 + j) * LDY + pbase;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(v[j], bi[j], yo[j], sc[j], e));
-            }
-          }
+        for (int j = 0; j < 16; ++j) {
+          const bool ok = d_oc0 + j < g.Co;
+          const int64_t po = ok ? ybp + (int64_t)(d_oc0 + j) * npixp + d_q : 0;
+          dv[j] = ok ? (float)ys[po] : 0.f;
+          yo[j] = ok ? (float)os[po] : 0.f;
+          bi[j] = ok ? wa.pidx[po] : (uint8_t)255;
+          sc[j] = ok ? (wa.pscale ? wa.pscale[(int64_t)n * g.Co + d_oc0 + j] : 1.f) : 0.f;
         }
       }
-      for (int i = tid; i < g.Cop * (g.npp - g.npix); i += 256) {  // (the MFMA K padding)
+    };
+    auto dy_round = [&]() {
+      if (dydt == kF32) load_dy(float{});
+      else if (dydt == kBF16) load_dy(__bf16{});
+      else load_dy(_Float16{});
+    };
+    auto store_dy_next = [&]() {  // store the loaded chunk, advance to the next one
+      if (!wa.pidx) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dys[(d_oc0 + j) * LDY + d_p] = Stor<T>::of(dv[j]);
+        d_oc0 += ocg * 8;
+        if (d_oc0 >= g.Cop) {
+          d_oc0 = og * 8;
+          d_p += pst;
+        }
+        d_more = d_p < g.npp;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (d_oc0 + j >= g.Cop) break;
+          S* d = dys + (d_oc0 + j) * LDY + d_pb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(dv[j], bi[j], yo[j], sc[j], e));
+        }
+        d_oc0 += wgr * 16;
+        if (d_oc0 >= g.Cop) {
+          d_oc0 = gq * 16;
+          d_q += wst;
+        }
+        d_more = d_q < npixp;
+      }
+    };
+    if (wa.pidx) d_oc0 = gq * 16;
+
+    rows_round();             // round 1: patch rows ...
+    if (d_more) dy_round();   // ... and the first dy chunk in flight together
+    store_rows();
+    if (d_more) store_dy_next();
+    while (prow && rr < nrows) {
+      rows_round();
+      store_rows();
+    }
+    while (d_more) {
+      dy_round();
+      store_dy_next();
+    }
+    if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
+    if (wa.pidx) {  // (the MFMA K padding past npix: the window writes cover pixels < npix only)
+      for (int i = tid; i < g.Cop * (g.npp - g.npix); i += 256) {
         const int oc = i / (g.npp - g.npix), pp = g.npix + i % (g.npp - g.npix);
         dys[oc * LDY + pp] = Stor<T>::of(0.f);
       }
-    };
-    if (wa.pidx) {
-      if (dydt == kF32) pdyrows(float{});
-      else if (dydt == kBF16) pdyrows(__bf16{});
-      else pdyrows(_Float16{});
-    } else if (dydt == kF32) dyrows(float{});
-    else if (dydt == kBF16) dyrows(__bf16{});
-    else dyrows(_Float16{});
+    }
     __syncthreads();
     if (my_nt0 >= NT) continue;
     // this lane's B-column patch offsets, one per N-tile (the same for every pixel step: read once
