@@ -170,9 +170,10 @@ __device__ __forceinline__ void store_tile(typename Stor<T>::S* lds, const Raw& 
   }
 }
 
-// Epilogue of one output element (acc = sum over K).
+// Epilogue of one output element (acc = sum over K); bias_v: the column's bias (0 without one).
 template <typename T>
-__device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale) {
+__device__ __forceinline__ void epilogue_b(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale,
+                                           float bias_v) {
   if (n == a.N) {  // ones column -> row sums of A (bias gradient)
     a.rowsum[m] = a.alpha * acc;
     return;
@@ -180,7 +181,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float 
   const int64_t co = (int64_t)m * a.scm + (int64_t)n * a.scn;
   float v = a.alpha * acc;
   if (a.beta != 0.f) v += a.beta * ld_any(a.C, a.c_dtype, co);
-  if (a.bias) v += a.bias[n];
+  v += bias_v;
   if (a.act >= 1) v = fmaxf(v, 0.f);
   if (a.act == 2) v = dropout_keep(a.seed, off, (uint64_t)m * a.N + n, a.drop_p) ? v * dscale : 0.f;
   switch (a.c_dtype) {
@@ -188,6 +189,11 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float 
     case kBF16: ((__bf16*)a.C)[co] = (__bf16)v; break;
     default: ((_Float16*)a.C)[co] = (_Float16)v; break;
   }
+}
+
+template <typename T>
+__device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale) {
+  epilogue_b<T>(a, m, n, acc, off, dscale, a.bias && n < a.N ? a.bias[n] : 0.f);
 }
 
 template <typename T>
@@ -314,8 +320,7 @@ __device__ __forceinline__ typename Mfma<T>::frag to_frag(const float (&f)[8]) {
 // sc1 store + vmcnt(0) + one relaxed counter add, the last tile reads every partial with sc1 loads
 // and sums them in tile order (reproducible), as lenet_update's split-K hand-off.
 __device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, int kq, const float (&v)[4], int lane,
-                                              const int64_t (&tgt)[4]) {
-  const float b = n < a.N && a.bias ? a.bias[n] : 0.f;
+                                              const int64_t (&tgt)[4], float b) {
   float nll = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -349,7 +354,7 @@ __device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, 
   }
 }
 
-template <typename T>
+template <typename T, bool HEAD>  // HEAD: the classifier-head epilogue may be asked for (a.head_part)
 __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk, float (*part)[256]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
   const int Np = a.N + (a.rowsum ? 1 : 0);
@@ -362,9 +367,13 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
   const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  // epilogue operands loaded ahead of the K loop (at the end they were one more dependent round
+  // trip): this lane's column bias and the dropout offset counter
+  const float bias_v = wave == 0 && a.bias && n < a.N ? a.bias[n] : 0.f;
+  const uint64_t off = wave == 0 && a.act == 2 ? rng_offset(a.offset, a.offset_dev) : 0;
   // the head's targets of this lane's 4 rows (loaded ahead of the K loop)
   int64_t tgt[4] = {-1, -1, -1, -1};
-  if (a.head_part && wave == 0) {
+  if (HEAD && a.head_part && wave == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int mm = mt * 16 + 4 * kq + r;
@@ -375,12 +384,10 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   const float lsm_g = a.lsm_target ? a.lsm_gout[0] / a.lsm_div : 0.f;
   for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
     float fa[4][8], fb[4][8], fg[4][8];
-    int nku[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int kb = (kb0 + u) * 32 + 8 * kq;
       const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
-      nku[u] = nk;
       const int kc = min(kb, a.K - 1);
       gather8<T>(fa[u], a.A, a.a_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak, a.sak, mv ? nk : 0,
                  avec);
@@ -398,9 +405,10 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int kb = (kb0 + u) * 32 + 8 * kq;
+        const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const bool in = mv && j < nku[u];
+          const bool in = mv && j < nk;
           const int r = a.lsm_rows_are_m ? m : kb + j, c = a.lsm_rows_are_m ? kb + j : m;
           const int64_t t = in ? a.lsm_target[r] : -1;
           fa[u][j] = in ? lsm_g * (__expf(fa[u][j]) - (c == t ? 1.f : 0.f)) : 0.f;
@@ -422,29 +430,28 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
   __syncthreads();
   if (wave != 0) return;
-  if (a.head_part) {  // classifier head: log_softmax rows + NLL (one 16-column tile holds a row)
+  if (HEAD && a.head_part) {  // classifier head: log_softmax rows + NLL (one 16-column tile holds a row)
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       v[r] = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) + part[3][r * 64 + lane];
-    head_epilogue(a, mt, n, kq, v, lane, tgt);
+    head_epilogue(a, mt, n, kq, v, lane, tgt, bias_v);
     return;
   }
-  const uint64_t off = rng_offset(a.offset, a.offset_dev);
   const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float v = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) +
                     part[3][r * 64 + lane];
     const int mm = mt * 16 + 4 * kq + r;
-    if (mm < a.M && n < Np) epilogue<T>(a, mm, n, v, off, dscale);
+    if (mm < a.M && n < Np) epilogue_b<T>(a, mm, n, v, off, dscale, bias_v);
   }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
   __shared__ float part[4][256];
-  gemm_small_body<T>(a, blockIdx.x, part);
+  gemm_small_body<T, true>(a, blockIdx.x, part);
 }
 
 // Two independent small GEMMs in one launch (nn.Linear's backward: dX = dY.W and dW = dY^T.X + the
@@ -452,8 +459,8 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_small_pair_kernel(GemmArgs a, GemmArgs b, int tiles_a) {
   __shared__ float part[4][256];
-  if ((int)blockIdx.x < tiles_a) gemm_small_body<T>(a, blockIdx.x, part);
-  else gemm_small_body<T>(b, blockIdx.x - tiles_a, part);
+  const bool first = (int)blockIdx.x < tiles_a;  // (one body on the selected argument block)
+  gemm_small_body<T, false>(first ? a : b, first ? blockIdx.x : blockIdx.x - tiles_a, part);
 }
 
 // Fixed-order sum of the split-K partials + the epilogue.
@@ -548,7 +555,7 @@ bool gemm_pairable(const GemmArgs& a, const GemmArgs& b) {
 }
 
 hipError_t launch_gemm_pair(const GemmArgs& in_a, const GemmArgs& in_b, hipStream_t s) {
-  if (!gemm_pairable(in_a, in_b)) return hipErrorInvalidValue;
+  if (!gemm_pairable(in_a, in_b) || in_a.head_part || in_b.head_part) return hipErrorInvalidValue;
   for (const GemmArgs* g : {&in_a, &in_b})
     if (g->lsm_target && (g->a_dtype != kF32 || g->G)) return hipErrorInvalidValue;
   const GemmArgs a = with_modes(in_a), b = with_modes(in_b);
