@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
-// 4 slices of the partials each (every lane's loads issued together, 8 in flight), then the
+// 4 slices of the partials each (every lane's loads issued together, 16 in flight), then the
 // slices combine in slice order through LDS.  One thread per output walking all nblocks partials
 // in a dependent add chain was latency-bound: 15.8 us for 64 partials (profiles/round5.md).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nblocks, int Co,
@@ -633,14 +633,14 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   if (i < L) {
     const int per = (nblocks + 3) >> 2, b0 = sl * per, b1 = min(nblocks, b0 + per);
     int b = b0;
-    for (; b + 8 <= b1; b += 8) {
-      float v[8];
+    for (; b < b1; b += 16) {  // 16 loads in flight (a slice of up to 16 partials: one round trip)
+      float v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(b + u) * L + i];
+      for (int u = 0; u < 16; ++u) v[u] = b + u < b1 ? slab[(int64_t)(b + u) * L + i] : 0.f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 16; ++u)
+        if (b + u < b1) s += v[u];
     }
-    for (; b < b1; ++b) s += slab[(int64_t)b * L + i];
   }
   part[sl][c] = s;
   __syncthreads();

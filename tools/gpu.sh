@@ -18,6 +18,7 @@
 #   pmc       three rocprofv3 --pmc passes over the train kernel (B=64), one over B=8,
 #             and three over the tile kernel (B=1024)
 #   modular   the modular engine: fusion + op tests, graph step times (B = 64), a kernel trace
+#   modpmc    one rocprofv3 --pmc pass over the modular step's kernels (fetch / memory waits)
 #   ddp       tools/ddp_overlap.py: the modular engine's bucketed reducer, per-bucket all-reduce on the
 #             comm stream vs after backward, step times + overlap share from kernel traces
 #   ab        same-box A/B of ab/A_C.so vs ab/B_C.so (tools/ab_build.sh REV) at global batch
@@ -94,6 +95,11 @@ task_modular() {  # the modular (per-op) engine: fusion / op tests, graph step t
   py 200 python -u tools/ddp_overlap.py --graph graph --steps 500 --loader >> $O/${T}_modddp.log 2>&1 && \
   cd /tmp && export TMPDIR=/tmp && \
   py 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_modkt -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt.log 2>&1
+}
+
+task_modpmc() {  # one PMC pass over the modular step's kernels (instruction-fetch vs memory waits)
+  cd /tmp && export TMPDIR=/tmp && \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_IFETCH SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $O/${T}_modpmc -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph eager > $O/${T}_modpmc.log 2>&1
 }
 
 task_ddp() {  # the modular engine's bucketed reducer: step times per mode + overlap from kernel traces
