@@ -72,7 +72,10 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
   return ((int)bi == sel && yo > 0.f) ? v * sc : 0.f;
 }
 
-template <typename T>
+// X: the input's element type, PIN: the input is given max-pooled (a.pidx) -- compile-time, so the
+// staging's loads are straight-line code (a runtime dtype / mode branch around them made the
+// compiler copy every loaded register at the join: a wait on each load before the next issued)
+template <typename T, typename X, bool PIN>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
                                               unsigned char* __restrict__ smem) {
   typedef typename Mfma<T>::frag frag;
@@ -109,26 +112,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   int64_t wb[2] = {-1, -1};
   int wko[2] = {0, 0};
   float wv[32];
-  if (wfast) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (i < wcols && tid + 256 * i < g.Kp) wcol(tid + 256 * i, wb[i], wko[i]);
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
-      wv[j] = wb[i] >= 0 && oc < g.Co ? a.w[wb[i] + oc * wstep] : 0.f;
-    }
-  }
-  // epilogue operands of this lane's channels (N-tiles 0..3)
   float eb[4], es[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int oc = j * 16 + (tid & 15);
-    const bool ok = j < NT && oc < g.Co;
-    eb[j] = ok && a.bias ? a.bias[oc] : 0.f;
-    es[j] = ok && a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
-  }
-  const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
 
   // the zero-padded input patch: a thread owns one patch column, rows step by 256 / PW
   const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
@@ -142,18 +126,18 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   float pv[16], yo[16], sc[16];
   uint8_t bi[16];
   int at[16], sel[16];
-  // (the input dtype dispatched once around each batch: a per-load switch kept the loads apart)
-  auto load_rows = [&](auto tag) {  // 16 rows' loads (pooled input: value / argmax / gate / scale)
-    typedef decltype(tag) X;
+  auto load_rows = [&]() {  // 16 rows' loads (pooled input: value / argmax / gate / scale)
     const X* xs = static_cast<const X*>(a.x);
     const X* ys = static_cast<const X*>(a.pout);
-    if (!a.pidx) {
+    if constexpr (!PIN) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int ih = oh0 - g.pad + pr;
         const bool in = prow && rr < nrows;
         at[j] = in ? rr : -1;
-        pv[j] = (in && colv && ih >= 0 && ih < g.H) ? (float)xs[xbase + ((int64_t)ic * g.H + ih) * g.W + iw] : 0.f;
+        const bool ok = in && colv && ih >= 0 && ih < g.H;
+        const X t = xs[ok ? xbase + ((int64_t)ic * g.H + ih) * g.W + iw : xbase];
+        pv[j] = ok ? (float)t : 0.f;
         rr += rpi;
         pr += rpi;
         while (pr >= g.PR) {
@@ -170,10 +154,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
         at[j] = in ? rr : -1;
         sel[j] = ((ih & 1) << 1) | (iw & 1);
         const int64_t po = ok ? ((nc0 + ic) * g.Hp + (ih >> 1)) * g.Wp + (iw >> 1) : 0;
-        pv[j] = ok ? (float)xs[po] : 0.f;
-        yo[j] = ok ? (float)ys[po] : 0.f;
-        bi[j] = ok ? a.pidx[po] : (uint8_t)255;
-        sc[j] = ok ? (a.pscale ? a.pscale[nc0 + ic] : 1.f) : 0.f;
+        const X t0 = xs[po], t1 = ys[po];
+        const uint8_t t2 = a.pidx[po];
+        const float t3 = (a.pscale ? a.pscale : a.w)[ok && a.pscale ? nc0 + ic : 0];
+        pv[j] = ok ? (float)t0 : 0.f;
+        yo[j] = ok ? (float)t1 : 0.f;
+        bi[j] = ok ? t2 : (uint8_t)255;
+        sc[j] = ok ? (a.pscale ? t3 : 1.f) : 0.f;
         rr += rpi;
         pr += rpi;
         while (pr >= g.PR) {
@@ -183,17 +170,41 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       }
     }
   };
-  auto rows_round = [&]() {
-    if (a.x_dtype == kF32) load_rows(float{});
-    else if (a.x_dtype == kBF16) load_rows(__bf16{});
-    else load_rows(_Float16{});
-  };
   auto store_rows = [&]() {
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(a.pidx ? unpool(pv[j], bi[j], yo[j], sc[j], sel[j]) : pv[j]);
+      if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(PIN ? unpool(pv[j], bi[j], yo[j], sc[j], sel[j]) : pv[j]);
   };
-  rows_round();  // (first batch: in flight with the weight loads)
+  // issue order: the patch rows first, then the weights and epilogue
+  // operands in straight-line code, then a scheduling barrier so no conversion / store of a loaded
+  // value is hoisted between them (it would wait on its load mid-issue: a second round trip)
+  load_rows();
+  if (wfast) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (i < wcols && tid + 256 * i < g.Kp) wcol(tid + 256 * i, wb[i], wko[i]);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {  // (unconditional loads at a clamped address, then a select)
+      const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
+      const bool ok = wb[i] >= 0 && oc < g.Co;
+      const float t = a.w[ok ? wb[i] + oc * wstep : 0];
+      wv[j] = ok ? t : 0.f;
+    }
+  }
+  {  // epilogue operands of this lane's channels (N-tiles 0..3)
+    const float* bp = a.bias ? a.bias : a.w;        // (a valid address when absent: loads stay
+    const float* cp = a.chscale ? a.chscale : a.w;  // unconditional, no branch + wait per element)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oc = j * 16 + (tid & 15);
+      const bool ok = j < NT && oc < g.Co;
+      const float tb = bp[ok ? oc : 0], tc = cp[ok ? (int64_t)n * g.Co + oc : 0];
+      eb[j] = ok && a.bias ? tb : 0.f;
+      es[j] = ok && a.chscale ? tc : 1.f;
+    }
+  }
+  const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- while the loads fly: the Dropout2d draw (channel_mask_kernel's draw, index n*Co + oc)
   if (a.chscale_out) {
@@ -224,7 +235,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       koff[k] = ko;
       for (int oc0 = 0; oc0 < g.Cop; oc0 += 32) {  // (Cop: a multiple of 16)
 #pragma unroll
-        for (int j = 0; j < 32; ++j) wv[j] = base >= 0 && oc0 + j < g.Co ? a.w[base + (oc0 + j) * wstep] : 0.f;
+        for (int j = 0; j < 32; ++j) {
+          const bool ok = base >= 0 && oc0 + j < g.Co;
+          const float t = a.w[ok ? base + (oc0 + j) * wstep : 0];
+          wv[j] = ok ? t : 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < 32; ++j)
           if (oc0 + j < g.Cop) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(wv[j]);
@@ -233,7 +248,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   }
   store_rows();
   while (prow && rr < nrows) {
-    rows_round();
+    load_rows();
     store_rows();
   }
   __syncthreads();
@@ -329,10 +344,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   }
 }
 
-template <typename T>
+template <typename T, typename X, bool PIN>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T>(a, g, blockIdx.x, smem);
+  conv_fwd_body<T, X, PIN>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -356,12 +371,13 @@ struct WgradGeo {
   int nblocks;
 };
 
-template <typename T>
+// X: the input's element type, DY: dy's, PIN: dy given max-pooled (compile-time, see conv_fwd_body)
+template <typename T, typename X, typename DY, bool PIN>
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const WgradGeo& g, const int blk,
                                                 unsigned char* __restrict__ smem) {
   const void* __restrict__ x = wa.x;
   const void* __restrict__ dy = wa.dy;
-  const int xdt = wa.xdt, dydt = wa.dydt, N = wa.N;
+  const int N = wa.N;
   float* __restrict__ slab = wa.slab;
   typedef typename Mfma<T>::frag frag;
   typedef typename Stor<T>::S S;
@@ -411,15 +427,16 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     const bool colv = iw >= 0 && iw < g.W;
     float xv[16];
     int at[16];
-    auto load_rows = [&](auto tag) {  // (dtype dispatched once per batch, see conv_fwd_body)
-      typedef decltype(tag) X;
+    auto load_rows = [&]() {
       const X* xs = static_cast<const X*>(x);
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int ih = pr - g.pad;
         const bool in = prow && rr < nrows;
         at[j] = in ? rr : -1;
-        xv[j] = (in && colv && ih >= 0 && ih < g.H) ? (float)xs[xb + ((int64_t)ic * g.H + ih) * g.W + iw] : 0.f;
+        const bool ok = in && colv && ih >= 0 && ih < g.H;
+        const X t = xs[ok ? xb + ((int64_t)ic * g.H + ih) * g.W + iw : xb];
+        xv[j] = ok ? (float)t : 0.f;
         rr += rpi;
         pr += rpi;
         while (pr >= g.PR) {
@@ -427,11 +444,6 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
           ++ic;
         }
       }
-    };
-    auto rows_round = [&]() {
-      if (xdt == kF32) load_rows(float{});
-      else if (xdt == kBF16) load_rows(__bf16{});
-      else load_rows(_Float16{});
     };
     auto store_rows = [&]() {
 #pragma unroll
@@ -449,36 +461,36 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     float dv[16], yo[16], sc[16];
     uint8_t bi[16];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
-    bool d_more = wa.pidx ? (gq < wgr && q0 < npixp && gq * 16 < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
-    auto load_dy = [&](auto tag) {  // one chunk's loads
-      typedef decltype(tag) X;
-      const X* ys = static_cast<const X*>(dy);
-      if (!wa.pidx) {
+    bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * 16 < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
+    auto load_dy = [&]() {  // one chunk's loads
+      const DY* ys = static_cast<const DY*>(dy);
+      if constexpr (!PIN) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          dv[j] = (d_oc0 + j < g.Co && d_p < g.npix) ? (float)ys[yb + (int64_t)(d_oc0 + j) * g.npix + d_p] : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          const bool ok = d_oc0 + j < g.Co && d_p < g.npix;
+          const DY t = ys[ok ? yb + (int64_t)(d_oc0 + j) * g.npix + d_p : yb];
+          dv[j] = ok ? (float)t : 0.f;
+        }
       } else {
-        const X* os = static_cast<const X*>(wa.pout);
+        const DY* os = static_cast<const DY*>(wa.pout);
         const int ph = d_q / PWp, pw = d_q - ph * PWp;
         d_pb = 2 * ph * g.OW + 2 * pw;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const bool ok = d_oc0 + j < g.Co;
-          const int64_t po = ok ? ybp + (int64_t)(d_oc0 + j) * npixp + d_q : 0;
-          dv[j] = ok ? (float)ys[po] : 0.f;
-          yo[j] = ok ? (float)os[po] : 0.f;
-          bi[j] = ok ? wa.pidx[po] : (uint8_t)255;
-          sc[j] = ok ? (wa.pscale ? wa.pscale[(int64_t)n * g.Co + d_oc0 + j] : 1.f) : 0.f;
+          const int64_t po = ok ? ybp + (int64_t)(d_oc0 + j) * npixp + d_q : ybp;
+          const DY t0 = ys[po], t1 = os[po];
+          const uint8_t t2 = wa.pidx[po];
+          const float t3 = (wa.pscale ? wa.pscale : wa.slab)[ok && wa.pscale ? (int64_t)n * g.Co + d_oc0 + j : 0];
+          dv[j] = ok ? (float)t0 : 0.f;
+          yo[j] = ok ? (float)t1 : 0.f;
+          bi[j] = ok ? t2 : (uint8_t)255;
+          sc[j] = ok ? (wa.pscale ? t3 : 1.f) : 0.f;
         }
       }
     };
-    auto dy_round = [&]() {
-      if (dydt == kF32) load_dy(float{});
-      else if (dydt == kBF16) load_dy(__bf16{});
-      else load_dy(_Float16{});
-    };
     auto store_dy_next = [&]() {  // store the loaded chunk, advance to the next one
-      if (!wa.pidx) {
+      if constexpr (!PIN) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) dys[(d_oc0 + j) * LDY + d_p] = Stor<T>::of(dv[j]);
         d_oc0 += ocg * 8;
@@ -503,22 +515,23 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         d_more = d_q < npixp;
       }
     };
-    if (wa.pidx) d_oc0 = gq * 16;
+    if (PIN) d_oc0 = gq * 16;
 
-    rows_round();             // round 1: patch rows ...
-    if (d_more) dy_round();   // ... and the first dy chunk in flight together
+    load_rows();              // round 1: patch rows ...
+    if (d_more) load_dy();    // ... and the first dy chunk in flight together
+    __builtin_amdgcn_sched_barrier(0);  // (no use of a loaded value hoisted between the loads)
     store_rows();
     if (d_more) store_dy_next();
     while (prow && rr < nrows) {
-      rows_round();
+      load_rows();
       store_rows();
     }
     while (d_more) {
-      dy_round();
+      load_dy();
       store_dy_next();
     }
     if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
-    if (wa.pidx) {  // (the MFMA K padding past npix: the window writes cover pixels < npix only)
+    if (PIN) {  // (the MFMA K padding past npix: the window writes cover pixels < npix only)
       for (int i = tid; i < g.Cop * (g.npp - g.npix); i += 256) {
         const int oc = i / (g.npp - g.npix), pp = g.npix + i % (g.npp - g.npix);
         dys[oc * LDY + pp] = Stor<T>::of(0.f);
@@ -601,21 +614,21 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   }
 }
 
-template <typename T>
+template <typename T, typename X, typename DY, bool PIN>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_wgrad_body<T>(wa, g, blockIdx.x, smem);
+  conv_wgrad_body<T, X, DY, PIN>(wa, g, blockIdx.x, smem);
 }
 
 // The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
 // partial slabs, the rest compute the data gradient (conv_fwd_body in mode 1); both read the same
 // (possibly pooled) dy.  A second launch for the data gradient was a kernel boundary (~1.4 us in a
 // graph) plus its own ramp.
-template <typename T>
+template <typename T, typename X, typename DY, bool PIN>
 __global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T>(wa, wg, blockIdx.x, smem);
-  else conv_fwd_body<T>(a, g, blockIdx.x - wg.nblocks, smem);
+  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN>(wa, wg, blockIdx.x, smem);
+  else conv_fwd_body<T, DY, PIN>(a, g, blockIdx.x - wg.nblocks, smem);
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
@@ -636,7 +649,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     for (; b < b1; b += 16) {  // 16 loads in flight (a slice of up to 16 partials: one round trip)
       float v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = b + u < b1 ? slab[(int64_t)(b + u) * L + i] : 0.f;
+      for (int u = 0; u < 16; ++u) v[u] = slab[(int64_t)(b + u < b1 ? b + u : b0) * L + i];  // (unconditional)
 #pragma unroll
       for (int u = 0; u < 16; ++u)
         if (b + u < b1) s += v[u];
@@ -657,6 +670,18 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 }
 
 inline int rup(int a, int b) { return (a + b - 1) / b * b; }
+
+// An operand's element type for compute type T: fp32, or T's own 16-bit type (the instantiated
+// combinations; anything else is rejected and the caller converts first)
+template <typename T, typename F>
+hipError_t with_in_type(int dt, F&& f) {
+  if (dt == kF32) return f(float{});
+  if constexpr (!__is_same(T, float)) {
+    constexpr int code = __is_same(T, __bf16) ? kBF16 : kF16;
+    if (dt == code) return f(T{});
+  }
+  return hipErrorInvalidValue;
+}
 
 }  // namespace
 
@@ -710,11 +735,17 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   hipError_t e = conv_geo(a, g, lds, grid);
   if (e != hipSuccess || grid == 0) return e;
   CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_fwd_kernel<scalar_t>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv_fwd_kernel<scalar_t>, dim3(grid), dim3(256), lds, s, a, g);
+    return with_in_type<scalar_t>(a.x_dtype, [&](auto xt) -> hipError_t {
+      typedef decltype(xt) X;
+      auto go = [&](auto kern) {
+        if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a, g);
+        return hipGetLastError();
+      };
+      return a.pidx ? go(conv_fwd_kernel<scalar_t, X, true>) : go(conv_fwd_kernel<scalar_t, X, false>);
+    });
   });
-  return hipGetLastError();
+  return hipSuccess;
 }
 
 static WgradGeo wgrad_geo(int N, int IC, int H, int W, int OC, int KH, int KW, int pad) {
@@ -770,18 +801,34 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
     if (g.OH != b.H || g.OW != b.W) return hipErrorInvalidValue;
     lds = std::max(lds, dl);
   }
-  CSED_DISPATCH_COMPUTE(b.mfma_dtype, {
-    if (dgrid > 0) {
-      if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_bwd_kernel<scalar_t>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(conv_bwd_kernel<scalar_t>, dim3(wg.nblocks + dgrid), dim3(256), lds, s, wa, wg, a, g);
-    } else {
-      if (lds > 64 * 1024) hipFuncSetAttribute((const void*)conv_wgrad_kernel<scalar_t>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(conv_wgrad_kernel<scalar_t>, dim3(wg.nblocks), dim3(256), lds, s, wa, wg);
-    }
-  });
-  hipError_t e = hipGetLastError();
+  hipError_t e = hipSuccess;
+  auto launch = [&](auto ct) -> hipError_t {
+    typedef decltype(ct) T;
+    return with_in_type<T>(b.x_dtype, [&](auto xt) -> hipError_t {
+      return with_in_type<T>(b.dy_dtype, [&](auto yt) -> hipError_t {
+        typedef decltype(xt) X;
+        typedef decltype(yt) DY;
+        auto go = [&](auto bwd, auto wgr) {
+          if (dgrid > 0) {
+            if (lds > 64 * 1024) hipFuncSetAttribute((const void*)bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(bwd, dim3(wg.nblocks + dgrid), dim3(256), lds, s, wa, wg, a, g);
+          } else {
+            if (lds > 64 * 1024) hipFuncSetAttribute((const void*)wgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(wgr, dim3(wg.nblocks), dim3(256), lds, s, wa, wg);
+          }
+          return hipGetLastError();
+        };
+        return b.pidx ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true>)
+                      : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false>);
+      });
+    });
+  };
+  switch (b.mfma_dtype) {
+    case kBF16: e = launch(__bf16{}); break;
+    case kF16: e = launch(_Float16{}); break;
+    case kF32: e = launch(float{}); break;
+    default: return hipErrorInvalidValue;
+  }
   if (e != hipSuccess) return e;
   const int L = b.OC * (wg.K + 1);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, b.ws, wg.nblocks, b.OC, wg.K, b.dw,
