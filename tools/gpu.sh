@@ -18,6 +18,7 @@
 #   pmc       three rocprofv3 --pmc passes over the train kernel (B=64), one over B=8,
 #             and three over the tile kernel (B=1024)
 #   modular   the modular engine: fusion + op tests, graph step times (B = 64), a kernel trace
+#   abops     tools/op_probe.py (per-op launch times of the modular step) for every ab/*_C.so build
 #   modpmc    one rocprofv3 --pmc pass over the modular step's kernels (fetch / memory waits)
 #   ddp       tools/ddp_overlap.py: the modular engine's bucketed reducer, per-bucket all-reduce on the
 #             comm stream vs after backward, step times + overlap share from kernel traces
@@ -100,6 +101,14 @@ task_modular() {  # the modular (per-op) engine: fusion / op tests, graph step t
 task_modpmc() {  # one PMC pass over the modular step's kernels (instruction-fetch vs memory waits)
   cd /tmp && export TMPDIR=/tmp && \
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_IFETCH SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $O/${T}_modpmc -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph eager > $O/${T}_modpmc.log 2>&1
+}
+
+task_abops() {  # per-op launch times of the modular step (tools/op_probe.py) for every ab/*_C.so build
+  cd $R && rm -f $O/${T}_abops.log && \
+  for i in $(seq ${N_AB:-2}); do for so in ab/*_C.so; do
+    echo "== $so" >> $O/${T}_abops.log && \
+    CSED_NATIVE_SO=$R/$so py 120 python tools/op_probe.py >> $O/${T}_abops.log 2>&1 || return 1
+  done; done
 }
 
 task_ddp() {  # the modular engine's bucketed reducer: step times per mode + overlap from kernel traces
