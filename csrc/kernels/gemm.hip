@@ -271,35 +271,33 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 // ran these as a chain of 1-10 dependent K-tiles on 1-6 workgroups plus a split-K reduce launch
 // (7-20 us each in the modular step's kernel trace, profiles/round5.md).
 // Lane (l16, kq) holds A[row l16][k 8kq .. 8kq+7] and B[k 8kq .. 8kq+7][col l16] (Mfma<T> layout).
-// Operand gathers are branch-free: eight dword loads at clamped addresses (the containing word of a
-// 16- / 8-bit element), the element extracted and converted only after every load of the K-steps is
-// issued.  (A dtype switch or a per-lane vector / scalar choice around the loads made the compiler
-// copy each loaded register at the join: a wait per load, the loads one round trip after another.)
-__device__ __forceinline__ int elem_size(int dt) { return dt == kF32 ? 4 : dt == kU8 ? 1 : 2; }
-
-__device__ __forceinline__ void gather8_words(uint32_t (&w)[8], const void* X, int es, int64_t off, int64_t sk,
-                                              int nk) {
-  const char* b = static_cast<const char*>(X);
+template <typename T>
+__device__ __forceinline__ void gather8(float (&f)[8], const void* X, int dt, int64_t off, int64_t sk, int nk,
+                                        bool vec) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) X_t;
+    const X_t* p = static_cast<const X_t*>(X) + off;
+    if (vec && nk == 8) {  // K-contiguous, 16-byte aligned (kKContig): one or two vector loads
+      if constexpr (sizeof(X_t) == 2) {
+        typedef X_t v8 __attribute__((ext_vector_type(8)));
+        const v8 q = *reinterpret_cast<const v8*>(p);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uintptr_t ad = reinterpret_cast<uintptr_t>(b + (off + (int64_t)(j < nk ? j : 0) * sk) * es);
-    w[j] = *reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
-  }
-}
-
-__device__ __forceinline__ void words_to_f32(float (&f)[8], const uint32_t (&w)[8], const void* X, int dt, int es,
-                                             int64_t off, int64_t sk, int nk) {
-  const uintptr_t b = reinterpret_cast<uintptr_t>(X);
+        for (int j = 0; j < 8; ++j) f[j] = (float)q[j];
+        return;
+      } else if constexpr (sizeof(X_t) == 4) {
+        const float4 q0 = *reinterpret_cast<const float4*>(p), q1 = *reinterpret_cast<const float4*>(p + 4);
+        f[0] = q0.x; f[1] = q0.y; f[2] = q0.z; f[3] = q0.w; f[4] = q1.x; f[5] = q1.y; f[6] = q1.z; f[7] = q1.w;
+        return;
+      }
+    }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t sh = (uint32_t)((b + (uintptr_t)((off + (int64_t)(j < nk ? j : 0) * sk) * es)) & 3) * 8;
-    const uint32_t v = w[j] >> sh;
-    float x;
-    if (dt == kF32) x = __uint_as_float(w[j]);
-    else if (dt == kBF16) x = __uint_as_float(v << 16);
-    else if (dt == kF16) x = (float)__builtin_bit_cast(_Float16, (unsigned short)(v & 0xffffu));
-    else x = (float)(v & 0xffu);
-    f[j] = j < nk ? x : 0.f;
+    for (int j = 0; j < 8; ++j) f[j] = j < nk ? (float)p[j * sk] : 0.f;
+  };
+  switch (dt) {
+    case kF32: run(float{}); break;
+    case kBF16: run(__bf16{}); break;
+    case kF16: run(_Float16{}); break;
+    default: run(uint8_t{}); break;
   }
 }
 
@@ -364,79 +362,56 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   const int mt = blk / tn, nt = blk - mt * tn;
   const int m = mt * 16 + l16, n = nt * 16 + l16;
   const bool mv = m < a.M;
-  const int esa = elem_size(a.a_dtype), esb = elem_size(a.b_dtype);
-  const void* gsrc = a.G ? a.G : a.A;  // (the gate's loads stay unconditional: A stands in)
-  const int gdt = a.G ? a.g_dtype : a.a_dtype, esg = elem_size(gdt);
-  const int nb = n < a.N ? n : 0;  // (B loads of the ones / padding columns at a valid column)
+  const bool avec = a.a_mode == kKContig, bvec = a.b_mode == kKContig;
   // this wave's K-steps [ks0, ks1) of 32
   const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
   const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  // epilogue operands loaded ahead of the K loop, unconditionally from valid addresses (used at the
-  // end: at the end they were one more dependent round trip): the column bias, the dropout offset
-  const float* bsrc = a.bias ? a.bias : static_cast<const float*>(a.C);
-  const float bias_raw = bsrc[n < a.N ? n : 0];
-  const int64_t* osrc = a.offset_dev ? a.offset_dev : static_cast<const int64_t*>(a.C);
-  const int64_t off_raw = osrc[0];
-  // the head's targets of this lane's 4 rows
+  // epilogue operands loaded ahead of the K loop (at the end they were one more dependent round
+  // trip): this lane's column bias and the dropout offset counter
+  const float bias_v = wave == 0 && a.bias && n < a.N ? a.bias[n] : 0.f;
+  const uint64_t off = wave == 0 && a.act == 2 ? rng_offset(a.offset, a.offset_dev) : 0;
+  // the head's targets of this lane's 4 rows (loaded ahead of the K loop)
   int64_t tgt[4] = {-1, -1, -1, -1};
-  if constexpr (HEAD) {
-    const int64_t* tsrc = a.head_part ? a.head_target : static_cast<const int64_t*>(a.C);
+  if (HEAD && a.head_part && wave == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int mm = mt * 16 + 4 * kq + r;
-      tgt[r] = tsrc[mm < a.M ? mm : 0];
+      tgt[r] = mm < a.M ? a.head_target[mm] : -1;
     }
   }
-  // the loss head's dz (a.lsm_target): the scalar upstream gradient
-  const float lsm_raw = (a.lsm_target ? a.lsm_gout : static_cast<const float*>(a.C))[0];
+  // the loss head's dz (a.lsm_target): the scalar upstream gradient, loaded once
+  const float lsm_g = a.lsm_target ? a.lsm_gout[0] / a.lsm_div : 0.f;
   for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
     float fa[4][8], fb[4][8], fg[4][8];
-    uint32_t wa[4][8], wb[4][8], wg[4][8];
-    // ---- every load of the 4 K-steps first
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int kb = (kb0 + u) * 32 + 8 * kq;
       const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
       const int kc = min(kb, a.K - 1);
-      const int64_t ao = (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak;
-      gather8_words(wa[u], a.A, esa, ao, a.sak, nk);
-      if (a.G) gather8_words(wg[u], gsrc, esg, ao, a.sak, nk);
-      gather8_words(wb[u], a.B, esb, (int64_t)kc * a.sbk + (int64_t)nb * a.sbn, a.sbk, nk);
-    }
-    // ---- then the conversions
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int kb = (kb0 + u) * 32 + 8 * kq;
-      const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
-      const int kc = min(kb, a.K - 1);
-      const int64_t ao = (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak;
-      words_to_f32(fa[u], wa[u], a.A, a.a_dtype, esa, ao, a.sak, mv ? nk : 0);
-      if (a.G) words_to_f32(fg[u], wg[u], gsrc, gdt, esg, ao, a.sak, mv ? nk : 0);
-      words_to_f32(fb[u], wb[u], a.B, a.b_dtype, esb, (int64_t)kc * a.sbk + (int64_t)nb * a.sbn, a.sbk, nk);
-      if (n >= a.N) {
+      gather8<T>(fa[u], a.A, a.a_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak, a.sak, mv ? nk : 0,
+                 avec);
+      if (a.G)
+        gather8<T>(fg[u], a.G, a.g_dtype, (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak, a.sak, mv ? nk : 0,
+                   avec);
+      if (n < a.N) {
+        gather8<T>(fb[u], a.B, a.b_dtype, (int64_t)kc * a.sbk + (int64_t)n * a.sbn, a.sbk, nk, bvec);
+      } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) fb[u][j] = (n == a.N && j < nk) ? 1.f : 0.f;  // the ones column / padding
       }
     }
     if (a.lsm_target) {  // log-probs -> dz = g * (exp(logp) - onehot(target)) (lsm_nll_bwd_kernel's rule)
-      const float lsm_g = lsm_raw / a.lsm_div;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int kb = (kb0 + u) * 32 + 8 * kq;
         const int nk = kb0 + u < ks1 ? min(8, max(0, a.K - kb)) : 0;
-        int64_t tl[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {  // (the target loads unconditional and together, then the math)
-          const bool in = mv && j < nk;
-          tl[j] = a.lsm_target[in ? (a.lsm_rows_are_m ? m : kb + j) : 0];
-        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool in = mv && j < nk;
-          const int c = a.lsm_rows_are_m ? kb + j : m;
-          const float e = lsm_g * (__expf(fa[u][j]) - ((int64_t)c == tl[j] ? 1.f : 0.f));
-          fa[u][j] = in ? e : 0.f;
+          const int r = a.lsm_rows_are_m ? m : kb + j, c = a.lsm_rows_are_m ? kb + j : m;
+          const int64_t t = in ? a.lsm_target[r] : -1;
+          fa[u][j] = in ? lsm_g * (__expf(fa[u][j]) - (c == t ? 1.f : 0.f)) : 0.f;
         }
       }
     }
@@ -455,8 +430,6 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
   for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
   __syncthreads();
   if (wave != 0) return;
-  const float bias_v = a.bias && n < a.N ? bias_raw : 0.f;
-  const uint64_t off = a.offset + (a.offset_dev ? ((uint64_t)off_raw << 20) : 0ull);  // (rng_offset)
   if (HEAD && a.head_part) {  // classifier head: log_softmax rows + NLL (one 16-column tile holds a row)
     float v[4];
 #pragma unroll
