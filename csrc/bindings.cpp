@@ -346,7 +346,7 @@ void colsum(const Tensor& x, const optional<Tensor>& gate, double gate_scale, Te
 void conv2d_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, Tensor& y, int64_t pad,
                 const optional<Tensor>& idx, const optional<Tensor>& chscale, int64_t pool_k, int64_t mfma_dtype,
                 double drop2d_p, int64_t seed, int64_t offset, const optional<Tensor>& offset_dev,
-                const optional<Tensor>& chscale_out) {
+                const optional<Tensor>& chscale_out, const optional<Tensor>& dbg) {
   dev(x, "x"); dev(w, "w"); dev(y, "y");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.scalar_type() == at::kFloat && x.size(1) == w.size(1));
   const int N = x.size(0), IC = x.size(1), H = x.size(2), W = x.size(3);
@@ -375,6 +375,12 @@ void conv2d_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, 
   a.drop_p = (float)drop2d_p; a.seed = (uint64_t)seed; a.offset = (uint64_t)offset;
   a.offset_dev = optpt<int64_t>(offset_dev);
   a.chscale_out = chscale_out.has_value() ? chscale_out->data_ptr<float>() : nullptr;
+  if (dbg.has_value()) {
+    dev(*dbg, "dbg");
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= (int64_t)N * ((OH + 1) / 2 + 1) * 8,
+                "conv2d_fwd: dbg must be int64 [>= blocks * 8]");
+    a.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr<int64_t>());
+  }
   CHECK_HIP(csed::launch_conv2d(a, cur_stream(x)));
 }
 
@@ -759,7 +765,7 @@ TORCH_LIBRARY(csed, m) {
   m.def("colsum(Tensor x, Tensor? gate, float gate_scale, Tensor(a!) out, float beta) -> ()");
   m.def("conv2d_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, int pad, Tensor(b!)? idx, Tensor? chscale, "
         "int pool_k, int mfma_dtype, float drop2d_p=0.0, int seed=0, int offset=0, Tensor? offset_dev=None, "
-        "Tensor(c!)? chscale_out=None) -> ()");
+        "Tensor(c!)? chscale_out=None, Tensor(d!)? dbg=None) -> ()");
   m.def("conv2d_bwd(Tensor x, Tensor dy, Tensor w, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, Tensor(d!)? dx, "
         "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype) -> ()");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? gate, float gate_scale, Tensor(a!)? dx, Tensor(b!)? dw, "

@@ -91,6 +91,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   const int npix = rows * g.OW;
   const int tid = threadIdx.x;
   const int NT = g.Cop >> 4;
+#define CONV_STAMP(i) \
+  if (a.dbg && tid == 0) a.dbg[(int64_t)blk * 8 + (i)] = __builtin_amdgcn_s_memtime();
+  CONV_STAMP(0);
 
   // ---- staging in ONE memory round trip: every global load of the weights (up to 32 per thread),
   // the first 16 patch rows and the epilogue operands is issued before any LDS store, the Dropout2d
@@ -205,6 +208,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   }
   const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
   __builtin_amdgcn_sched_barrier(0);
+  CONV_STAMP(1);
 
   // ---- while the loads fly: the Dropout2d draw (channel_mask_kernel's draw, index n*Co + oc)
   if (a.chscale_out) {
@@ -251,7 +255,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     load_rows();
     store_rows();
   }
+  CONV_STAMP(2);
   __syncthreads();
+  CONV_STAMP(3);
 
   const int lane = tid & 63, wave = tid >> 6;
   const int mtiles = (npix + 15) >> 4;
@@ -342,6 +348,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       }
     }
   }
+  CONV_STAMP(4);
+#undef CONV_STAMP
 }
 
 template <typename T, typename X, bool PIN>

@@ -145,6 +145,7 @@ struct ConvArgs {
   int mfma_dtype;
   float drop_p; uint64_t seed, offset; const int64_t* offset_dev; float* chscale_out;
   const uint8_t* pidx; const void* pout; const float* pscale;
+  uint64_t* dbg;  // optional [grid, 8] s_memtime stamps per block (diagnostics, tools/conv_stamps.py)
 };
 hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s);
 // Backward of y = conv(x, w, b, pad) [+ maxpool2 + relu + channel scale]: the weight / bias
