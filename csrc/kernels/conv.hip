@@ -75,7 +75,7 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // X: the input's element type, PIN: the input is given max-pooled (a.pidx) -- compile-time, so the
 // staging's loads are straight-line code (a runtime dtype / mode branch around them made the
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
-template <typename T, typename X, bool PIN>
+template <typename T, typename X, typename Y, bool PIN>  // Y: the output's element type
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
                                               unsigned char* __restrict__ smem) {
   typedef typename Mfma<T>::frag frag;
@@ -358,7 +358,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
           if (a.chscale_out && band == 0 && wbase == 0) a.chscale_out[(int64_t)n * g.Co + oc] = sc;  // once per (n, oc)
           const float v = fmaxf(best + b, 0.f) * sc;
           const int64_t o = (((int64_t)n * g.Co + oc) * PH + ph) * PWb + pw;
-          stf(a.y, a.y_dtype, o, v);
+          static_cast<Y*>(a.y)[o] = (Y)v;
           a.idx[o] = (uint8_t)bi;
         } else {
 #pragma unroll
@@ -366,7 +366,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
             const int mm = mt * 16 + 4 * (lane >> 4) + r;
             if (mm >= npix) continue;
             const int ohh = oh0 + mm / g.OW, oww = mm % g.OW;
-            stf(a.y, a.y_dtype, (((int64_t)n * g.Co + oc) * g.OH + ohh) * g.OW + oww, acc[j][r] + b);
+            static_cast<Y*>(a.y)[(((int64_t)n * g.Co + oc) * g.OH + ohh) * g.OW + oww] = (Y)(acc[j][r] + b);
           }
         }
       }
@@ -376,10 +376,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 #undef CONV_STAMP
 }
 
-template <typename T, typename X, bool PIN>
+template <typename T, typename X, typename Y, bool PIN>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T, X, PIN>(a, g, blockIdx.x, smem);
+  conv_fwd_body<T, X, Y, PIN>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -660,7 +660,7 @@ template <typename T, typename X, typename DY, bool PIN>
 __global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN>(wa, wg, blockIdx.x, smem);
-  else conv_fwd_body<T, DY, PIN>(a, g, blockIdx.x - wg.nblocks, smem);
+  else conv_fwd_body<T, DY, X, PIN>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
@@ -768,13 +768,16 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   if (e != hipSuccess || grid == 0) return e;
   CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
     return with_in_type<scalar_t>(a.x_dtype, [&](auto xt) -> hipError_t {
-      typedef decltype(xt) X;
-      auto go = [&](auto kern) {
-        if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a, g);
-        return hipGetLastError();
-      };
-      return a.pidx ? go(conv_fwd_kernel<scalar_t, X, true>) : go(conv_fwd_kernel<scalar_t, X, false>);
+      return with_in_type<scalar_t>(a.y_dtype, [&](auto yt) -> hipError_t {
+        typedef decltype(xt) X;
+        typedef decltype(yt) Y;
+        auto go = [&](auto kern) {
+          if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a, g);
+          return hipGetLastError();
+        };
+        return a.pidx ? go(conv_fwd_kernel<scalar_t, X, Y, true>) : go(conv_fwd_kernel<scalar_t, X, Y, false>);
+      });
     });
   });
   return hipSuccess;
@@ -822,6 +825,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
   ConvGeo g{};
   int dgrid = 0;
   if (b.dx) {
+    if (b.dx_dtype != b.x_dtype) return hipErrorInvalidValue;  // (the data gradient has x's dtype)
     a.x = b.dy; a.x_dtype = b.dy_dtype; a.w = b.w; a.bias = nullptr;
     a.y = b.dx; a.y_dtype = b.dx_dtype;
     a.N = b.N; a.IC = b.OC; a.H = wg.OH; a.W = wg.OW; a.OC = b.IC; a.KH = b.KH; a.KW = b.KW; a.pad = b.pad;
