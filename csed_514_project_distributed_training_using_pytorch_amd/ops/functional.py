@@ -96,6 +96,8 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, pad, pool, chscale, drop):
         x = x.contiguous()
+        if x.dtype not in (torch.float32, _compute_dtype):  # (the kernels take fp32 or the compute dtype)
+            x = x.to(_compute_dtype)
         N, IC, H, W = x.shape
         OC, _, KH, KW = w.shape
         OH, OW = H + 2 * pad - KH + 1, W + 2 * pad - KW + 1
