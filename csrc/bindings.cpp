@@ -318,6 +318,18 @@ void linear_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const option
                     dy.scalar_type() == at::kFloat && !gate.has_value() && lsm_target->scalar_type() == at::kLong &&
                     lsm_target->numel() == dy.size(0) && lsm_target->is_contiguous(),
                 "linear_bwd: the loss-head form needs fp32 log-probs, int64 targets, a scalar gout, no gate");
+    bool small = true;
+    for (const auto& a : todo) small = small && csed::gemm_is_small(a);
+    if (!small) {  // (large batches: dz materialised by the loss-backward kernel, then plain GEMMs)
+      const int red = lsm_div == 1.0 ? 2 : 1;
+      TORCH_CHECK(red == 2 || lsm_div == (double)dy.size(0), "linear_bwd: lsm_div must be 1 (sum) or rows (mean)");
+      Tensor dz = at::empty_like(dy);
+      CHECK_HIP(csed::launch_lsm_nll_bwd(lsm_gout->data_ptr<float>(), dy.data_ptr<float>(),
+                                         lsm_target->data_ptr<int64_t>(), dz.data_ptr(), csed::kF32, (int)dy.size(0),
+                                         (int)dy.size(1), red, cur_stream(dy)));
+      linear_bwd(dz, x, w, gate, gate_scale, dx, dw, db, mfma_dtype, none, none, 1.0);
+      return;
+    }
     for (size_t i = 0; i < todo.size(); ++i) {
       todo[i].lsm_target = lsm_target->data_ptr<int64_t>();
       todo[i].lsm_gout = lsm_gout->data_ptr<float>();

@@ -523,6 +523,8 @@ static bool gemm_small(const GemmArgs& a) {
   return cdiv(a.M, 16) * cdiv(Np, 16) <= 1024 && a.K <= 1024;
 }
 
+bool gemm_is_small(const GemmArgs& a) { return gemm_small(a); }
+
 int gemm_splits(const GemmArgs& a) {
   if (gemm_small(a)) return 1;
   const int Np = a.N + (a.rowsum ? 1 : 0);

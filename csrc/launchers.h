@@ -111,6 +111,7 @@ struct GemmArgs {
 bool gemm_head_ok(const GemmArgs& a);
 // Number of K splits launch_gemm will use for these shapes (1 = no workspace needed).
 int gemm_splits(const GemmArgs& a);
+bool gemm_is_small(const GemmArgs& a);  // the small-GEMM path (few 16 x 16 tiles, K <= 1024)
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 // Two independent GEMMs of the small-GEMM path in one launch (nn.Linear's backward); pairable ==
 // both fit that path (few 16 x 16 tiles, K <= 1024) with the same compute dtype.

@@ -216,3 +216,24 @@ def test_head_forward_matches_gemm_then_loss(dt, rows, red):
         torch.testing.assert_close(lp, lp_ref, rtol=0, atol=2e-6)
         torch.testing.assert_close(out, out_ref, rtol=2e-6, atol=2e-6)
         assert int(cnt.item()) == 0
+
+
+@pytest.mark.parametrize("rows", [4096, 20000])
+def test_head_large_batch_fallback(rows):
+    """Past the small-GEMM path (K = batch > 1024 in dW, more than 1024 row tiles) the head runs
+    gemm + loss kernel forward and materialises dz backward; same values as the fp32 reference."""
+    g = torch.Generator(device=DEV).manual_seed(10)
+    x = torch.randn(rows, 50, device=DEV, generator=g).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(10, 50, device=DEV, generator=g) * 0.3).requires_grad_(True)
+    b = torch.randn(10, device=DEV, generator=g).requires_grad_(True)
+    t = torch.randint(0, 10, (rows,), device=DEV, generator=g)
+    loss = ops.linear_log_softmax_nll(x, w, b, t)
+    loss.backward()
+    xr = x.detach().float().cpu().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().cpu().requires_grad_(True)
+    br = b.detach().cpu().requires_grad_(True)
+    lr = F.nll_loss(F.log_softmax(F.linear(xr, wr, br), 1), t.cpu())
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-3 * abs(lr.item())
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert (got.float().cpu() - ref).abs().max().item() <= 3e-2 * max(ref.abs().max().item(), 1e-6)
