@@ -819,6 +819,8 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
   const size_t lds_red = (size_t)4 * 4 * 16 * 16 * 4;
   size_t lds = std::max(lds_main, lds_red);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+  const size_t lds_w = lds;  // (the weight-gradient launch alone)
+  size_t lds_d = 0;          // (the data-gradient launch alone)
   WgradArgs wa{b.x, b.x_dtype, b.dy, b.dy_dtype, b.pidx, b.pout, b.pscale, b.N, b.ws};
   // the data gradient (optional): conv of dy (un-pooled on load) with the flipped weights
   ConvArgs a{};
@@ -836,6 +838,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
     if (e != hipSuccess) return e;
     if (g.OH != b.H || g.OW != b.W) return hipErrorInvalidValue;
     lds = std::max(lds, dl);
+    lds_d = dl;
   }
   hipError_t e = hipSuccess;
   auto launch = [&](auto ct) -> hipError_t {
@@ -844,18 +847,28 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
       return with_in_type<T>(b.dy_dtype, [&](auto yt) -> hipError_t {
         typedef decltype(xt) X;
         typedef decltype(yt) DY;
-        auto go = [&](auto bwd, auto wgr) {
-          if (dgrid > 0) {
+        // one launch for both while the grid is about one wave of the chip; past that the merged
+        // kernel's register budget (the wgrad body's) would cap the many data-gradient blocks'
+        // occupancy, so they run as their own launch (B = 4096: 750 -> see profiles/round5.md)
+        const bool merged = dgrid > 0 && wg.nblocks + dgrid <= 2 * 256;
+        auto go = [&](auto bwd, auto wgr, auto dgr) {
+          if (merged) {
             if (lds > 64 * 1024) hipFuncSetAttribute((const void*)bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(bwd, dim3(wg.nblocks + dgrid), dim3(256), lds, s, wa, wg, a, g);
-          } else {
-            if (lds > 64 * 1024) hipFuncSetAttribute((const void*)wgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(wgr, dim3(wg.nblocks), dim3(256), lds, s, wa, wg);
+            return hipGetLastError();
           }
+          if (lds_w > 64 * 1024) hipFuncSetAttribute((const void*)wgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);
+          hipLaunchKernelGGL(wgr, dim3(wg.nblocks), dim3(256), lds_w, s, wa, wg);
+          hipError_t e2 = hipGetLastError();
+          if (e2 != hipSuccess || dgrid == 0) return e2;
+          if (lds_d > 64 * 1024) hipFuncSetAttribute((const void*)dgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
+          hipLaunchKernelGGL(dgr, dim3(dgrid), dim3(256), lds_d, s, a, g);
           return hipGetLastError();
         };
-        return b.pidx ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true>)
-                      : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false>);
+        return b.pidx ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true>,
+                           conv_fwd_kernel<T, DY, X, true>)
+                      : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false>,
+                           conv_fwd_kernel<T, DY, X, false>);
       });
     });
   };
