@@ -76,7 +76,7 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // staging's loads are straight-line code (a runtime dtype / mode branch around them made the
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
 template <typename T, typename X, typename Y, bool PIN>  // Y: the output's element type
-__device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk, const int nblk,
+__device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
                                               unsigned char* __restrict__ smem) {
   typedef typename Mfma<T>::frag frag;
   typedef typename Stor<T>::S S;
@@ -85,15 +85,14 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   int* koff = (int*)(Ws + g.Cop * LDW);             // [Kp]
   S* patch = (S*)(koff + g.Kp);                     // [Ci][PR][PW]
 
-  // Work items: (image, band) pairs it = blk, blk + nblk, ... (one per block at small batch; a
-  // large batch loops, the weights staged once and the next item's patch loads issued while the
-  // current one is on the MFMAs)
-  const int items = a.N * g.bands;
+  const int n = blk / g.bands, band = blk % g.bands;
+  const int oh0 = band * g.TR;
+  const int rows = min(g.TR, g.OH - oh0);
+  const int npix = rows * g.OW;
   const int tid = threadIdx.x;
   const int NT = g.Cop >> 4;
 #define CONV_STAMP(i) \
-  if (a.dbg && tid == 0 && it == blk) a.dbg[(int64_t)blk * 8 + (i)] = __builtin_amdgcn_s_memtime();
-  int it = blk;
+  if (a.dbg && tid == 0) a.dbg[(int64_t)blk * 8 + (i)] = __builtin_amdgcn_s_memtime();
   CONV_STAMP(0);
 
   // ---- staging in ONE memory round trip: every global load of the weights (up to 32 per thread),
@@ -116,26 +115,17 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   int64_t wb[2] = {-1, -1};
   int wko[2] = {0, 0};
   float wv[32];
+  float eb[4], es[4];
 
-  // per-item state: the patch walk (a thread owns one patch column, rows step by 256 / PW)
+  // the zero-padded input patch: a thread owns one patch column, rows step by 256 / PW
+  const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
   const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
-  const bool prow = tid / g.PW < rpi;
-  const bool one_batch = (nrows + rpi - 1) / rpi <= 16;  // (an item's rows in one batch per thread)
+  int rr = tid / g.PW;
+  const bool prow = rr < rpi;
+  int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
   const int iw = pc - g.pad;
   const bool colv = iw >= 0 && iw < g.W;
-  int n = 0, band = 0, oh0 = 0, npix = 0, rr = 0, ic = 0, pr = 0;
-  int64_t xbase = 0, nc0 = 0;
-  auto setup_item = [&](int t) {
-    n = t / g.bands;
-    band = t - n * g.bands;
-    oh0 = band * g.TR;
-    npix = min(g.TR, g.OH - oh0) * g.OW;
-    xbase = (int64_t)n * g.Ci * g.H * g.W;
-    nc0 = (int64_t)n * g.Ci;
-    rr = tid / g.PW;
-    ic = prow ? rr / g.PR : 0;
-    pr = rr - ic * g.PR;
-  };
+  const int64_t nc0 = (int64_t)n * g.Ci;
   float pv[16], yo[16], sc[16];
   uint8_t bi[16];
   int at[16], sel[16];
@@ -188,39 +178,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     for (int j = 0; j < 16; ++j)
       if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(PIN ? unpool(pv[j], bi[j], yo[j], sc[j], sel[j]) : pv[j]);
   };
-  // epilogue operands of this lane's channels (N-tiles 0..3) for image n: loads (unconditional at
-  // valid addresses), then the Dropout2d draw (channel_mask_kernel's draw, index n*Co + oc)
-  const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
-  auto load_ep = [&](float (&eb)[4], float (&es)[4]) {
-    const float* bp = a.bias ? a.bias : a.w;
-    const float* cp = a.chscale ? a.chscale : a.w;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int oc = j * 16 + (tid & 15);
-      const bool ok = j < NT && oc < g.Co;
-      const float tb = bp[ok ? oc : 0], tc = cp[ok ? (int64_t)n * g.Co + oc : 0];
-      eb[j] = ok && a.bias ? tb : 0.f;
-      es[j] = ok && a.chscale ? tc : 1.f;
-    }
-  };
-  auto draw_ep = [&](float (&es)[4]) {
-    if (a.chscale_out) {
-      const float keep_sc = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int oc = j * 16 + (tid & 15);
-        es[j] = j < NT && oc < g.Co && dropout_keep(a.seed, drop_off, (uint64_t)n * g.Co + oc, a.drop_p) ? keep_sc : 0.f;
-      }
-    }
-  };
-  float eb[4], es[4];
-
-  // ---- the first item: its patch rows, the weights and its epilogue operands in one round trip
-  // (issue order: the patch rows first, then the weights and epilogue operands in straight-line
-  // code, then a scheduling barrier so no conversion / store of a loaded value is hoisted between
-  // them: it would wait on its load mid-issue, a second round trip)
-  if (it >= items) return;
-  setup_item(it);
+  // issue order: the patch rows first, then the weights and epilogue
+  // operands in straight-line code, then a scheduling barrier so no conversion / store of a loaded
+  // value is hoisted between them (it would wait on its load mid-issue: a second round trip)
   load_rows();
   if (wfast) {
 #pragma unroll
@@ -234,10 +194,31 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       wv[j] = ok ? t : 0.f;
     }
   }
-  load_ep(eb, es);
+  {  // epilogue operands of this lane's channels (N-tiles 0..3)
+    const float* bp = a.bias ? a.bias : a.w;        // (a valid address when absent: loads stay
+    const float* cp = a.chscale ? a.chscale : a.w;  // unconditional, no branch + wait per element)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oc = j * 16 + (tid & 15);
+      const bool ok = j < NT && oc < g.Co;
+      const float tb = bp[ok ? oc : 0], tc = cp[ok ? (int64_t)n * g.Co + oc : 0];
+      eb[j] = ok && a.bias ? tb : 0.f;
+      es[j] = ok && a.chscale ? tc : 1.f;
+    }
+  }
+  const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
   __builtin_amdgcn_sched_barrier(0);
   CONV_STAMP(1);
-  draw_ep(es);
+
+  // ---- while the loads fly: the Dropout2d draw (channel_mask_kernel's draw, index n*Co + oc)
+  if (a.chscale_out) {
+    const float keep_sc = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oc = j * 16 + (tid & 15);
+      es[j] = j < NT && oc < g.Co && dropout_keep(a.seed, drop_off, (uint64_t)n * g.Co + oc, a.drop_p) ? keep_sc : 0.f;
+    }
+  }
 
   // ---- LDS stores of the first round, then any further rounds
   if (wfast) {
@@ -279,23 +260,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   CONV_STAMP(3);
 
   const int lane = tid & 63, wave = tid >> 6;
+  const int mtiles = (npix + 15) >> 4;
   const int pooled = a.pool_k == 2;
   const int PWb = g.OW >> 1;
-  for (;;) {
-  // the next item's patch loads go out before this item's MFMAs (one batch per thread: its rows
-  // stay in registers until the barrier after the compute)
-  const int cur_n = n, cur_band = band, cur_oh0 = oh0, cur_npix = npix;
-  float ebn[4], esn[4];
-  const int nxt = it + nblk;
-  const bool have_next = nxt < items;
-  if (have_next && one_batch) {
-    setup_item(nxt);
-    load_rows();
-    load_ep(ebn, esn);
-  }
-  {
-  const int n = cur_n, band = cur_band, oh0 = cur_oh0, npix = cur_npix;
-  const int mtiles = (npix + 15) >> 4;
   for (int mt = wave; mt < mtiles; mt += 4) {
     // pixel owned by this lane as an A row
     const int m = mt * 16 + (lane & 15);
@@ -405,39 +372,14 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       }
     }
   }
-  }  // (this item's compute)
   CONV_STAMP(4);
-  if (!have_next) break;
-  __syncthreads();  // every wave is done reading this item's patch
-  it = nxt;
-  if (one_batch) {  // the prefetched rows and operands of the next item
-    draw_ep(esn);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      eb[j] = ebn[j];
-      es[j] = esn[j];
-    }
-    store_rows();
-  } else {
-    setup_item(it);
-    load_rows();
-    load_ep(eb, es);
-    draw_ep(es);
-    store_rows();
-    while (prow && rr < nrows) {
-      load_rows();
-      store_rows();
-    }
-  }
-  __syncthreads();
-  }  // for (;;) over the items
 #undef CONV_STAMP
 }
 
 template <typename T, typename X, typename Y, bool PIN>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T, X, Y, PIN>(a, g, blockIdx.x, gridDim.x, smem);
+  conv_fwd_body<T, X, Y, PIN>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -718,7 +660,7 @@ template <typename T, typename X, typename DY, bool PIN>
 __global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN>(wa, wg, blockIdx.x, smem);
-  else conv_fwd_body<T, DY, X, PIN>(a, g, blockIdx.x - wg.nblocks, gridDim.x - wg.nblocks, smem);  // (dx: x's dtype)
+  else conv_fwd_body<T, DY, X, PIN>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
@@ -814,7 +756,7 @@ static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid
   g.PR = tr + g.KH - 1;
   g.bands = (g.OH + tr - 1) / tr;
   lds = lds_bytes(tr);
-  grid = std::min(a.N * g.bands, 4 * 256);  // (up to 4 blocks per CU; more items loop in the block)
+  grid = a.N * g.bands;
   return hipSuccess;
 }
 
