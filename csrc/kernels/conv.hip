@@ -75,7 +75,9 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // X: the input's element type, PIN: the input is given max-pooled (a.pidx) -- compile-time, so the
 // staging's loads are straight-line code (a runtime dtype / mode branch around them made the
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
-template <typename T, typename X, typename Y, bool PIN>  // Y: the output's element type
+template <typename T, typename X, typename Y, bool PIN, bool WIDE>  // Y: the output's element type
+// WIDE: 32 weight / 16 patch-row loads per thread in flight (one round trip: small grids); narrow:
+// 8 / 8 (fewer registers, more blocks per CU: large grids, where other blocks hide the latency)
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
                                               unsigned char* __restrict__ smem) {
   typedef typename Mfma<T>::frag frag;
@@ -110,11 +112,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     base = !kv ? -1 : a.mode == 0 ? (int64_t)k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
   };
   // single-round weight form: a thread's columns k = tid + 256 i (i < 32 / COP) x all COP channels
-  const int wcols = 32 / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
-  const bool wfast = g.Cop <= 32 && g.Kp <= 256 * wcols;
+  constexpr int WB = WIDE ? 32 : 8, RB = WIDE ? 16 : 8;  // weight / row loads per batch
+  const int wcols = WB / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
+  const bool wfast = WIDE && g.Cop <= 32 && g.Kp <= 256 * wcols;
   int64_t wb[2] = {-1, -1};
   int wko[2] = {0, 0};
-  float wv[32];
+  float wv[WB];
   float eb[4], es[4];
 
   // the zero-padded input patch: a thread owns one patch column, rows step by 256 / PW
@@ -126,15 +129,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   const int iw = pc - g.pad;
   const bool colv = iw >= 0 && iw < g.W;
   const int64_t nc0 = (int64_t)n * g.Ci;
-  float pv[16], yo[16], sc[16];
-  uint8_t bi[16];
-  int at[16], sel[16];
-  auto load_rows = [&]() {  // 16 rows' loads (pooled input: value / argmax / gate / scale)
+  float pv[RB], yo[RB], sc[RB];
+  uint8_t bi[RB];
+  int at[RB], sel[RB];
+  auto load_rows = [&]() {  // RB rows' loads (pooled input: value / argmax / gate / scale)
     const X* xs = static_cast<const X*>(a.x);
     const X* ys = static_cast<const X*>(a.pout);
     if constexpr (!PIN) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < RB; ++j) {
         const int ih = oh0 - g.pad + pr;
         const bool in = prow && rr < nrows;
         at[j] = in ? rr : -1;
@@ -150,7 +153,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < RB; ++j) {
         const int ih = oh0 - g.pad + pr;
         const bool in = prow && rr < nrows;
         const bool ok = in && colv && ih >= 0 && ih < g.H;
@@ -175,7 +178,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   };
   auto store_rows = [&]() {
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
+    for (int j = 0; j < RB; ++j)
       if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(PIN ? unpool(pv[j], bi[j], yo[j], sc[j], sel[j]) : pv[j]);
   };
   // issue order: the patch rows first, then the weights and epilogue
@@ -187,7 +190,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     for (int i = 0; i < 2; ++i)
       if (i < wcols && tid + 256 * i < g.Kp) wcol(tid + 256 * i, wb[i], wko[i]);
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {  // (unconditional loads at a clamped address, then a select)
+    for (int j = 0; j < WB; ++j) {  // (unconditional loads at a clamped address, then a select)
       const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
       const bool ok = wb[i] >= 0 && oc < g.Co;
       const float t = a.w[ok ? wb[i] + oc * wstep : 0];
@@ -226,7 +229,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     for (int i = 0; i < 2; ++i)
       if (i < wcols && tid + 256 * i < g.Kp) koff[tid + 256 * i] = wko[i];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
+    for (int j = 0; j < WB; ++j) {
       const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
       const int k = tid + 256 * i;
       if (i < wcols && k < g.Kp) Ws[oc * LDW + k] = Stor<T>::of(wv[j]);
@@ -237,15 +240,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       int ko;
       wcol(k, base, ko);
       koff[k] = ko;
-      for (int oc0 = 0; oc0 < g.Cop; oc0 += 32) {  // (Cop: a multiple of 16)
+      for (int oc0 = 0; oc0 < g.Cop; oc0 += WB) {  // (Cop: a multiple of 16)
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
+        for (int j = 0; j < WB; ++j) {
           const bool ok = base >= 0 && oc0 + j < g.Co;
           const float t = a.w[ok ? base + (oc0 + j) * wstep : 0];
           wv[j] = ok ? t : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < 32; ++j)
+        for (int j = 0; j < WB; ++j)
           if (oc0 + j < g.Cop) Ws[(oc0 + j) * LDW + k] = Stor<T>::of(wv[j]);
       }
     }
@@ -376,10 +379,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 #undef CONV_STAMP
 }
 
-template <typename T, typename X, typename Y, bool PIN>
+template <typename T, typename X, typename Y, bool PIN, bool WIDE>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T, X, Y, PIN>(a, g, blockIdx.x, smem);
+  conv_fwd_body<T, X, Y, PIN, WIDE>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -404,7 +407,7 @@ struct WgradGeo {
 };
 
 // X: the input's element type, DY: dy's, PIN: dy given max-pooled (compile-time, see conv_fwd_body)
-template <typename T, typename X, typename DY, bool PIN>
+template <typename T, typename X, typename DY, bool PIN, bool WIDE>  // WIDE: as conv_fwd_body
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const WgradGeo& g, const int blk,
                                                 unsigned char* __restrict__ smem) {
   const void* __restrict__ x = wa.x;
@@ -420,6 +423,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   S* patch = (S*)(pbase + g.npp);                           // [Ci][PR][PW] (+1 slot holding 1.0)
   const int pe = g.Ci * g.PR * g.PW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int RB = WIDE ? 16 : 8;  // patch rows / pooled dy channels per batch
 
   for (int k = tid; k < g.Kc; k += 256) {
     int o = pe;  // the constant-one slot (db column) / zero-weight padding
@@ -457,12 +461,12 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
     const int iw = pc - g.pad;
     const bool colv = iw >= 0 && iw < g.W;
-    float xv[16];
-    int at[16];
+    float xv[RB];
+    int at[RB];
     auto load_rows = [&]() {
       const X* xs = static_cast<const X*>(x);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < RB; ++j) {
         const int ih = pr - g.pad;
         const bool in = prow && rr < nrows;
         at[j] = in ? rr : -1;
@@ -479,7 +483,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     };
     auto store_rows = [&]() {
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < RB; ++j)
         if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(xv[j]);
     };
 
@@ -490,10 +494,10 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
     const int64_t ybp = (int64_t)n * g.Co * npixp;
     const int wst = max(1, min(npixp, 256)), wgr = 256 / wst, q0 = tid % wst, gq = tid / wst;
-    float dv[16], yo[16], sc[16];
-    uint8_t bi[16];
+    float dv[RB], yo[RB], sc[RB];
+    uint8_t bi[RB];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
-    bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * 16 < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
+    bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
     auto load_dy = [&]() {  // one chunk's loads
       const DY* ys = static_cast<const DY*>(dy);
       if constexpr (!PIN) {
@@ -508,7 +512,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         const int ph = d_q / PWp, pw = d_q - ph * PWp;
         d_pb = 2 * ph * g.OW + 2 * pw;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < RB; ++j) {
           const bool ok = d_oc0 + j < g.Co;
           const int64_t po = ok ? ybp + (int64_t)(d_oc0 + j) * npixp + d_q : ybp;
           const DY t0 = ys[po], t1 = os[po];
@@ -533,21 +537,21 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         d_more = d_p < g.npp;
       } else {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < RB; ++j) {
           if (d_oc0 + j >= g.Cop) break;
           S* d = dys + (d_oc0 + j) * LDY + d_pb;
 #pragma unroll
           for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(dv[j], bi[j], yo[j], sc[j], e));
         }
-        d_oc0 += wgr * 16;
+        d_oc0 += wgr * RB;
         if (d_oc0 >= g.Cop) {
-          d_oc0 = gq * 16;
+          d_oc0 = gq * RB;
           d_q += wst;
         }
         d_more = d_q < npixp;
       }
     };
-    if (PIN) d_oc0 = gq * 16;
+    if (PIN) d_oc0 = gq * RB;
 
     load_rows();              // round 1: patch rows ...
     if (d_more) load_dy();    // ... and the first dy chunk in flight together
@@ -646,10 +650,10 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   }
 }
 
-template <typename T, typename X, typename DY, bool PIN>
+template <typename T, typename X, typename DY, bool PIN, bool WIDE>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_wgrad_body<T, X, DY, PIN>(wa, g, blockIdx.x, smem);
+  conv_wgrad_body<T, X, DY, PIN, WIDE>(wa, g, blockIdx.x, smem);
 }
 
 // The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
@@ -659,8 +663,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs wa, WgradGeo 
 template <typename T, typename X, typename DY, bool PIN>
 __global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN>(wa, wg, blockIdx.x, smem);
-  else conv_fwd_body<T, DY, X, PIN>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
+  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN, true>(wa, wg, blockIdx.x, smem);
+  else conv_fwd_body<T, DY, X, PIN, true>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
@@ -776,7 +780,9 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
           hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a, g);
           return hipGetLastError();
         };
-        return a.pidx ? go(conv_fwd_kernel<scalar_t, X, Y, true>) : go(conv_fwd_kernel<scalar_t, X, Y, false>);
+        const bool wide = grid <= 2 * 256;  // (see conv_fwd_body: WIDE for about a wave of blocks)
+        if (a.pidx) return wide ? go(conv_fwd_kernel<scalar_t, X, Y, true, true>) : go(conv_fwd_kernel<scalar_t, X, Y, true, false>);
+        return wide ? go(conv_fwd_kernel<scalar_t, X, Y, false, true>) : go(conv_fwd_kernel<scalar_t, X, Y, false, false>);
       });
     });
   });
@@ -865,10 +871,22 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
           hipLaunchKernelGGL(dgr, dim3(dgrid), dim3(256), lds_d, s, a, g);
           return hipGetLastError();
         };
-        return b.pidx ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true>,
-                           conv_fwd_kernel<T, DY, X, true>)
-                      : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false>,
-                           conv_fwd_kernel<T, DY, X, false>);
+        if (merged)
+          return b.pidx ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>,
+                             conv_fwd_kernel<T, DY, X, true, true>)
+                        : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>,
+                             conv_fwd_kernel<T, DY, X, false, true>);
+        const bool ww = wg.nblocks <= 2 * 256, dw = dgrid <= 2 * 256;  // (WIDE per launch)
+        if (b.pidx) {
+          if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, true>)
+                            : go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, false>);
+          return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, true>)
+                    : go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, false>);
+        }
+        if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, true>)
+                          : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, false>);
+        return dw ? go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, true>)
+                  : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, false>);
       });
     });
   };
