@@ -284,53 +284,78 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // Software-pipelined K loop: K-step s+1's patch gathers and weight fragments are read (LDS)
-      // while step s runs on the MFMAs, and the k -> patch offsets two steps ahead.  Every read is
-      // unconditional at a valid address (a pixel past npix reads the block's first and is zeroed
-      // after; N-tiles past NT read row 0): a predicated LDS read was a branch + wait per element.
-      const int kq8 = 8 * (lane >> 4);
-      int wrow[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wrow[j] = (nc + j < NT ? (nc + j) * 16 + (lane & 15) : 0) * LDW;
-      typename Stor<T>::V8 raw;
-      frag fb[4];
-      int4 o0 = *reinterpret_cast<const int4*>(koff + kq8);
-      int4 o1 = *reinterpret_cast<const int4*>(koff + kq8 + 4);
-      {
-        const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kq8);
-      }
-      {
-        const int kn = min(kq8 + 32, g.Kp - 8);  // (step 1's offsets; clamped: a valid slot)
-        o0 = *reinterpret_cast<const int4*>(koff + kn);
-        o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
-      }
-      for (int k0 = 0; k0 < g.Kp; k0 += 32) {
-        const typename Stor<T>::V8 cur = raw;
-        frag fbc[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fbc[j] = fb[j];
-        {  // step s+1's reads (clamped past the last step: valid slots, unused)
-          const int kb1 = min(k0 + 32, g.Kp - 32) + kq8;
+      if constexpr (WIDE) {
+        // Software-pipelined K loop: K-step s+1's patch gathers and weight fragments are read (LDS)
+        // while step s runs on the MFMAs, and the k -> patch offsets two steps ahead.  Every read is
+        // unconditional at a valid address (a pixel past npix reads the block's first and is zeroed
+        // after; N-tiles past NT read row 0): a predicated LDS read was a branch + wait per element.
+        const int kq8 = 8 * (lane >> 4);
+        int wrow[4];
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) wrow[j] = (nc + j < NT ? (nc + j) * 16 + (lane & 15) : 0) * LDW;
+        typename Stor<T>::V8 raw;
+        frag fb[4];
+        int4 o0 = *reinterpret_cast<const int4*>(koff + kq8);
+        int4 o1 = *reinterpret_cast<const int4*>(koff + kq8 + 4);
+        {
           const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-#pragma unroll
+  #pragma unroll
           for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kb1);
-          const int kn = min(k0 + 64 + kq8, g.Kp - 8);
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kq8);
+        }
+        {
+          const int kn = min(kq8 + 32, g.Kp - 8);  // (step 1's offsets; clamped: a valid slot)
           o0 = *reinterpret_cast<const int4*>(koff + kn);
           o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
         }
-        typename Stor<T>::V8 am;
+        for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+          const typename Stor<T>::V8 cur = raw;
+          frag fbc[4];
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) fbc[j] = fb[j];
+          {  // step s+1's reads (clamped past the last step: valid slots, unused)
+            const int kb1 = min(k0 + 32, g.Kp - 32) + kq8;
+            const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+  #pragma unroll
+            for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
+  #pragma unroll
+            for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kb1);
+            const int kn = min(k0 + 64 + kq8, g.Kp - 8);
+            o0 = *reinterpret_cast<const int4*>(koff + kn);
+            o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
+          }
+          typename Stor<T>::V8 am;
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) am[j] = valid ? cur[j] : (S)0;
+          const frag fa = __builtin_bit_cast(frag, am);
+  #pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (nc + j < NT) acc[j] = Mfma<T>::mma(fa, fbc[j], acc[j]);
+        }
+      } else {
+        // narrow form (large grids: fewer registers, more blocks per CU hide the LDS latency):
+        // one K-step's reads, then its MFMAs; reads unconditional at valid addresses as above
+        const int kq8 = 8 * (lane >> 4);
+        for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+          const int kb = k0 + kq8;
+          const int4 o0 = *reinterpret_cast<const int4*>(koff + kb);
+          const int4 o1 = *reinterpret_cast<const int4*>(koff + kb + 4);
+          const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+          typename Stor<T>::V8 raw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) am[j] = valid ? cur[j] : (S)0;
-        const frag fa = __builtin_bit_cast(frag, am);
+          for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (nc + j < NT) acc[j] = Mfma<T>::mma(fa, fbc[j], acc[j]);
+          for (int j = 0; j < 8; ++j) raw[j] = valid ? raw[j] : (S)0;
+          const frag fa = __builtin_bit_cast(frag, raw);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (nc + j < NT) {
+              const frag fb = *reinterpret_cast<const frag*>(Ws + ((nc + j) * 16 + (lane & 15)) * LDW + kb);
+              acc[j] = Mfma<T>::mma(fa, fb, acc[j]);
+            }
+          }
+        }
       }
       // ---- epilogue
 #pragma unroll
