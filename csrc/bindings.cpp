@@ -431,7 +431,8 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 // pool_out / pool_scale the forward's argmax bytes, pooled output and channel scale.
 void conv2d_bwd(const Tensor& x, const Tensor& dy, const Tensor& w, Tensor& dw, const optional<Tensor>& db,
                 Tensor& ws, const optional<Tensor>& dx, int64_t pad, const optional<Tensor>& pool_idx,
-                const optional<Tensor>& pool_out, const optional<Tensor>& pool_scale, int64_t mfma_dtype) {
+                const optional<Tensor>& pool_out, const optional<Tensor>& pool_scale, int64_t mfma_dtype,
+                const optional<Tensor>& dbg) {
   dev(x, "x"); dev(dy, "dy"); dev(w, "w"); dev(dw, "dw"); dev(ws, "ws");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && dy.dim() == 4 && w.scalar_type() == at::kFloat);
   TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.sizes() == w.sizes() && ws.scalar_type() == at::kFloat);
@@ -471,6 +472,12 @@ void conv2d_bwd(const Tensor& x, const Tensor& dy, const Tensor& w, Tensor& dw, 
   b.beta = 0.f;
   b.N = N; b.IC = IC; b.H = H; b.W = W; b.OC = OC; b.KH = KH; b.KW = KW; b.pad = (int)pad;
   b.mfma_dtype = mcode(mfma_dtype);
+  if (dbg.has_value()) {
+    dev(*dbg, "dbg");
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= (int64_t)std::min(N, 256) * 8,
+                "conv2d_bwd: dbg must be int64 [>= weight-gradient blocks * 8]");
+    b.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr<int64_t>());
+  }
   CHECK_HIP(csed::launch_conv2d_bwd(b, cur_stream(x)));
 }
 
@@ -779,7 +786,7 @@ TORCH_LIBRARY(csed, m) {
         "int pool_k, int mfma_dtype, float drop2d_p=0.0, int seed=0, int offset=0, Tensor? offset_dev=None, "
         "Tensor(c!)? chscale_out=None, Tensor(d!)? dbg=None) -> ()");
   m.def("conv2d_bwd(Tensor x, Tensor dy, Tensor w, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, Tensor(d!)? dx, "
-        "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype) -> ()");
+        "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype, Tensor(e!)? dbg=None) -> ()");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? gate, float gate_scale, Tensor(a!)? dx, Tensor(b!)? dw, "
         "Tensor(c!)? db, int mfma_dtype, Tensor? lsm_target=None, Tensor? lsm_gout=None, float lsm_div=1.0) -> ()");
   m.def("lsm_nll_fwd(Tensor z, Tensor target, Tensor(a!) logp, Tensor(b!) out, int reduction) -> ()");

@@ -419,6 +419,7 @@ struct WgradArgs {
   const uint8_t* pidx; const void* pout; const float* pscale;
   int N;
   float* slab;
+  uint64_t* dbg;  // optional [blocks, 8] s_memtime stamps of the first image (diagnostics)
 };
 
 struct WgradGeo {
@@ -449,6 +450,9 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   const int pe = g.Ci * g.PR * g.PW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int RB = WIDE ? 16 : 8;  // patch rows / pooled dy channels per batch
+#define WG_STAMP(i) \
+  if (wa.dbg && tid == 0 && n == blk * g.per_block) wa.dbg[(int64_t)blk * 8 + (i)] = __builtin_amdgcn_s_memtime();
+  if (wa.dbg && tid == 0) wa.dbg[(int64_t)blk * 8] = __builtin_amdgcn_s_memtime();
 
   for (int k = tid; k < g.Kc; k += 256) {
     int o = pe;  // the constant-one slot (db column) / zero-weight padding
@@ -581,6 +585,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     load_rows();              // round 1: patch rows ...
     if (d_more) load_dy();    // ... and the first dy chunk in flight together
     __builtin_amdgcn_sched_barrier(0);  // (no use of a loaded value hoisted between the loads)
+    WG_STAMP(1);
     store_rows();
     if (d_more) store_dy_next();
     while (prow && rr < nrows) {
@@ -599,6 +604,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       }
     }
     __syncthreads();
+    WG_STAMP(2);
     if (my_nt0 >= NT) continue;
     // this lane's B-column patch offsets, one per N-tile (the same for every pixel step: read once
     // per image instead of once per MFMA, a dependent LDS round trip less per pixel step)
@@ -634,6 +640,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     }
   }
 
+  if (wa.dbg && tid == 0) wa.dbg[(int64_t)blk * 8 + 3] = __builtin_amdgcn_s_memtime();
   // ---- write this block's partial [Co][K+1] slab (fixed-order combine of split waves)
   float* out = slab + (int64_t)blk * g.Co * (g.K + 1);
   if (psplit == 1) {
@@ -673,6 +680,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       out[(int64_t)oc * (g.K + 1) + col] = s;
     }
   }
+  if (wa.dbg && tid == 0) wa.dbg[(int64_t)blk * 8 + 4] = __builtin_amdgcn_s_memtime();
+#undef WG_STAMP
 }
 
 template <typename T, typename X, typename DY, bool PIN, bool WIDE>
@@ -852,7 +861,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
   const size_t lds_w = lds;  // (the weight-gradient launch alone)
   size_t lds_d = 0;          // (the data-gradient launch alone)
-  WgradArgs wa{b.x, b.x_dtype, b.dy, b.dy_dtype, b.pidx, b.pout, b.pscale, b.N, b.ws};
+  WgradArgs wa{b.x, b.x_dtype, b.dy, b.dy_dtype, b.pidx, b.pout, b.pscale, b.N, b.ws, b.dbg};
   // the data gradient (optional): conv of dy (un-pooled on load) with the flipped weights
   ConvArgs a{};
   ConvGeo g{};

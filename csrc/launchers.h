@@ -163,6 +163,7 @@ struct ConvBwdArgs {
   void* dx; int dx_dtype;
   int N, IC, H, W, OC, KH, KW, pad;
   int mfma_dtype;
+  uint64_t* dbg;  // optional [weight-gradient blocks, 8] stamps (diagnostics, tools/conv_stamps.py)
 };
 hipError_t launch_conv2d_bwd(const ConvBwdArgs& a, hipStream_t s);
 // Weight gradient: dW[OC, IC*KH*KW] (fp32) and db[OC] (fp32, optional) of a

@@ -54,6 +54,27 @@ def main() -> int:
               ", ".join(f"{n} {m:.0f}" for n, m in zip(names, med)) +
               f"; block start spread p50/max {start.median():.0f}/{start.max():.0f}, end p50/max {end.median():.0f}/{end.max():.0f}",
               flush=True)
+    # the weight-gradient blocks of the two backward launches (first image of each block)
+    from csed_514_project_distributed_training_using_pytorch_amd.ops.functional import wgrad_workspace_elems
+    dy2 = torch.randn(y2.shape, device=dev, generator=g).to(torch.bfloat16)
+    dw2, db2, dx2 = torch.empty_like(w2), torch.empty_like(b2), torch.empty_like(y1)
+    ws2 = torch.empty(wgrad_workspace_elems(B, 10, 5, 5, 20), device=dev)
+    dw1, db1 = torch.empty_like(w1), torch.empty_like(b1)
+    ws1 = torch.empty(wgrad_workspace_elems(B, 1, 5, 5, 10), device=dev)
+    wnames = ["loads issued", "stores + barrier", "MFMA", "slab write"]
+    for label, fn in (
+            ("conv2 bwd (wgrad blocks)", lambda d: o.conv2d_bwd(y1, dy2, w2, dw2, db2, ws2, dx2, 0, i2, y2, sc2, 1, d)),
+            ("conv1 bwd (wgrad blocks)", lambda d: o.conv2d_bwd(x0, dx2, w1, dw1, db1, ws1, None, 0, i1, y1, None, 1, d))):
+        for _ in range(5):
+            dbg.zero_()
+            fn(dbg)
+        torch.cuda.synchronize()
+        t = dbg.view(-1, 8).cpu()
+        t = t[t[:, 0] > 0]
+        d = (t[:, 1:5] - t[:, 0:4]).double()
+        med = d.median(0).values.tolist()
+        print(f"{label}: {len(t)} blocks; median cycles per phase: " +
+              ", ".join(f"{n} {m:.0f}" for n, m in zip(wnames, med)), flush=True)
     return 0
 
 
