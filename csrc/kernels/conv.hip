@@ -123,6 +123,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   // the zero-padded input patch: a thread owns one patch column, rows step by 256 / PW
   const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
   const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+  const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
   int rr = tid / g.PW;
   const bool prow = rr < rpi;
   int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
@@ -144,12 +145,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
         const bool ok = in && colv && ih >= 0 && ih < g.H;
         const X t = xs[ok ? xbase + ((int64_t)ic * g.H + ih) * g.W + iw : xbase];
         pv[j] = ok ? (float)t : 0.f;
-        rr += rpi;
-        pr += rpi;
-        while (pr >= g.PR) {
-          pr -= g.PR;
-          ++ic;
-        }
+        rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
+        pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
+        ic += ic_step;
+        const int wrap = pr >= g.PR;
+        pr -= wrap * g.PR;
+        ic += wrap;
       }
     } else {
 #pragma unroll
@@ -167,12 +168,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
         yo[j] = ok ? (float)t1 : 0.f;
         bi[j] = ok ? t2 : (uint8_t)255;
         sc[j] = ok ? (a.pscale ? t3 : 1.f) : 0.f;
-        rr += rpi;
-        pr += rpi;
-        while (pr >= g.PR) {
-          pr -= g.PR;
-          ++ic;
-        }
+        rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
+        pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
+        ic += ic_step;
+        const int wrap = pr >= g.PR;
+        pr -= wrap * g.PR;
+        ic += wrap;
       }
     }
   };
@@ -485,6 +486,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     const int64_t xb = (int64_t)n * g.Ci * g.H * g.W;
     // the zero-padded input patch: one patch column per thread, rows stepping by 256 / PW
     const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+    const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
     int rr = tid / g.PW;
     const bool prow = rr < rpi;
     int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
@@ -502,12 +504,12 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         const bool ok = in && colv && ih >= 0 && ih < g.H;
         const X t = xs[ok ? xb + ((int64_t)ic * g.H + ih) * g.W + iw : xb];
         xv[j] = ok ? (float)t : 0.f;
-        rr += rpi;
-        pr += rpi;
-        while (pr >= g.PR) {
-          pr -= g.PR;
-          ++ic;
-        }
+        rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
+        pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
+        ic += ic_step;
+        const int wrap = pr >= g.PR;
+        pr -= wrap * g.PR;
+        ic += wrap;
       }
     };
     auto store_rows = [&]() {
