@@ -75,9 +75,11 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // X: the input's element type, PIN: the input is given max-pooled (a.pidx) -- compile-time, so the
 // staging's loads are straight-line code (a runtime dtype / mode branch around them made the
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE>  // Y: the output's element type
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256>  // Y: the output's element type
 // WIDE: 32 weight / 16 patch-row loads per thread in flight (one round trip: small grids); narrow:
-// 8 / 8 (fewer registers, more blocks per CU: large grids, where other blocks hide the latency)
+// 8 / 8 (fewer registers, more blocks per CU: large grids, where other blocks hide the latency).
+// NTHR: the block size (512 for a standalone launch: two waves per SIMD interleave the staging's
+// long instruction stream; 256 inside the merged backward kernel)
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
                                               unsigned char* __restrict__ smem) {
   typedef typename Mfma<T>::frag frag;
@@ -111,18 +113,18 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     ko = kv ? (ic * g.PR + kh) * g.PW + kw : 0;
     base = !kv ? -1 : a.mode == 0 ? (int64_t)k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
   };
-  // single-round weight form: a thread's columns k = tid + 256 i (i < 32 / COP) x all COP channels
+  // single-round weight form: a thread's columns k = tid + NTHR i (i < 32 / COP) x all COP channels
   constexpr int WB = WIDE ? 32 : 8, RB = WIDE ? 16 : 8;  // weight / row loads per batch
   const int wcols = WB / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
-  const bool wfast = WIDE && g.Cop <= 32 && g.Kp <= 256 * wcols;
+  const bool wfast = WIDE && g.Cop <= 32 && g.Kp <= NTHR * wcols;
   int64_t wb[2] = {-1, -1};
   int wko[2] = {0, 0};
   float wv[WB];
   float eb[4], es[4];
 
-  // the zero-padded input patch: a thread owns one patch column, rows step by 256 / PW
+  // the zero-padded input patch: a thread owns one patch column, rows step by NTHR / PW
   const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
-  const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+  const int rpi = NTHR / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
   const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
   int rr = tid / g.PW;
   const bool prow = rr < rpi;
@@ -189,7 +191,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   if (wfast) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      if (i < wcols && tid + 256 * i < g.Kp) wcol(tid + 256 * i, wb[i], wko[i]);
+      if (i < wcols && tid + NTHR * i < g.Kp) wcol(tid + NTHR * i, wb[i], wko[i]);
 #pragma unroll
     for (int j = 0; j < WB; ++j) {  // (unconditional loads at a clamped address, then a select)
       const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
@@ -228,15 +230,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   if (wfast) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      if (i < wcols && tid + 256 * i < g.Kp) koff[tid + 256 * i] = wko[i];
+      if (i < wcols && tid + NTHR * i < g.Kp) koff[tid + NTHR * i] = wko[i];
 #pragma unroll
     for (int j = 0; j < WB; ++j) {
       const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
-      const int k = tid + 256 * i;
+      const int k = tid + NTHR * i;
       if (i < wcols && k < g.Kp) Ws[oc * LDW + k] = Stor<T>::of(wv[j]);
     }
   } else {
-    for (int k = tid; k < g.Kp; k += 256) {
+    for (int k = tid; k < g.Kp; k += NTHR) {
       int64_t base;
       int ko;
       wcol(k, base, ko);
@@ -267,7 +269,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   const int mtiles = (npix + 15) >> 4;
   const int pooled = a.pool_k == 2;
   const int PWb = g.OW >> 1;
-  for (int mt = wave; mt < mtiles; mt += 4) {
+  for (int mt = wave; mt < mtiles; mt += NTHR / 64) {
     // pixel owned by this lane as an A row
     const int m = mt * 16 + (lane & 15);
     int oh, ow;
@@ -405,10 +407,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 #undef CONV_STAMP
 }
 
+// (small grids: 512 threads, two waves per SIMD interleaving the staging's instruction stream --
+// conv1 fwd at B = 64 10.8 -> 9.6 us; large grids: 256, more blocks per CU -- 512 there was slower)
 template <typename T, typename X, typename Y, bool PIN, bool WIDE>
-__global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
+__global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T, X, Y, PIN, WIDE>(a, g, blockIdx.x, smem);
+  conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -811,12 +815,13 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
       return with_in_type<scalar_t>(a.y_dtype, [&](auto yt) -> hipError_t {
         typedef decltype(xt) X;
         typedef decltype(yt) Y;
+        const bool wide = grid <= 2 * 256;  // (see conv_fwd_body: WIDE for about a wave of blocks)
+        const dim3 block(wide ? 512 : 256);
         auto go = [&](auto kern) {
           if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a, g);
+          hipLaunchKernelGGL(kern, dim3(grid), block, lds, s, a, g);
           return hipGetLastError();
         };
-        const bool wide = grid <= 2 * 256;  // (see conv_fwd_body: WIDE for about a wave of blocks)
         if (a.pidx) return wide ? go(conv_fwd_kernel<scalar_t, X, Y, true, true>) : go(conv_fwd_kernel<scalar_t, X, Y, true, false>);
         return wide ? go(conv_fwd_kernel<scalar_t, X, Y, false, true>) : go(conv_fwd_kernel<scalar_t, X, Y, false, false>);
       });
@@ -893,6 +898,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
         // kernel's register budget (the wgrad body's) would cap the many data-gradient blocks'
         // occupancy, so they run as their own launch (B = 4096: 750 -> see profiles/round5.md)
         const bool merged = dgrid > 0 && wg.nblocks + dgrid <= 2 * 256;
+        const bool ww = wg.nblocks <= 2 * 256, dw = dgrid <= 2 * 256;  // (WIDE per launch)
         auto go = [&](auto bwd, auto wgr, auto dgr) {
           if (merged) {
             if (lds > 64 * 1024) hipFuncSetAttribute((const void*)bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -904,7 +910,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
           hipError_t e2 = hipGetLastError();
           if (e2 != hipSuccess || dgrid == 0) return e2;
           if (lds_d > 64 * 1024) hipFuncSetAttribute((const void*)dgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
-          hipLaunchKernelGGL(dgr, dim3(dgrid), dim3(256), lds_d, s, a, g);
+          hipLaunchKernelGGL(dgr, dim3(dgrid), dim3(dw ? 512 : 256), lds_d, s, a, g);
           return hipGetLastError();
         };
         if (merged)
@@ -912,7 +918,6 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
                              conv_fwd_kernel<T, DY, X, true, true>)
                         : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>,
                              conv_fwd_kernel<T, DY, X, false, true>);
-        const bool ww = wg.nblocks <= 2 * 256, dw = dgrid <= 2 * 256;  // (WIDE per launch)
         if (b.pidx) {
           if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, true>)
                             : go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, false>);
