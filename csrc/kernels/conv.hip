@@ -438,7 +438,7 @@ struct WgradGeo {
 };
 
 // X: the input's element type, DY: dy's, PIN: dy given max-pooled (compile-time, see conv_fwd_body)
-template <typename T, typename X, typename DY, bool PIN, bool WIDE>  // WIDE: as conv_fwd_body
+template <typename T, typename X, typename DY, bool PIN, bool WIDE, int NTHR = 256>  // WIDE, NTHR: as conv_fwd_body
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const WgradGeo& g, const int blk,
                                                 unsigned char* __restrict__ smem) {
   const void* __restrict__ x = wa.x;
@@ -454,12 +454,14 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   S* patch = (S*)(pbase + g.npp);                           // [Ci][PR][PW] (+1 slot holding 1.0)
   const int pe = g.Ci * g.PR * g.PW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int RB = WIDE ? 16 : 8;  // patch rows / pooled dy channels per batch
+  // patch rows / pooled dy channels per batch (512 threads: 8, the same loads per block in flight)
+  constexpr int RB = (WIDE && NTHR == 256) ? 16 : 8;
 #define WG_STAMP(i) \
   if (wa.dbg && tid == 0 && n == blk * g.per_block) wa.dbg[(int64_t)blk * 8 + (i)] = __builtin_amdgcn_s_memtime();
   if (wa.dbg && tid == 0) wa.dbg[(int64_t)blk * 8] = __builtin_amdgcn_s_memtime();
 
-  for (int k = tid; k < g.Kc; k += 256) {
+  constexpr int NW = NTHR / 64;  // waves
+  for (int k = tid; k < g.Kc; k += NTHR) {
     int o = pe;  // the constant-one slot (db column) / zero-weight padding
     if (k < g.K) {
       const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
@@ -467,14 +469,14 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     }
     koff[k] = o;
   }
-  for (int p = tid; p < g.npp; p += 256) pbase[p] = p < g.npix ? (p / g.OW) * g.PW + p % g.OW : 0;
+  for (int p = tid; p < g.npp; p += NTHR) pbase[p] = p < g.npix ? (p / g.OW) * g.PW + p % g.OW : 0;
 
   const int MT = g.Cop >> 4, NT = g.Kc >> 4;
-  const int psplit = NT >= 4 ? 1 : 4 / NT;
-  const int my_nt0 = NT >= 4 ? wave : wave / psplit;
-  const int my_s = NT >= 4 ? 0 : wave % psplit;
-  const int nt_step = NT >= 4 ? 4 : 1 << 30;
-  constexpr int MAXMT = 4, MAXNTW = 8;
+  const int psplit = NT >= NW ? 1 : NW / NT;
+  const int my_nt0 = NT >= NW ? wave : wave / psplit;
+  const int my_s = NT >= NW ? 0 : wave % psplit;
+  const int nt_step = NT >= NW ? NW : 1 << 30;
+  constexpr int MAXMT = 4, MAXNTW = NTHR == 512 ? 4 : 8;  // (N-tiles per wave: NT <= NW * MAXNTW)
   f32x4 acc[MAXMT][MAXNTW];
 #pragma unroll
   for (int i = 0; i < MAXMT; ++i)
@@ -488,8 +490,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     // ---- this image's staging in ONE memory round trip where it fits: the first 16 patch rows and
     // the first dy chunk are loaded before any LDS store (two serial rounds were ~2 us each)
     const int64_t xb = (int64_t)n * g.Ci * g.H * g.W;
-    // the zero-padded input patch: one patch column per thread, rows stepping by 256 / PW
-    const int rpi = 256 / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
+    // the zero-padded input patch: one patch column per thread, rows stepping by NTHR / PW
+    const int rpi = NTHR / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
     const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
     int rr = tid / g.PW;
     const bool prow = rr < rpi;
@@ -522,13 +524,13 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(xv[j]);
     };
 
-    // dy: plain (pst threads per pixel row, 256 / pst channel groups of 8 side by side) or pooled (a
+    // dy: plain (pst threads per pixel row, NTHR / pst channel groups of 8 side by side) or pooled (a
     // thread owns one pooling window x 16 channels and writes the window's 4 pixels, one nonzero)
     const int64_t yb = (int64_t)n * g.Co * g.npix;
-    const int pst = min(g.npp, 256), ocg = 256 / pst, p0 = tid % pst, og = tid / pst;
+    const int pst = min(g.npp, NTHR), ocg = NTHR / pst, p0 = tid % pst, og = tid / pst;
     const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
     const int64_t ybp = (int64_t)n * g.Co * npixp;
-    const int wst = max(1, min(npixp, 256)), wgr = 256 / wst, q0 = tid % wst, gq = tid / wst;
+    const int wst = max(1, min(npixp, NTHR)), wgr = NTHR / wst, q0 = tid % wst, gq = tid / wst;
     float dv[RB], yo[RB], sc[RB];
     uint8_t bi[RB];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
@@ -604,7 +606,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     }
     if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
     if (PIN) {  // (the MFMA K padding past npix: the window writes cover pixels < npix only)
-      for (int i = tid; i < g.Cop * (g.npp - g.npix); i += 256) {
+      for (int i = tid; i < g.Cop * (g.npp - g.npix); i += NTHR) {
         const int oc = i / (g.npp - g.npix), pp = g.npix + i % (g.npp - g.npix);
         dys[oc * LDY + pp] = Stor<T>::of(0.f);
       }
@@ -617,7 +619,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     int kos[MAXNTW];
 #pragma unroll
     for (int jj = 0; jj < MAXNTW; ++jj) {
-      const int nt = (jj == 0 || NT >= 4) ? my_nt0 + jj * 4 : NT;  // (NT < 4: only jj = 0 is used)
+      const int nt = (jj == 0 || NT >= NW) ? my_nt0 + jj * NW : NT;  // (NT < NW: only jj = 0 is used)
       kos[jj] = nt < NT ? koff[nt * 16 + (lane & 15)] : pe;
     }
     for (int ps = my_s; ps * 32 < g.npp; ps += psplit) {
@@ -632,7 +634,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
 #pragma unroll
       for (int jj = 0; jj < MAXNTW; ++jj) {
         const int nt = my_nt0 + jj * nt_step;
-        if (jj > 0 && NT < 4) break;
+        if (jj > 0 && NT < NW) break;
         if (nt >= NT) break;
         const int ko = kos[jj];
         typename Stor<T>::V8 raw;
@@ -652,7 +654,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   if (psplit == 1) {
 #pragma unroll
     for (int jj = 0; jj < MAXNTW; ++jj) {
-      const int nt = my_nt0 + jj * 4;
+      const int nt = my_nt0 + jj * NW;
       if (nt >= NT) break;
       const int col = nt * 16 + (lane & 15);
 #pragma unroll
@@ -667,7 +669,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     }
   } else {
     __syncthreads();
-    float* red = (float*)smem;  // [4 waves][MAXMT*16][16]
+    float* red = (float*)smem;  // [NW waves][MAXMT*16][16]
     if (my_nt0 < NT) {
 #pragma unroll
       for (int mt = 0; mt < MAXMT; ++mt) {
@@ -677,7 +679,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       }
     }
     __syncthreads();
-    for (int i = tid; i < g.Co * NT * 16; i += 256) {
+    for (int i = tid; i < g.Co * NT * 16; i += NTHR) {
       const int oc = i / (NT * 16), col = i % (NT * 16);
       if (col > g.K) continue;
       const int nt = col >> 4;
@@ -691,9 +693,9 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
 }
 
 template <typename T, typename X, typename DY, bool PIN, bool WIDE>
-__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g) {
+__global__ void __launch_bounds__(WIDE ? 512 : 256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_wgrad_body<T, X, DY, PIN, WIDE>(wa, g, blockIdx.x, smem);
+  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256>(wa, g, blockIdx.x, smem);
 }
 
 // The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
@@ -701,10 +703,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs wa, WgradGeo 
 // (possibly pooled) dy.  A second launch for the data gradient was a kernel boundary (~1.4 us in a
 // graph) plus its own ramp.
 template <typename T, typename X, typename DY, bool PIN>
-__global__ void __launch_bounds__(256) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
+__global__ void __launch_bounds__(512) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN, true>(wa, wg, blockIdx.x, smem);
-  else conv_fwd_body<T, DY, X, PIN, true>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
+  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN, true, 512>(wa, wg, blockIdx.x, smem);
+  else conv_fwd_body<T, DY, X, PIN, true, 512>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
 }
 
 // Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
@@ -863,7 +865,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
   const size_t es = b.mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
   const size_t lds_main = (size_t)wg.Cop * (wg.npp + 8) * es + (size_t)wg.Kc * 4 + (size_t)wg.npp * 4 +
                           ((size_t)wg.Ci * wg.PR * wg.PW + 1) * es + 16;
-  const size_t lds_red = (size_t)4 * 4 * 16 * 16 * 4;
+  const size_t lds_red = (size_t)8 * 4 * 16 * 16 * 4;  // (up to 8 waves x MAXMT x 16 x 16 floats)
   size_t lds = std::max(lds_main, lds_red);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
   const size_t lds_w = lds;  // (the weight-gradient launch alone)
@@ -902,11 +904,11 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
         auto go = [&](auto bwd, auto wgr, auto dgr) {
           if (merged) {
             if (lds > 64 * 1024) hipFuncSetAttribute((const void*)bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(bwd, dim3(wg.nblocks + dgrid), dim3(256), lds, s, wa, wg, a, g);
+            hipLaunchKernelGGL(bwd, dim3(wg.nblocks + dgrid), dim3(512), lds, s, wa, wg, a, g);
             return hipGetLastError();
           }
           if (lds_w > 64 * 1024) hipFuncSetAttribute((const void*)wgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);
-          hipLaunchKernelGGL(wgr, dim3(wg.nblocks), dim3(256), lds_w, s, wa, wg);
+          hipLaunchKernelGGL(wgr, dim3(wg.nblocks), dim3(ww ? 512 : 256), lds_w, s, wa, wg);
           hipError_t e2 = hipGetLastError();
           if (e2 != hipSuccess || dgrid == 0) return e2;
           if (lds_d > 64 * 1024) hipFuncSetAttribute((const void*)dgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
