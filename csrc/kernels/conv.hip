@@ -105,78 +105,78 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   // (Weights, patch and epilogue operands as three dependent rounds cost ~2 us each: the per-op
   // step's conv launches were latency chains, profiles/round5.md.)
   const int KHW = g.KH * g.KW;
-  const int64_t wstep = a.mode == 0 ? g.K : KHW;
+  const int wstep = a.mode == 0 ? g.K : KHW;
   // effective weight (oc, ic, kh, kw) of column k = w[wbase(k) + oc * wstep] (see weff); koff(k) its patch offset
-  auto wcol = [&](int k, int64_t& base, int& ko) {
+  // (32-bit: a weight tensor is far below 2^31 elements)
+  auto wcol = [&](int k, int& base, int& ko) {
     const bool kv = k < g.K;
     const int ic = kv ? k / KHW : 0, r = k - ic * KHW, kh = r / g.KW, kw = r - kh * g.KW;
     ko = kv ? (ic * g.PR + kh) * g.PW + kw : 0;
-    base = !kv ? -1 : a.mode == 0 ? (int64_t)k : ((int64_t)ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
+    base = !kv ? -1 : a.mode == 0 ? k : (ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
   };
   // single-round weight form: a thread's columns k = tid + NTHR i (i < 32 / COP) x all COP channels
   constexpr int WB = WIDE ? 32 : 8, RB = WIDE ? 16 : 8;  // weight / row loads per batch
   const int wcols = WB / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
   const bool wfast = WIDE && g.Cop <= 32 && g.Kp <= NTHR * wcols;
-  int64_t wb[2] = {-1, -1};
+  int wb[2] = {-1, -1};
   int wko[2] = {0, 0};
   float wv[WB];
   float eb[4], es[4];
 
-  // the zero-padded input patch: a thread owns one patch column, rows step by NTHR / PW
-  const int64_t xbase = (int64_t)n * g.Ci * g.H * g.W;
+  // the zero-padded input patch: a thread owns one patch column, rows step by NTHR / PW.
+  // Addresses: per-image base pointers (scalar) + 32-bit element offsets advanced incrementally.
+  // (64-bit index products per row made the compiler branch around each row's address arithmetic
+  // -- an exec-mask save / restore per row -- and spill SGPRs to VGPR lanes by the hundred.)
   const int rpi = NTHR / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
   const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
   int rr = tid / g.PW;
   const bool prow = rr < rpi;
   int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
+  int ih = oh0 - g.pad + pr;  // this row's input row
   const int iw = pc - g.pad;
   const bool colv = iw >= 0 && iw < g.W;
-  const int64_t nc0 = (int64_t)n * g.Ci;
+  // element offset of (ic, ih, iw) in the image (plain) / of (ic, ih / 2, iw / 2) (pooled input)
+  const int HWi = PIN ? g.Hp * g.Wp : g.H * g.W;
+  int xo = PIN ? ic * HWi : ic * HWi + ih * g.W + iw;
+  const int xo_step = ic_step * HWi + (PIN ? 0 : pr_step * g.W), xo_wrap = HWi - (PIN ? 0 : g.PR * g.W);
+  const int64_t img = (int64_t)n * g.Ci * HWi;
+  const X* xs = static_cast<const X*>(a.x) + img;
+  const X* ys = static_cast<const X*>(a.pout) + (PIN ? img : 0);
+  const uint8_t* is = a.pidx + (PIN ? img : 0);
+  const float* ss = a.pscale ? a.pscale + (int64_t)n * g.Ci : a.w;
   float pv[RB], yo[RB], sc[RB];
   uint8_t bi[RB];
   int at[RB], sel[RB];
   auto load_rows = [&]() {  // RB rows' loads (pooled input: value / argmax / gate / scale)
-    const X* xs = static_cast<const X*>(a.x);
-    const X* ys = static_cast<const X*>(a.pout);
-    if constexpr (!PIN) {
 #pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        const int ih = oh0 - g.pad + pr;
-        const bool in = prow && rr < nrows;
-        at[j] = in ? rr : -1;
-        const bool ok = in && colv && ih >= 0 && ih < g.H;
-        const X t = xs[ok ? xbase + ((int64_t)ic * g.H + ih) * g.W + iw : xbase];
+    for (int j = 0; j < RB; ++j) {
+      const bool in = prow && rr < nrows;
+      at[j] = in ? rr : -1;
+      const bool ok = in && colv && (unsigned)ih < (unsigned)g.H;
+      if constexpr (!PIN) {
+        const X t = xs[(unsigned)(ok ? xo : 0)];
         pv[j] = ok ? (float)t : 0.f;
-        rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
-        pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
-        ic += ic_step;
-        const int wrap = pr >= g.PR;
-        pr -= wrap * g.PR;
-        ic += wrap;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        const int ih = oh0 - g.pad + pr;
-        const bool in = prow && rr < nrows;
-        const bool ok = in && colv && ih >= 0 && ih < g.H;
-        at[j] = in ? rr : -1;
+      } else {
         sel[j] = ((ih & 1) << 1) | (iw & 1);
-        const int64_t po = ok ? ((nc0 + ic) * g.Hp + (ih >> 1)) * g.Wp + (iw >> 1) : 0;
+        const unsigned po = ok ? xo + (ih >> 1) * g.Wp + (iw >> 1) : 0;
         const X t0 = xs[po], t1 = ys[po];
-        const uint8_t t2 = a.pidx[po];
-        const float t3 = (a.pscale ? a.pscale : a.w)[ok && a.pscale ? nc0 + ic : 0];
+        const uint8_t t2 = is[po];
+        const float t3 = ss[(unsigned)(ok && a.pscale ? ic : 0)];
         pv[j] = ok ? (float)t0 : 0.f;
         yo[j] = ok ? (float)t1 : 0.f;
         bi[j] = ok ? t2 : (uint8_t)255;
         sc[j] = ok ? (a.pscale ? t3 : 1.f) : 0.f;
-        rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
-        pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
-        ic += ic_step;
-        const int wrap = pr >= g.PR;
-        pr -= wrap * g.PR;
-        ic += wrap;
       }
+      rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
+      pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
+      ih += pr_step;
+      ic += ic_step;
+      xo += xo_step;
+      const bool wrap = pr >= g.PR;
+      pr -= wrap ? g.PR : 0;
+      ih -= wrap ? g.PR : 0;
+      ic += wrap ? 1 : 0;
+      xo += wrap ? xo_wrap : 0;
     }
   };
   auto store_rows = [&]() {
@@ -196,7 +196,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     for (int j = 0; j < WB; ++j) {  // (unconditional loads at a clamped address, then a select)
       const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
       const bool ok = wb[i] >= 0 && oc < g.Co;
-      const float t = a.w[ok ? wb[i] + oc * wstep : 0];
+      const float t = a.w[(unsigned)(ok ? wb[i] + oc * wstep : 0)];
       wv[j] = ok ? t : 0.f;
     }
   }
@@ -207,7 +207,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     for (int j = 0; j < 4; ++j) {
       const int oc = j * 16 + (tid & 15);
       const bool ok = j < NT && oc < g.Co;
-      const float tb = bp[ok ? oc : 0], tc = cp[ok ? (int64_t)n * g.Co + oc : 0];
+      const float tb = bp[(unsigned)(ok ? oc : 0)], tc = cp[(unsigned)(ok ? n * g.Co + oc : 0)];
       eb[j] = ok && a.bias ? tb : 0.f;
       es[j] = ok && a.chscale ? tc : 1.f;
     }
@@ -239,15 +239,14 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     }
   } else {
     for (int k = tid; k < g.Kp; k += NTHR) {
-      int64_t base;
-      int ko;
+      int base, ko;
       wcol(k, base, ko);
       koff[k] = ko;
       for (int oc0 = 0; oc0 < g.Cop; oc0 += WB) {  // (Cop: a multiple of 16)
 #pragma unroll
         for (int j = 0; j < WB; ++j) {
           const bool ok = base >= 0 && oc0 + j < g.Co;
-          const float t = a.w[ok ? base + (oc0 + j) * wstep : 0];
+          const float t = a.w[(unsigned)(ok ? base + (oc0 + j) * wstep : 0)];
           wv[j] = ok ? t : 0.f;
         }
 #pragma unroll
@@ -489,33 +488,40 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     __syncthreads();  // previous image's LDS reads are done
     // ---- this image's staging in ONE memory round trip where it fits: the first 16 patch rows and
     // the first dy chunk are loaded before any LDS store (two serial rounds were ~2 us each)
-    const int64_t xb = (int64_t)n * g.Ci * g.H * g.W;
-    // the zero-padded input patch: one patch column per thread, rows stepping by NTHR / PW
+    // the zero-padded input patch: one patch column per thread, rows stepping by NTHR / PW;
+    // addresses as in conv_fwd_body (per-image base pointer, 32-bit offsets advanced incrementally)
     const int rpi = NTHR / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
     const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
     int rr = tid / g.PW;
     const bool prow = rr < rpi;
     int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
+    int ih = pr - g.pad;
     const int iw = pc - g.pad;
     const bool colv = iw >= 0 && iw < g.W;
+    const int HWi = g.H * g.W;
+    int xo = ic * HWi + ih * g.W + iw;
+    const int xo_step = ic_step * HWi + pr_step * g.W, xo_wrap = HWi - g.PR * g.W;
+    const X* xs = static_cast<const X*>(x) + (int64_t)n * g.Ci * HWi;
     float xv[RB];
     int at[RB];
     auto load_rows = [&]() {
-      const X* xs = static_cast<const X*>(x);
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
-        const int ih = pr - g.pad;
         const bool in = prow && rr < nrows;
         at[j] = in ? rr : -1;
-        const bool ok = in && colv && ih >= 0 && ih < g.H;
-        const X t = xs[ok ? xb + ((int64_t)ic * g.H + ih) * g.W + iw : xb];
+        const bool ok = in && colv && (unsigned)ih < (unsigned)g.H;
+        const X t = xs[(unsigned)(ok ? xo : 0)];
         xv[j] = ok ? (float)t : 0.f;
         rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
         pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
+        ih += pr_step;
         ic += ic_step;
-        const int wrap = pr >= g.PR;
-        pr -= wrap * g.PR;
-        ic += wrap;
+        xo += xo_step;
+        const bool wrap = pr >= g.PR;
+        pr -= wrap ? g.PR : 0;
+        ih -= wrap ? g.PR : 0;
+        ic += wrap ? 1 : 0;
+        xo += wrap ? xo_wrap : 0;
       }
     };
     auto store_rows = [&]() {
@@ -526,35 +532,38 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
 
     // dy: plain (pst threads per pixel row, NTHR / pst channel groups of 8 side by side) or pooled (a
     // thread owns one pooling window x 16 channels and writes the window's 4 pixels, one nonzero)
-    const int64_t yb = (int64_t)n * g.Co * g.npix;
     const int pst = min(g.npp, NTHR), ocg = NTHR / pst, p0 = tid % pst, og = tid / pst;
     const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
-    const int64_t ybp = (int64_t)n * g.Co * npixp;
+    const int64_t yimg = (int64_t)n * g.Co * (PIN ? npixp : g.npix);  // (per-image bases, 32-bit offsets)
+    const DY* ys = static_cast<const DY*>(dy) + yimg;
+    const DY* os = static_cast<const DY*>(wa.pout) + (PIN ? yimg : 0);
+    const uint8_t* is = wa.pidx + (PIN ? yimg : 0);
+    const float* ss = wa.pscale ? wa.pscale + (int64_t)n * g.Co : slab;
     const int wst = max(1, min(npixp, NTHR)), wgr = NTHR / wst, q0 = tid % wst, gq = tid / wst;
     float dv[RB], yo[RB], sc[RB];
     uint8_t bi[RB];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
     bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
     auto load_dy = [&]() {  // one chunk's loads
-      const DY* ys = static_cast<const DY*>(dy);
       if constexpr (!PIN) {
+        const int yo0 = d_oc0 * g.npix + d_p;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool ok = d_oc0 + j < g.Co && d_p < g.npix;
-          const DY t = ys[ok ? yb + (int64_t)(d_oc0 + j) * g.npix + d_p : yb];
+          const DY t = ys[(unsigned)(ok ? yo0 + j * g.npix : 0)];
           dv[j] = ok ? (float)t : 0.f;
         }
       } else {
-        const DY* os = static_cast<const DY*>(wa.pout);
         const int ph = d_q / PWp, pw = d_q - ph * PWp;
         d_pb = 2 * ph * g.OW + 2 * pw;
+        const int po0 = d_oc0 * npixp + d_q;
 #pragma unroll
         for (int j = 0; j < RB; ++j) {
           const bool ok = d_oc0 + j < g.Co;
-          const int64_t po = ok ? ybp + (int64_t)(d_oc0 + j) * npixp + d_q : ybp;
+          const unsigned po = ok ? po0 + j * npixp : 0;
           const DY t0 = ys[po], t1 = os[po];
-          const uint8_t t2 = wa.pidx[po];
-          const float t3 = (wa.pscale ? wa.pscale : wa.slab)[ok && wa.pscale ? (int64_t)n * g.Co + d_oc0 + j : 0];
+          const uint8_t t2 = is[po];
+          const float t3 = ss[(unsigned)(ok && wa.pscale ? d_oc0 + j : 0)];
           dv[j] = ok ? (float)t0 : 0.f;
           yo[j] = ok ? (float)t1 : 0.f;
           bi[j] = ok ? t2 : (uint8_t)255;
@@ -779,6 +788,11 @@ static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid
   g.OH = g.H + 2 * g.pad - g.KH + 1;
   g.OW = g.W + 2 * g.pad - g.KW + 1;
   if (g.OH <= 0 || g.OW <= 0 || a.N <= 0) return hipSuccess;
+  // (the stagings' offsets are 32-bit: within one image, one weight tensor, one channel-scale tensor)
+  const int64_t lim = INT32_MAX;
+  if ((int64_t)g.Ci * g.H * g.W >= lim || (int64_t)g.Co * g.OH * g.OW >= lim ||
+      (int64_t)g.Ci * g.Co * g.KH * g.KW >= lim || (int64_t)a.N * std::max(g.Ci, g.Co) >= lim)
+    return hipErrorInvalidConfiguration;
   if (a.pool_k != 0 && (a.pool_k != 2 || a.mode != 0 || (g.OH & 1) || (g.OW & 1))) return hipErrorInvalidValue;
   if (a.chscale_out && (a.pool_k != 2 || a.chscale)) return hipErrorInvalidValue;
   g.K = g.Ci * g.KH * g.KW;
@@ -861,6 +875,8 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
   if (wg.OH <= 0 || wg.OW <= 0) return hipErrorInvalidValue;
   if (wg.PW > 256) return hipErrorInvalidConfiguration;  // (patch staging: one column per thread)
   if (wg.Cop > 64 || (wg.Kc / 16) > 32) return hipErrorInvalidConfiguration;  // accumulator budget
+  if ((int64_t)b.IC * b.H * b.W >= INT32_MAX || (int64_t)b.OC * wg.npix >= INT32_MAX || (int64_t)b.N * b.OC >= INT32_MAX)
+    return hipErrorInvalidConfiguration;  // (32-bit staging offsets, see conv_geo)
   if (b.pidx && (!b.pout || (wg.OH & 1) || (wg.OW & 1))) return hipErrorInvalidValue;
   const size_t es = b.mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
   const size_t lds_main = (size_t)wg.Cop * (wg.npp + 8) * es + (size_t)wg.Kc * 4 + (size_t)wg.npp * 4 +
