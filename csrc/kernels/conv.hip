@@ -42,6 +42,14 @@ struct ConvGeo {
   int Hp, Wp;            // pooled input dims (a.pidx set: the input is given max-pooled)
 };
 
+// a / d for small non-negative ints (0 <= a < 2^20, d >= 1): (a + 0.5) * rcp(d) truncated.  v_rcp_f32
+// is within 1 ulp, so the product's relative error (< 1.5 * 2^-23) stays below the 0.5 / d margin
+// that a + 0.5 keeps from the neighbouring integers.  4 VALU instructions instead of a ~25-instruction
+// signed integer division (the stagings had a dozen per thread in front of their first load).
+__device__ __forceinline__ int qdiv(int a, int d) {
+  return (int)(((float)a + 0.5f) * __builtin_amdgcn_rcpf((float)d));
+}
+
 __device__ __forceinline__ float ldf(const void* p, int dt, int64_t i) {
   switch (dt) {
     case kF32: return ((const float*)p)[i];
@@ -110,7 +118,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   // (32-bit: a weight tensor is far below 2^31 elements)
   auto wcol = [&](int k, int& base, int& ko) {
     const bool kv = k < g.K;
-    const int ic = kv ? k / KHW : 0, r = k - ic * KHW, kh = r / g.KW, kw = r - kh * g.KW;
+    const int ic = kv ? qdiv(k, KHW) : 0, r = k - ic * KHW, kh = qdiv(r, g.KW), kw = r - kh * g.KW;
     ko = kv ? (ic * g.PR + kh) * g.PW + kw : 0;
     base = !kv ? -1 : a.mode == 0 ? k : (ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
   };
@@ -127,11 +135,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   // Addresses: per-image base pointers (scalar) + 32-bit element offsets advanced incrementally.
   // (64-bit index products per row made the compiler branch around each row's address arithmetic
   // -- an exec-mask save / restore per row -- and spill SGPRs to VGPR lanes by the hundred.)
-  const int rpi = NTHR / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
-  const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
-  int rr = tid / g.PW;
+  const int rpi = qdiv(NTHR, g.PW), nrows = g.Ci * g.PR;
+  const int ic_step = qdiv(rpi, g.PR), pr_step = rpi - ic_step * g.PR;
+  int rr = qdiv(tid, g.PW);
+  const int pc = tid - rr * g.PW;
   const bool prow = rr < rpi;
-  int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
+  int ic = prow ? qdiv(rr, g.PR) : 0, pr = rr - ic * g.PR;
   int ih = oh0 - g.pad + pr;  // this row's input row
   const int iw = pc - g.pad;
   const bool colv = iw >= 0 && iw < g.W;
@@ -273,12 +282,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     const int m = mt * 16 + (lane & 15);
     int oh, ow;
     if (pooled) {
-      const int p = m >> 2, q = m & 3;
-      oh = 2 * (p / PWb) + (q >> 1);
-      ow = 2 * (p % PWb) + (q & 1);
+      const int p = m >> 2, q = m & 3, pq = qdiv(p, PWb);
+      oh = 2 * pq + (q >> 1);
+      ow = 2 * (p - pq * PWb) + (q & 1);
     } else {
-      oh = m / g.OW;
-      ow = m % g.OW;
+      oh = qdiv(m, g.OW);
+      ow = m - oh * g.OW;
     }
     const bool valid = m < npix;
     const int pb = valid ? oh * g.PW + ow : 0;     // oh is band-relative
@@ -374,8 +383,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 #pragma unroll
           for (int r = 1; r < 4; ++r)
             if (acc[j][r] > best) { best = acc[j][r]; bi = r; }
-          const int p = wbase >> 2;
-          const int ph = (oh0 >> 1) + p / PWb, pw = p % PWb;
+          const int p = wbase >> 2, pq = qdiv(p, PWb);
+          const int ph = (oh0 >> 1) + pq, pw = p - pq * PWb;
           const int PH = g.OH >> 1;
           float sc = es[j];
           if (nc != 0) {  // (channels past the first 64: operands not preloaded)
@@ -395,7 +404,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
           for (int r = 0; r < 4; ++r) {
             const int mm = mt * 16 + 4 * (lane >> 4) + r;
             if (mm >= npix) continue;
-            const int ohh = oh0 + mm / g.OW, oww = mm % g.OW;
+            const int mq = qdiv(mm, g.OW), ohh = oh0 + mq, oww = mm - mq * g.OW;
             static_cast<Y*>(a.y)[(((int64_t)n * g.Co + oc) * g.OH + ohh) * g.OW + oww] = (Y)(acc[j][r] + b);
           }
         }
@@ -463,12 +472,15 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   for (int k = tid; k < g.Kc; k += NTHR) {
     int o = pe;  // the constant-one slot (db column) / zero-weight padding
     if (k < g.K) {
-      const int ic = k / (g.KH * g.KW), r = k % (g.KH * g.KW);
-      o = (ic * g.PR + r / g.KW) * g.PW + r % g.KW;
+      const int ic = qdiv(k, g.KH * g.KW), r = k - ic * (g.KH * g.KW), kh = qdiv(r, g.KW);
+      o = (ic * g.PR + kh) * g.PW + r - kh * g.KW;
     }
     koff[k] = o;
   }
-  for (int p = tid; p < g.npp; p += NTHR) pbase[p] = p < g.npix ? (p / g.OW) * g.PW + p % g.OW : 0;
+  for (int p = tid; p < g.npp; p += NTHR) {
+    const int ph = qdiv(p, g.OW);
+    pbase[p] = p < g.npix ? ph * g.PW + p - ph * g.OW : 0;
+  }
 
   const int MT = g.Cop >> 4, NT = g.Kc >> 4;
   const int psplit = NT >= NW ? 1 : NW / NT;
@@ -490,11 +502,12 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     // the first dy chunk are loaded before any LDS store (two serial rounds were ~2 us each)
     // the zero-padded input patch: one patch column per thread, rows stepping by NTHR / PW;
     // addresses as in conv_fwd_body (per-image base pointer, 32-bit offsets advanced incrementally)
-    const int rpi = NTHR / g.PW, pc = tid % g.PW, nrows = g.Ci * g.PR;
-    const int ic_step = rpi / g.PR, pr_step = rpi - ic_step * g.PR;
-    int rr = tid / g.PW;
+    const int rpi = qdiv(NTHR, g.PW), nrows = g.Ci * g.PR;
+    const int ic_step = qdiv(rpi, g.PR), pr_step = rpi - ic_step * g.PR;
+    int rr = qdiv(tid, g.PW);
+    const int pc = tid - rr * g.PW;
     const bool prow = rr < rpi;
-    int ic = prow ? rr / g.PR : 0, pr = rr - ic * g.PR;
+    int ic = prow ? qdiv(rr, g.PR) : 0, pr = rr - ic * g.PR;
     int ih = pr - g.pad;
     const int iw = pc - g.pad;
     const bool colv = iw >= 0 && iw < g.W;
@@ -532,14 +545,14 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
 
     // dy: plain (pst threads per pixel row, NTHR / pst channel groups of 8 side by side) or pooled (a
     // thread owns one pooling window x 16 channels and writes the window's 4 pixels, one nonzero)
-    const int pst = min(g.npp, NTHR), ocg = NTHR / pst, p0 = tid % pst, og = tid / pst;
+    const int pst = min(g.npp, NTHR), ocg = qdiv(NTHR, pst), og = qdiv(tid, pst), p0 = tid - og * pst;
     const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
     const int64_t yimg = (int64_t)n * g.Co * (PIN ? npixp : g.npix);  // (per-image bases, 32-bit offsets)
     const DY* ys = static_cast<const DY*>(dy) + yimg;
     const DY* os = static_cast<const DY*>(wa.pout) + (PIN ? yimg : 0);
     const uint8_t* is = wa.pidx + (PIN ? yimg : 0);
     const float* ss = wa.pscale ? wa.pscale + (int64_t)n * g.Co : slab;
-    const int wst = max(1, min(npixp, NTHR)), wgr = NTHR / wst, q0 = tid % wst, gq = tid / wst;
+    const int wst = max(1, min(npixp, NTHR)), wgr = qdiv(NTHR, wst), gq = qdiv(tid, wst), q0 = tid - gq * wst;
     float dv[RB], yo[RB], sc[RB];
     uint8_t bi[RB];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
@@ -554,7 +567,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
           dv[j] = ok ? (float)t : 0.f;
         }
       } else {
-        const int ph = d_q / PWp, pw = d_q - ph * PWp;
+        const int ph = qdiv(d_q, PWp), pw = d_q - ph * PWp;
         d_pb = 2 * ph * g.OW + 2 * pw;
         const int po0 = d_oc0 * npixp + d_q;
 #pragma unroll
@@ -616,7 +629,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
     if (PIN) {  // (the MFMA K padding past npix: the window writes cover pixels < npix only)
       for (int i = tid; i < g.Cop * (g.npp - g.npix); i += NTHR) {
-        const int oc = i / (g.npp - g.npix), pp = g.npix + i % (g.npp - g.npix);
+        const int oc = qdiv(i, g.npp - g.npix), pp = g.npix + i - oc * (g.npp - g.npix);
         dys[oc * LDY + pp] = Stor<T>::of(0.f);
       }
     }
@@ -689,7 +702,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     }
     __syncthreads();
     for (int i = tid; i < g.Co * NT * 16; i += NTHR) {
-      const int oc = i / (NT * 16), col = i % (NT * 16);
+      const int oc = qdiv(i, NT * 16), col = i - oc * (NT * 16);
       if (col > g.K) continue;
       const int nt = col >> 4;
       float s = 0.f;
