@@ -354,6 +354,157 @@ __device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, 
   }
 }
 
+// A small-GEMM tile's end: fixed-order combine of the four waves' K ranges (wave order) through
+// LDS, then the epilogue (or the classifier head's) on wave 0.
+template <typename T, bool HEAD>
+__device__ __forceinline__ void small_finish(const GemmArgs& a, const f32x4& acc, float (*part)[256], int mt, int n,
+                                             int Np, const int64_t (&tgt)[4], float bias_v, uint64_t off) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, kq = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
+  __syncthreads();
+  if (wave != 0) return;
+  if (HEAD && a.head_part) {  // classifier head: log_softmax rows + NLL (one 16-column tile holds a row)
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      v[r] = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) + part[3][r * 64 + lane];
+    head_epilogue(a, mt, n, kq, v, lane, tgt, bias_v);
+    return;
+  }
+  const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float v = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) +
+                    part[3][r * 64 + lane];
+    const int mm = mt * 16 + 4 * kq + r;
+    if (mm < a.M && n < Np) epilogue_b<T>(a, mm, n, v, off, dscale, bias_v);
+  }
+}
+
+// Raw storage of 8 operand elements between load and conversion: the 16-bit bits, or fp32 values.
+template <typename X> struct RawV { typedef u16x8 t; };
+template <> struct RawV<float> { typedef f32x8 t; };
+template <typename X>
+__device__ __forceinline__ float raw_f(typename RawV<X>::t r, int j) {
+  if constexpr (__is_same(X, float)) return r[j];
+  else return (float)of_bits<X>(r[j]);
+}
+
+// 8 elements p[0], p[sk], .., p[7 sk] as raw storage: one vector load (vec: K-contiguous, aligned,
+// all 8 inside K), else 8 element loads at clamped, valid offsets (the caller masks j >= nk).  No
+// arithmetic on the loaded values: they stay in flight until the conversion phase (gather8
+// converted inside its dtype / vector branches, which made every gather wait for its own loads).
+template <typename X>
+__device__ __forceinline__ typename RawV<X>::t load8_raw(const X* p, int64_t sk, int nk, bool vec) {
+  typedef typename RawV<X>::t V;
+  if (vec) return *reinterpret_cast<const V*>(p);
+  V r;
+  const int last = max(nk - 1, 0);
+  if constexpr (__is_same(X, float)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = p[(int64_t)min(j, last) * sk];
+  } else {
+    const unsigned short* q = reinterpret_cast<const unsigned short*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = q[(int64_t)min(j, last) * sk];
+  }
+  return r;
+}
+
+__device__ int64_t kSmallZero[16];  // a valid address for absent optional operands (reads 0)
+
+// The small GEMM for operand element types known at compile time (XA: A's and the gate's, XB: B's;
+// fp32 or the compute type's 16-bit type): all of a wave's K-steps' operand loads (up to 4 x
+// (A, gate, B) fragments, the log-softmax targets) are issued before any is converted, and the
+// epilogue operands are unconditional loads from valid addresses -- one memory round trip per 4
+// K-steps instead of one per fragment.  Same arithmetic as gemm_small_body (bitwise equal).
+template <typename T, bool HEAD, typename XA, typename XB>
+__device__ __forceinline__ void gemm_small_typed(const GemmArgs& a, const int blk, float (*part)[256]) {
+  typedef typename RawV<XA>::t VA;
+  typedef typename RawV<XB>::t VB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+  const int Np = a.N + (a.rowsum ? 1 : 0);
+  const int tn = (Np + 15) >> 4;
+  const int mt = blk / tn, nt = blk - mt * tn;
+  const int m = mt * 16 + l16, n = nt * 16 + l16;
+  const bool mv = m < a.M, nv = n < a.N;
+  const bool avec = a.a_mode == kKContig, bvec = a.b_mode == kKContig;
+  const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
+  const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  // epilogue operands: unconditional loads (absent ones read kSmallZero), issued with the first K-steps'
+  const float* bp = a.bias ? a.bias : reinterpret_cast<const float*>(kSmallZero);
+  const float bias_t = bp[a.bias && nv ? n : 0];
+  const int64_t* odp = a.offset_dev ? a.offset_dev : kSmallZero;
+  const int64_t od = odp[0];
+  int64_t tgt[4] = {-1, -1, -1, -1};
+  if (HEAD && a.head_part) {
+    const int64_t* tp = a.head_target;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int mm = mt * 16 + 4 * kq + r;
+      tgt[r] = tp[mm < a.M ? mm : 0];
+    }
+  }
+  const float* gp = a.lsm_target ? a.lsm_gout : reinterpret_cast<const float*>(kSmallZero);
+  const float gout = gp[0];
+  const int64_t* lt = a.lsm_target ? a.lsm_target : kSmallZero;
+  const int64_t tgt_m = lt[a.lsm_target && a.lsm_rows_are_m && mv ? m : 0];  // (dX of the head: row m's target)
+  const XA* Ap = static_cast<const XA*>(a.A);
+  const XA* Gp = a.G ? static_cast<const XA*>(a.G) : Ap;
+  const XB* Bp = static_cast<const XB*>(a.B);
+  for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
+    VA ra[4], rg[4];
+    VB rb[4];
+    int64_t tk[4][8];  // (dW of the head: the targets of the 8 k rows)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ks = kb0 + u;
+      if (ks >= ks1) break;  // (uniform)
+      const int kb = ks * 32 + 8 * kq;
+      const int nk = min(8, max(0, a.K - kb));
+      const bool full = ks * 32 + 32 <= a.K;  // (uniform: every lane's 8 elements inside K)
+      const int kc = min(kb, a.K - 1);
+      const int64_t ao = (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak;
+      ra[u] = load8_raw<XA>(Ap + ao, a.sak, mv ? nk : 0, avec && full);
+      if (a.G) rg[u] = load8_raw<XA>(Gp + ao, a.sak, mv ? nk : 0, avec && full);
+      rb[u] = load8_raw<XB>(Bp + (int64_t)kc * a.sbk + (int64_t)(nv ? n : 0) * a.sbn, a.sbk, nv ? nk : 0,
+                            bvec && full);  // (uniform: rows past M / N read row 0, masked later)
+      if (a.lsm_target && !a.lsm_rows_are_m) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tk[u][j] = lt[min(kc + j, a.K - 1)];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const float lsm_g = gout / a.lsm_div;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kb0 + u >= ks1) break;
+      const int kb = (kb0 + u) * 32 + 8 * kq;
+      const int nk = min(8, max(0, a.K - kb));
+      float fa[8], fb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ia = mv && j < nk;
+        float v = ia ? raw_f<XA>(ra[u], j) : 0.f;
+        if (a.lsm_target) {  // log-probs -> dz = g * (exp(logp) - onehot(target)) (lsm_nll_bwd_kernel's rule)
+          const int c = a.lsm_rows_are_m ? kb + j : m;
+          const int64_t t = a.lsm_rows_are_m ? tgt_m : tk[u][j];
+          v = ia ? lsm_g * (__expf(v) - (c == t ? 1.f : 0.f)) : 0.f;
+        }
+        if (a.G) v = (ia ? raw_f<XA>(rg[u], j) : 0.f) > 0.f ? v * a.gate_scale : 0.f;
+        fa[j] = v;
+        fb[j] = nv ? (j < nk ? raw_f<XB>(rb[u], j) : 0.f) : (n == a.N && j < nk) ? 1.f : 0.f;  // (ones column)
+      }
+      acc = Mfma<T>::mma(to_frag<T>(fa), to_frag<T>(fb), acc);
+    }
+  }
+  const float bias_v = a.bias && nv ? bias_t : 0.f;
+  const uint64_t off = a.offset + (a.offset_dev ? ((uint64_t)od << 20) : 0ull);  // (rng_offset)
+  small_finish<T, HEAD>(a, acc, part, mt, n, Np, tgt, bias_v, off);
+}
+
 template <typename T, bool HEAD>  // HEAD: the classifier-head epilogue may be asked for (a.head_part)
 __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk, float (*part)[256]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
@@ -425,33 +576,28 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk
       acc = Mfma<T>::mma(to_frag<T>(fa[u]), to_frag<T>(fb[u]), acc);
     }
   }
-  // fixed-order combine of the four K ranges (wave order), then the epilogue on wave 0
-#pragma unroll
-  for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
-  __syncthreads();
-  if (wave != 0) return;
-  if (HEAD && a.head_part) {  // classifier head: log_softmax rows + NLL (one 16-column tile holds a row)
-    float v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      v[r] = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) + part[3][r * 64 + lane];
-    head_epilogue(a, mt, n, kq, v, lane, tgt, bias_v);
-    return;
+  small_finish<T, HEAD>(a, acc, part, mt, n, Np, tgt, bias_v, off);
+}
+
+// a small-GEMM tile: the typed body for the operand dtypes it is instantiated for (fp32 or the
+// compute type's 16-bit type; a gate of A's dtype), else the generic gathers
+template <typename T, bool HEAD>
+__device__ __forceinline__ void gemm_small_any(const GemmArgs& a, int blk, float (*part)[256]) {
+  const bool g_ok = !a.G || a.g_dtype == a.a_dtype;
+  if (g_ok && a.a_dtype == kF32 && a.b_dtype == kF32) return gemm_small_typed<T, HEAD, float, float>(a, blk, part);
+  if constexpr (!__is_same(T, float)) {
+    constexpr int c16 = __is_same(T, __bf16) ? kBF16 : kF16;
+    if (g_ok && a.a_dtype == c16 && a.b_dtype == kF32) return gemm_small_typed<T, HEAD, T, float>(a, blk, part);
+    if (g_ok && a.a_dtype == kF32 && a.b_dtype == c16) return gemm_small_typed<T, HEAD, float, T>(a, blk, part);
+    if (g_ok && a.a_dtype == c16 && a.b_dtype == c16) return gemm_small_typed<T, HEAD, T, T>(a, blk, part);
   }
-  const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float v = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + part[2][r * 64 + lane]) +
-                    part[3][r * 64 + lane];
-    const int mm = mt * 16 + 4 * kq + r;
-    if (mm < a.M && n < Np) epilogue_b<T>(a, mm, n, v, off, dscale, bias_v);
-  }
+  gemm_small_body<T, HEAD>(a, blk, part);
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs a) {
   __shared__ float part[4][256];
-  gemm_small_body<T, true>(a, blockIdx.x, part);
+  gemm_small_any<T, true>(a, blockIdx.x, part);
 }
 
 // Two independent small GEMMs in one launch (nn.Linear's backward: dX = dY.W and dW = dY^T.X + the
@@ -460,7 +606,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) gemm_small_pair_kernel(GemmArgs a, GemmArgs b, int tiles_a) {
   __shared__ float part[4][256];
   const bool first = (int)blockIdx.x < tiles_a;  // (one body on the selected argument block)
-  gemm_small_body<T, false>(first ? a : b, first ? blockIdx.x : blockIdx.x - tiles_a, part);
+  gemm_small_any<T, false>(first ? a : b, first ? blockIdx.x : blockIdx.x - tiles_a, part);
 }
 
 // Fixed-order sum of the split-K partials + the epilogue.
