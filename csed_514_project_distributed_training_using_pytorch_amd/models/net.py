@@ -13,7 +13,8 @@ The GPU forward is five fused HIP kernels instead of ~15 ATen ops:
     fc2 + bias                                  (linear, fp32 logits)
     log_softmax                                 (log_softmax)
 
-(with targets: fc2 + log_softmax + NLL as ops.linear_log_softmax_nll, the loss returned)
+(with targets: fc1 + relu + dropout + fc2 + log_softmax + NLL as ops.mlp_head_nll, one launch, the
+loss returned)
 
 The CPU forward is the reference forward verbatim in stock PyTorch (the fp32
 oracle used by the tests).
@@ -54,10 +55,11 @@ class Net(nn.Module):
         x = ops.conv2d_pool_relu(x, self.conv2.weight, self.conv2.bias,
                                  dropout2d_p=p2 if self.training else 0.0)  # Dropout2d drawn in-kernel
         x = x.view(-1, 320)
-        x = ops.linear(x, self.fc1.weight, self.fc1.bias,
-                       act="relu_dropout" if self.training else "relu", p=0.5)
-        if target is not None:
-            return ops.linear_log_softmax_nll(x, self.fc2.weight, self.fc2.bias, target)
+        act = "relu_dropout" if self.training else "relu"
+        if target is not None:  # fc1 + relu + dropout + fc2 + log_softmax + NLL: one forward launch
+            return ops.mlp_head_nll(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, target,
+                                    act=act, p=0.5)
+        x = ops.linear(x, self.fc1.weight, self.fc1.bias, act=act, p=0.5)
         x = ops.linear(x, self.fc2.weight, self.fc2.bias, out_dtype=torch.float32)
         return ops.log_softmax(x, dim=1)
 

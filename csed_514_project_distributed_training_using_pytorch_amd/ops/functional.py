@@ -418,7 +418,7 @@ def log_softmax_nll(z, target, reduction: str = "mean"):
     return _LogSoftmaxNLL.apply(z, target, _RED[reduction])
 
 
-# arrival counters of the fused head's tile hand-off, one per head weight (zero between launches;
+# the fused head's loss words (fixed-point sum + arrival count, int64), one per head weight (zero between launches;
 # launches of one head are stream-ordered)
 _head_cnt: dict[int, tuple[weakref.ref, torch.Tensor]] = {}
 
@@ -428,7 +428,7 @@ def _head_counter(w: torch.Tensor) -> torch.Tensor:
     if hit is None or hit[0]() is not w or hit[1].device != w.device:
         for k in [k for k, (r, _) in _head_cnt.items() if r() is None]:
             del _head_cnt[k]
-        hit = (weakref.ref(w), torch.zeros(1, device=w.device, dtype=torch.int32))
+        hit = (weakref.ref(w), torch.zeros(1, device=w.device, dtype=torch.int64))
         _head_cnt[id(w)] = hit
     return hit[1]
 
@@ -490,3 +490,79 @@ def cross_entropy(x, target, reduction: str = "mean"):
 def accuracy_count(logp: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     """Number of argmax hits, kept on device (no host sync)."""
     return (logp.argmax(dim=1) == target).sum()
+
+
+_DT_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+class _MlpHeadNLL(torch.autograd.Function):
+    """nll(log_softmax(act(x W1^T + b1) W2^T + b2)): fc1 with its ReLU / dropout and the classifier
+    head + loss in ONE forward launch (h kept in LDS between them, written once for the backward);
+    the backward is the two layers' own: the head's paired GEMMs from the log-probs, then fc1's
+    (gate = h), so gradients are those of linear() + linear_log_softmax_nll()."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, target, act, p, seed, off, dev, reduction):
+        x2 = x.contiguous()
+        target = target.contiguous().long()
+        M = x2.shape[0]
+        h = torch.empty((M, w1.shape[0]), device=x.device, dtype=_act_dtype(x2))
+        logp = torch.empty((M, w2.shape[0]), device=x.device, dtype=torch.float32)
+        out = torch.empty((), device=x.device, dtype=torch.float32)
+        part = torch.empty((M + 15) // 16, device=x.device, dtype=torch.float32)
+        _ops().mlp_head_fwd(x2, w1, b1, act, p, seed, off, dev, h, w2, b2, target, logp, out, part,
+                            _head_counter(w2), reduction, _mfma())
+        ctx.save_for_backward(x2, w1, h, w2, logp, target)
+        ctx.act, ctx.p, ctx.reduction = act, p, reduction
+        ctx.b1, ctx.b2 = b1, b2
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x2, w1, h, w2, logp, target = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        mf = _mfma()
+        # the head (linear_log_softmax_nll's backward): dh, dW2, db2 from the kept log-probs
+        dh = torch.empty(h.shape, device=h.device, dtype=h.dtype) if (need[0] or need[1] or need[2]) else None
+        dw2 = db2 = None
+        if need[3] or (ctx.b2 is not None and need[4]):
+            dw2 = _grad_buffer(w2, w2.shape, w2.device)
+            if ctx.b2 is not None:
+                db2 = _grad_buffer(ctx.b2, (w2.shape[0],), w2.device)
+        div = float(logp.shape[0]) if ctx.reduction == 1 else 1.0
+        _ops().linear_bwd(logp, h, w2, None, 1.0, dh, dw2, db2, mf, target, gout.contiguous().float(), div)
+        # fc1 (linear()'s backward, gate = h)
+        dx = dw1 = db1 = None
+        if dh is not None:
+            gs = 1.0 / (1.0 - ctx.p) if ctx.act == 2 else 1.0
+            if need[0]:
+                dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
+            if need[1] or (ctx.b1 is not None and need[2]):
+                dw1 = _grad_buffer(w1, w1.shape, w1.device)
+                if ctx.b1 is not None:
+                    db1 = _grad_buffer(ctx.b1, (w1.shape[0],), w1.device)
+            _ops().linear_bwd(dh, x2, w1, h if ctx.act else None, gs, dx, dw1, db1, mf)
+        return (dx, dw1 if need[1] else None, db1 if need[2] else None, dw2 if need[3] else None,
+                db2 if need[4] else None, None, None, None, None, None, None, None)
+
+
+def mlp_head_nll(x, w1, b1, w2, b2, target, act: str = "relu", p: float = 0.0, reduction: str = "mean"):
+    """nll_loss(log_softmax(linear(linear(x, w1, b1, act, p), w2, b2), 1), target) -- an MLP classifier
+    head and its loss (ref src/model.py:19-22 + src/train.py:74): one forward launch when the shapes fit
+    (fc1 width <= 64, <= 16 classes, a small batch), else linear() + linear_log_softmax_nll()."""
+    if reduction not in ("mean", "sum"):
+        raise ValueError("mlp_head_nll supports reduction 'mean' or 'sum'")
+    if act not in _ACT:
+        raise ValueError(f"unknown activation {act!r}")
+    if not x.is_cuda:
+        return linear_log_softmax_nll(linear(x, w1, b1, act, p), w2, b2, target, reduction)
+    a = _ACT[act]
+    if a == 2 and p == 0.0:
+        a = 1
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.dtype not in (torch.bfloat16, torch.float16, torch.float32) or not _ops().mlp_head_ok(
+            x2, w1, w2, _DT_CODE[_act_dtype(x2)], _mfma()):
+        return linear_log_softmax_nll(linear(x, w1, b1, act, p), w2, b2, target, reduction)
+    seed, off, dev = default_state.next() if a == 2 else (0, 0, None)  # (linear()'s draw, same order)
+    return _MlpHeadNLL.apply(x2, w1, b1, w2, b2, target, a, float(p), seed, off, dev, _RED[reduction])
+

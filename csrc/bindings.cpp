@@ -271,16 +271,57 @@ void linear_lsm_nll_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>
   dev(cnt, "cnt");
   TORCH_CHECK(reduction == 1 || reduction == 2, "linear_lsm_nll_fwd: reduction mean (1) or sum (2)");
   TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == x.size(0) && out.numel() == 1 &&
-                  out.scalar_type() == at::kFloat && cnt.scalar_type() == at::kInt && part.scalar_type() == at::kFloat &&
+                  out.scalar_type() == at::kFloat && cnt.scalar_type() == at::kLong && part.scalar_type() == at::kFloat &&
                   part.numel() >= (x.size(0) + 15) / 16,
               "linear_lsm_nll_fwd: bad target / out / scratch");
   const optional<Tensor> none;
   const c10::DeviceGuard gd(x.device());
   csed::GemmArgs a = make_gemm(x, w.t(), logp, b, 1.0, 0.0, 0, 0.0, 0, 0, none, none, 1.0, mfma_dtype, none);
-  a.head_target = target.data_ptr<int64_t>(); a.head_part = part.data_ptr<float>(); a.head_cnt = cnt.data_ptr<int>();
+  a.head_target = target.data_ptr<int64_t>(); a.head_part = part.data_ptr<float>(); a.head_cnt = reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>());
   a.head_out = out.data_ptr<float>(); a.head_mean = reduction == 1;
   TORCH_CHECK(csed::gemm_head_ok(a), "linear_lsm_nll_fwd: shapes outside the fused head (C <= 16, small GEMM)");
   CHECK_HIP(csed::launch_gemm(a, cur_stream(x)));
+}
+
+// fc1 + activation (relu / relu + dropout) and the classifier head + loss forward in ONE launch:
+// h = act(x W1^T + b1) (written: the backward's gate and operand), logp = log_softmax(h W2^T + b2),
+// out = nll(logp, target); part / cnt as linear_lsm_nll_fwd.
+void mlp_head_fwd(const Tensor& x, const Tensor& w1, const optional<Tensor>& b1, int64_t act, double drop_p,
+                  int64_t seed, int64_t offset, const optional<Tensor>& offset_dev, Tensor& h, const Tensor& w2,
+                  const optional<Tensor>& b2, const Tensor& target, Tensor& logp, Tensor& out, Tensor& part,
+                  Tensor& cnt, int64_t reduction, int64_t mfma_dtype, const optional<Tensor>& dbg) {
+  dev(x, "x"); dev(w1, "w1"); dev(h, "h"); dev(w2, "w2"); dev(target, "target"); dev(logp, "logp");
+  dev(out, "out"); dev(part, "part"); dev(cnt, "cnt");
+  TORCH_CHECK(reduction == 1 || reduction == 2, "mlp_head_fwd: reduction mean (1) or sum (2)");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == x.size(0) && out.numel() == 1 &&
+                  out.scalar_type() == at::kFloat && cnt.scalar_type() == at::kLong && part.scalar_type() == at::kFloat &&
+                  part.numel() >= (x.size(0) + 15) / 16 && target.is_contiguous(),
+              "mlp_head_fwd: bad target / out / scratch");
+  const optional<Tensor> none;
+  const c10::DeviceGuard gd(x.device());
+  csed::GemmArgs a = make_gemm(x, w1.t(), h, b1, 1.0, 0.0, act, drop_p, seed, offset, offset_dev, none, 1.0,
+                               mfma_dtype, none);
+  csed::GemmArgs g = make_gemm(h, w2.t(), logp, b2, 1.0, 0.0, 0, 0.0, 0, 0, none, none, 1.0, mfma_dtype, none);
+  g.head_target = target.data_ptr<int64_t>(); g.head_part = part.data_ptr<float>(); g.head_cnt = reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>());
+  g.head_out = out.data_ptr<float>(); g.head_mean = reduction == 1;
+  if (dbg.has_value()) {  // (phase stamps, diagnostics: [cdiv(M, 16)][8] int64)
+    dev(*dbg, "dbg");
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= (x.size(0) + 15) / 16 * 8, "mlp_head_fwd: dbg");
+    g.ws = reinterpret_cast<float*>(dbg->data_ptr<int64_t>());
+  }
+  TORCH_CHECK(csed::mlp_head_ok(a, g), "mlp_head_fwd: shapes / dtypes outside the fused MLP head");
+  CHECK_HIP(csed::launch_mlp_head(a, g, cur_stream(x)));
+}
+
+// whether mlp_head_fwd takes these operands (x [M, K] in dtype xdt, h in hdt)
+bool mlp_head_ok(const Tensor& x, const Tensor& w1, const Tensor& w2, int64_t h_dtype_code, int64_t mfma_dtype) {
+  csed::GemmArgs a{}, g{};
+  a.M = x.size(0); a.N = w1.size(0); a.K = x.size(1); a.a_dtype = dcode(x); a.b_dtype = dcode(w1);
+  a.c_dtype = (int)h_dtype_code; a.act = 2; a.mfma_dtype = mcode(mfma_dtype);
+  g.M = x.size(0); g.N = w2.size(0); g.K = w2.size(1); g.a_dtype = a.c_dtype; g.b_dtype = dcode(w2);
+  g.c_dtype = csed::kF32; g.mfma_dtype = a.mfma_dtype;
+  g.head_part = reinterpret_cast<float*>(1); g.head_target = reinterpret_cast<const int64_t*>(1);  // (present)
+  return csed::mlp_head_ok(a, g);
 }
 
 bool linear_lsm_nll_ok(const Tensor& x, const Tensor& w) {
@@ -793,6 +834,10 @@ TORCH_LIBRARY(csed, m) {
   m.def("linear_lsm_nll_fwd(Tensor x, Tensor w, Tensor? b, Tensor target, Tensor(a!) logp, Tensor(b!) out, "
         "Tensor(c!) part, Tensor(d!) cnt, int reduction, int mfma_dtype) -> ()");
   m.def("linear_lsm_nll_ok(Tensor x, Tensor w) -> bool", &linear_lsm_nll_ok);
+  m.def("mlp_head_fwd(Tensor x, Tensor w1, Tensor? b1, int act, float drop_p, int seed, int offset, "
+        "Tensor? offset_dev, Tensor(a!) h, Tensor w2, Tensor? b2, Tensor target, Tensor(b!) logp, Tensor(c!) out, "
+        "Tensor(d!) part, Tensor(e!) cnt, int reduction, int mfma_dtype, Tensor(f!)? dbg=None) -> ()");
+  m.def("mlp_head_ok(Tensor x, Tensor w1, Tensor w2, int h_dtype_code, int mfma_dtype) -> bool", &mlp_head_ok);
   m.def("lsm_nll_bwd(Tensor gout, Tensor logp, Tensor target, Tensor(a!) dz, int reduction) -> ()");
   m.def("conv2d_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int pad, int mfma_dtype) -> ()");
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, int pad, int mfma_dtype, "
@@ -820,6 +865,7 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("linear_bwd", &linear_bwd);
   m.impl("lsm_nll_fwd", &lsm_nll_fwd);
   m.impl("linear_lsm_nll_fwd", &linear_lsm_nll_fwd);
+  m.impl("mlp_head_fwd", &mlp_head_fwd);
   m.impl("lsm_nll_bwd", &lsm_nll_bwd);
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);

@@ -171,6 +171,17 @@ __device__ __forceinline__ void store_tile(typename Stor<T>::S* lds, const Raw& 
 }
 
 // Epilogue of one output element (acc = sum over K); bias_v: the column's bias (0 without one).
+// the output value of element (m, n) before its store (C's address co)
+__device__ __forceinline__ float epilogue_val(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale,
+                                              float bias_v, int64_t co) {
+  float v = a.alpha * acc;
+  if (a.beta != 0.f) v += a.beta * ld_any(a.C, a.c_dtype, co);
+  v += bias_v;
+  if (a.act >= 1) v = fmaxf(v, 0.f);
+  if (a.act == 2) v = dropout_keep(a.seed, off, (uint64_t)m * a.N + n, a.drop_p) ? v * dscale : 0.f;
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ void epilogue_b(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale,
                                            float bias_v) {
@@ -179,11 +190,7 @@ __device__ __forceinline__ void epilogue_b(const GemmArgs& a, int m, int n, floa
     return;
   }
   const int64_t co = (int64_t)m * a.scm + (int64_t)n * a.scn;
-  float v = a.alpha * acc;
-  if (a.beta != 0.f) v += a.beta * ld_any(a.C, a.c_dtype, co);
-  v += bias_v;
-  if (a.act >= 1) v = fmaxf(v, 0.f);
-  if (a.act == 2) v = dropout_keep(a.seed, off, (uint64_t)m * a.N + n, a.drop_p) ? v * dscale : 0.f;
+  const float v = epilogue_val(a, m, n, acc, off, dscale, bias_v, co);
   switch (a.c_dtype) {
     case kF32: ((float*)a.C)[co] = v; break;
     case kBF16: ((__bf16*)a.C)[co] = (__bf16)v; break;
@@ -316,9 +323,13 @@ __device__ __forceinline__ typename Mfma<T>::frag to_frag(const float (&f)[8]) {
 
 // Classifier-head epilogue (a.head_part): row-wise log_softmax over the tile's 16 columns (the
 // lanes of one kq group hold one row's columns: xor-shuffles within 16 lanes), the NLL of each row's
-// target, the tile's sum (fixed xor tree), then the write-through hand-off of the per-tile sums:
-// sc1 store + vmcnt(0) + one relaxed counter add, the last tile reads every partial with sc1 loads
-// and sums them in tile order (reproducible), as lenet_update's split-K hand-off.
+// target, the tile's sum (fixed xor tree), then ONE returning 64-bit atomic per tile into a.head_cnt:
+// bits 48-63 count the arrived tiles, bits 0-47 accumulate the tile sums in fixed point (2^-20; bit
+// 47 flags a non-finite or out-of-range sum).  Integer addition is associative, so the total does not
+// depend on the arrival order (reproducible), and the tile whose add completes the count writes the
+// loss and re-arms the word.  (A float hand-off -- write-through partial, vmcnt(0), counter add, the
+// last tile re-reading every partial -- was three dependent round trips, ~5k cycles.)
+constexpr int kHeadFrac = 20;
 __device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, int kq, const float (&v)[4], int lane,
                                               const int64_t (&tgt)[4], float b) {
   float nll = 0.f;
@@ -341,13 +352,16 @@ __device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, 
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) nll += __shfl_xor(nll, o);
   if (lane == 0) {
-    const int ntiles = (a.M + 15) >> 4;
-    __hip_atomic_store(a.head_part + mt, nll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(a.head_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == ntiles - 1) {
-      float t = 0.f;
-      for (int i = 0; i < ntiles; ++i) t += __hip_atomic_load(a.head_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long ntiles = (unsigned long long)((a.M + 15) >> 4);
+    constexpr unsigned long long kFlag = 1ull << 47, kOne = 1ull << 48;
+    const float sc = nll * (float)(1 << kHeadFrac);  // (nll >= 0: a sum of -log-probs)
+    const unsigned long long q =
+        (sc >= 0.f && sc < 1.0e14f) ? (unsigned long long)__builtin_rintf(sc) : kFlag;  // (NaN fails both)
+    const unsigned long long old = __hip_atomic_fetch_add(a.head_cnt, kOne + q, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+    if ((old >> 48) == ntiles - 1) {
+      const unsigned long long tot = (old + q) & (kOne - 1);
+      const float t = (tot & kFlag) ? __builtin_nanf("") : (float)((double)tot / (double)(1ull << kHeadFrac));
       *a.head_out = a.head_mean ? t / (float)a.M : t;
       *a.head_cnt = 0;  // (the next launch reads it after the kernel boundary)
     }
@@ -419,20 +433,102 @@ __device__ int64_t kSmallZero[16];  // a valid address for absent optional opera
 // (A, gate, B) fragments, the log-softmax targets) are issued before any is converted, and the
 // epilogue operands are unconditional loads from valid addresses -- one memory round trip per 4
 // K-steps instead of one per fragment.  Same arithmetic as gemm_small_body (bitwise equal).
-template <typename T, bool HEAD, typename XA, typename XB>
-__device__ __forceinline__ void gemm_small_typed(const GemmArgs& a, const int blk, float (*part)[256]) {
+// The typed K loop of one 16 x 16 tile (row m / column n of this lane, K-steps [ks0, ks1) of 32):
+// all of the range's operand loads (up to 4 x (A, gate, B) fragments, the log-softmax targets) are
+// issued before any is converted.  tgt_m / gout: the loss head's row target and upstream gradient.
+// PLAIN: no gate and no log-softmax transform (compile-time: their registers are not allocated)
+template <typename T, typename XA, typename XB, bool PLAIN = false>
+__device__ __forceinline__ f32x4 small_kloop(const GemmArgs& a, int m, int n, int ks0, int ks1, int64_t tgt_m,
+                                             float gout) {
+  const bool has_g = !PLAIN && a.G, has_lsm = !PLAIN && a.lsm_target;
   typedef typename RawV<XA>::t VA;
   typedef typename RawV<XB>::t VB;
+  const int kq = (threadIdx.x & 63) >> 4;
+  const bool mv = m < a.M, nv = n < a.N;
+  const bool avec = a.a_mode == kKContig, bvec = a.b_mode == kKContig;
+  const int64_t* lt = has_lsm ? a.lsm_target : kSmallZero;
+  const XA* Ap = static_cast<const XA*>(a.A);
+  const XA* Gp = has_g ? static_cast<const XA*>(a.G) : Ap;
+  const XB* Bp = static_cast<const XB*>(a.B);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
+    VA ra[4], rg[4];
+    VB rb[4];
+    int64_t tk[PLAIN ? 1 : 4][8];  // (dW of the head: the targets of the 8 k rows)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ks = kb0 + u;
+      if (ks >= ks1) break;  // (uniform)
+      const int kb = ks * 32 + 8 * kq;
+      const int nk = min(8, max(0, a.K - kb));
+      const bool full = ks * 32 + 32 <= a.K;  // (uniform: every lane's 8 elements inside K)
+      const int kc = min(kb, a.K - 1);
+      const int64_t ao = (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak;
+      ra[u] = load8_raw<XA>(Ap + ao, a.sak, mv ? nk : 0, avec && full);
+      if (has_g) rg[u] = load8_raw<XA>(Gp + ao, a.sak, mv ? nk : 0, avec && full);
+      rb[u] = load8_raw<XB>(Bp + (int64_t)kc * a.sbk + (int64_t)(nv ? n : 0) * a.sbn, a.sbk, nv ? nk : 0,
+                            bvec && full);  // (uniform: rows past M / N read row 0, masked later)
+      if (has_lsm && !a.lsm_rows_are_m) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tk[PLAIN ? 0 : u][j] = lt[min(kc + j, a.K - 1)];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const float lsm_g = gout / a.lsm_div;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kb0 + u >= ks1) break;
+      const int kb = (kb0 + u) * 32 + 8 * kq;
+      const int nk = min(8, max(0, a.K - kb));
+      float fa[8], fb[8];
+      // A already in the compute type with no transform: its bits are the fragment (zeroed past K on
+      // a ragged last K-step only; rows past M are not masked -- their outputs are discarded)
+      constexpr bool kA16 = !__is_same(T, float) && __is_same(XA, T);
+      const bool a_bits = kA16 && !has_g && !has_lsm;
+      typename Mfma<T>::frag fra;
+      if constexpr (kA16) {
+        if (a_bits) {
+          u16x8 r = ra[u];
+          if ((kb0 + u) * 32 + 32 > a.K) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] = j < nk ? r[j] : (unsigned short)0;
+          }
+          fra = __builtin_bit_cast(typename Mfma<T>::frag, r);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ia = mv && j < nk;
+        float v = ia && !a_bits ? raw_f<XA>(ra[u], j) : 0.f;
+        if (has_lsm) {  // log-probs -> dz = g * (exp(logp) - onehot(target)) (lsm_nll_bwd_kernel's rule)
+          const int c = a.lsm_rows_are_m ? kb + j : m;
+          const int64_t t = a.lsm_rows_are_m ? tgt_m : tk[PLAIN ? 0 : u][j];
+          v = ia ? lsm_g * (__expf(v) - (c == t ? 1.f : 0.f)) : 0.f;
+        }
+        if (has_g) v = (ia ? raw_f<XA>(rg[u], j) : 0.f) > 0.f ? v * a.gate_scale : 0.f;
+        fa[j] = v;
+        fb[j] = nv ? (j < nk ? raw_f<XB>(rb[u], j) : 0.f) : (n == a.N && j < nk) ? 1.f : 0.f;  // (ones column)
+      }
+      acc = Mfma<T>::mma(a_bits ? fra : to_frag<T>(fa), to_frag<T>(fb), acc);
+    }
+  }
+  return acc;
+}
+
+// The small GEMM for operand element types known at compile time (XA: A's and the gate's, XB: B's;
+// fp32 or the compute type's 16-bit type): small_kloop's single-batch loads, and the epilogue
+// operands as unconditional loads from valid addresses -- one memory round trip per 4 K-steps
+// instead of one per fragment.  Same arithmetic as gemm_small_body (bitwise equal).
+template <typename T, bool HEAD, typename XA, typename XB>
+__device__ __forceinline__ void gemm_small_typed(const GemmArgs& a, const int blk, float (*part)[256]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
   const int Np = a.N + (a.rowsum ? 1 : 0);
   const int tn = (Np + 15) >> 4;
   const int mt = blk / tn, nt = blk - mt * tn;
   const int m = mt * 16 + l16, n = nt * 16 + l16;
   const bool mv = m < a.M, nv = n < a.N;
-  const bool avec = a.a_mode == kKContig, bvec = a.b_mode == kKContig;
   const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
   const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
-  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   // epilogue operands: unconditional loads (absent ones read kSmallZero), issued with the first K-steps'
   const float* bp = a.bias ? a.bias : reinterpret_cast<const float*>(kSmallZero);
   const float bias_t = bp[a.bias && nv ? n : 0];
@@ -451,58 +547,113 @@ __device__ __forceinline__ void gemm_small_typed(const GemmArgs& a, const int bl
   const float gout = gp[0];
   const int64_t* lt = a.lsm_target ? a.lsm_target : kSmallZero;
   const int64_t tgt_m = lt[a.lsm_target && a.lsm_rows_are_m && mv ? m : 0];  // (dX of the head: row m's target)
-  const XA* Ap = static_cast<const XA*>(a.A);
-  const XA* Gp = a.G ? static_cast<const XA*>(a.G) : Ap;
-  const XB* Bp = static_cast<const XB*>(a.B);
-  for (int kb0 = ks0; kb0 < ks1; kb0 += 4) {
-    VA ra[4], rg[4];
-    VB rb[4];
-    int64_t tk[4][8];  // (dW of the head: the targets of the 8 k rows)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ks = kb0 + u;
-      if (ks >= ks1) break;  // (uniform)
-      const int kb = ks * 32 + 8 * kq;
-      const int nk = min(8, max(0, a.K - kb));
-      const bool full = ks * 32 + 32 <= a.K;  // (uniform: every lane's 8 elements inside K)
-      const int kc = min(kb, a.K - 1);
-      const int64_t ao = (int64_t)(mv ? m : 0) * a.sam + (int64_t)kc * a.sak;
-      ra[u] = load8_raw<XA>(Ap + ao, a.sak, mv ? nk : 0, avec && full);
-      if (a.G) rg[u] = load8_raw<XA>(Gp + ao, a.sak, mv ? nk : 0, avec && full);
-      rb[u] = load8_raw<XB>(Bp + (int64_t)kc * a.sbk + (int64_t)(nv ? n : 0) * a.sbn, a.sbk, nv ? nk : 0,
-                            bvec && full);  // (uniform: rows past M / N read row 0, masked later)
-      if (a.lsm_target && !a.lsm_rows_are_m) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) tk[u][j] = lt[min(kc + j, a.K - 1)];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const float lsm_g = gout / a.lsm_div;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (kb0 + u >= ks1) break;
-      const int kb = (kb0 + u) * 32 + 8 * kq;
-      const int nk = min(8, max(0, a.K - kb));
-      float fa[8], fb[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bool ia = mv && j < nk;
-        float v = ia ? raw_f<XA>(ra[u], j) : 0.f;
-        if (a.lsm_target) {  // log-probs -> dz = g * (exp(logp) - onehot(target)) (lsm_nll_bwd_kernel's rule)
-          const int c = a.lsm_rows_are_m ? kb + j : m;
-          const int64_t t = a.lsm_rows_are_m ? tgt_m : tk[u][j];
-          v = ia ? lsm_g * (__expf(v) - (c == t ? 1.f : 0.f)) : 0.f;
-        }
-        if (a.G) v = (ia ? raw_f<XA>(rg[u], j) : 0.f) > 0.f ? v * a.gate_scale : 0.f;
-        fa[j] = v;
-        fb[j] = nv ? (j < nk ? raw_f<XB>(rb[u], j) : 0.f) : (n == a.N && j < nk) ? 1.f : 0.f;  // (ones column)
-      }
-      acc = Mfma<T>::mma(to_frag<T>(fa), to_frag<T>(fb), acc);
-    }
-  }
+  const f32x4 acc = small_kloop<T, XA, XB>(a, m, n, ks0, ks1, tgt_m, gout);
   const float bias_v = a.bias && nv ? bias_t : 0.f;
   const uint64_t off = a.offset + (a.offset_dev ? ((uint64_t)od << 20) : 0ull);  // (rng_offset)
   small_finish<T, HEAD>(a, acc, part, mt, n, Np, tgt, bias_v, off);
+}
+
+// fc1 (+ bias, ReLU, dropout) and the classifier head (fc2 + log_softmax + NLL) of a small batch in
+// ONE launch (a: fc1, h: the head, its A being a's output).  A block per 16 rows, 16 waves = fc1's 4
+// N-tiles x the small GEMM's 4-way K split (the same K ranges, chains and combine order as
+// gemm_small: h is bitwise the two-launch h); h goes to memory (the backward's gate / operand) and
+// to LDS, where the head's two K-steps read it (waves 0, 1: the small GEMM's split of K <= 64), and
+// the head's epilogue runs on wave 0.  Saves a launch and h's round trip through memory.
+template <typename T, typename XA>
+__global__ void __launch_bounds__(1024) mlp_head_kernel(GemmArgs a, GemmArgs h) {
+  typedef typename Stor<T>::S S;
+  typedef typename Mfma<T>::frag frag;
+  constexpr int HP = 72;  // h tile row pitch (64 columns + 8: 16-byte aligned rows)
+  __shared__ float part[16][256];
+  __shared__ __attribute__((aligned(16))) S hs[16 * HP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+  const int nt = wave & 3, sk = wave >> 2;  // fc1 N-tile, K-split slot
+  const int mt = blockIdx.x;
+  const int m = mt * 16 + l16, n = nt * 16 + l16;
+  const bool nv = n < a.N;
+  // optional phase stamps (diagnostics: h.ws, unused by the head, as [blocks][8] u64)
+  uint64_t* dbg = reinterpret_cast<uint64_t*>(h.ws);
+#define MH_STAMP(i) \
+  if (dbg && threadIdx.x == 0) dbg[(int64_t)mt * 8 + (i)] = __builtin_amdgcn_s_memtime();
+  MH_STAMP(0);
+  // the head's operands first (all unconditional): W2 fragments of K-step `wave` (waves 0, 1), bias,
+  // targets; then fc1's epilogue operands
+  const int hn = l16;
+  const bool hnv = hn < h.N;
+  const int hks = wave & 1;
+  const int hkb = hks * 32 + 8 * kq, hnk = min(8, max(0, h.K - hkb)), hkc = min(hkb, h.K - 1);
+  const typename RawV<float>::t rw2 =
+      load8_raw<float>(static_cast<const float*>(h.B) + (int64_t)hkc * h.sbk + (int64_t)(hnv ? hn : 0) * h.sbn, h.sbk,
+                       hnv ? hnk : 0, false);
+  const float* hbp = h.bias ? h.bias : reinterpret_cast<const float*>(kSmallZero);
+  const float hbias_t = hbp[h.bias && hnv ? hn : 0];
+  int64_t tgt[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int mm = mt * 16 + 4 * kq + r;
+    tgt[r] = h.head_target[mm < h.M ? mm : 0];
+  }
+  const float* bp = a.bias ? a.bias : reinterpret_cast<const float*>(kSmallZero);
+  const float bias_t = bp[a.bias && nv ? n : 0];
+  const int64_t* odp = a.offset_dev ? a.offset_dev : kSmallZero;
+  const int64_t od = odp[0];
+  // fc1: this wave's (N-tile, K range)
+  const int nks = (a.K + 31) >> 5, per = (nks + 3) >> 2;
+  const int ks0 = sk * per, ks1 = min(nks, ks0 + per);
+  const f32x4 acc = small_kloop<T, XA, float, true>(a, m, n, ks0, ks1, -1, 0.f);
+  MH_STAMP(1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = acc[r];
+  __syncthreads();
+  MH_STAMP(2);
+  if (sk == 0) {  // waves 0-3: fc1's epilogue of N-tile nt (epilogue_b's arithmetic), h to memory and LDS
+    const float bias_v = a.bias && nv ? bias_t : 0.f;
+    const uint64_t off = a.offset + (a.offset_dev ? ((uint64_t)od << 20) : 0ull);
+    const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = ((part[nt][r * 64 + lane] + part[nt + 4][r * 64 + lane]) + part[nt + 8][r * 64 + lane]) +
+                      part[nt + 12][r * 64 + lane];
+      const int rr = 4 * kq + r, mm = mt * 16 + rr;
+      const bool in = mm < a.M && nv;
+      const int64_t co = (int64_t)(in ? mm : 0) * a.scm + (int64_t)(in ? n : 0) * a.scn;
+      const float v = epilogue_val(a, mm, n, s, off, dscale, bias_v, co);
+      float vc = v;  // (the value as stored: the head reads h in its stored precision)
+      if (a.c_dtype == kBF16) vc = (float)(__bf16)v;
+      else if (a.c_dtype == kF16) vc = (float)(_Float16)v;
+      if (in) {
+        switch (a.c_dtype) {
+          case kF32: ((float*)a.C)[co] = v; break;
+          case kBF16: ((__bf16*)a.C)[co] = (__bf16)v; break;
+          default: ((_Float16*)a.C)[co] = (_Float16)v; break;
+        }
+      }
+      hs[rr * HP + n] = Stor<T>::of(in ? vc : 0.f);  // (columns past N, rows past M: 0, as the head's masks)
+    }
+  }
+  MH_STAMP(3);
+  __syncthreads();
+  MH_STAMP(4);
+  if (wave < 2) {  // the head's K-steps 0 / 1 (gemm_small's split of K <= 64 over waves 0, 1)
+    const frag fa = *reinterpret_cast<const frag*>(hs + l16 * HP + hks * 32 + 8 * kq);
+    float fb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[j] = hnv && j < hnk ? rw2[j] : 0.f;
+    const bool live = hks * 32 < h.K;
+    const f32x4 hacc = live ? Mfma<T>::mma(fa, to_frag<T>(fb), f32x4{0.f, 0.f, 0.f, 0.f}) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[wave][r * 64 + lane] = hacc[r];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = ((part[0][r * 64 + lane] + part[1][r * 64 + lane]) + 0.f) + 0.f;
+    MH_STAMP(5);
+    head_epilogue(h, mt, hn, kq, v, lane, tgt, h.bias && hnv ? hbias_t : 0.f);
+    MH_STAMP(6);
+  }
+#undef MH_STAMP
 }
 
 template <typename T, bool HEAD>  // HEAD: the classifier-head epilogue may be asked for (a.head_part)
@@ -710,6 +861,29 @@ hipError_t launch_gemm_pair(const GemmArgs& in_a, const GemmArgs& in_b, hipStrea
   const int ta = small_tiles(a);
   CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
     hipLaunchKernelGGL(gemm_small_pair_kernel<scalar_t>, dim3(ta + small_tiles(b)), dim3(256), 0, s, a, b, ta);
+  });
+  return hipGetLastError();
+}
+
+bool mlp_head_ok(const GemmArgs& a, const GemmArgs& h) {
+  const int c16 = a.mfma_dtype;
+  auto typed = [&](int dt) { return dt == kF32 || (c16 != kF32 && dt == c16); };
+  return a.M > 0 && a.N > 0 && a.N <= 64 && a.M == h.M && h.K == a.N && gemm_small(a) && gemm_head_ok(h) &&
+         a.beta == 0.f && !a.rowsum && !a.G && !a.lsm_target && !a.head_part && a.act >= 0 && a.act <= 2 &&
+         typed(a.a_dtype) && a.b_dtype == kF32 && h.b_dtype == kF32 && typed(a.c_dtype) && a.mfma_dtype == h.mfma_dtype &&
+         h.head_part && h.head_target;
+}
+
+hipError_t launch_mlp_head(const GemmArgs& in_a, const GemmArgs& in_h, hipStream_t s) {
+  if (!mlp_head_ok(in_a, in_h)) return hipErrorInvalidValue;
+  const GemmArgs a = with_modes(in_a), h = with_modes(in_h);
+  CSED_DISPATCH_COMPUTE(a.mfma_dtype, {
+    if (a.a_dtype == kF32) {
+      hipLaunchKernelGGL((mlp_head_kernel<scalar_t, float>), dim3(cdiv(a.M, 16)), dim3(1024), 0, s, a, h);
+    } else {
+      if constexpr (!__is_same(scalar_t, float))
+        hipLaunchKernelGGL((mlp_head_kernel<scalar_t, scalar_t>), dim3(cdiv(a.M, 16)), dim3(1024), 0, s, a, h);
+    }
   });
   return hipGetLastError();
 }

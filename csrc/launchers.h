@@ -104,8 +104,8 @@ struct GemmArgs {
   // the epilogue turns each row of z = A B + bias into fp32 log-probs (written to C) and the NLL of
   // head_target; each 16-row tile's NLL sum goes to head_part[tile] (write-through) and the tile
   // whose arrival (head_cnt, re-armed to 0) comes last sums them in tile order into head_out
-  // (/ M for the mean)
-  const int64_t* head_target; float* head_part; int* head_cnt; float* head_out; int head_mean;
+  // (/ M for the mean).  head_cnt: a zero 64-bit word (the tiles' fixed-point sums and arrival count)
+  const int64_t* head_target; float* head_part; unsigned long long* head_cnt; float* head_out; int head_mean;
 };
 // The classifier head + NLL forward above; false if the shapes do not fit it.
 bool gemm_head_ok(const GemmArgs& a);
@@ -116,6 +116,10 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 // Two independent GEMMs of the small-GEMM path in one launch (nn.Linear's backward); pairable ==
 // both fit that path (few 16 x 16 tiles, K <= 1024) with the same compute dtype.
 bool gemm_pairable(const GemmArgs& a, const GemmArgs& b);
+// fc1 (a: bias / ReLU / dropout epilogue, N <= 64) and the classifier head (h: the fused head + NLL
+// forward above, A = a's output C) of a small batch in one launch; ok == the shapes / dtypes fit
+bool mlp_head_ok(const GemmArgs& a, const GemmArgs& h);
+hipError_t launch_mlp_head(const GemmArgs& a, const GemmArgs& h, hipStream_t s);
 hipError_t launch_gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s);
 
 // Column sums of a (gated) [rows, cols] matrix -> fp32 out[cols] (fixed order).

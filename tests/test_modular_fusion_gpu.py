@@ -208,7 +208,7 @@ def test_head_forward_matches_gemm_then_loss(dt, rows, red):
     o.gemm(x, w.t(), z, b, 1.0, 0.0, 0, 0.0, 0, 0, None, None, 1.0, MF[dt])
     lp_ref, out_ref = torch.empty_like(z), torch.empty((), device=DEV)
     o.lsm_nll_fwd(z, t, lp_ref, out_ref, red)
-    cnt = torch.zeros(1, device=DEV, dtype=torch.int32)
+    cnt = torch.zeros(1, device=DEV, dtype=torch.int64)
     part = torch.empty((rows + 15) // 16, device=DEV)
     for _ in range(3):
         lp, out = torch.full_like(z, 7.0), torch.full((), 7.0, device=DEV)
@@ -237,3 +237,61 @@ def test_head_large_batch_fallback(rows):
     assert abs(loss.item() - lr.item()) <= 1e-3 * abs(lr.item())
     for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
         assert (got.float().cpu() - ref).abs().max().item() <= 3e-2 * max(ref.abs().max().item(), 1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,act,red", [(64, "relu_dropout", "mean"), (37, "relu", "sum"),
+                                          (200, "relu_dropout", "mean"), (8, "relu_dropout", "sum")])
+def test_mlp_head_matches_two_launch_path_bitwise(dt, rows, act, red):
+    """mlp_head_nll (fc1 + relu / dropout + fc2 + log_softmax + NLL in ONE launch, h kept in LDS) ==
+    linear() + linear_log_softmax_nll() bitwise: the same K split and combine order for fc1, the same
+    dropout draw, the head's K-steps and epilogue as the small GEMM's; the backward is theirs."""
+    from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
+
+    prev = fn.compute_dtype()
+    fn.set_compute_dtype(dt)
+    try:
+        g = torch.Generator(device=DEV).manual_seed(11)
+        x0 = torch.randn(rows, 320, device=DEV, generator=g).relu().to(dt if dt != torch.float32 else torch.float32)
+        w1 = torch.randn(50, 320, device=DEV, generator=g) * 0.05
+        b1 = torch.randn(50, device=DEV, generator=g) * 0.1
+        w2 = torch.randn(10, 50, device=DEV, generator=g) * 0.2
+        b2 = torch.randn(10, device=DEV, generator=g) * 0.1
+        t = torch.randint(0, 10, (rows,), device=DEV, generator=g)
+        assert _native.ops().mlp_head_ok(x0, w1, w2, fn._DT_CODE[fn._act_dtype(x0)], MF[dt])
+        res = []
+        for fused in (True, False):
+            ops.rng.default_state.reset_offset()  # (the same dropout masks in both passes)
+            leaves = [v.detach().clone().requires_grad_(True) for v in (x0, w1, b1, w2, b2)]
+            x, a1, c1, a2, c2 = leaves
+            if fused:
+                loss = ops.mlp_head_nll(x, a1, c1, a2, c2, t, act=act, p=0.5, reduction=red)
+            else:
+                loss = ops.linear_log_softmax_nll(ops.linear(x, a1, c1, act=act, p=0.5), a2, c2, t, reduction=red)
+            loss.backward()
+            res.append((loss.detach(), [v.grad for v in leaves]))
+        (l1, g1), (l2, g2) = res
+        assert torch.equal(l1, l2), (l1.item(), l2.item())
+        for a, b in zip(g1, g2):
+            assert torch.equal(a, b)
+        # and against an fp32 reference of the same masks (loose: 16-bit operands)
+        if act == "relu":
+            lr = F.nll_loss(F.log_softmax(F.linear(F.relu(F.linear(x0.float(), w1, b1)), w2, b2), 1), t, reduction=red)
+            assert abs(l1.item() - lr.item()) <= 2e-2 * max(abs(lr.item()), 1.0)
+    finally:
+        fn.set_compute_dtype(prev)
+
+
+def test_mlp_head_repeated_launches_rearm_counter():
+    """The fused MLP head's loss hand-off counter is zero again after every launch."""
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = torch.randn(64, 320, device=DEV, generator=g).to(torch.bfloat16)
+    w1, w2 = torch.randn(50, 320, device=DEV, generator=g) * 0.05, torch.randn(10, 50, device=DEV, generator=g) * 0.2
+    t = torch.randint(0, 10, (64,), device=DEV, generator=g)
+    first = None
+    for _ in range(4):
+        loss = ops.mlp_head_nll(x, w1, None, w2, None, t, act="relu")
+        first = loss if first is None else first
+        assert torch.equal(loss, first)
+    from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
+    assert int(fn._head_counter(w2).item()) == 0

@@ -48,7 +48,7 @@ def main() -> int:
     wf2, bf2 = r(10, 50) * 0.1, r(10)
     t = torch.randint(0, 10, (B,), device=dev, generator=g)
     logp, loss = torch.empty(B, 10, device=dev), torch.empty((), device=dev)
-    part, cnt = torch.empty((B + 15) // 16, device=dev), torch.zeros(1, device=dev, dtype=torch.int32)
+    part, cnt = torch.empty((B + 15) // 16, device=dev), torch.zeros(1, device=dev, dtype=torch.int64)
     gout = torch.ones((), device=dev)
     dh, dwf2, dbf2 = torch.empty_like(h), torch.empty_like(wf2), torch.empty(10, device=dev)
     dp2, dwf1, dbf1 = torch.empty(B, 320, device=dev, dtype=bf), torch.empty_like(wf1), torch.empty(50, device=dev)
@@ -68,6 +68,8 @@ def main() -> int:
         "fc1 fwd (relu+dropout)": lambda: o.gemm(y2.view(B, 320), wf1.t(), h, bf1, 1.0, 0.0, 2, 0.5, 7, 1, off,
                                                  None, 1.0, 1),
         "head fwd (fc2+lsm+nll)": lambda: o.linear_lsm_nll_fwd(h, wf2, bf2, t, logp, loss, part, cnt, 1, 1),
+        "fc1 + head fwd (one launch)": lambda: o.mlp_head_fwd(y2.view(B, 320), wf1, bf1, 2, 0.5, 7, 1, off, h, wf2,
+                                                              bf2, t, logp, loss, part, cnt, 1, 1),
         "head bwd (pair)": lambda: o.linear_bwd(logp, h, wf2, None, 1.0, dh, dwf2, dbf2, 1, t, gout, float(B)),
         "fc1 bwd (pair)": lambda: o.linear_bwd(dh, y2.view(B, 320), wf1, h, 2.0, dp2, dwf1, dbf1, 1),
         "conv2 bwd (wgrad+dgrad+reduce)": lambda: o.conv2d_bwd(y1, dp2.view(B, 20, 4, 4), w2, dw2, db2, ws2, dx2, 0,
