@@ -44,6 +44,7 @@ import torch.distributed as dist
 from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
+from ..parallel import comm
 from ..parallel.comm import DistContext
 from ..parallel.ipc import allreduce_mode, open_exchange, open_loopback_exchange, wait_timeout_s
 from ..utils.flat import FlatParams
@@ -650,6 +651,7 @@ class FusedLeNetTrainer:
         for t, v in zip(state, saved):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
+        comm.quiesce()  # (no pending collective for the watchdog to query during the capture)
         # thread_local: only this thread's unsafe calls invalidate the capture.  The process
         # group's watchdog thread keeps querying the events of earlier collectives while a step
         # that contains an RCCL all-reduce is captured; in the default (global) mode that query

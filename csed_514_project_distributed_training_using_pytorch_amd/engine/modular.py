@@ -33,6 +33,7 @@ import torch
 
 from .. import ops
 from ..optim.sgd import FusedSGD
+from ..parallel import comm
 from ..parallel.ddp import DistributedDataParallel
 
 
@@ -148,6 +149,7 @@ class ModularTrainer:
             for t, v in zip(state, saved):
                 t.copy_(v)
             torch.cuda.synchronize(dev)
+            comm.quiesce()  # (no pending collective for the watchdog to query during the capture)
             graph = torch.cuda.CUDAGraph()
             # thread_local: the process group's watchdog thread may query earlier collectives'
             # events during the capture (see engine/fused.py _capture)

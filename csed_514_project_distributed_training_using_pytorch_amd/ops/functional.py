@@ -522,6 +522,16 @@ class _MlpHeadNLL(torch.autograd.Function):
         x2, w1, h, w2, logp, target = ctx.saved_tensors
         need = ctx.needs_input_grad
         mf = _mfma()
+        div = float(logp.shape[0]) if ctx.reduction == 1 else 1.0
+        gs = 1.0 / (1.0 - ctx.p) if ctx.act == 2 else 1.0
+        if ctx.act and all(need[:5]) and ctx.b1 is not None and ctx.b2 is not None:
+            # the whole head's backward in one launch when it fits (dh recomputed per block, never stored)
+            dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
+            dw1, db1 = _grad_buffer(w1, w1.shape, w1.device), _grad_buffer(ctx.b1, (w1.shape[0],), w1.device)
+            dw2, db2 = _grad_buffer(w2, w2.shape, w2.device), _grad_buffer(ctx.b2, (w2.shape[0],), w2.device)
+            if _ops().mlp_head_bwd(logp, target, gout.contiguous().float(), div, h, x2, w1, w2, gs, dx, dw1, db1,
+                                   dw2, db2, mf):
+                return dx, dw1, db1, dw2, db2, None, None, None, None, None, None, None
         # the head (linear_log_softmax_nll's backward): dh, dW2, db2 from the kept log-probs
         dh = torch.empty(h.shape, device=h.device, dtype=h.dtype) if (need[0] or need[1] or need[2]) else None
         dw2 = db2 = None
@@ -529,12 +539,10 @@ class _MlpHeadNLL(torch.autograd.Function):
             dw2 = _grad_buffer(w2, w2.shape, w2.device)
             if ctx.b2 is not None:
                 db2 = _grad_buffer(ctx.b2, (w2.shape[0],), w2.device)
-        div = float(logp.shape[0]) if ctx.reduction == 1 else 1.0
         _ops().linear_bwd(logp, h, w2, None, 1.0, dh, dw2, db2, mf, target, gout.contiguous().float(), div)
         # fc1 (linear()'s backward, gate = h)
         dx = dw1 = db1 = None
         if dh is not None:
-            gs = 1.0 / (1.0 - ctx.p) if ctx.act == 2 else 1.0
             if need[0]:
                 dx = torch.empty(x2.shape, device=x2.device, dtype=x2.dtype)
             if need[1] or (ctx.b1 is not None and need[2]):

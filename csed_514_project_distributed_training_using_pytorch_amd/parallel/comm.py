@@ -95,6 +95,29 @@ def destroy() -> None:
         dist.destroy_process_group()
 
 
+def quiesce() -> None:
+    """Block until every process group's watchdog has retired its outstanding collectives.
+
+    Call right before a HIP graph capture.  The watchdog thread polls each pending collective's
+    completion event; HIP refuses an event query while the event's stream is capturing
+    (``hipErrorCapturedEvent``), and the watchdog then aborts the process -- a race with the
+    watchdog's ~100 ms poll that a capture shortly after a collective (the warm-up step's
+    all-reduces, the initial parameter broadcast) could lose.  Collectives issued inside a capture
+    are not handed to the watchdog, so an empty list stays empty for the capture.
+    """
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    try:
+        groups = list(dist.distributed_c10d._world.pg_map.keys())
+    except AttributeError:  # (private registry moved: the default group at least)
+        groups = [dist.group.WORLD]
+    for pg in groups:
+        try:
+            pg._wait_for_pending_works()
+        except (AttributeError, RuntimeError, NotImplementedError):  # (gloo / older builds: nothing to wait for)
+            pass
+
+
 def barrier(ctx: DistContext) -> None:
     if ctx.is_distributed:
         if ctx.backend == "nccl":

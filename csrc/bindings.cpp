@@ -385,6 +385,42 @@ void linear_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const option
   for (const auto& a : todo) run_gemm(a, dy);
 }
 
+// The MLP head's backward (mlp_head_fwd's forward, the loss-head form) in one launch when it fits:
+// dW2 / db2 from the log-probs, dh = dz W2 recomputed per block (never written), dx = gate(dh) W1,
+// dW1 / db1 = gate(dh)^T x (gate: h > 0, scaled by gate_scale).  Returns false (nothing launched) when
+// the shapes do not fit, for the caller's two linear_bwd launches.
+bool mlp_head_bwd(const Tensor& logp, const Tensor& target, const Tensor& gout, double lsm_div, const Tensor& h,
+                  const Tensor& x, const Tensor& w1, const Tensor& w2, double gate_scale, Tensor& dx, Tensor& dw1,
+                  Tensor& db1, Tensor& dw2, Tensor& db2, int64_t mfma_dtype) {
+  dev(logp, "logp"); dev(target, "target"); dev(gout, "gout"); dev(h, "h"); dev(x, "x"); dev(w1, "w1");
+  dev(w2, "w2"); dev(dx, "dx"); dev(dw1, "dw1"); dev(db1, "db1"); dev(dw2, "dw2"); dev(db2, "db2");
+  TORCH_CHECK(logp.dim() == 2 && h.dim() == 2 && x.dim() == 2 && logp.scalar_type() == at::kFloat &&
+                  target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == logp.size(0) &&
+                  gout.numel() == 1 && gout.scalar_type() == at::kFloat && h.size(0) == logp.size(0) &&
+                  x.size(0) == h.size(0) && w2.size(0) == logp.size(1) && w2.size(1) == h.size(1) &&
+                  w1.size(0) == h.size(1) && w1.size(1) == x.size(1) && dx.sizes() == x.sizes() &&
+                  dw1.sizes() == w1.sizes() && dw2.sizes() == w2.sizes() && db1.numel() == w1.size(0) &&
+                  db2.numel() == w2.size(0),
+              "mlp_head_bwd: shape / dtype mismatch");
+  const c10::DeviceGuard gd(logp.device());
+  const optional<Tensor> none;
+  Tensor dh = at::empty(h.sizes(), h.options());  // (the layout the four GEMMs describe; never written)
+  csed::GemmArgs x2 = make_gemm(logp, w2, dh, none, 1.0, 0.0, 0, 0.0, 0, 0, none, none, 1.0, mfma_dtype, none);
+  csed::GemmArgs g2 = make_gemm(logp.t(), h, dw2, none, 1.0, 0.0, 0, 0.0, 0, 0, none, none, 1.0, mfma_dtype,
+                                optional<Tensor>(db2));
+  for (csed::GemmArgs* a : {&x2, &g2}) {
+    a->lsm_target = target.data_ptr<int64_t>(); a->lsm_gout = gout.data_ptr<float>(); a->lsm_div = (float)lsm_div;
+  }
+  x2.lsm_rows_are_m = 1; g2.lsm_rows_are_m = 0;
+  csed::GemmArgs x1 = make_gemm(dh, w1, dx, none, 1.0, 0.0, 0, 0.0, 0, 0, none, optional<Tensor>(h), gate_scale,
+                                mfma_dtype, none);
+  csed::GemmArgs g1 = make_gemm(dh.t(), x, dw1, none, 1.0, 0.0, 0, 0.0, 0, 0, none, optional<Tensor>(h.t()),
+                                gate_scale, mfma_dtype, optional<Tensor>(db1));
+  if (!csed::mlp_head_bwd_ok(x2, g2, x1, g1)) return false;
+  CHECK_HIP(csed::launch_mlp_head_bwd(x2, g2, x1, g1, cur_stream(logp)));
+  return true;
+}
+
 void colsum(const Tensor& x, const optional<Tensor>& gate, double gate_scale, Tensor& out, double beta) {
   dev(x, "x"); dev(out, "out");
   TORCH_CHECK(x.dim() == 2 && out.scalar_type() == at::kFloat && out.numel() == x.size(1));
@@ -838,6 +874,9 @@ TORCH_LIBRARY(csed, m) {
         "Tensor? offset_dev, Tensor(a!) h, Tensor w2, Tensor? b2, Tensor target, Tensor(b!) logp, Tensor(c!) out, "
         "Tensor(d!) part, Tensor(e!) cnt, int reduction, int mfma_dtype, Tensor(f!)? dbg=None) -> ()");
   m.def("mlp_head_ok(Tensor x, Tensor w1, Tensor w2, int h_dtype_code, int mfma_dtype) -> bool", &mlp_head_ok);
+  m.def("mlp_head_bwd(Tensor logp, Tensor target, Tensor gout, float lsm_div, Tensor h, Tensor x, Tensor w1, "
+        "Tensor w2, float gate_scale, Tensor(a!) dx, Tensor(b!) dw1, Tensor(c!) db1, Tensor(d!) dw2, Tensor(e!) db2, "
+        "int mfma_dtype) -> bool");
   m.def("lsm_nll_bwd(Tensor gout, Tensor logp, Tensor target, Tensor(a!) dz, int reduction) -> ()");
   m.def("conv2d_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int pad, int mfma_dtype) -> ()");
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, int pad, int mfma_dtype, "
@@ -866,6 +905,7 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("lsm_nll_fwd", &lsm_nll_fwd);
   m.impl("linear_lsm_nll_fwd", &linear_lsm_nll_fwd);
   m.impl("mlp_head_fwd", &mlp_head_fwd);
+  m.impl("mlp_head_bwd", &mlp_head_bwd);
   m.impl("lsm_nll_bwd", &lsm_nll_bwd);
   m.impl("lenet_pack", &lenet_pack);
   m.impl("lenet_train", &lenet_train);

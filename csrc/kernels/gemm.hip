@@ -656,6 +656,95 @@ __global__ void __launch_bounds__(1024) mlp_head_kernel(GemmArgs a, GemmArgs h) 
 #undef MH_STAMP
 }
 
+// The backward of the MLP head (mlp_head_kernel's forward) in ONE launch, batch M <= 64:
+//   blocks [0, t2)          dW2 (+ db2)            = gemm_small_typed on gW2 (A = dz^T from the log-probs)
+//   blocks [t2, t2 + tx)    dX1 = gate(dh) W1      (gX1's tiles)
+//   blocks [t2 + tx, ..)    dW1 = gate(dh)^T x (+ db1, the ones column)   (gW1's tiles)
+// dh = dz W2 (K = the classes: one MFMA) never goes to memory: each dX1 / dW1 block recomputes the
+// dh tiles it needs with small_kloop on gX2 -- the unfused dX2 GEMM's own call, so the same bits --
+// rounds them to h's dtype and gates them with h (gX1's gate rule), into LDS; its two K-steps then
+// run on waves 0, 1 and small_finish combines them as gemm_small would (bitwise the 2-launch result).
+template <typename T, typename XH>
+__global__ void __launch_bounds__(256) mlp_head_bwd_kernel(GemmArgs gX2, GemmArgs gW2, GemmArgs gX1, GemmArgs gW1,
+                                                           int t2, int tx) {
+  typedef typename Stor<T>::S S;
+  typedef typename Mfma<T>::frag frag;
+  constexpr int AP = 72;  // LDS A tile pitch (64 + 8)
+  __shared__ float part[4][256];
+  __shared__ __attribute__((aligned(16))) S As[16 * AP];
+  const int blk = blockIdx.x;
+  if (blk < t2) {
+    gemm_small_typed<T, false, float, XH>(gW2, blk, part);
+    return;
+  }
+  const bool dxr = blk < t2 + tx;
+  const GemmArgs& g = dxr ? gX1 : gW1;  // this block's output GEMM
+  const int b = dxr ? blk - t2 : blk - t2 - tx;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+  const int Np = g.N + (g.rowsum ? 1 : 0);
+  const int tn = (Np + 15) >> 4;
+  const int mt = b / tn, nt = b - mt * tn;
+  const int n = nt * 16 + l16;
+  const bool nv = n < g.N;
+  // the output GEMM's B fragment of K-step `wave` (waves 0, 1; W1 for dX1, x for dW1), loaded first
+  const int ks = wave & 1;
+  const int kb = ks * 32 + 8 * kq, nk = min(8, max(0, g.K - kb)), kc = min(kb, g.K - 1);
+  const typename RawV<float>::t rbf = load8_raw<float>(static_cast<const float*>(g.B) + (int64_t)kc * g.sbk +
+                                                           (int64_t)(nv ? n : 0) * g.sbn, g.sbk, nv ? nk : 0, false);
+  typename RawV<XH>::t rbh = {};
+  if constexpr (!__is_same(XH, float)) {  // (dW1's B is x: h's dtype; dX1's is W1: fp32)
+    if (!dxr)
+      rbh = load8_raw<XH>(static_cast<const XH*>(g.B) + (int64_t)kc * g.sbk + (int64_t)(nv ? n : 0) * g.sbn, g.sbk,
+                          nv ? nk : 0, false);
+  }
+  // the dh tile of this wave: dX1 -- rows of tile mt, features 16 * wave ..; dW1 -- batch rows 16 * wave ..,
+  // features of tile mt (the feature tile is dW1's row tile)
+  const int dm = dxr ? mt * 16 + l16 : wave * 16 + l16;  // dh row of this lane (the A row of gX2)
+  const int dn = dxr ? wave * 16 + l16 : mt * 16 + l16;  // dh column (feature) of this lane
+  const int64_t tgt_m = gX2.lsm_target[dm < gX2.M ? dm : 0];
+  const float gout = gX2.lsm_gout[0];
+  // the gate h[row][feature] of this lane's four C rows (h has gX1's gate layout: G(m, k) = h[m][k])
+  float hg[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = (dxr ? mt * 16 : wave * 16) + 4 * kq + r;
+    const bool ok = row < gX1.M && dn < gX2.N;
+    const XH hv = static_cast<const XH*>(gX1.G)[(int64_t)(ok ? row : 0) * gX1.sam + (int64_t)(ok ? dn : 0) * gX1.sak];
+    hg[r] = ok ? (float)hv : 0.f;
+  }
+  const f32x4 dacc = small_kloop<T, float, float>(gX2, dm, dn, 0, (gX2.K + 31) >> 5, tgt_m, gout);
+  // dh as the unfused dX2 GEMM stores it (epilogue_val, rounded to h's dtype), gated as gX1 reads it
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = (dxr ? mt * 16 : wave * 16) + 4 * kq + r;
+    const bool in = row < gX2.M && dn < gX2.N;
+    const float p = ((dacc[r] + 0.f) + 0.f) + 0.f;  // (gemm_small's combine of a one-K-step tile)
+    float v = epilogue_val(gX2, row, dn, p, 0, 1.f, 0.f, 0);
+    if (gX2.c_dtype == kBF16) v = (float)(__bf16)v;
+    else if (gX2.c_dtype == kF16) v = (float)(_Float16)v;
+    const float a = in ? (hg[r] > 0.f ? v * gX1.gate_scale : 0.f) : 0.f;
+    // dX1: A rows = batch rows of tile mt, K = features; dW1: A rows = features of tile mt, K = batch
+    if (dxr) As[(4 * kq + r) * AP + dn] = Stor<T>::of(a);
+    else As[l16 * AP + row] = Stor<T>::of(a);
+  }
+  __syncthreads();
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (wave < 2 && ks * 32 < g.K) {  // (gemm_small's split of K <= 64: K-steps 0 / 1 on waves 0 / 1)
+    const frag fa = *reinterpret_cast<const frag*>(As + l16 * AP + ks * 32 + 8 * kq);
+    float fb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float raw;
+      if constexpr (__is_same(XH, float)) raw = rbf[j];
+      else raw = dxr ? rbf[j] : raw_f<XH>(rbh, j);
+      fb[j] = nv ? (j < nk ? raw : 0.f) : (n == g.N && j < nk) ? 1.f : 0.f;  // (ones column: db1)
+    }
+    acc = Mfma<T>::mma(fa, to_frag<T>(fb), acc);
+  }
+  const int64_t tgt_none[4] = {-1, -1, -1, -1};
+  small_finish<T, false>(g, acc, part, mt, n, Np, tgt_none, 0.f, 0);
+}
+
 template <typename T, bool HEAD>  // HEAD: the classifier-head epilogue may be asked for (a.head_part)
 __device__ __forceinline__ void gemm_small_body(const GemmArgs& a, const int blk, float (*part)[256]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
@@ -883,6 +972,37 @@ hipError_t launch_mlp_head(const GemmArgs& in_a, const GemmArgs& in_h, hipStream
     } else {
       if constexpr (!__is_same(scalar_t, float))
         hipLaunchKernelGGL((mlp_head_kernel<scalar_t, scalar_t>), dim3(cdiv(a.M, 16)), dim3(1024), 0, s, a, h);
+    }
+  });
+  return hipGetLastError();
+}
+
+bool mlp_head_bwd_ok(const GemmArgs& x2, const GemmArgs& w2, const GemmArgs& x1, const GemmArgs& w1) {
+  const int c16 = x2.mfma_dtype;
+  const int hdt = x2.c_dtype;  // (dh is stored in h's dtype; h = x1's gate, w2's B, w1's gate)
+  const bool hok = hdt == kF32 || (c16 != kF32 && hdt == c16);
+  return hok && x2.M > 0 && x2.M <= 64 && x2.K <= 32 && x2.N <= 64 && gemm_small(x2) && gemm_small(w2) &&
+         gemm_small(x1) && gemm_small(w1) && x2.lsm_target && x2.lsm_rows_are_m && !x2.G && x2.a_dtype == kF32 &&
+         x2.b_dtype == kF32 && w2.lsm_target && !w2.lsm_rows_are_m && w2.a_dtype == kF32 && w2.b_dtype == hdt &&
+         x1.G && x1.g_dtype == hdt && x1.M == x2.M && x1.K == x2.N && x1.b_dtype == kF32 && !x1.rowsum &&
+         w1.G && w1.g_dtype == hdt && w1.M == x2.N && w1.K == x2.M && w1.b_dtype == hdt && w1.gate_scale == x1.gate_scale &&
+         x1.mfma_dtype == c16 && w1.mfma_dtype == c16 && w2.mfma_dtype == c16 && x1.beta == 0.f && w1.beta == 0.f &&
+         x2.beta == 0.f && x2.act == 0 && x1.act == 0 && w1.act == 0;
+}
+
+hipError_t launch_mlp_head_bwd(const GemmArgs& in_x2, const GemmArgs& in_w2, const GemmArgs& in_x1,
+                               const GemmArgs& in_w1, hipStream_t s) {
+  if (!mlp_head_bwd_ok(in_x2, in_w2, in_x1, in_w1)) return hipErrorInvalidValue;
+  const GemmArgs x2 = with_modes(in_x2), w2 = with_modes(in_w2), x1 = with_modes(in_x1), w1 = with_modes(in_w1);
+  const int t2 = small_tiles(w2), tx = small_tiles(x1), tw = small_tiles(w1);
+  CSED_DISPATCH_COMPUTE(x2.mfma_dtype, {
+    if (x2.c_dtype == kF32) {
+      hipLaunchKernelGGL((mlp_head_bwd_kernel<scalar_t, float>), dim3(t2 + tx + tw), dim3(256), 0, s, x2, w2, x1, w1,
+                         t2, tx);
+    } else {
+      if constexpr (!__is_same(scalar_t, float))
+        hipLaunchKernelGGL((mlp_head_bwd_kernel<scalar_t, scalar_t>), dim3(t2 + tx + tw), dim3(256), 0, s, x2, w2,
+                           x1, w1, t2, tx);
     }
   });
   return hipGetLastError();

@@ -120,6 +120,12 @@ bool gemm_pairable(const GemmArgs& a, const GemmArgs& b);
 // forward above, A = a's output C) of a small batch in one launch; ok == the shapes / dtypes fit
 bool mlp_head_ok(const GemmArgs& a, const GemmArgs& h);
 hipError_t launch_mlp_head(const GemmArgs& a, const GemmArgs& h, hipStream_t s);
+// Its backward in one launch (batch <= 64): x2 = the head's dX GEMM (dh = dz W2, the loss-head form
+// reading the log-probs; never written), w2 = the head's dW GEMM (+ db2), x1 / w1 = fc1's dX / dW GEMMs
+// (gate h; + db1) -- the four GEMMs linear_bwd would run, as make_gemm builds them
+bool mlp_head_bwd_ok(const GemmArgs& x2, const GemmArgs& w2, const GemmArgs& x1, const GemmArgs& w1);
+hipError_t launch_mlp_head_bwd(const GemmArgs& x2, const GemmArgs& w2, const GemmArgs& x1, const GemmArgs& w1,
+                               hipStream_t s);
 hipError_t launch_gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s);
 
 // Column sums of a (gated) [rows, cols] matrix -> fp32 out[cols] (fixed order).

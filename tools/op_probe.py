@@ -72,6 +72,8 @@ def main() -> int:
                                                               bf2, t, logp, loss, part, cnt, 1, 1),
         "head bwd (pair)": lambda: o.linear_bwd(logp, h, wf2, None, 1.0, dh, dwf2, dbf2, 1, t, gout, float(B)),
         "fc1 bwd (pair)": lambda: o.linear_bwd(dh, y2.view(B, 320), wf1, h, 2.0, dp2, dwf1, dbf1, 1),
+        "head + fc1 bwd (one launch)": lambda: o.mlp_head_bwd(logp, t, gout, float(B), h, y2.view(B, 320), wf1, wf2,
+                                                              2.0, dp2, dwf1, dbf1, dwf2, dbf2, 1),
         "conv2 bwd (wgrad+dgrad+reduce)": lambda: o.conv2d_bwd(y1, dp2.view(B, 20, 4, 4), w2, dw2, db2, ws2, dx2, 0,
                                                               i2, y2, sc2, 1),
         "conv1 bwd (wgrad+reduce)": lambda: o.conv2d_bwd(x0, dx2, w1, dw1, db1, ws1, None, 0, i1, y1, None, 1),
