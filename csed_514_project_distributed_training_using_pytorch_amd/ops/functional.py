@@ -22,6 +22,8 @@ Reference parity map (ref = /root/reference):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -91,6 +93,35 @@ def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
     return max(1, min(N, 256)) * OC * (IC * KH * KW + 1)
 
 
+# The deferred weight-gradient slab reduce.  A conv backward normally ends with its own reduce
+# launch (the partial slabs -> dW, db); when deferral is on and no hook watches the parameters
+# (a DDP reducer's post-accumulate-grad hooks would read dW before it is final), the reduce is left
+# pending: the NEXT conv backward of the same autograd pass runs it as extra blocks of its own launch
+# (it does not depend on it), and a callback queued on the autograd engine flushes whatever is still
+# pending when the pass ends -- before any optimizer or user code can read the gradients.  One launch
+# fewer per step in the modular engine (conv2's reduce rides on conv1's backward).
+_defer_reduce = os.environ.get("CSED_DEFER_WGRAD_REDUCE", "1") != "0"
+_pending_reduce = None  # (ws, dw, db, N, IC, KH, KW) of the conv whose reduce is pending
+
+
+def set_defer_wgrad_reduce(on: bool) -> None:
+    """Enable / disable carrying a conv's weight-gradient reduce into the next conv backward."""
+    global _defer_reduce
+    _defer_reduce = bool(on)
+
+
+def _flush_pending_reduce() -> None:
+    global _pending_reduce
+    p, _pending_reduce = _pending_reduce, None
+    if p is not None:
+        ws, dw, db, N, IC, KH, KW = p
+        _ops().wgrad_reduce(ws, dw, db, N, IC, KH, KW)
+
+
+def _watched(t) -> bool:
+    return t is not None and bool(getattr(t, "_post_accumulate_grad_hooks", None) or getattr(t, "_backward_hooks", None))
+
+
 # ----------------------------------------------------------------- conv ----
 class _Conv2d(torch.autograd.Function):
     @staticmethod
@@ -144,7 +175,17 @@ class _Conv2d(torch.autograd.Function):
             ws = torch.empty(wgrad_workspace_elems(N, IC, KH, KW, OC), device=w.device, dtype=torch.float32)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
-            _ops().conv2d_bwd(x, dy, w, dw, db, ws, dx, ctx.pad, *pooled, ctx.mf)
+            global _pending_reduce
+            carry, _pending_reduce = _pending_reduce, None  # (another conv's reduce rides on this launch)
+            defer = _defer_reduce and not _watched(w) and not _watched(ctx.bias_param)
+            ck = {} if carry is None else dict(carry_ws=carry[0], carry_dw=carry[1], carry_db=carry[2],
+                                               carry_n=carry[3], carry_ic=carry[4], carry_kh=carry[5],
+                                               carry_kw=carry[6])
+            _ops().conv2d_bwd(x, dy, w, dw, db, ws, dx, ctx.pad, *pooled, ctx.mf, defer_reduce=defer, **ck)
+            if defer:  # (detached aliases: a second reference to dw / db themselves would make autograd's
+                # AccumulateGrad clone them -- before the deferred reduce has written them -- not adopt them)
+                _pending_reduce = (ws, dw.detach(), db.detach() if db is not None else None, N, IC, KH, KW)
+                torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_reduce)
         elif ctx.needs_input_grad[0]:
             if ctx.pool:
                 dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)

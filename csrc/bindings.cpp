@@ -509,7 +509,9 @@ void conv2d_wgrad(const Tensor& x, const Tensor& dy, Tensor& dw, const optional<
 void conv2d_bwd(const Tensor& x, const Tensor& dy, const Tensor& w, Tensor& dw, const optional<Tensor>& db,
                 Tensor& ws, const optional<Tensor>& dx, int64_t pad, const optional<Tensor>& pool_idx,
                 const optional<Tensor>& pool_out, const optional<Tensor>& pool_scale, int64_t mfma_dtype,
-                const optional<Tensor>& dbg) {
+                const optional<Tensor>& dbg, const optional<Tensor>& carry_ws, const optional<Tensor>& carry_dw,
+                const optional<Tensor>& carry_db, int64_t carry_n, int64_t carry_ic, int64_t carry_kh,
+                int64_t carry_kw, bool defer_reduce) {
   dev(x, "x"); dev(dy, "dy"); dev(w, "w"); dev(dw, "dw"); dev(ws, "ws");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && dy.dim() == 4 && w.scalar_type() == at::kFloat);
   TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.sizes() == w.sizes() && ws.scalar_type() == at::kFloat);
@@ -555,7 +557,37 @@ void conv2d_bwd(const Tensor& x, const Tensor& dy, const Tensor& w, Tensor& dw, 
                 "conv2d_bwd: dbg must be int64 [>= weight-gradient blocks * 8]");
     b.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr<int64_t>());
   }
+  if (carry_ws.has_value()) {  // another conv's deferred slab reduce rides on this launch
+    TORCH_CHECK(carry_dw.has_value() && carry_n > 0, "conv2d_bwd: carry needs its dW and shape");
+    dev(*carry_ws, "carry_ws"); dev(*carry_dw, "carry_dw");
+    const int cOC = carry_dw->size(0);
+    TORCH_CHECK(carry_dw->scalar_type() == at::kFloat && carry_dw->numel() == (int64_t)cOC * carry_ic * carry_kh * carry_kw &&
+                    carry_ws->numel() >= csed::conv2d_wgrad_workspace(carry_n, carry_ic, carry_kh, carry_kw, cOC),
+                "conv2d_bwd: carried reduce shape mismatch");
+    if (carry_db.has_value()) {
+      dev(*carry_db, "carry_db");
+      TORCH_CHECK(carry_db->scalar_type() == at::kFloat && carry_db->numel() == cOC);
+    }
+    b.carry_ws = carry_ws->data_ptr<float>(); b.carry_dw = carry_dw->data_ptr<float>();
+    b.carry_db = optpt<float>(carry_db);
+    b.carry_N = (int)carry_n; b.carry_IC = (int)carry_ic; b.carry_KH = (int)carry_kh; b.carry_KW = (int)carry_kw;
+    b.carry_OC = cOC;
+  }
+  b.defer_reduce = defer_reduce ? 1 : 0;
   CHECK_HIP(csed::launch_conv2d_bwd(b, cur_stream(x)));
+}
+
+// A conv's deferred weight-gradient slab reduce on its own (conv2d_bwd(defer_reduce=True) left it).
+void wgrad_reduce(const Tensor& ws, Tensor& dw, const optional<Tensor>& db, int64_t N, int64_t IC, int64_t KH,
+                  int64_t KW) {
+  dev(ws, "ws"); dev(dw, "dw");
+  const int OC = dw.size(0);
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.numel() == (int64_t)OC * IC * KH * KW &&
+                  ws.numel() >= csed::conv2d_wgrad_workspace(N, IC, KH, KW, OC), "wgrad_reduce: shape mismatch");
+  if (db.has_value()) dev(*db, "db");
+  const c10::DeviceGuard gd(ws.device());
+  CHECK_HIP(csed::launch_wgrad_reduce(ws.data_ptr<float>(), dw.data_ptr<float>(), optpt<float>(db), (int)N, (int)IC,
+                                      (int)KH, (int)KW, OC, cur_stream(ws)));
 }
 
 // ----------------------------------------------------------- fused lenet
@@ -863,7 +895,10 @@ TORCH_LIBRARY(csed, m) {
         "int pool_k, int mfma_dtype, float drop2d_p=0.0, int seed=0, int offset=0, Tensor? offset_dev=None, "
         "Tensor(c!)? chscale_out=None, Tensor(d!)? dbg=None) -> ()");
   m.def("conv2d_bwd(Tensor x, Tensor dy, Tensor w, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws, Tensor(d!)? dx, "
-        "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype, Tensor(e!)? dbg=None) -> ()");
+        "int pad, Tensor? pool_idx, Tensor? pool_out, Tensor? pool_scale, int mfma_dtype, Tensor(e!)? dbg=None, "
+        "Tensor? carry_ws=None, Tensor(f!)? carry_dw=None, Tensor(g!)? carry_db=None, int carry_n=0, int carry_ic=0, "
+        "int carry_kh=0, int carry_kw=0, bool defer_reduce=False) -> ()");
+  m.def("wgrad_reduce(Tensor ws, Tensor(a!) dw, Tensor(b!)? db, int N, int IC, int KH, int KW) -> ()");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? gate, float gate_scale, Tensor(a!)? dx, Tensor(b!)? dw, "
         "Tensor(c!)? db, int mfma_dtype, Tensor? lsm_target=None, Tensor? lsm_gout=None, float lsm_div=1.0) -> ()");
   m.def("lsm_nll_fwd(Tensor z, Tensor target, Tensor(a!) logp, Tensor(b!) out, int reduction) -> ()");
@@ -901,6 +936,7 @@ TORCH_LIBRARY_IMPL(csed, CUDA, m) {
   m.impl("conv2d_dgrad", &conv2d_dgrad);
   m.impl("conv2d_wgrad", &conv2d_wgrad);
   m.impl("conv2d_bwd", &conv2d_bwd);
+  m.impl("wgrad_reduce", &wgrad_reduce);
   m.impl("linear_bwd", &linear_bwd);
   m.impl("lsm_nll_fwd", &lsm_nll_fwd);
   m.impl("linear_lsm_nll_fwd", &linear_lsm_nll_fwd);

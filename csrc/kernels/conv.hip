@@ -714,34 +714,19 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
 #undef WG_STAMP
 }
 
-template <typename T, typename X, typename DY, bool PIN, bool WIDE>
-__global__ void __launch_bounds__(WIDE ? 512 : 256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256>(wa, g, blockIdx.x, smem);
-}
+// Fixed-order sum of the per-block partial slabs (wgrad_reduce_kernel, and carried by another conv's
+// backward launch as extra blocks)
+struct RedArgs {  // a conv's slab reduce (wgrad_reduce_body); blocks == 0: none
+  const float* slab; int nblocks, Co, K; float* dw; float* db; float beta; int blocks;
+};
 
-// The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
-// partial slabs, the rest compute the data gradient (conv_fwd_body in mode 1); both read the same
-// (possibly pooled) dy.  A second launch for the data gradient was a kernel boundary (~1.4 us in a
-// graph) plus its own ramp.
-template <typename T, typename X, typename DY, bool PIN>
-__global__ void __launch_bounds__(512) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if ((int)blockIdx.x < wg.nblocks) conv_wgrad_body<T, X, DY, PIN, true, 512>(wa, wg, blockIdx.x, smem);
-  else conv_fwd_body<T, DY, X, PIN, true, 512>(a, g, blockIdx.x - wg.nblocks, smem);  // (dx: x's dtype)
-}
-
-// Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
-// 4 slices of the partials each (every lane's loads issued together, 16 in flight), then the
-// slices combine in slice order through LDS.  One thread per output walking all nblocks partials
-// in a dependent add chain was latency-bound: 15.8 us for 64 partials (profiles/round5.md).
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nblocks, int Co,
-                                                           int K, float* __restrict__ dw, float* __restrict__ db,
-                                                           float beta) {
-  __shared__ float part[4][64];
+// one 256-thread group's 64 outputs (vb: the group's block index of the reduce's grid)
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, int nblocks, int Co, int K,
+                                                  float* __restrict__ dw, float* __restrict__ db, float beta,
+                                                  int vb, int t, float (*part)[64]) {
   const int L = Co * (K + 1);
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + c;
+  const int c = t & 63, sl = t >> 6;
+  const int i = vb * 64 + c;
   float s = 0.f;
   if (i < L) {
     const int per = (nblocks + 3) >> 2, b0 = sl * per, b1 = min(nblocks, b0 + per);
@@ -768,6 +753,51 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     }
   }
 }
+
+// A carried reduce inside another conv's backward launch: block rb of r's range, NTHR threads = NTHR / 256
+// groups of wgrad_reduce_kernel's 256 (the same per-output arithmetic, so the same bits)
+template <int NTHR>
+__device__ __forceinline__ void carried_reduce(const RedArgs& r, int rb, unsigned char* smem) {
+  float (*part)[64] = reinterpret_cast<float (*)[64]>(smem) + 4 * (threadIdx.x >> 8);
+  const int vb = rb * (NTHR / 256) + (threadIdx.x >> 8);
+  wgrad_reduce_body(r.slab, r.nblocks, r.Co, r.K, r.dw, r.db, r.beta, vb, threadIdx.x & 255, part);
+}
+
+template <typename T, typename X, typename DY, bool PIN, bool WIDE>
+__global__ void __launch_bounds__(WIDE ? 512 : 256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g, RedArgs r) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if ((int)blockIdx.x >= g.nblocks) {  // (a carried reduce of another conv)
+    carried_reduce<WIDE ? 512 : 256>(r, blockIdx.x - g.nblocks, smem);
+    return;
+  }
+  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256>(wa, g, blockIdx.x, smem);
+}
+
+// The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
+// partial slabs, the rest compute the data gradient (conv_fwd_body in mode 1); both read the same
+// (possibly pooled) dy.  A second launch for the data gradient was a kernel boundary (~1.4 us in a
+// graph) plus its own ramp.
+template <typename T, typename X, typename DY, bool PIN>
+__global__ void __launch_bounds__(512) conv_bwd_kernel(WgradArgs wa, WgradGeo wg, ConvArgs a, ConvGeo g, int dblocks,
+                                                       RedArgs r) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  if (b < wg.nblocks) conv_wgrad_body<T, X, DY, PIN, true, 512>(wa, wg, b, smem);
+  else if (b < wg.nblocks + dblocks) conv_fwd_body<T, DY, X, PIN, true, 512>(a, g, b - wg.nblocks, smem);  // (dx: x's dtype)
+  else carried_reduce<512>(r, b - wg.nblocks - dblocks, smem);  // (another conv's reduce)
+}
+
+// Fixed-order sum of the per-block partial slabs: a block covers 64 consecutive outputs with
+// 4 slices of the partials each (every lane's loads issued together, 16 in flight), then the
+// slices combine in slice order through LDS.  One thread per output walking all nblocks partials
+// in a dependent add chain was latency-bound: 15.8 us for 64 partials (profiles/round5.md).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nblocks, int Co,
+                                                           int K, float* __restrict__ dw, float* __restrict__ db,
+                                                           float beta) {
+  __shared__ float part[4][64];
+  wgrad_reduce_body(slab, nblocks, Co, K, dw, db, beta, blockIdx.x, threadIdx.x, part);
+}
+
 
 inline int rup(int a, int b) { return (a + b - 1) / b * b; }
 
@@ -918,6 +948,16 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
     lds = std::max(lds, dl);
     lds_d = dl;
   }
+  // another conv's deferred slab reduce, carried as extra blocks of the first launch below
+  RedArgs red{};
+  if (b.carry_ws) {
+    const int cK = b.carry_IC * b.carry_KH * b.carry_KW;
+    red.slab = b.carry_ws; red.nblocks = std::max(1, std::min(b.carry_N, 256));
+    red.nblocks = cdiv(b.carry_N, cdiv(b.carry_N, red.nblocks));  // (wgrad_geo's block count)
+    red.Co = b.carry_OC; red.K = cK; red.dw = b.carry_dw; red.db = b.carry_db; red.beta = 0.f;
+    red.blocks = cdiv(b.carry_OC * (cK + 1), 64);  // (256-thread groups)
+  }
+  auto red_blocks = [&](int nthr) { return cdiv(red.blocks, nthr / 256); };
   hipError_t e = hipSuccess;
   auto launch = [&](auto ct) -> hipError_t {
     typedef decltype(ct) T;
@@ -933,11 +973,13 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
         auto go = [&](auto bwd, auto wgr, auto dgr) {
           if (merged) {
             if (lds > 64 * 1024) hipFuncSetAttribute((const void*)bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(bwd, dim3(wg.nblocks + dgrid), dim3(512), lds, s, wa, wg, a, g);
+            hipLaunchKernelGGL(bwd, dim3(wg.nblocks + dgrid + red_blocks(512)), dim3(512), lds, s, wa, wg, a, g, dgrid,
+                               red);
             return hipGetLastError();
           }
           if (lds_w > 64 * 1024) hipFuncSetAttribute((const void*)wgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);
-          hipLaunchKernelGGL(wgr, dim3(wg.nblocks), dim3(ww ? 512 : 256), lds_w, s, wa, wg);
+          hipLaunchKernelGGL(wgr, dim3(wg.nblocks + red_blocks(ww ? 512 : 256)), dim3(ww ? 512 : 256), lds_w, s, wa, wg,
+                             red);
           hipError_t e2 = hipGetLastError();
           if (e2 != hipSuccess || dgrid == 0) return e2;
           if (lds_d > 64 * 1024) hipFuncSetAttribute((const void*)dgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
@@ -968,10 +1010,19 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
     case kF32: e = launch(float{}); break;
     default: return hipErrorInvalidValue;
   }
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || b.defer_reduce) return e;
   const int L = b.OC * (wg.K + 1);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, b.ws, wg.nblocks, b.OC, wg.K, b.dw,
                      b.db, b.beta);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad_reduce(const float* ws, float* dw, float* db, int N, int IC, int KH, int KW, int OC,
+                               hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  const int nb = cdiv(N, cdiv(N, std::max(1, std::min(N, 256))));  // (wgrad_geo's block count)
+  const int K = IC * KH * KW, L = OC * (K + 1);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, ws, nb, OC, K, dw, db, 0.f);
   return hipGetLastError();
 }
 

@@ -174,8 +174,16 @@ struct ConvBwdArgs {
   int N, IC, H, W, OC, KH, KW, pad;
   int mfma_dtype;
   uint64_t* dbg;  // optional [weight-gradient blocks, 8] stamps (diagnostics, tools/conv_stamps.py)
+  // optional: ANOTHER conv's deferred slab reduce (its workspace, outputs and shape), run as extra
+  // blocks of this launch; defer_reduce: leave this conv's own reduce to the caller (see WgradReduce)
+  const float* carry_ws; float* carry_dw; float* carry_db; int carry_N, carry_IC, carry_KH, carry_KW, carry_OC;
+  int defer_reduce;
 };
 hipError_t launch_conv2d_bwd(const ConvBwdArgs& a, hipStream_t s);
+// The fixed-order sum of a conv's weight-gradient partial slabs into dW / db (the reduce that
+// launch_conv2d_bwd runs unless defer_reduce), on its own.
+hipError_t launch_wgrad_reduce(const float* ws, float* dw, float* db, int N, int IC, int KH, int KW, int OC,
+                               hipStream_t s);
 // Weight gradient: dW[OC, IC*KH*KW] (fp32) and db[OC] (fp32, optional) of a
 // stride-1 conv; dY may be given gated (dY *= (G > 0) * gs is NOT applied
 // here -- pass the already-unpooled gradient).  `ws` is a workspace of at

@@ -295,3 +295,44 @@ def test_mlp_head_repeated_launches_rearm_counter():
         assert torch.equal(loss, first)
     from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
     assert int(fn._head_counter(w2).item()) == 0
+
+
+def test_deferred_wgrad_reduce_matches_immediate_bitwise():
+    """conv2's weight-gradient reduce carried by conv1's backward launch (and the end-of-backward flush)
+    == every conv reducing in its own launch, bitwise; nothing stays pending after backward; a
+    parameter watched by a post-accumulate-grad hook (a DDP reducer's) is reduced before its hook."""
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+    from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
+
+    torch.manual_seed(1)
+    net = Net().to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.rand(64, 1, 28, 28, device=DEV, generator=g)
+    t = torch.randint(0, 10, (64,), device=DEV, generator=g)
+    res = []
+    try:
+        for defer in (True, False):
+            fn.set_defer_wgrad_reduce(defer)
+            ops.rng.default_state.reset_offset()
+            net.zero_grad(set_to_none=True)
+            net(x, target=t).backward()
+            assert fn._pending_reduce is None
+            res.append([p.grad.clone() for p in net.parameters()])
+        for a, b in zip(*res):
+            assert torch.equal(a, b)
+        fn.set_defer_wgrad_reduce(True)
+        seen = {}
+
+        def hook(p):
+            seen["g"] = p.grad.clone()
+
+        hk = net.conv2.weight.register_post_accumulate_grad_hook(hook)
+        try:
+            ops.rng.default_state.reset_offset()
+            net.zero_grad(set_to_none=True)
+            net(x, target=t).backward()
+        finally:
+            hk.remove()
+        assert torch.equal(seen["g"], res[1][2])  # (conv2.weight: its final gradient inside the hook)
+    finally:
+        fn.set_defer_wgrad_reduce(True)

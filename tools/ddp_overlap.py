@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def _modes():
-    return [("nocomm", 25.0, True), ("overlap", 25.0, True), ("serial", 25.0, False),
+    return [("single", 25.0, True), ("nocomm", 25.0, True), ("overlap", 25.0, True), ("serial", 25.0, False),
             ("overlap", 0.01, True), ("serial", 0.01, False)]
 
 
@@ -66,9 +66,11 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(Fal
                 continue
             torch.manual_seed(1)
             net = Net().to(dev).train()
-            tr = ModularTrainer(net, lr=0.01, momentum=0.5, ctx=ctx, bucket_cap_mb=cap, graph=graph,
-                                overlap=overlap)
-            tr.ddp.world_size = 2  # force the collective path (see the module docstring)
+            # single: the one-GPU trainer (no reducer, no grad hooks: src/train.py --engine modular)
+            tr = ModularTrainer(net, lr=0.01, momentum=0.5, ctx=None if mode == "single" else ctx, bucket_cap_mb=cap,
+                                graph=graph, overlap=overlap)
+            if tr.ddp is not None:
+                tr.ddp.world_size = 2  # force the collective path (see the module docstring)
 
             batches = None
             if loader:
@@ -87,7 +89,7 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(Fal
 
             def step():
                 xb, tb = next(batches) if batches is not None else (x, t)
-                with tr.ddp.no_sync() if mode == "nocomm" else contextlib.nullcontext():
+                with tr.ddp.no_sync() if mode == "nocomm" and tr.ddp is not None else contextlib.nullcontext():
                     tr.train_batch(xb, tb, clone_loss=False)
 
             for _ in range(warmup):
@@ -102,10 +104,10 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(Fal
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / steps
             rows.append({"mode": mode, "graph": graph and tr.use_graph, "batch": batch, "loader": loader, "bucket_mb": cap,
-                         "buckets": len(tr.ddp.buckets),
+                         "buckets": len(tr.ddp.buckets) if tr.ddp is not None else 0,
                          "us_per_step_gpu": round(e0.elapsed_time(e1) * 1000 / steps, 2),
                          "us_per_step_wall": round(wall * 1e6, 2)})
-            for h in tr.ddp._hooks:
+            for h in (tr.ddp._hooks if tr.ddp is not None else []):
                 h.remove()
             del tr
     dist.destroy_process_group()

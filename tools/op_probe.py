@@ -77,6 +77,11 @@ def main() -> int:
         "conv2 bwd (wgrad+dgrad+reduce)": lambda: o.conv2d_bwd(y1, dp2.view(B, 20, 4, 4), w2, dw2, db2, ws2, dx2, 0,
                                                               i2, y2, sc2, 1),
         "conv1 bwd (wgrad+reduce)": lambda: o.conv2d_bwd(x0, dx2, w1, dw1, db1, ws1, None, 0, i1, y1, None, 1),
+        "conv2 bwd, reduce deferred": lambda: o.conv2d_bwd(y1, dp2.view(B, 20, 4, 4), w2, dw2, db2, ws2, dx2, 0,
+                                                          i2, y2, sc2, 1, defer_reduce=True),
+        "conv1 bwd carrying conv2's reduce": lambda: o.conv2d_bwd(x0, dx2, w1, dw1, db1, ws1, None, 0, i1, y1, None, 1,
+                                                                 carry_ws=ws2, carry_dw=dw2, carry_db=db2, carry_n=B,
+                                                                 carry_ic=10, carry_kh=5, carry_kw=5),
         "sgd (21840)": lambda: o.sgd_flat(flat, gflat, mom, 0.01, 0.5, 0.0, 0.0, False, 1.0, step, ticket),
     }
     s = torch.cuda.Stream()
