@@ -463,7 +463,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   const int pe = g.Ci * g.PR * g.PW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // patch rows / pooled dy channels per batch (512 threads: 8, the same loads per block in flight)
-  constexpr int RB = (WIDE && NTHR == 256) ? 16 : 8;
+  constexpr int RB = (WIDE && NTHR == 256) ? 16 : NTHR == 512 ? 4 : 8;
 #define WG_STAMP(i) \
   if (wa.dbg && tid == 0 && n == blk * g.per_block) wa.dbg[(int64_t)blk * 8 + (i)] = __builtin_amdgcn_s_memtime();
   if (wa.dbg && tid == 0) wa.dbg[(int64_t)blk * 8] = __builtin_amdgcn_s_memtime();
@@ -553,7 +553,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     const uint8_t* is = wa.pidx + (PIN ? yimg : 0);
     const float* ss = wa.pscale ? wa.pscale + (int64_t)n * g.Co : slab;
     const int wst = max(1, min(npixp, NTHR)), wgr = qdiv(NTHR, wst), gq = qdiv(tid, wst), q0 = tid - gq * wst;
-    float dv[RB], yo[RB], sc[RB];
+    float dv[RB > 8 ? RB : 8], yo[RB], sc[RB];  // (plain dy: chunks of 8 channels whatever RB)
     uint8_t bi[RB];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
     bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
