@@ -123,7 +123,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     base = !kv ? -1 : a.mode == 0 ? k : (ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
   };
   // single-round weight form: a thread's columns k = tid + NTHR i (i < 32 / COP) x all COP channels
-  constexpr int WB = WIDE ? 32 : 8, RB = WIDE ? 16 : 8;  // weight / row loads per batch
+  constexpr int WB = WIDE ? 32 : 8, RB = 8;  // weight / row loads per batch
   const int wcols = WB / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
   const bool wfast = WIDE && g.Cop <= 32 && g.Kp <= NTHR * wcols;
   int wb[2] = {-1, -1};
