@@ -83,7 +83,7 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // X: the input's element type, PIN: the input is given max-pooled (a.pidx) -- compile-time, so the
 // staging's loads are straight-line code (a runtime dtype / mode branch around them made the
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256>  // Y: the output's element type
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256, int RB = 8>  // Y: the output's element type
 // WIDE: 32 weight / 16 patch-row loads per thread in flight (one round trip: small grids); narrow:
 // 8 / 8 (fewer registers, more blocks per CU: large grids, where other blocks hide the latency).
 // NTHR: the block size (512 for a standalone launch: two waves per SIMD interleave the staging's
@@ -123,7 +123,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     base = !kv ? -1 : a.mode == 0 ? k : (ic * g.Co * KHW + (g.KH - 1 - kh) * g.KW + (g.KW - 1 - kw));
   };
   // single-round weight form: a thread's columns k = tid + NTHR i (i < 32 / COP) x all COP channels
-  constexpr int WB = WIDE ? 32 : 8, RB = 8;  // weight / row loads per batch
+  constexpr int WB = WIDE ? 32 : 8;  // weight loads per batch (RB: patch rows per batch, per thread)
   const int wcols = WB / g.Cop;  // (Cop 16: two columns, 32: one, larger: the round loop below)
   const bool wfast = WIDE && g.Cop <= 32 && g.Kp <= NTHR * wcols;
   int wb[2] = {-1, -1};
@@ -417,10 +417,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 
 // (small grids: 512 threads, two waves per SIMD interleaving the staging's instruction stream --
 // conv1 fwd at B = 64 10.8 -> 9.6 us; large grids: 256, more blocks per CU -- 512 there was slower)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE>
+// RB: patch rows per thread per staging batch -- the host picks 4 when the geometry needs no more
+// (an unrolled batch's unused rows are VALU issue, the stagings' bound), else 8 (more: extra rounds)
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8>
 __global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256>(a, g, blockIdx.x, smem);
+  conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -881,8 +883,11 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
           hipLaunchKernelGGL(kern, dim3(grid), block, lds, s, a, g);
           return hipGetLastError();
         };
-        if (a.pidx) return wide ? go(conv_fwd_kernel<scalar_t, X, Y, true, true>) : go(conv_fwd_kernel<scalar_t, X, Y, true, false>);
-        return wide ? go(conv_fwd_kernel<scalar_t, X, Y, false, true>) : go(conv_fwd_kernel<scalar_t, X, Y, false, false>);
+        const bool rb4 = wide && cdiv(g.Ci * g.PR, 512 / g.PW) <= 4;  // (patch rows per thread)
+        if (a.pidx) return wide ? (rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, true, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, true, true>))
+                                : go(conv_fwd_kernel<scalar_t, X, Y, true, false>);
+        return wide ? (rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, false, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, false, true>))
+                    : go(conv_fwd_kernel<scalar_t, X, Y, false, false>);
       });
     });
   });
