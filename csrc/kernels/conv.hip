@@ -197,7 +197,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   // operands in straight-line code, then a scheduling barrier so no conversion / store of a loaded
   // value is hoisted between them (it would wait on its load mid-issue: a second round trip)
   load_rows();
-  if (wfast) {
+  // (wave-uniform: a wave that owns no weight column -- conv1's Kp = 32 of 512 threads -- skips the
+  // weight batch; the loads were unconditional at clamped addresses, pure VALU / address cost)
+  const int wave0 = tid & ~63;
+  if (wfast && (wave0 < g.Kp || (wcols > 1 && wave0 + NTHR < g.Kp))) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < wcols && tid + NTHR * i < g.Kp) wcol(tid + NTHR * i, wb[i], wko[i]);
