@@ -115,7 +115,8 @@ def _flush_pending_reduce() -> None:
     p, _pending_reduce = _pending_reduce, None
     if p is not None:
         ws, dw, db, N, IC, KH, KW = p
-        _ops().wgrad_reduce(ws, dw, db, N, IC, KH, KW)
+        with torch.cuda.device(dw.device):
+            _ops().wgrad_reduce(ws, dw, db, N, IC, KH, KW)
 
 
 def _watched(t) -> bool:
@@ -176,6 +177,8 @@ class _Conv2d(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
             global _pending_reduce
+            if _pending_reduce is not None and _pending_reduce[1].device != w.device:
+                _flush_pending_reduce()  # (another device's pending reduce: run it there, on its own)
             carry, _pending_reduce = _pending_reduce, None  # (another conv's reduce rides on this launch)
             defer = _defer_reduce and not _watched(w) and not _watched(ctx.bias_param)
             ck = {} if carry is None else dict(carry_ws=carry[0], carry_dw=carry[1], carry_db=carry[2],
