@@ -127,6 +127,8 @@ def _watched(t) -> bool:
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, pad, pool, chscale, drop):
+        if _pending_reduce is not None:  # (left by a backward pass that did not finish: run it now)
+            _flush_pending_reduce()
         x = x.contiguous()
         if x.dtype not in (torch.float32, _compute_dtype):  # (the kernels take fp32 or the compute dtype)
             x = x.to(_compute_dtype)
