@@ -204,9 +204,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < wcols && tid + NTHR * i < g.Kp) wcol(tid + NTHR * i, wb[i], wko[i]);
+    const bool col1 = wcols > 1 && g.Kp > NTHR;  // (a second column per thread exists at all: uniform)
 #pragma unroll
     for (int j = 0; j < WB; ++j) {  // (unconditional loads at a clamped address, then a select)
       const int i = g.Cop == 16 ? j >> 4 : 0, oc = g.Cop == 16 ? j & 15 : j;
+      if (i == 1 && !col1) break;  // (conv2's data gradient: Kp = 512, the second half was 16 dead loads)
       const bool ok = wb[i] >= 0 && oc < g.Co;
       const float t = a.w[(unsigned)(ok ? wb[i] + oc * wstep : 0)];
       wv[j] = ok ? t : 0.f;
