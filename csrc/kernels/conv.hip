@@ -219,8 +219,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     const float* cp = a.chscale ? a.chscale : a.w;  // unconditional, no branch + wait per element)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      eb[j] = 0.f;
+      es[j] = 1.f;
+      if (j >= NT) continue;  // (uniform: N-tiles past the channels' -- conv1 has 1 of 4)
       const int oc = j * 16 + (tid & 15);
-      const bool ok = j < NT && oc < g.Co;
+      const bool ok = oc < g.Co;
       const float tb = bp[(unsigned)(ok ? oc : 0)], tc = cp[(unsigned)(ok ? n * g.Co + oc : 0)];
       eb[j] = ok && a.bias ? tb : 0.f;
       es[j] = ok && a.chscale ? tc : 1.f;
