@@ -83,7 +83,9 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // X: the input's element type, PIN: the input is given max-pooled (a.pidx) -- compile-time, so the
 // staging's loads are straight-line code (a runtime dtype / mode branch around them made the
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256, int RB = 8>  // Y: the output's element type
+// NTM: N-tiles per accumulator group (4; 1 when the output channels fit one tile -- conv1, the
+// data gradients -- so no fragment of an absent tile is read from LDS)
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256, int RB = 8, int NTM = 4>  // Y: the output's element type
 // WIDE: 32 weight / 16 patch-row loads per thread in flight (one round trip: small grids); narrow:
 // 8 / 8 (fewer registers, more blocks per CU: large grids, where other blocks hide the latency).
 // NTHR: the block size (512 for a standalone launch: two waves per SIMD interleave the staging's
@@ -299,21 +301,21 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     }
     const bool valid = m < npix;
     const int pb = valid ? oh * g.PW + ow : 0;     // oh is band-relative
-    for (int nc = 0; nc < NT; nc += 4) {
-      f32x4 acc[4];
+    for (int nc = 0; nc < NT; nc += NTM) {
+      f32x4 acc[NTM];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NTM; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (WIDE) {
         // Software-pipelined K loop: K-step s+1's patch gathers and weight fragments are read (LDS)
         // while step s runs on the MFMAs, and the k -> patch offsets two steps ahead.  Every read is
         // unconditional at a valid address (a pixel past npix reads the block's first and is zeroed
         // after; N-tiles past NT read row 0): a predicated LDS read was a branch + wait per element.
         const int kq8 = 8 * (lane >> 4);
-        int wrow[4];
+        int wrow[NTM];
   #pragma unroll
-        for (int j = 0; j < 4; ++j) wrow[j] = (nc + j < NT ? (nc + j) * 16 + (lane & 15) : 0) * LDW;
+        for (int j = 0; j < NTM; ++j) wrow[j] = (nc + j < NT ? (nc + j) * 16 + (lane & 15) : 0) * LDW;
         typename Stor<T>::V8 raw;
-        frag fb[4];
+        frag fb[NTM];
         int4 o0 = *reinterpret_cast<const int4*>(koff + kq8);
         int4 o1 = *reinterpret_cast<const int4*>(koff + kq8 + 4);
         {
@@ -321,7 +323,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   #pragma unroll
           for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
   #pragma unroll
-          for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kq8);
+          for (int j = 0; j < NTM; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kq8);
         }
         {
           const int kn = min(kq8 + 32, g.Kp - 8);  // (step 1's offsets; clamped: a valid slot)
@@ -330,16 +332,16 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
         }
         for (int k0 = 0; k0 < g.Kp; k0 += 32) {
           const typename Stor<T>::V8 cur = raw;
-          frag fbc[4];
+          frag fbc[NTM];
   #pragma unroll
-          for (int j = 0; j < 4; ++j) fbc[j] = fb[j];
+          for (int j = 0; j < NTM; ++j) fbc[j] = fb[j];
           {  // step s+1's reads (clamped past the last step: valid slots, unused)
             const int kb1 = min(k0 + 32, g.Kp - 32) + kq8;
             const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
   #pragma unroll
             for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
   #pragma unroll
-            for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kb1);
+            for (int j = 0; j < NTM; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kb1);
             const int kn = min(k0 + 64 + kq8, g.Kp - 8);
             o0 = *reinterpret_cast<const int4*>(koff + kn);
             o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
@@ -349,7 +351,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
           for (int j = 0; j < 8; ++j) am[j] = valid ? cur[j] : (S)0;
           const frag fa = __builtin_bit_cast(frag, am);
   #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < NTM; ++j)
             if (nc + j < NT) acc[j] = Mfma<T>::mma(fa, fbc[j], acc[j]);
         }
       } else {
@@ -368,7 +370,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
           for (int j = 0; j < 8; ++j) raw[j] = valid ? raw[j] : (S)0;
           const frag fa = __builtin_bit_cast(frag, raw);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < NTM; ++j) {
             if (nc + j < NT) {
               const frag fb = *reinterpret_cast<const frag*>(Ws + ((nc + j) * 16 + (lane & 15)) * LDW + kb);
               acc[j] = Mfma<T>::mma(fa, fb, acc[j]);
@@ -378,7 +380,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       }
       // ---- epilogue
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NTM; ++j) {
         if (nc + j >= NT) continue;
         const int oc = (nc + j) * 16 + (lane & 15);
         if (oc >= g.Co) continue;
@@ -430,7 +432,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8>
 __global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blockIdx.x, smem);
+  if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blockIdx.x, smem);
+  else conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -793,7 +796,10 @@ __global__ void __launch_bounds__(512) conv_bwd_kernel(WgradArgs wa, WgradGeo wg
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   if (b < wg.nblocks) conv_wgrad_body<T, X, DY, PIN, true, 512>(wa, wg, b, smem);
-  else if (b < wg.nblocks + dblocks) conv_fwd_body<T, DY, X, PIN, true, 512>(a, g, b - wg.nblocks, smem);  // (dx: x's dtype)
+  else if (b < wg.nblocks + dblocks) {  // (dx: x's dtype)
+    if (g.Cop == 16) conv_fwd_body<T, DY, X, PIN, true, 512, 8, 1>(a, g, b - wg.nblocks, smem);
+    else conv_fwd_body<T, DY, X, PIN, true, 512>(a, g, b - wg.nblocks, smem);
+  }
   else carried_reduce<512>(r, b - wg.nblocks - dblocks, smem);  // (another conv's reduce)
 }
 
