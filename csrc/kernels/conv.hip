@@ -433,6 +433,7 @@ template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8>
 __global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blockIdx.x, smem);
+  else if (g.Cop == 32) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 2>(a, g, blockIdx.x, smem);
   else conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blockIdx.x, smem);
 }
 
