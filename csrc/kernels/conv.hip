@@ -570,7 +570,9 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     float dv[RB > 8 ? RB : 8], yo[RB], sc[RB];  // (plain dy: chunks of 8 channels whatever RB)
     uint8_t bi[RB];
     int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
-    bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Cop) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
+    // (pooled: channels up to Co only -- dY rows Co..Cop-1 feed only the MFMA rows the slab write
+    // drops, and zero-filling them cost conv1 (10 of 16) a second staging round trip)
+    bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Co) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
     auto load_dy = [&]() {  // one chunk's loads
       if constexpr (!PIN) {
         const int yo0 = d_oc0 * g.npix + d_p;
@@ -611,13 +613,13 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       } else {
 #pragma unroll
         for (int j = 0; j < RB; ++j) {
-          if (d_oc0 + j >= g.Cop) break;
+          if (d_oc0 + j >= g.Co) break;
           S* d = dys + (d_oc0 + j) * LDY + d_pb;
 #pragma unroll
           for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(dv[j], bi[j], yo[j], sc[j], e));
         }
         d_oc0 += wgr * RB;
-        if (d_oc0 >= g.Cop) {
+        if (d_oc0 >= g.Co) {
           d_oc0 = gq * RB;
           d_q += wst;
         }
