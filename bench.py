@@ -81,6 +81,9 @@ def parse(argv=None) -> argparse.Namespace:
                     help="cpu: plumbing only (launch/rendezvous/JSON contract), stock PyTorch ops")
     ap.add_argument("--no-fp32-record", action="store_true",
                     help="skip the exact-fp32 sub-record (step 7) of a 16-bit run")
+    ap.add_argument("--epoch0-stamps", action="store_true",
+                    help="keep every launch's GPU / host time of epoch 0 and the warm epoch in the JSON "
+                         "(epoch0_breakdown.replay_gpu_ms); the summary is always there")
     ap.add_argument("--inject-exchange-fault", action="store_true",
                     help="fault-injection test hook: the last rank's exchange pushes go to a dead-end buffer "
                          "(in loopback mode: every virtual peer is dead), so peer waits time out; the bench "
@@ -181,7 +184,7 @@ def start_native_data():
     return ns.Job(60000, 10000, seed=0)
 
 
-def start_gpu_context(phases: dict | None = None, torch_too: bool = True):
+def start_gpu_context(phases: dict | None = None, torch_too: bool = True, preload_mask: int = 0):
     """This rank's HIP context, created in a thread started at t0 that runs while the data set
     is generated and the process group comes up.  ctypes loads the HIP runtime that torch
     itself links (torch/lib/libamdhip64.so), so torch later finds this process's primary
@@ -201,28 +204,102 @@ def start_gpu_context(phases: dict | None = None, torch_too: bool = True):
         return None
     dev = int(os.environ.get("LOCAL_RANK", "0"))
 
+    def preload(d):
+        t = time.time()
+        try:
+            import torch
+
+            from csed_514_project_distributed_training_using_pytorch_amd.ops import _native
+
+            if _native.load(build_if_missing=False):
+                torch.ops.csed.preload_kernels(d, preload_mask)
+        except Exception as e:  # (diagnostic only: the kernels then load at their first launch)
+            print(f"[bench] kernel preload failed: {e!r}", file=sys.stderr)
+        if phases is not None:
+            phases["preload_thread"] = time.time() - t
+
     def run():
         t = time.time()
+        sub = {}
         n = ctypes.c_int(0)
         if hip.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value <= 0:
             return
+        sub["ctx.device_count"] = time.time() - t
         if hip.hipSetDevice(dev % n.value) == 0:
+            t1 = time.time()
             hip.hipFree(ctypes.c_void_p(0))  # (the context's creation)
+            sub["ctx.hip_context"] = time.time() - t1
+            if preload_mask:
+                # the kernels' code objects load in a thread of their own, beside torch's CUDA
+                # set-up below and the engine's: the HIP runtime would otherwise load each
+                # translation unit's at its first launch (lenet_tile's: the epoch-0 validation,
+                # 5-60 ms on a fresh box, profiles/r6/epoch0.md)
+                threading.Thread(target=preload, args=(dev % n.value,), name="csed-preload", daemon=True).start()
             if torch_too:
                 # torch's own CUDA state (lazy init, caching allocator: ~0.09 s, round-5 bring-up
                 # breakdown engine.net) comes up here too, behind the data generator
                 import torch
 
+                t1 = time.time()
                 torch.cuda.set_device(dev % n.value)
+                sub["ctx.torch_init"] = time.time() - t1
                 # (the process's first pageable host -> device copy sets up the runtime's staging
                 # buffers: 0.09 s, measured as engine.net in round 5 -- done here, off the path)
+                t1 = time.time()
                 torch.empty(1, device=torch.device("cuda", dev % n.value)).copy_(torch.zeros(1))
+                sub["ctx.first_copy"] = time.time() - t1
         if phases is not None:
+            phases.update(sub)
             phases["hip_ctx_thread"] = time.time() - t
 
     t = threading.Thread(target=run, name="csed-hip-context", daemon=True)
     t.start()
     return t
+
+
+class EpochStamps:
+    """HIP events + host clock at each launch boundary of one epoch (graph replays, the tail step,
+    the validation pass).  Recording an event is one small packet per replay (30 per epoch), so
+    epoch 0 is always stamped: its breakdown shows where a cold epoch loses time against a warm one
+    (a slow first replay: graph upload / first launch; slow early replays that speed up: GPU clock
+    ramp; a slow validation: first launch of the eval kernel)."""
+
+    def __init__(self, device):
+        import torch
+
+        self.torch = torch
+        self.device = device
+        self.marks: list[tuple[str, object, float]] = []
+
+    def mark(self, name: str) -> None:
+        ev = self.torch.cuda.Event(enable_timing=True)
+        ev.record(self.torch.cuda.current_stream(self.device))
+        self.marks.append((name, ev, time.perf_counter()))
+
+    def summary(self, detail: bool = False) -> dict | None:
+        if len(self.marks) < 2:
+            return None
+        self.marks[-1][1].synchronize()
+        gpu = [a[1].elapsed_time(b[1]) for a, b in zip(self.marks, self.marks[1:])]
+        host = [1e3 * (b[2] - a[2]) for a, b in zip(self.marks, self.marks[1:])]
+        names = [b[0] for b in self.marks[1:]]
+        rep = [g for g, n in zip(gpu, names) if n == "replay"]
+        rh = [h for h, n in zip(host, names) if n == "replay"]
+        srt = sorted(rep[1:]) if len(rep) > 1 else rep
+        med = srt[len(srt) // 2] if srt else None
+        r = lambda v: round(v, 4) if v is not None else None  # noqa: E731
+        out = {"replays": len(rep), "replay_gpu_ms_total": r(sum(rep)), "first_replay_gpu_ms": r(rep[0]) if rep else None,
+               "replay_gpu_ms_median_after_first": r(med), "replay_gpu_ms_last": r(rep[-1]) if rep else None,
+               "replays_over_1p2x_median": sum(1 for g in rep if med and g > 1.2 * med),
+               "first_replay_host_ms": r(rh[0]) if rh else None, "replay_host_ms_total": r(sum(rh)),
+               "tail_gpu_ms": r(sum(g for g, n in zip(gpu, names) if n == "tail")),
+               "eval_gpu_ms": r(sum(g for g, n in zip(gpu, names) if n == "eval")),
+               "eval_host_ms": r(sum(h for h, n in zip(host, names) if n == "eval")),
+               "gpu_ms_total": r(sum(gpu)), "host_ms_total": r(sum(host))}
+        if detail:
+            out["replay_gpu_ms"] = [r(g) for g in rep]
+            out["replay_host_ms"] = [r(h) for h in rh]
+        return out
 
 
 # the order of bring-up events on this rank, for tests/test_bench_contract_cpu.py: (name, time)
@@ -254,7 +331,11 @@ def bringup(args, phases: dict):
         native_job = start_native_data()
     if args.device == "cuda":
         BRINGUP_EVENTS.append(("hip_ctx_thread", time.time()))
-        ctx_job = start_gpu_context(phases)
+        # code objects: lenet_fused (the step), lenet_tile (the 10k validation, and large batches),
+        # lenet_fused_f32 (--dtype fp32 and the fp32 sub-record), the exchange (N > 1)
+        # (CSED_PRELOAD=1: a third thread loads them beside the context's creation -- measured, it
+        # only contends with it: profiles/r6/epoch0.md; by default each loads at its first launch)
+        ctx_job = start_gpu_context(phases, preload_mask=0b1111 if os.environ.get("CSED_PRELOAD") == "1" else 0)
     return t_start, native_job, ctx_job
 
 
@@ -305,7 +386,7 @@ def main(argv=None) -> int:
         time_elapsed, epoch0_s, epoch_s, val, loss_avg, comm_err, comm_retry = r["time_elapsed_s"], None, None, \
             None, None, 0, None
         process_elapsed, replicas, fp32_rec = r["process_elapsed_s"], r["replicas"], None
-        data_src = None
+        data_src = e0_rec = ew_rec = None
     else:
         from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
         from csed_514_project_distributed_training_using_pytorch_amd.models import Net
@@ -318,6 +399,7 @@ def main(argv=None) -> int:
                 from csed_514_project_distributed_training_using_pytorch_amd.data.mnist import MNISTData
 
                 (xi, xl), (ti, tl) = native_job.result()
+                phases["data_gen_thread"] = native_job.elapsed_s
                 train = MNISTData(torch.from_numpy(xi), torch.from_numpy(xl), synthetic=True)
                 test = MNISTData(torch.from_numpy(ti), torch.from_numpy(tl), synthetic=True)
                 data_src = "native generator (csrc/data/synth_mnist.cpp), overlapped with import torch"
@@ -365,32 +447,50 @@ def main(argv=None) -> int:
                     eng.run_steps(n_, spg, use_graph=use_graph)
                     state["pos"] += n_
 
-            def full_epoch():
-                eng.run_steps(eng.full_steps(), spg, use_graph=use_graph)
+            def full_epoch(stamps: EpochStamps | None = None):
+                plan = eng.step_plan(eng.full_steps(), spg, use_graph)
+                if stamps is not None:
+                    stamps.mark("start")
+                for launch in plan:
+                    launch()
+                    if stamps is not None:
+                        stamps.mark("replay")
                 eng.last_partial_step(use_graph=use_graph)
-                return eng.evaluate(test)
+                if stamps is not None:
+                    stamps.mark("tail")
+                res = eng.evaluate(test)
+                if stamps is not None:
+                    stamps.mark("eval")
+                return res
 
             new_epoch()
             full = eng.full_steps()
             t_mark = time.time()
-            if use_graph:  # every graph this run replays: epoch, tail, timed K (from an epoch start)
+            if use_graph:  # the graphs epoch 0 replays (the timed K-step graph: after the span)
                 with prof.range("bench:capture"):
-                    eng.prepare(spg, ks=(full, *epoch_chunks(args.steps, 0, full)))
+                    eng.prepare(spg, ks=(full,))
             ph["capture"] = time.time() - t_mark
+            ph.update({k: v for k, v in eng.bringup_s.items() if k.startswith("capture.")})
             t_mark = time.time()
             eng._device_data(test)  # test set upload is data loading (ref: DataLoader), not epoch work
             ph["test_upload"] = time.time() - t_mark
-            # 2. epoch 0, cold: the reference's time_elapsed (process start -> epoch-0 validation)
+            # 2. epoch 0, cold: the reference's time_elapsed (process start -> epoch-0 validation),
+            # every launch stamped (HIP events + host clock; --epoch0-stamps keeps the per-replay list)
             sync_barrier()
+            st0 = EpochStamps(ctx.device)
             te = time.perf_counter()
             with prof.range("bench:epoch0"):
-                full_epoch()
+                full_epoch(st0)
             sync_barrier()
             ph["epoch0"] = time.perf_counter() - te
             epoch0 = all_reduce_max(ctx, ph["epoch0"])
             now = time.time()
             t_el = all_reduce_max(ctx, now - t_start)  # the reference's span (t0 after the imports)
             p_el = all_reduce_max(ctx, now - t_proc)  # from process start
+            if use_graph:  # the timed window's graphs (outside the span: not epoch-0 work)
+                t_mark = time.time()
+                eng.prepare(spg, ks=tuple(epoch_chunks(args.steps, 0, full)), tail=False)
+                ph["capture_timed"] = time.time() - t_mark
             # 3. warm-up, then a rehearsal of the timed sequence (same graphs, same order)
             with prof.range("bench:warmup"):
                 new_epoch()
@@ -420,15 +520,16 @@ def main(argv=None) -> int:
             dev_ms = all_reduce_max(ctx, ev.ms())
             loss_sum, _ = eng.take_loss()
             # 5. one more full epoch + validation, warm (order prepared before the clock starts)
-            epoch_s = val = None
+            epoch_s = val = stw = None
             if not args.no_epoch:
                 sampler.set_epoch(state["epoch"])
                 order = sampler.indices()
                 new_epoch(order)
                 sync_barrier()
+                stw = EpochStamps(ctx.device)
                 te = time.perf_counter()
                 with prof.range("bench:epoch"):
-                    vloss, vcorrect = full_epoch()
+                    vloss, vcorrect = full_epoch(stw)
                 sync_barrier()
                 epoch_s = all_reduce_max(ctx, time.perf_counter() - te)
                 val = {"val_loss": vloss / len(test), "val_acc": vcorrect / len(test)}
@@ -441,6 +542,7 @@ def main(argv=None) -> int:
             return dict(eng=eng, elapsed=elapsed, dev_ms=dev_ms, loss_sum=loss_sum, epoch0=epoch0, t_el=t_el,
                         p_el=p_el,
                         epoch_s=epoch_s, val=val, err=err, replicas=same_p and same_m,
+                        e0=st0.summary(args.epoch0_stamps), ew=stw.summary(args.epoch0_stamps) if stw else None,
                         diag=eng.comm_diag() if err else None)
 
         from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc
@@ -467,6 +569,7 @@ def main(argv=None) -> int:
             r = run_once(0, False, retry_phases)
             phases.update({f"retry.{k}": v for k, v in retry_phases.items()})
         eng = r["eng"]
+        e0_rec, ew_rec = r["e0"], r["ew"]
         elapsed, time_elapsed, epoch0_s, epoch_s, val = r["elapsed"], r["t_el"], r["epoch0"], r["epoch_s"], r["val"]
         process_elapsed = r["p_el"]
         comm_err, replicas = r["err"], r["replicas"]
@@ -510,6 +613,7 @@ def main(argv=None) -> int:
                         "device_ms_per_step": round(f["dev_ms"] / args.steps, 5),
                         "epoch_s": round(f["epoch_s"], 4) if f["epoch_s"] is not None else None,
                         "epoch0_s": round(f["epoch0"], 4),
+                        "epoch0_breakdown": f["e0"],
                         "engine": f"fused HIP ({fe.kernel_names}), allreduce {fe.allreduce_kind}",
                         "replicas_identical": f["replicas"], "comm_error_word": f["err"]}
             if f["val"]:
@@ -566,6 +670,10 @@ def main(argv=None) -> int:
             # engine.self_test of the fused exchange), capture (HIP graphs), test_upload, epoch0
             # (938 steps + validation)
             "bringup_s": bringup_rec,
+            # epoch 0 (inside time_elapsed_s) and the warm epoch, stamped launch by launch (GPU ms
+            # between HIP events, host ms between enqueues): where a cold epoch loses time
+            "epoch0_breakdown": e0_rec,
+            "epoch_breakdown": ew_rec,
         }
         if comm_retry:
             rec["config"]["comm_retry"] = f"{comm_retry} path timed out; re-measured on the process-group all-reduce"

@@ -80,7 +80,10 @@ def _threads() -> int:
         pass
     # ranks of one node share its CPUs (torchrun / bench.py --gpus N export LOCAL_WORLD_SIZE)
     per_rank = n // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
-    return max(1, min(16, per_rank))
+    # (two CPUs left to the rank's HIP-context thread and main thread, which bring the runtime up
+    # while the generator runs: 16 generator threads on a 16-CPU share slowed the context's
+    # creation, profiles/r6/epoch0.md)
+    return max(1, min(14, per_rank - 2))
 
 
 def generate(n: int, seed: int = 0, train: bool = True, classes: int = 10,
@@ -105,14 +108,19 @@ class Job:
     def __init__(self, n_train: int = 60000, n_test: int = 10000, seed: int = 0):
         self._out = None
         self._err = None
+        self.elapsed_s = None  # the generator's own wall time
         self._t = threading.Thread(target=self._run, args=(n_train, n_test, seed), daemon=True)
         self._t.start()
 
     def _run(self, n_train, n_test, seed):
+        import time
+
+        t = time.perf_counter()
         try:
             self._out = (generate(n_train, seed, True), generate(n_test, seed, False))
         except BaseException as e:  # re-raised in result()
             self._err = e
+        self.elapsed_s = time.perf_counter() - t
 
     def result(self):
         self._t.join()

@@ -52,19 +52,45 @@ from ..utils.flat import FlatParams
 N_VEC = 464  # per-sample fc vector length (kernels/lenet_layout.h VEC)
 
 
+_HIP_LIBS: list | None = None
+
+
+def _hip_libs() -> list:
+    """ctypes handles of the HIP runtime this process already loaded (via torch), never a second
+    copy."""
+    global _HIP_LIBS
+    if _HIP_LIBS is None:
+        import ctypes
+
+        try:
+            with open("/proc/self/maps") as f:
+                paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+            _HIP_LIBS = [ctypes.CDLL(p) for p in sorted(paths)]
+        except OSError:
+            _HIP_LIBS = []
+    return _HIP_LIBS
+
+
 def _clear_hip_error() -> None:
     """Reset this thread's sticky HIP error after a failed stream capture.  Our ops report
     ``hipGetLastError()`` after each launch, so an invalidated capture would otherwise
     surface as a failure of the next (eager) launch."""
+    for lib in _hip_libs():
+        lib.hipGetLastError()
+
+
+def _graph_upload(g: torch.cuda.CUDAGraph, stream: torch.cuda.Stream) -> bool:
+    """hipGraphUpload of an instantiated graph on ``stream``: the executable graph's launch
+    resources (kernel-argument blocks, AQL packet templates) are put on the device now, enqueued
+    behind whatever the stream runs, instead of on the graph's first replay."""
     import ctypes
 
-    try:  # the HIP runtime this process already loaded (via torch), never a second copy
-        with open("/proc/self/maps") as f:
-            paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
-        for path in paths:
-            ctypes.CDLL(path).hipGetLastError()
-    except OSError:
-        pass
+    libs = _hip_libs()
+    if not libs:
+        return False
+    fn = libs[0].hipGraphUpload
+    fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int
+    return fn(ctypes.c_void_p(g.raw_cuda_graph_exec()), ctypes.c_void_p(stream.cuda_stream)) == 0
 
 
 def layout() -> tuple[int, int, int, int]:
@@ -210,6 +236,8 @@ class FusedLeNetTrainer:
         self.repack()  # (the extension's first kernel launch: its code object loads here)
         self.bringup_s["first_kernel"] = time.perf_counter() - t_mark
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._warmed: set[str] = set()  # step kinds whose capture warm-up has run (see _capture)
+        self._cap_stream: torch.cuda.Stream | None = None
         self._stepper: tuple | None = None  # (key, csed.LenetStepper), see stepper()
         self.native_max = native_max_steps()
         # which training kernel runs a step: 0 auto (the sample-tile kernel, csrc/kernels/
@@ -522,10 +550,23 @@ class FusedLeNetTrainer:
 
 
 
+    def uses_tile_kernel(self, B: int | None = None, grid: int | None = None) -> bool:
+        """Whether a full step of per-rank batch B on ``grid`` workgroups runs the sample-tile kernel
+        (csrc/kernels/lenet_tile.hip) -- the launcher's own rule (bindings.cpp lenet_train) for
+        kernel_for()'s choice: 16-bit, and kernel 2, or kernel 0 (auto) with B >= tile_min_batch()."""
+        B = self.B if B is None else B
+        grid = self.grid if grid is None else grid
+        if self.fp32:
+            return False
+        k = self.kernel_for(B, grid)
+        return k == 2 or (k == 0 and B >= tile_min_batch())
+
     @property
     def kernel_names(self) -> str:
-        """The HIP kernels of one training step (reports)."""
-        return "lenet_train_f32 + lenet_update" if self.fp32 else "lenet_train + lenet_update"
+        """The HIP kernels of one full training step, as launched (reports)."""
+        if self.fp32:
+            return "lenet_train_f32 + lenet_update"
+        return ("lenet_tile" if self.uses_tile_kernel() else "lenet_train") + " + lenet_update"
 
     @property
     def step_kind(self) -> str:
@@ -635,32 +676,76 @@ class FusedLeNetTrainer:
         return [self.flat.data, self.momentum_buf, self.wimg, self.step_count, self.cursor, self.rng_offset,
                 self.loss_acc] + ([self.xstage, self.lstage] if self.xstage is not None else [])
 
+    def _stamp(self, key: str, dt: float) -> None:
+        self.bringup_s[key] = self.bringup_s.get(key, 0.0) + dt
+
     def _capture(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph:
+        """Capture ``nsteps`` full steps (or the epoch's tail step) into a HIP graph.
+
+        The first capture of each step kind (full / tail x all-reduce path x kernel) runs one eager warm-up step on the
+        capture stream first (lazy RCCL communicator set-up, each kernel's first-launch symbol
+        lookup -- neither may happen inside a capture), the engine state snapshotted before and
+        restored after it; later captures of the same kind skip it.  The capture itself calls
+        capture_begin / capture_end directly: ``torch.cuda.graph``'s device synchronize and
+        ``empty_cache`` are not needed here (the steps allocate nothing), and the graph is
+        instantiated explicitly, then uploaded to the device on the current stream
+        when ``CSED_GRAPH_UPLOAD=1`` (off by default: measured, a first replay costs the same either way,
+        profiles/r6/epoch0.md).  Host
+        seconds accumulate in ``bringup_s``: capture.warmup / .record / .instantiate / .upload."""
+        import time
+
         step = self._tail_step if tail else self.step
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(self.device)
-        # snapshot the state the capture warm-up will advance; the side stream must
-        # wait for the snapshot copies too (they are enqueued on the current stream)
-        state = self._state()
-        saved = [t.clone() for t in state]
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            step()  # warm-up on the capture stream (lazy RCCL init etc.)
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
-        for t, v in zip(state, saved):
-            t.copy_(v)
-        torch.cuda.synchronize(self.device)
+        cur = torch.cuda.current_stream(self.device)
+        t0 = time.perf_counter()
+        if self._cap_stream is None:  # (one capture stream per engine: creating a stream costs ms)
+            self._cap_stream = torch.cuda.Stream(self.device)
+        s = self._cap_stream
+        kind = f"{'tail' if tail else 'full'}/{self.allreduce_kind}/{self.train_kernel}"
+        self._stamp("capture.stream", time.perf_counter() - t0)
+        if kind not in self._warmed:
+            # snapshot the state the capture warm-up will advance; the side stream must
+            # wait for the snapshot copies too (they are enqueued on the current stream)
+            ta = time.perf_counter()
+            state = self._state()
+            saved = [t.clone() for t in state]
+            s.wait_stream(cur)
+            tb = time.perf_counter()
+            with torch.cuda.stream(s):
+                step()
+            cur.wait_stream(s)
+            tc = time.perf_counter()
+            torch.cuda.synchronize(self.device)
+            td = time.perf_counter()
+            for t, v in zip(state, saved):
+                t.copy_(v)
+            torch.cuda.synchronize(self.device)
+            te = time.perf_counter()
+            self._warmed.add(kind)
+            for k, dt in (("snapshot", tb - ta), ("step", tc - tb), ("sync", td - tc), ("restore", te - td)):
+                self._stamp(f"capture.warmup.{k}", dt)
+        t1 = time.perf_counter()
         comm.quiesce()  # (no pending collective for the watchdog to query during the capture)
         # thread_local: only this thread's unsafe calls invalidate the capture.  The process
         # group's watchdog thread keeps querying the events of earlier collectives while a step
         # that contains an RCCL all-reduce is captured; in the default (global) mode that query
         # invalidates the capture and the watchdog then aborts the process (seen on the GPU box,
         # profiles/round5.md)
-        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-            for _ in range(nsteps):
-                step()
-        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.stream(s):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                for _ in range(nsteps):
+                    step()
+            finally:
+                g.capture_end()
+        t2 = time.perf_counter()
+        g.instantiate()
+        t3 = time.perf_counter()
+        if os.environ.get("CSED_GRAPH_UPLOAD", "0") == "1":
+            _graph_upload(g, cur)
+        t4 = time.perf_counter()
+        for k, dt in (("warmup", t1 - t0), ("record", t2 - t1), ("instantiate", t3 - t2), ("upload", t4 - t3)):
+            self._stamp(f"capture.{k}", dt)
         return g
 
     def graph(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph | None:
@@ -789,7 +874,9 @@ class FusedLeNetTrainer:
         nparts = min(n, 256)
         torch.ops.csed.lenet_eval(test.images, test.labels, order, n, self.wimg, self.flat.data, MNIST_MEAN,
                                   MNIST_STD, self.eval_parts, None, self.mfma)
-        parts = self.eval_parts[: 2 * nparts].view(nparts, 2).double().sum(0).tolist()
+        # (the 256 partial pairs summed on the host, in fixed order: a device reduction would be a
+        # torch kernel whose code object loads at its first launch -- inside epoch 0)
+        parts = self.eval_parts[: 2 * nparts].cpu().view(nparts, 2).double().sum(0).tolist()
         return parts[0], int(round(parts[1]))
 
     @torch.no_grad()

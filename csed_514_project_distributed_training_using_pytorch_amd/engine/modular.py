@@ -86,6 +86,7 @@ class ModularTrainer:
         """set_to_none (torch's default): the next backward writes every gradient in place."""
         for p in self.flat.params:
             p.grad = None
+        ops.functional.release_grad_buffers(self.flat.params)
 
     def _step(self, x: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         ops.rng.default_state.reset_offset()
@@ -106,7 +107,7 @@ class ModularTrainer:
         self.model.train()
         if not self.use_graph:
             return self._step(x, target)
-        key = (tuple(x.shape), x.dtype, tuple(target.shape))
+        key = self._graph_key(x, target)
         g = self._graphs.get(key)
         if g is None:
             g = self._capture(x, target)
@@ -120,11 +121,21 @@ class ModularTrainer:
         graph.replay()
         return sloss.clone() if clone_loss else sloss
 
+    def _hyper(self) -> tuple:
+        """The optimizer hyper-parameters a captured step bakes into its SGD launch: a change (an LR
+        schedule, manual decay through ``opt.param_groups``) selects a new capture."""
+        g = self.opt.param_groups[0]
+        return (float(g["lr"]), float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]),
+                bool(g["nesterov"]), float(self.opt.grad_scale))
+
+    def _graph_key(self, x: torch.Tensor, target: torch.Tensor) -> tuple:
+        return (tuple(x.shape), x.dtype, tuple(target.shape), self._hyper())
+
     def bind_loader(self, loader) -> None:
         """Let ``loader`` (data/loader.py DeviceLoader) gather each batch straight into the captured
         step's input buffers once a graph exists for its shape: no copy launches per step."""
         def into(B: int, dtype: torch.dtype):
-            g = self._graphs.get(((B, 1, 28, 28), dtype, (B,))) if self.use_graph else None
+            g = self._graphs.get(((B, 1, 28, 28), dtype, (B,), self._hyper())) if self.use_graph else None
             return (g[1], g[2]) if g is not None else None
 
         loader.into = into
@@ -164,7 +175,7 @@ class ModularTrainer:
             self.use_graph = False
             return None
         g = (graph, sx, st, sloss)
-        self._graphs[(tuple(x.shape), x.dtype, tuple(target.shape))] = g
+        self._graphs[self._graph_key(x, target)] = g
         return g
 
     @torch.no_grad()

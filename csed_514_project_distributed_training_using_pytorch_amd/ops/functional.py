@@ -64,10 +64,20 @@ def _act_dtype(x: torch.Tensor) -> torch.dtype:
 # (a view of the flat gradient), which autograd's AccumulateGrad then adopts as ``.grad`` without
 # a copy or an add kernel.  A parameter that already holds a gradient gets a fresh buffer, so
 # accumulation (no zero_grad between two backwards) keeps its usual semantics.
+#
+# A parameter used more than once in one forward (shared weights, a layer applied twice) has one
+# backward call per use within ONE autograd pass, and autograd sums their outputs before
+# AccumulateGrad.  Only the pass's first call may get the registered buffer (else every call would
+# write the same memory and the sum would add aliases of it); the first hand-out is marked, later
+# calls of the pass get fresh buffers, and the mark is dropped by a callback queued on the autograd
+# engine for the end of the pass (or by the next zero_grad's set_to_none).
+import threading  # noqa: E402
 import weakref  # noqa: E402
 
 # id(param) -> (weak reference to param, buffer); keyed by identity (tensors compare elementwise)
 _grad_dest: dict[int, tuple[weakref.ref, torch.Tensor]] = {}
+_handed_out: set[int] = set()  # ids of parameters handed a gradient buffer in the running pass
+_lock = threading.Lock()  # (autograd runs one worker thread per device)
 
 
 def set_grad_destination(param: torch.Tensor, buf: torch.Tensor | None) -> None:
@@ -82,11 +92,55 @@ def set_grad_destination(param: torch.Tensor, buf: torch.Tensor | None) -> None:
     _grad_dest[id(param)] = (weakref.ref(param), buf)
 
 
+def _queue_end_of_pass(fn) -> bool:
+    """Run ``fn`` when the running autograd pass ends.  False outside a backward pass."""
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(fn)
+        return True
+    except RuntimeError:
+        return False
+
+
+def _take_grad_buffer(param: torch.Tensor | None, shape, device) -> tuple[torch.Tensor, bool]:
+    """(gradient buffer for ``param``, adopted).  Adopted: the buffer is the registered destination,
+    the only gradient this pass produces for ``param``, and autograd's AccumulateGrad will take it
+    as ``.grad`` as it is -- ``.grad`` is None, grad mode is off (no create_graph) and no earlier
+    call of this pass was handed one -- so nothing reads it before the pass's end-of-pass callbacks
+    have run (the condition for deferring the conv weight-gradient reduce).  Parameters without a
+    registered destination (e.g. under torch's own DDP, whose C++ grad hooks are invisible here)
+    never count as adopted."""
+    if param is None:
+        return torch.empty(shape, device=device, dtype=torch.float32), False
+    key = id(param)
+    hit = _grad_dest.get(key)
+    if hit is None or hit[0]() is not param:
+        return torch.empty(shape, device=device, dtype=torch.float32), False
+    with _lock:
+        first = param.grad is None and key not in _handed_out and not torch.is_grad_enabled()
+        if first and _queue_end_of_pass(lambda: _release(key)):
+            _handed_out.add(key)
+        else:
+            first = False
+    if first:
+        return hit[1].view(hit[1].shape), True  # (a fresh view: AccumulateGrad steals only a sole reference)
+    return torch.empty(shape, device=device, dtype=torch.float32), False
+
+
+def _release(key: int) -> None:
+    with _lock:
+        _handed_out.discard(key)
+
+
 def _grad_buffer(param: torch.Tensor | None, shape, device) -> torch.Tensor:
-    hit = _grad_dest.get(id(param)) if param is not None else None
-    if hit is not None and hit[0]() is param and param.grad is None:
-        return hit[1].view(hit[1].shape)  # (a fresh view: AccumulateGrad steals only a sole reference)
-    return torch.empty(shape, device=device, dtype=torch.float32)
+    return _take_grad_buffer(param, shape, device)[0]
+
+
+def release_grad_buffers(params) -> None:
+    """Forget this pass's hand-out marks of ``params`` (zero_grad with set_to_none; a pass that
+    raised before its end-of-pass callbacks ran)."""
+    with _lock:
+        for p in params:
+            _handed_out.discard(id(p))
 
 
 def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
@@ -94,14 +148,19 @@ def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
 
 
 # The deferred weight-gradient slab reduce.  A conv backward normally ends with its own reduce
-# launch (the partial slabs -> dW, db); when deferral is on and no hook watches the parameters
-# (a DDP reducer's post-accumulate-grad hooks would read dW before it is final), the reduce is left
-# pending: the NEXT conv backward of the same autograd pass runs it as extra blocks of its own launch
-# (it does not depend on it), and a callback queued on the autograd engine flushes whatever is still
-# pending when the pass ends -- before any optimizer or user code can read the gradients.  One launch
+# launch (the partial slabs -> dW, db); when deferral is on, no hook watches the parameters (a DDP
+# reducer's post-accumulate-grad hooks would read dW before it is final) and autograd will adopt
+# dW / db as they are (``_take_grad_buffer``: ``.grad`` None, first use in the pass, no
+# create_graph -- an accumulating ``grad += dW`` or a shared weight's sum would be enqueued as soon
+# as this backward returns, before the reduce), the reduce is left pending: the NEXT conv backward
+# of the same autograd pass on that device runs it as extra blocks of its own launch (it does not
+# depend on it), and a callback queued on the autograd engine flushes whatever is still pending
+# when the pass ends -- before any optimizer or user code can read the gradients.  One launch
 # fewer per step in the modular engine (conv2's reduce rides on conv1's backward).
 _defer_reduce = os.environ.get("CSED_DEFER_WGRAD_REDUCE", "1") != "0"
-_pending_reduce = None  # (ws, dw, db, N, IC, KH, KW) of the conv whose reduce is pending
+# device index -> (ws, dw, db, N, IC, KH, KW) of the conv whose reduce is pending on that device
+# (autograd's per-device worker threads each touch their own entry; the swaps hold _lock)
+_pending: dict[int, tuple] = {}
 
 
 def set_defer_wgrad_reduce(on: bool) -> None:
@@ -110,11 +169,18 @@ def set_defer_wgrad_reduce(on: bool) -> None:
     _defer_reduce = bool(on)
 
 
-def _flush_pending_reduce() -> None:
-    global _pending_reduce
-    p, _pending_reduce = _pending_reduce, None
-    if p is not None:
-        ws, dw, db, N, IC, KH, KW = p
+def pending_reduce_count() -> int:
+    """Number of weight-gradient reduces still pending (0 after every completed backward)."""
+    with _lock:
+        return len(_pending)
+
+
+def _flush_pending_reduce(dev: int | None = None) -> None:
+    """Run the pending reduce of device ``dev`` (None: of every device)."""
+    with _lock:
+        keys = list(_pending) if dev is None else [dev]
+        todo = [_pending.pop(k) for k in keys if k in _pending]
+    for ws, dw, db, N, IC, KH, KW in todo:
         with torch.cuda.device(dw.device):
             _ops().wgrad_reduce(ws, dw, db, N, IC, KH, KW)
 
@@ -127,7 +193,7 @@ def _watched(t) -> bool:
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, pad, pool, chscale, drop):
-        if _pending_reduce is not None:  # (left by a backward pass that did not finish: run it now)
+        if _pending:  # (left by a backward pass that did not finish: run it now)
             _flush_pending_reduce()
         x = x.contiguous()
         if x.dtype not in (torch.float32, _compute_dtype):  # (the kernels take fp32 or the compute dtype)
@@ -173,24 +239,28 @@ class _Conv2d(torch.autograd.Function):
             # expanded inside the kernels' staging (dL/dconv never materialised)
             N, IC = x.shape[:2]
             OC, _, KH, KW = w.shape
-            dw = _grad_buffer(w, w.shape, w.device)
-            db = _grad_buffer(ctx.bias_param, (OC,), w.device) if ctx.has_bias else None
+            dw, dw_adopt = _take_grad_buffer(w, w.shape, w.device)
+            db, db_adopt = _take_grad_buffer(ctx.bias_param, (OC,), w.device) if ctx.has_bias else (None, True)
             ws = torch.empty(wgrad_workspace_elems(N, IC, KH, KW, OC), device=w.device, dtype=torch.float32)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
-            global _pending_reduce
-            if _pending_reduce is not None and _pending_reduce[1].device != w.device:
-                _flush_pending_reduce()  # (another device's pending reduce: run it there, on its own)
-            carry, _pending_reduce = _pending_reduce, None  # (another conv's reduce rides on this launch)
-            defer = _defer_reduce and not _watched(w) and not _watched(ctx.bias_param)
+            dev = w.device.index if w.device.index is not None else torch.cuda.current_device()
+            with _lock:  # (another conv's reduce on this device rides on this launch)
+                carry = _pending.pop(dev, None)
+            defer = (_defer_reduce and dw_adopt and db_adopt and ctx.needs_input_grad[1]
+                     and (not ctx.has_bias or ctx.needs_input_grad[2])
+                     and not _watched(w) and not _watched(ctx.bias_param))
             ck = {} if carry is None else dict(carry_ws=carry[0], carry_dw=carry[1], carry_db=carry[2],
                                                carry_n=carry[3], carry_ic=carry[4], carry_kh=carry[5],
                                                carry_kw=carry[6])
             _ops().conv2d_bwd(x, dy, w, dw, db, ws, dx, ctx.pad, *pooled, ctx.mf, defer_reduce=defer, **ck)
-            if defer:  # (detached aliases: a second reference to dw / db themselves would make autograd's
+            if defer and _queue_end_of_pass(lambda: _flush_pending_reduce(dev)):
+                # (detached aliases: a second reference to dw / db themselves would make autograd's
                 # AccumulateGrad clone them -- before the deferred reduce has written them -- not adopt them)
-                _pending_reduce = (ws, dw.detach(), db.detach() if db is not None else None, N, IC, KH, KW)
-                torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_reduce)
+                with _lock:
+                    _pending[dev] = (ws, dw.detach(), db.detach() if db is not None else None, N, IC, KH, KW)
+            elif defer:  # (not inside an autograd pass: nothing would flush it)
+                _ops().wgrad_reduce(ws, dw, db, N, IC, KH, KW)
         elif ctx.needs_input_grad[0]:
             if ctx.pool:
                 dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)

@@ -5,6 +5,7 @@
 // kernel(s) on the current PyTorch HIP stream.  No op allocates, copies to
 // host or synchronises, so every op is safe inside torch.cuda.graph capture
 // (= hipStreamBeginCapture).
+#include <chrono>
 #include <vector>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -601,6 +602,30 @@ std::vector<int64_t> lenet_layout() {
           csed::lenet_split_k(), csed::lenet_tile_samples(), csed::lenet_tile_min_batch()};
 }
 
+// Load the code objects of the kernel translation units named by `mask` on `device` now, from
+// any host thread (bit 0 lenet_fused, 1 lenet_tile, 2 lenet_fused_f32, 3 comm, 4 conv, 5 gemm,
+// 6 elementwise).  The HIP runtime loads a TU's code object lazily at its first launch -- measured
+// on a fresh box: lenet_tile's (the 10k-image validation) 5-60 ms inside epoch 0.  Returns the
+// host milliseconds spent.
+double preload_kernels(int64_t device, int64_t mask) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int prev = 0;
+  CHECK_HIP(hipGetDevice(&prev));
+  CHECK_HIP(hipSetDevice((int)device));
+  hipError_t (*const fns[])() = {csed::preload_lenet_fused, csed::preload_lenet_tile, csed::preload_lenet_f32,
+                                 csed::comm::preload_comm, csed::preload_conv, csed::preload_gemm,
+                                 csed::preload_elementwise};
+  hipError_t err = hipSuccess;
+  for (int i = 0; i < 7; ++i)
+    if ((mask >> i) & 1) {
+      const hipError_t e = fns[i]();
+      if (err == hipSuccess) err = e;
+    }
+  (void)hipSetDevice(prev);
+  CHECK_HIP(err);
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
   dev(params, "params"); dev(wimg, "wimg");
   TORCH_CHECK(params.scalar_type() == at::kFloat && params.numel() >= csed::lenet_param_count());
@@ -858,6 +883,7 @@ TORCH_LIBRARY(csed, m) {
       .def("set_update", &LenetStepper::set_update)
       .def("run", &LenetStepper::run);
   m.def("lenet_layout() -> int[]", &lenet_layout);
+  m.def("preload_kernels(int device, int mask=127) -> float", &preload_kernels);
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
         "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "

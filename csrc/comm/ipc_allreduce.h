@@ -58,5 +58,7 @@ struct IpcPeers {
 };
 hipError_t ipc_peers(int id, IpcPeers* out);
 
+hipError_t preload_comm();  // the exchange TU's code object (csed::preload_kernels)
+
 }  // namespace comm
 }  // namespace csed

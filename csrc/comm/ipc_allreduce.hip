@@ -340,5 +340,12 @@ hipError_t ipc_diag(int id, int* out) {
   return hipMemcpy(out, c->err + 1, kDiagWords * sizeof(int), hipMemcpyDeviceToHost);
 }
 
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_comm() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(ipc_allreduce_kernel));
+}
+
 }  // namespace comm
 }  // namespace csed

@@ -1059,4 +1059,11 @@ hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int d
   return launch_conv2d_bwd(b, s);
 }
 
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_conv() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(wgrad_reduce_kernel));
+}
+
 }  // namespace csed

@@ -459,4 +459,11 @@ hipError_t launch_gate_bwd(const void* dout, int dout_dtype, const void* y, int 
   return hipGetLastError();
 }
 
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_elementwise() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(sgd_flat_kernel));
+}
+
 }  // namespace csed

@@ -354,9 +354,16 @@ __device__ __forceinline__ void head_epilogue(const GemmArgs& a, int mt, int n, 
   if (lane == 0) {
     const unsigned long long ntiles = (unsigned long long)((a.M + 15) >> 4);
     constexpr unsigned long long kFlag = 1ull << 47, kOne = 1ull << 48;
+    // Each tile adds at most (2^47 - 1) / ntiles, so the sum bits can never carry into the flag bit
+    // or the count, however many tiles overflow.  A non-finite or larger tile sum adds 0 and sets
+    // the flag with an OR (idempotent: any number of flagged tiles leave the count intact).  The OR
+    // precedes the tile's count add on the same word, and atomics on one address are ordered, so the
+    // last-arriving tile sees every flag.
+    const float cap = (float)((kFlag - 1) / ntiles);
     const float sc = nll * (float)(1 << kHeadFrac);  // (nll >= 0: a sum of -log-probs)
-    const unsigned long long q =
-        (sc >= 0.f && sc < 1.0e14f) ? (unsigned long long)__builtin_rintf(sc) : kFlag;  // (NaN fails both)
+    const bool in_range = sc >= 0.f && sc < cap;  // (NaN fails both)
+    const unsigned long long q = in_range ? (unsigned long long)__builtin_rintf(sc) : 0ull;
+    if (!in_range) __hip_atomic_fetch_or(a.head_cnt, kFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long old = __hip_atomic_fetch_add(a.head_cnt, kOne + q, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
     if ((old >> 48) == ntiles - 1) {
@@ -1009,7 +1016,9 @@ hipError_t launch_mlp_head_bwd(const GemmArgs& in_x2, const GemmArgs& in_w2, con
 }
 
 bool gemm_head_ok(const GemmArgs& a) {
-  return a.M > 0 && a.N > 0 && a.N <= 16 && !a.rowsum && a.act == 0 && !a.G && !a.lsm_target && a.beta == 0.f &&
+  // (head_epilogue's hand-off word counts arrived 16-row tiles in 16 bits)
+  return a.M > 0 && (a.M + 15) / 16 < 65536 && a.N > 0 && a.N <= 16 && !a.rowsum && a.act == 0 && !a.G &&
+         !a.lsm_target && a.beta == 0.f &&
          a.c_dtype == kF32 && gemm_small(a);
 }
 
@@ -1054,6 +1063,13 @@ hipError_t launch_colsum(const void* x, int x_dtype, const void* gate, int g_dty
     }
   });
   return hipGetLastError();
+}
+
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_gemm() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(gemm_splitk_reduce<float>));
 }
 
 }  // namespace csed

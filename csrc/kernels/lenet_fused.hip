@@ -2508,4 +2508,11 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   return hipGetLastError();
 }
 
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_lenet_fused() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(lenet_pack_kernel<__bf16>));
+}
+
 }  // namespace csed

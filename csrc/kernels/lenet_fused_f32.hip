@@ -867,4 +867,11 @@ hipError_t launch_lenet_train_f32(const LenetTrainArgs& a, int write_logp, float
   return hipGetLastError();
 }
 
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_lenet_f32() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(lenet32::lenet_train_f32_kernel<false>));
+}
+
 }  // namespace csed

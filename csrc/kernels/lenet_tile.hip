@@ -890,4 +890,11 @@ hipError_t launch_lenet_tile(const LenetTrainArgs& a, int write_logp, float* log
   return hipGetLastError();
 }
 
+// Load this translation unit's code object on the current device now (the HIP runtime loads it
+// lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
+hipError_t preload_lenet_tile() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(lenet_tile::lenet_tile_kernel<__bf16, false, false>));
+}
+
 }  // namespace csed

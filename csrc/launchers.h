@@ -295,4 +295,13 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
                              float std_, float* out_parts, float* logp_out, int mfma_dtype, hipStream_t s,
                              int kernel = 0);
 
+// Per-translation-unit code-object preloads (each calls hipFuncGetAttributes on one of the TU's
+// kernels on the current device): csed::preload_kernels in csrc/bindings.cpp.
+hipError_t preload_lenet_fused();
+hipError_t preload_lenet_tile();
+hipError_t preload_lenet_f32();
+hipError_t preload_conv();
+hipError_t preload_gemm();
+hipError_t preload_elementwise();
+
 }  // namespace csed

@@ -25,7 +25,7 @@ def test_bringup_starts_no_job_work_before_t0(monkeypatch):
     calls = []
     monkeypatch.setattr(bench, "start_native_data", lambda: calls.append(("native_data", time.time())) or None)
     monkeypatch.setattr(bench, "start_gpu_context",
-                        lambda phases=None: calls.append(("hip_ctx_thread", time.time())) or None)
+                        lambda phases=None, **kw: calls.append(("hip_ctx_thread", time.time())) or None)
     phases = {}
     t0, native_job, ctx_job = bench.bringup(types.SimpleNamespace(device="cuda"), phases)
     # the imports are timed and come first

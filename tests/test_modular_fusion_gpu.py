@@ -297,26 +297,82 @@ def test_mlp_head_repeated_launches_rearm_counter():
     assert int(fn._head_counter(w2).item()) == 0
 
 
+@pytest.mark.parametrize("head", ["linear", "mlp"])
+def test_head_loss_recovers_after_nonfinite_and_huge_losses(head):
+    """A NaN logit, then huge losses in many tiles, then a finite batch: the first two report a
+    non-finite loss, the finite batch's loss is right again (the hand-off word never carried into its
+    arrival count) and the word is re-armed to 0 after each launch."""
+    from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
+
+    g = torch.Generator(device=DEV).manual_seed(21)
+    M = 256  # 16 tiles
+    x = torch.randn(M, 50, device=DEV, generator=g)
+    w = torch.randn(10, 50, device=DEV, generator=g) * 0.2
+    b = torch.zeros(10, device=DEV)
+    t = torch.randint(0, 10, (M,), device=DEV, generator=g)
+
+    def loss_of(xx, bb=b):
+        if head == "linear":
+            return ops.linear_log_softmax_nll(xx, w, bb, t, reduction="sum")
+        return ops.mlp_head_nll(xx.to(torch.bfloat16), w1, None, w, bb, t, act="relu", reduction="sum")
+
+    w1 = torch.eye(50, device=DEV)  # (mlp: relu(x) feeds the head)
+    bad = b.clone()
+    bad[7] = float("nan")  # (a NaN logit in every row; the fc1 ReLU would turn a NaN input into 0)
+    assert not torch.isfinite(loss_of(x, bad)).item()
+    assert int(fn._head_counter(w).item()) == 0
+    huge = x * 1e8  # every tile's sum far above the fixed-point range
+    assert not torch.isfinite(loss_of(huge)).item()
+    assert int(fn._head_counter(w).item()) == 0
+    got = loss_of(x).item()
+    xr = x if head == "linear" else torch.relu(x.to(torch.bfloat16).float())
+    want = F.nll_loss(F.log_softmax(xr @ w.t() + b, 1), t, reduction="sum").item()
+    assert abs(got - want) <= 2e-2 * abs(want), (got, want)
+    assert int(fn._head_counter(w).item()) == 0
+
+
+def _net_with_destinations():
+    """Net on the GPU with its gradients registered into a flat buffer (as ModularTrainer does):
+    the only configuration in which the conv weight-gradient reduce is deferred."""
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+    from csed_514_project_distributed_training_using_pytorch_amd.utils.flat import FlatParams
+
+    torch.manual_seed(1)
+    net = Net().to(DEV).train()
+    flat = FlatParams(list(net.parameters()))
+    for i, p in enumerate(flat.params):
+        ops.set_grad_destination(p, flat.grad_view(i))
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.rand(64, 1, 28, 28, device=DEV, generator=g)
+    t = torch.randint(0, 10, (64,), device=DEV, generator=g)
+    return net, flat, x, t
+
+
+def _drop_destinations(flat):
+    for p in flat.params:
+        ops.set_grad_destination(p, None)
+
+
+def _backward(net, x, t):
+    ops.rng.default_state.reset_offset()
+    net(x, target=t).backward()
+
+
 def test_deferred_wgrad_reduce_matches_immediate_bitwise():
     """conv2's weight-gradient reduce carried by conv1's backward launch (and the end-of-backward flush)
     == every conv reducing in its own launch, bitwise; nothing stays pending after backward; a
     parameter watched by a post-accumulate-grad hook (a DDP reducer's) is reduced before its hook."""
-    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
     from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
 
-    torch.manual_seed(1)
-    net = Net().to(DEV).train()
-    g = torch.Generator(device=DEV).manual_seed(13)
-    x = torch.rand(64, 1, 28, 28, device=DEV, generator=g)
-    t = torch.randint(0, 10, (64,), device=DEV, generator=g)
+    net, flat, x, t = _net_with_destinations()
     res = []
     try:
         for defer in (True, False):
             fn.set_defer_wgrad_reduce(defer)
-            ops.rng.default_state.reset_offset()
             net.zero_grad(set_to_none=True)
-            net(x, target=t).backward()
-            assert fn._pending_reduce is None
+            _backward(net, x, t)
+            assert fn.pending_reduce_count() == 0
+            assert flat.grads_are_views()  # (adopted: written in place)
             res.append([p.grad.clone() for p in net.parameters()])
         for a, b in zip(*res):
             assert torch.equal(a, b)
@@ -328,11 +384,85 @@ def test_deferred_wgrad_reduce_matches_immediate_bitwise():
 
         hk = net.conv2.weight.register_post_accumulate_grad_hook(hook)
         try:
-            ops.rng.default_state.reset_offset()
             net.zero_grad(set_to_none=True)
-            net(x, target=t).backward()
+            _backward(net, x, t)
         finally:
             hk.remove()
         assert torch.equal(seen["g"], res[1][2])  # (conv2.weight: its final gradient inside the hook)
     finally:
         fn.set_defer_wgrad_reduce(True)
+        _drop_destinations(flat)
+
+
+def test_deferred_wgrad_reduce_with_zeroed_grads_and_accumulation():
+    """Deferral on, .grad NOT None (FusedSGD.zero_grad keeps flat views; a second backward without
+    zero_grad): AccumulateGrad adds dW as soon as the conv backward returns, so the reduce must not
+    be deferred -- conv gradients equal the set_to_none step's, and twice them after two backwards."""
+    from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
+    from csed_514_project_distributed_training_using_pytorch_amd.optim import FusedSGD
+
+    net, flat, x, t = _net_with_destinations()
+    try:
+        fn.set_defer_wgrad_reduce(True)
+        net.zero_grad(set_to_none=True)
+        _backward(net, x, t)
+        ref = [p.grad.clone() for p in net.parameters()]
+        opt = FusedSGD(list(net.parameters()), lr=0.01, momentum=0.5, flat=flat)
+        opt.zero_grad()  # flat.grad zeroed, .grad = the flat views (not None)
+        assert all(p.grad is not None for p in net.parameters())
+        _backward(net, x, t)
+        assert fn.pending_reduce_count() == 0
+        for a, p in zip(ref, net.parameters()):
+            assert torch.equal(p.grad, a)
+        _backward(net, x, t)  # no zero_grad: accumulates
+        for a, p in zip(ref, net.parameters()):
+            assert torch.equal(p.grad, 2 * a)
+    finally:
+        fn.set_defer_wgrad_reduce(True)
+        _drop_destinations(flat)
+
+
+@pytest.mark.parametrize("defer", [True, False])
+def test_shared_weights_with_destinations_match_cpu(defer):
+    """A conv and a linear each applied twice in one forward, gradients registered into a flat buffer
+    (ModularTrainer's setup): every use's dW must be summed, not written into one shared buffer --
+    compared with the same model on the CPU (fp32 kernels, so the tolerance is the fp32 one)."""
+    from csed_514_project_distributed_training_using_pytorch_amd.ops import functional as fn
+    from csed_514_project_distributed_training_using_pytorch_amd.utils.flat import FlatParams
+
+    torch.manual_seed(3)
+    conv = torch.nn.Conv2d(4, 4, 3, padding=1)
+    lin = torch.nn.Linear(16, 16)
+    x = torch.randn(8, 4, 4, 4)
+
+    def model(x, c, lw, lb):
+        y = ops.conv2d(ops.conv2d(x, c.weight, c.bias, padding=1), c.weight, c.bias, padding=1)
+        y = y.reshape(8, 64)[:, :16].float()
+        return ops.linear(ops.linear(y, lw, lb), lw, lb).float().square().sum()
+
+    model(x, conv, lin.weight, lin.bias).backward()
+    want = [p.grad.clone() for p in (conv.weight, conv.bias, lin.weight, lin.bias)]
+    gconv = torch.nn.Conv2d(4, 4, 3, padding=1).to(DEV)
+    glin = torch.nn.Linear(16, 16).to(DEV)
+    with torch.no_grad():
+        for a, b in ((gconv, conv), (glin, lin)):
+            a.weight.copy_(b.weight)
+            a.bias.copy_(b.bias)
+    params = [gconv.weight, gconv.bias, glin.weight, glin.bias]
+    flat = FlatParams(params)
+    for i, p in enumerate(flat.params):
+        ops.set_grad_destination(p, flat.grad_view(i))
+    ops.set_compute_dtype(torch.float32)
+    fn.set_defer_wgrad_reduce(defer)
+    try:
+        for p in params:
+            p.grad = None
+        model(x.to(DEV), gconv, glin.weight, glin.bias).backward()
+        torch.cuda.synchronize()
+        assert fn.pending_reduce_count() == 0
+        for g, p in zip(want, params):
+            torch.testing.assert_close(p.grad.cpu(), g, rtol=1e-4, atol=1e-4)
+    finally:
+        ops.set_compute_dtype(torch.bfloat16)
+        fn.set_defer_wgrad_reduce(True)
+        _drop_destinations(flat)

@@ -49,6 +49,29 @@ def test_graph_step_equals_eager_step():
     assert len(set(loss_g.tolist())) == len(batches)
 
 
+def test_graph_step_follows_lr_changes():
+    """An LR schedule written through opt.param_groups mid-run: the graph path must use the new lr
+    (a new capture), like the eager path -- bitwise."""
+    from csed_514_project_distributed_training_using_pytorch_amd.engine.modular import ModularTrainer
+    from csed_514_project_distributed_training_using_pytorch_amd.models import Net
+
+    dev = torch.device("cuda", 0)
+    batches = _batches(6, 64, dev)[:5]
+    res = []
+    for graph in (False, True):
+        torch.manual_seed(1)
+        tr = ModularTrainer(Net().cuda().train(), lr=0.05, momentum=0.5, graph=graph)
+        for i, (x, t) in enumerate(batches):
+            if i == 2:
+                tr.opt.param_groups[0]["lr"] = 0.01
+            tr.train_batch(x, t)
+        torch.cuda.synchronize()
+        res.append(tr)
+    assert len(res[1]._graphs) == 2  # one capture per lr
+    assert torch.equal(res[0].flat.data, res[1].flat.data)
+    assert torch.equal(res[0].opt.momentum_flat, res[1].opt.momentum_flat)
+
+
 def test_graph_step_with_captured_bucketed_allreduce():
     """A one-rank RCCL process group with the reducer forced into its collective path: every
     bucket's all-reduce is captured on the comm stream inside the step graph; the result equals

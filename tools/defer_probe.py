@@ -27,7 +27,7 @@ def main() -> int:
         loss = net(x, target=t) if mode.startswith("fused") else ops.nll_loss(net(x), t)
         loss.backward()
         torch.cuda.synchronize()
-        print(mode, "pending after backward:", fn._pending_reduce is not None)
+        print(mode, "pending after backward:", fn.pending_reduce_count())
         res[mode] = {n: p.grad.clone() for n, p in net.named_parameters()}
     for a, b in (("fused-defer", "fused-nodefer"), ("logp-defer", "logp-nodefer"), ("fused-nodefer", "logp-nodefer")):
         print(a, "vs", b, {n: round((res[a][n] - res[b][n]).abs().max().item(), 6) for n in res[a]})

@@ -28,6 +28,12 @@
 #   pmctile   the three PMC passes over the tile kernel only (B = 1024)
 #   abenv     same-box A/B of one build under ENV_A vs ENV_B (BENCH_ARGS / AB_ARGS / N_AB)
 #   abcfg     same-box A/B of ab/A_C.so vs ab/B_C.so over several bench configs (AB_CFGS, N_AB)
+#   splitk    rocprofv3 kernel stats of the B = 8192 fp16 step for ab/A_C.so vs ab/B_C.so, alternating
+#             (was gpu_r5j.sh), and the loopback world-8 soak
+#   ipcmem    the exchange receive buffer's allocation: uncached (default) vs CSED_IPC_MEM=finegrained
+#             (was gpu_ipcmem.sh)
+#   epoch0    the reference span on a fresh process, stamped: bench.py --epoch0-stamps at N = 1 (bf16,
+#             fp32) + the driver's own command
 TASKS=${1:?task list}
 T=${2:-run}
 R=$GRAFT_REPO_ROOT
@@ -167,6 +173,34 @@ task_abenv() {
     if [ $v = A ]; then E="$ENV_A"; else E="$ENV_B"; fi
     echo "$v $(env $E timeout -k 10 100 python bench.py ${BENCH_ARGS:---steps 3000 --warmup 300 --no-epoch} $AB_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*')" >> $O/${T}_abenv.log || return 1
   done; done
+}
+
+task_splitk() {
+  cd /tmp && export TMPDIR=/tmp && \
+  for i in 1 2; do for v in A B; do
+    CSED_NATIVE_SO=$R/ab/${v}_C.so py 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_splitk_${v}$i -o run -- python3 $R/bench.py --global-batch 8192 --dtype fp16 --steps 60 --warmup 6 --no-epoch --no-fp32-record > $O/${T}_splitk_${v}$i.log 2>&1 || return 1
+  done; done && \
+  cd $R && py 400 python -u tools/loopback_soak.py --rounds 20 > $O/${T}_soak.log 2>&1
+}
+
+task_ipcmem() {
+  cd $R && CSED_IPC_MEM=finegrained py 300 python -u -m pytest tests/test_exchange_loopback_gpu.py tests/test_comm_gpu.py -v --timeout 200 --timeout-method thread > $O/${T}_tests_fine.log 2>&1 && \
+  py 200 python -u tools/exchange_trace.py --batch 8 32 --worlds 1 2 8 > $O/${T}_trace_uncached.log 2>&1 && \
+  CSED_IPC_MEM=finegrained py 200 python -u tools/exchange_trace.py --batch 8 32 --worlds 1 2 8 > $O/${T}_trace_fine.log 2>&1
+}
+
+task_epoch0() {
+  cd $R && py 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/${T}_e0_driver.json 2>$O/${T}_e0_driver.err && \
+  py 200 python bench.py --gpus 1 --steps 20 --warmup 5 --epoch0-stamps > $O/${T}_e0_stamps.json 2>$O/${T}_e0_stamps.err && \
+  py 200 python bench.py --gpus 1 --steps 20 --warmup 5 --dtype fp32 --epoch0-stamps > $O/${T}_e0_fp32.json 2>$O/${T}_e0_fp32.err && \
+  CSED_PRELOAD=1 py 200 python bench.py --gpus 1 --steps 20 --warmup 5 --epoch0-stamps > $O/${T}_e0_preload.json 2>$O/${T}_e0_preload.err && \
+  py 120 python tools/firstlaunch_probe.py > $O/${T}_e0_probe.json 2>$O/${T}_e0_probe.err && \
+  py 120 python tools/firstlaunch_probe.py --preload > $O/${T}_e0_probe_pre.json 2>$O/${T}_e0_probe_pre.err && \
+  py 200 python bench.py --gpus 1 --steps 20 --warmup 5 --epoch0-stamps > $O/${T}_e0_stamps2.json 2>$O/${T}_e0_stamps2.err
+}
+
+task_quick() {  # the test files this round's changes touch
+  cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_modular_graph_gpu.py tests/test_fused_gpu.py tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > $O/${T}_quick.log 2>&1
 }
 
 for task in ${TASKS//,/ }; do
