@@ -184,23 +184,23 @@ class FusedLeNetTrainer:
                 host = self.flat.data.cpu()
                 dist.broadcast(host, src=0)
                 self.flat.data.copy_(host)
-        self.momentum_buf = torch.zeros_like(self.flat.data)
+        self.momentum_buf = _native.zeros(self.flat.data.shape, torch.float32, self.flat.data.device)
         wimg_elems, conv_params, vec_len, stage_max = layout()
         # zero-initialised: padding rows / columns of the images must stay zero
-        self.wimg = torch.zeros(wimg_elems, dtype=torch.int16, device=dev)
+        self.wimg = _native.zeros(wimg_elems, torch.int16, dev)
         # per-WG conv partial gradients and per-sample fc vectors (see lenet_fused.hip)
         self.slab = torch.empty((self._max_grid(), conv_params), dtype=torch.float32, device=dev)
         # (fp32 [B, 464] for the exact-fp32 kernel; the 16-bit kernels keep raw 16-bit values
         # feature-major, [464, round_up(B, 64)], in the same bytes: fc_vectors() decodes either)
-        self.vslab = torch.zeros(((self.B + 63) // 64 * 64, vec_len), dtype=torch.float32, device=dev)
-        self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
-        self.loss_acc = torch.zeros(2, dtype=torch.float32, device=dev)  # running (loss sum, correct)
-        self.step_count = torch.zeros(1, dtype=torch.long, device=dev)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.cursor = torch.zeros(1, dtype=torch.long, device=dev)
-        self.rng_offset = torch.zeros(1, dtype=torch.long, device=dev)
-        self.eval_parts = torch.zeros(2 * 256, dtype=torch.float32, device=dev)
-        self.perm = torch.arange(self.B, dtype=torch.long, device=dev)
+        self.vslab = _native.zeros(((self.B + 63) // 64 * 64, vec_len), torch.float32, dev)
+        self.loss_parts = _native.zeros(2 * self._max_grid(), torch.float32, dev)
+        self.loss_acc = _native.zeros(2, torch.float32, dev)  # running (loss sum, correct)
+        self.step_count = _native.zeros(1, torch.long, dev)
+        self.ticket = _native.zeros(1, torch.int32, dev)
+        self.cursor = _native.zeros(1, torch.long, dev)
+        self.rng_offset = _native.zeros(1, torch.long, dev)
+        self.eval_parts = _native.zeros(2 * 256, torch.float32, dev)
+        self.perm = _native.arange(self.B, dev)
         # batch staging (per-rank batch <= stage_max): lenet_update gathers the next step's
         # pixels + labels one step ahead, so lenet_train starts with no dependent index chain
         # (the exact-fp32 kernel, lenet_fused_f32.hip, gathers its samples itself)
@@ -209,7 +209,7 @@ class FusedLeNetTrainer:
         # without the fused exchange form the fc weight gradients as up to 8 batch slices per
         # tile on all CUs, the tile's last slice finishing it (8 x 88 tiles x 256 partial sums,
         # then 88 arrival counters that must start at zero)
-        self.fc_part = torch.zeros(8 * 88 * 256 + 128, dtype=torch.float32, device=dev) if self.B > 1024 else None
+        self.fc_part = _native.zeros(8 * 88 * 256 + 128, torch.float32, dev) if self.B > 1024 else None
         # split step (lenet_fused.hip / lenet_fused_f32.hip KS > 1): split_k workgroups per sample
         # share the backward conv stages; used whenever the whole grid fits one wave of the GPU
         # (split_k * B <= 256 CUs).  CSED_SPLIT=0 keeps one workgroup per sample.  The exact-fp32
@@ -223,15 +223,15 @@ class FusedLeNetTrainer:
         if self.split:
             self.grid = split_k * self.B
             self.slab = torch.empty((self._max_grid(), conv_params), dtype=torch.float32, device=dev)
-            self.loss_parts = torch.zeros(2 * self._max_grid(), dtype=torch.float32, device=dev)
+            self.loss_parts = _native.zeros(2 * self._max_grid(), torch.float32, dev)
         # one staging row per workgroup (split step: row r holds sample r % B)
         # the sample-tile kernel (16-bit, per-rank batch >= tile_min_batch()) stages the first tile
         # of every workgroup instead: grid * tile_samples() rows (csrc/kernels/lenet_tile.hip)
         self.tile_staged = (not self.fp32 and not self.staged and self.B >= tile_min_batch()
                             and self.grid == tile_grid(self.B))
         srows = self.grid if self.staged else (self.grid * tile_samples() if self.tile_staged else 0)
-        self.xstage = torch.zeros((srows, 784), dtype=torch.uint8, device=dev) if srows else None
-        self.lstage = torch.zeros(srows, dtype=torch.long, device=dev) if srows else None
+        self.xstage = _native.zeros((srows, 784), torch.uint8, dev) if srows else None
+        self.lstage = _native.zeros(srows, torch.long, dev) if srows else None
         t_mark = time.perf_counter()
         self.repack()  # (the extension's first kernel launch: its code object loads here)
         self.bringup_s["first_kernel"] = time.perf_counter() - t_mark
@@ -526,7 +526,7 @@ class FusedLeNetTrainer:
             self._order_host = host  # alive until the copy below has run
             if host.numel() == self.perm.numel():  # straight into the captured buffer: one copy
                 self.perm.copy_(host, non_blocking=True)
-                self.cursor.zero_()
+                _native.zero_(self.cursor)
                 self._stage_current()
                 return
             order = torch.empty(host.shape, dtype=torch.long, device=self.device)
@@ -539,7 +539,7 @@ class FusedLeNetTrainer:
             self.perm.copy_(order)
         else:
             self.perm = order
-        self.cursor.zero_()
+        _native.zero_(self.cursor)
         self._stage_current()
 
     def _stage_current(self) -> None:
@@ -657,7 +657,7 @@ class FusedLeNetTrainer:
         gb = rem * self.world * max(1, self.loopback_world)  # (the sampler pads to a multiple: same on every rank)
         self._launch_step(rem, min(rem, self.grid), 1.0 / gb, None, tail)
         # the tail step does not use the cursor; keep it consistent for the next epoch
-        self.cursor.add_(1)
+        torch.ops.csed.lenet_add_(self.cursor, 1)
 
     def last_partial_step(self, use_graph: bool = True) -> None:
         """The epoch's final short batch (ref DataLoader drop_last=False semantics); replayed
@@ -861,7 +861,7 @@ class FusedLeNetTrainer:
         hit = self._eval_cache.get(id(data))
         if hit is None or hit[0] is not data:
             dev = data if data.images.device == self.device else data.to(self.device)
-            hit = (data, dev, torch.arange(len(data), device=self.device))
+            hit = (data, dev, _native.arange(len(data), self.device))
             self._eval_cache = {id(data): hit}
         return hit[1], hit[2]
 

@@ -65,3 +65,37 @@ def require() -> None:
 def ops():
     require()
     return torch.ops.csed
+
+
+def zeros(shape, dtype: torch.dtype = torch.float32, device=None) -> torch.Tensor:
+    """torch.zeros on a GPU through the extension's own zero-fill kernel (lenet_fused.hip): torch's
+    fill kernel sits in a large code object the HIP runtime loads at its first launch (5-60 ms on a
+    fresh box, profiles/r6/epoch0.md), which the fused engine's bring-up should not pay."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if t.device.type == "cuda":
+        if t.numel():
+            ops().lenet_zero_(t)
+    else:
+        t.zero_()
+    return t
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """In-place zero of a contiguous tensor (see ``zeros``)."""
+    if t.device.type == "cuda" and t.is_contiguous():
+        if t.numel():
+            ops().lenet_zero_(t)
+    else:
+        t.zero_()
+    return t
+
+
+def arange(n: int, device=None) -> torch.Tensor:
+    """int64 0..n-1 (torch.arange's int64 case; see ``zeros``)."""
+    t = torch.empty(int(n), dtype=torch.long, device=device)
+    if t.device.type == "cuda":
+        if t.numel():
+            ops().lenet_iota_(t)
+    else:
+        torch.arange(int(n), out=t)
+    return t

@@ -33,8 +33,10 @@ class FlatParams:
         self.numel = off
         # pad the allocation to a multiple of 4 floats (16-B vector kernels)
         alloc = (off + 3) // 4 * 4
-        self.data = torch.zeros(alloc, device=dev, dtype=torch.float32)
-        self.grad = torch.zeros(alloc, device=dev, dtype=torch.float32)
+        from ..ops import _native  # (GPU: the extension's zero fill, not torch's -- see _native.zeros)
+
+        self.data = _native.zeros(alloc, torch.float32, dev)
+        self.grad = _native.zeros(alloc, torch.float32, dev)
         with torch.no_grad():
             for p, o, n in zip(self.params, self.offsets, self.numels):
                 self.data[o:o + n].copy_(p.detach().reshape(-1))

@@ -626,6 +626,28 @@ double preload_kernels(int64_t device, int64_t mask) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// zero / iota / scalar add on contiguous device tensors with the fused engine's own kernels
+void lenet_zero_(Tensor& t) {
+  dev(t, "t");
+  TORCH_CHECK(t.is_contiguous(), "lenet_zero_: contiguous tensor");
+  const c10::DeviceGuard gd(t.device());
+  CHECK_HIP(csed::launch_lenet_zero(t.data_ptr(), (int64_t)t.numel() * t.element_size(), cur_stream(t)));
+}
+
+void lenet_iota_(Tensor& t) {
+  dev(t, "t");
+  TORCH_CHECK(t.is_contiguous() && t.scalar_type() == at::kLong, "lenet_iota_: contiguous int64 tensor");
+  const c10::DeviceGuard gd(t.device());
+  CHECK_HIP(csed::launch_lenet_iota(t.data_ptr<int64_t>(), t.numel(), cur_stream(t)));
+}
+
+void lenet_add_(Tensor& t, int64_t v) {
+  dev(t, "t");
+  TORCH_CHECK(t.is_contiguous() && t.scalar_type() == at::kLong, "lenet_add_: contiguous int64 tensor");
+  const c10::DeviceGuard gd(t.device());
+  CHECK_HIP(csed::launch_lenet_add_i64(t.data_ptr<int64_t>(), t.numel(), v, cur_stream(t)));
+}
+
 void lenet_pack(const Tensor& params, Tensor& wimg, int64_t mfma_dtype) {
   dev(params, "params"); dev(wimg, "wimg");
   TORCH_CHECK(params.scalar_type() == at::kFloat && params.numel() >= csed::lenet_param_count());
@@ -884,6 +906,9 @@ TORCH_LIBRARY(csed, m) {
       .def("run", &LenetStepper::run);
   m.def("lenet_layout() -> int[]", &lenet_layout);
   m.def("preload_kernels(int device, int mask=127) -> float", &preload_kernels);
+  m.def("lenet_zero_(Tensor(a!) t) -> ()", &lenet_zero_);
+  m.def("lenet_iota_(Tensor(a!) t) -> ()", &lenet_iota_);
+  m.def("lenet_add_(Tensor(a!) t, int v) -> ()", &lenet_add_);
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
         "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "

@@ -2508,6 +2508,51 @@ hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const
   return hipGetLastError();
 }
 
+// Small device-state helpers of the fused engine (zero fill, int64 iota, scalar add) in this
+// translation unit, whose code object the step loads anyway: torch's own fill / arange / add
+// kernels live in large code objects that the HIP runtime loads at their first launch -- 5-60 ms
+// each on a fresh box, inside the reference span (profiles/r6/epoch0.md).
+__global__ void lenet_zero_kernel(unsigned char* __restrict__ p, int64_t nbytes) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    const int64_t n16 = nbytes >> 4;
+    for (int64_t i = i0; i < n16; i += stride) reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
+    for (int64_t i = (n16 << 4) + i0; i < nbytes; i += stride) p[i] = 0;
+  } else {
+    for (int64_t i = i0; i < nbytes; i += stride) p[i] = 0;
+  }
+}
+
+__global__ void lenet_iota_kernel(int64_t* __restrict__ p, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = i;
+}
+
+__global__ void lenet_add_i64_kernel(int64_t* __restrict__ p, int64_t n, int64_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] += v;
+}
+
+hipError_t launch_lenet_zero(void* p, int64_t nbytes, hipStream_t s) {
+  if (nbytes <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>(1024, (nbytes / 16 + 255) / 256 + 1);
+  hipLaunchKernelGGL(lenet_zero_kernel, dim3(blocks), dim3(256), 0, s, (unsigned char*)p, nbytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_lenet_iota(int64_t* p, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lenet_iota_kernel, dim3((int)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, s, p, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_lenet_add_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lenet_add_i64_kernel, dim3((int)((n + 255) / 256)), dim3(256), 0, s, p, n, v);
+  return hipGetLastError();
+}
+
 // Load this translation unit's code object on the current device now (the HIP runtime loads it
 // lazily, at the TU's first launch): csed::preload_kernels, so a cold epoch does not pay it.
 hipError_t preload_lenet_fused() {

@@ -289,6 +289,10 @@ int64_t lenet_exch_words();
 hipError_t launch_lenet_update(const LenetUpdateArgs& a, float* loss_parts, int nparts, float* loss_acc,
                                hipStream_t s, const comm::IpcPeers* px = nullptr);
 hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype, hipStream_t s);
+// device-state helpers in lenet_fused.hip's code object (no torch kernel launches in the bring-up)
+hipError_t launch_lenet_zero(void* p, int64_t nbytes, hipStream_t s);
+hipError_t launch_lenet_iota(int64_t* p, int64_t n, hipStream_t s);
+hipError_t launch_lenet_add_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 // Forward-only evaluation: out_parts [min(n,256), 2] per-workgroup (loss sum, correct).
 hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,
                              int64_t n, const uint16_t* wimg, const float* params, float mean,

@@ -32,6 +32,7 @@
 #             (was gpu_r5j.sh), and the loopback world-8 soak
 #   ipcmem    the exchange receive buffer's allocation: uncached (default) vs CSED_IPC_MEM=finegrained
 #             (was gpu_ipcmem.sh)
+#   bringtrace rocprofv3 HIP-API + kernel + memory-copy trace of the bench bring-up, summarised
 #   epoch0    the reference span on a fresh process, stamped: bench.py --epoch0-stamps at N = 1 (bf16,
 #             fp32) + the driver's own command
 TASKS=${1:?task list}
@@ -197,6 +198,12 @@ task_epoch0() {
   py 120 python tools/firstlaunch_probe.py > $O/${T}_e0_probe.json 2>$O/${T}_e0_probe.err && \
   py 120 python tools/firstlaunch_probe.py --preload > $O/${T}_e0_probe_pre.json 2>$O/${T}_e0_probe_pre.err && \
   py 200 python bench.py --gpus 1 --steps 20 --warmup 5 --epoch0-stamps > $O/${T}_e0_stamps2.json 2>$O/${T}_e0_stamps2.err
+}
+
+task_bringtrace() {  # HIP-API + kernel + copy trace of the bench's bring-up (tools/bringup_trace.py)
+  cd /tmp && export TMPDIR=/tmp && \
+  py 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d $O/${T}_bt -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-fp32-record --no-epoch > $O/${T}_bt.log 2>&1 && \
+  cd $R && python3 tools/bringup_trace.py $O/${T}_bt --min-ms 0.3 > $O/${T}_bt_summary.txt 2>&1
 }
 
 task_quick() {  # the test files this round's changes touch
