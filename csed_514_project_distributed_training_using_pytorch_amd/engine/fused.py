@@ -79,18 +79,39 @@ def _clear_hip_error() -> None:
         lib.hipGetLastError()
 
 
-def _graph_upload(g: torch.cuda.CUDAGraph, stream: torch.cuda.Stream) -> bool:
-    """hipGraphUpload of an instantiated graph on ``stream``: the executable graph's launch
-    resources (kernel-argument blocks, AQL packet templates) are put on the device now, enqueued
-    behind whatever the stream runs, instead of on the graph's first replay."""
+class NativeGraph:
+    """A step graph captured with ``torch.classes.csed.HipGraph`` (csrc/bindings.cpp), replayed by
+    one ctypes ``hipGraphLaunch`` on the current stream (the ScriptObject keeps the graph alive)."""
+
+    _launch = None
+
+    def __init__(self, obj, device: torch.device):
+        import ctypes
+
+        self.obj = obj
+        self.device_index = device.index
+        self.exec = ctypes.c_void_p(obj.exec_handle())
+        if NativeGraph._launch is None:
+            fn = _hip_libs()[0].hipGraphLaunch
+            fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int
+            NativeGraph._launch = fn
+
+    def replay(self) -> None:
+        e = NativeGraph._launch(self.exec, torch._C._cuda_getCurrentRawStream(self.device_index))
+        if e != 0:
+            raise RuntimeError(f"hipGraphLaunch failed ({e})")
+
+    def num_nodes(self) -> int:
+        return int(self.obj.num_nodes())
+
+
+def _hip_graph_upload(exec_handle: int, stream: int) -> bool:
+    """hipGraphUpload of an instantiated graph on a stream (CSED_GRAPH_UPLOAD=1)."""
     import ctypes
 
-    libs = _hip_libs()
-    if not libs:
-        return False
-    fn = libs[0].hipGraphUpload
+    fn = _hip_libs()[0].hipGraphUpload
     fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int
-    return fn(ctypes.c_void_p(g.raw_cuda_graph_exec()), ctypes.c_void_p(stream.cuda_stream)) == 0
+    return fn(ctypes.c_void_p(exec_handle), ctypes.c_void_p(stream)) == 0
 
 
 def layout() -> tuple[int, int, int, int]:
@@ -235,7 +256,7 @@ class FusedLeNetTrainer:
         t_mark = time.perf_counter()
         self.repack()  # (the extension's first kernel launch: its code object loads here)
         self.bringup_s["first_kernel"] = time.perf_counter() - t_mark
-        self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._graphs: dict[tuple, object] = {}  # torch.cuda.CUDAGraph (or NativeGraph)
         self._warmed: set[str] = set()  # step kinds whose capture warm-up has run (see _capture)
         self._cap_stream: torch.cuda.Stream | None = None
         self._stepper: tuple | None = None  # (key, csed.LenetStepper), see stepper()
@@ -679,19 +700,25 @@ class FusedLeNetTrainer:
     def _stamp(self, key: str, dt: float) -> None:
         self.bringup_s[key] = self.bringup_s.get(key, 0.0) + dt
 
-    def _capture(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph:
+    def _capture(self, nsteps: int, tail: bool = False):
         """Capture ``nsteps`` full steps (or the epoch's tail step) into a HIP graph.
 
         The first capture of each step kind (full / tail x all-reduce path x kernel) runs one eager warm-up step on the
         capture stream first (lazy RCCL communicator set-up, each kernel's first-launch symbol
         lookup -- neither may happen inside a capture), the engine state snapshotted before and
-        restored after it; later captures of the same kind skip it.  The capture itself calls
+        restored after it; later captures of the same kind skip it.  The capture calls
         capture_begin / capture_end directly: ``torch.cuda.graph``'s device synchronize and
-        ``empty_cache`` are not needed here (the steps allocate nothing), and the graph is
-        instantiated explicitly, then uploaded to the device on the current stream
-        when ``CSED_GRAPH_UPLOAD=1`` (off by default: measured, a first replay costs the same either way,
-        profiles/r6/epoch0.md).  Host
-        seconds accumulate in ``bringup_s``: capture.warmup / .record / .instantiate / .upload."""
+        ``empty_cache`` are not needed (the steps allocate nothing).
+
+        ``CSED_NATIVE_GRAPH=1`` captures a native HIP graph instead (``torch.classes.csed.HipGraph``,
+        replayed by a ctypes hipGraphLaunch): it skips torch's capture_begin generator set-up (a
+        torch fill kernel, ~5 ms of first-launch code-object load in the reference span), but
+        measured on one box its replays start later -- 14.9-15.7 vs 14.1-14.5 us per step in the
+        driver's 20-step window, 13.34 vs 13.26 us at 3000 steps (profiles/r6/graph_ab.log) -- so
+        torch's graphs stay the default.  ``CSED_GRAPH_UPLOAD=1`` uploads each graph after its
+        instantiation (no measured effect on the first replay).  Host seconds accumulate in
+        ``bringup_s``: capture.stream / .warmup(.snapshot/.step/.sync/.restore) / .record /
+        .instantiate / .upload."""
         import time
 
         step = self._tail_step if tail else self.step
@@ -730,25 +757,40 @@ class FusedLeNetTrainer:
         # that contains an RCCL all-reduce is captured; in the default (global) mode that query
         # invalidates the capture and the watchdog then aborts the process (seen on the GPU box,
         # profiles/round5.md)
-        g = torch.cuda.CUDAGraph(keep_graph=True)
-        with torch.cuda.stream(s):
-            g.capture_begin(capture_error_mode="thread_local")
-            try:
-                for _ in range(nsteps):
-                    step()
-            finally:
-                g.capture_end()
-        t2 = time.perf_counter()
-        g.instantiate()
-        t3 = time.perf_counter()
-        if os.environ.get("CSED_GRAPH_UPLOAD", "0") == "1":
-            _graph_upload(g, cur)
+        if os.environ.get("CSED_NATIVE_GRAPH") == "1":
+            ng = torch.classes.csed.HipGraph()  # (csrc/bindings.cpp)
+            with torch.cuda.stream(s):
+                ng.begin(self.device.index)
+                try:
+                    for _ in range(nsteps):
+                        step()
+                finally:
+                    ng.end()  # (ends the capture even after a failed step; raises if it was invalidated)
+            t2 = t3 = time.perf_counter()  # (end() instantiated it)
+            if os.environ.get("CSED_GRAPH_UPLOAD", "0") == "1":
+                with torch.cuda.stream(cur):
+                    ng.upload()
+            g = NativeGraph(ng, self.device)
+        else:
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            with torch.cuda.stream(s):
+                g.capture_begin(capture_error_mode="thread_local")
+                try:
+                    for _ in range(nsteps):
+                        step()
+                finally:
+                    g.capture_end()
+            t2 = time.perf_counter()
+            g.instantiate()
+            t3 = time.perf_counter()
+            if os.environ.get("CSED_GRAPH_UPLOAD", "0") == "1":
+                _hip_graph_upload(g.raw_cuda_graph_exec(), cur.cuda_stream)
         t4 = time.perf_counter()
         for k, dt in (("warmup", t1 - t0), ("record", t2 - t1), ("instantiate", t3 - t2), ("upload", t4 - t3)):
             self._stamp(f"capture.{k}", dt)
         return g
 
-    def graph(self, nsteps: int, tail: bool = False) -> torch.cuda.CUDAGraph | None:
+    def graph(self, nsteps: int, tail: bool = False):
         """The captured graph of ``nsteps`` full steps (or of the epoch's tail step), cached."""
         key = (nsteps, self.perm.data_ptr(), self.perm.numel(), self.B, tail)
         if key in self._graphs:

@@ -6,6 +6,7 @@
 // host or synchronises, so every op is safe inside torch.cuda.graph capture
 // (= hipStreamBeginCapture).
 #include <chrono>
+#include <cstdlib>
 #include <vector>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -845,6 +846,84 @@ void lenet_eval(const Tensor& images, const Tensor& labels, const Tensor& order,
 // checked once, then `run(k)` enqueues the 2k launches on the current stream from C++.  A
 // short run (the driver's 20-step window) pays no graph-launch setup and no Python per
 // launch; long runs use the captured graphs (engine/fused.py:step_plan picks).
+// A HIP graph of the work this host thread enqueues on the current stream of `device` between
+// begin() and end() (hipStreamBeginCapture in thread-local mode: another thread's unsafe call -- a
+// process group watchdog's event query -- does not invalidate it), instantiated at end(), replayed
+// on the then-current stream.  The fused engine's step graphs use it instead of torch.cuda.CUDAGraph,
+// whose capture_begin registers the default Philox generator and initialises its seed / offset
+// tensors with torch's fill kernel: a code object loaded at its first launch (5-20 ms) inside the
+// reference span (profiles/r6/epoch0.md).  The steps allocate nothing, so no capture memory pool.
+struct HipGraph : torch::CustomClassHolder {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipStream_t cap = nullptr;
+  int device = -1;
+  bool capturing = false;
+
+  void begin(int64_t dev) {
+    TORCH_CHECK(!capturing && !exec, "HipGraph: already captured");
+    device = (int)dev;
+    const c10::DeviceGuard gd(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev));
+    cap = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+    TORCH_CHECK(cap != nullptr, "HipGraph: capture needs a side stream (the null stream cannot be captured)");
+    CHECK_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    capturing = true;
+  }
+
+  void end() {
+    TORCH_CHECK(capturing, "HipGraph: end() without begin()");
+    capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(cap, &g);
+    if (e != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      TORCH_CHECK(false, "HipGraph: capture failed: ", hipGetErrorString(e));
+    }
+    graph = g;
+    // CSED_GRAPH_FLAGS: 1 = hipGraphInstantiateFlagAutoFreeOnLaunch (torch.cuda.CUDAGraph's flags), else none
+    static const int flags = [] {
+      const char* e = std::getenv("CSED_GRAPH_FLAGS");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (flags == 1) {
+      CHECK_HIP(hipGraphInstantiateWithFlags(&exec, graph, hipGraphInstantiateFlagAutoFreeOnLaunch));
+    } else {
+      CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    }
+  }
+
+  void upload() {
+    TORCH_CHECK(exec, "HipGraph: not captured");
+    CHECK_HIP(hipGraphUpload(exec, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream()));
+  }
+
+  void replay() {
+    TORCH_CHECK(exec, "HipGraph: not captured");
+    CHECK_HIP(hipGraphLaunch(exec, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream()));
+  }
+
+  // the executable graph as an integer (hipGraphExec_t): the engine replays it with one ctypes
+  // hipGraphLaunch -- a custom-class method call is a boxed dispatch, ~1 us per step of a 20-step graph
+  int64_t exec_handle() { return reinterpret_cast<int64_t>(exec); }
+
+  int64_t num_nodes() {
+    size_t n = 0;
+    if (graph) CHECK_HIP(hipGraphGetNodes(graph, nullptr, &n));
+    return (int64_t)n;
+  }
+
+  ~HipGraph() override {
+    if (capturing) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(cap, &g);
+      if (g) (void)hipGraphDestroy(g);
+    }
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+  }
+};
+
 struct LenetStepper : torch::CustomClassHolder {
   csed::LenetTrainArgs ta{};
   csed::LenetUpdateArgs ua{};
@@ -899,6 +978,14 @@ struct LenetStepper : torch::CustomClassHolder {
 }  // namespace
 
 TORCH_LIBRARY(csed, m) {
+  m.class_<HipGraph>("HipGraph")
+      .def(torch::init<>())
+      .def("begin", &HipGraph::begin)
+      .def("end", &HipGraph::end)
+      .def("upload", &HipGraph::upload)
+      .def("replay", &HipGraph::replay)
+      .def("exec_handle", &HipGraph::exec_handle)
+      .def("num_nodes", &HipGraph::num_nodes);
   m.class_<LenetStepper>("LenetStepper")
       .def(torch::init<>())
       .def("set_train", &LenetStepper::set_train)

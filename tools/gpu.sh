@@ -206,6 +206,16 @@ task_bringtrace() {  # HIP-API + kernel + copy trace of the bench's bring-up (to
   cd $R && python3 tools/bringup_trace.py $O/${T}_bt --min-ms 0.3 > $O/${T}_bt_summary.txt 2>&1
 }
 
+task_graphab() {  # native HipGraph vs torch.cuda.CUDAGraph step graphs, alternating (driver command + long window;
+                 # GRAPH_AB: native nativeflags nativeupload torch)
+  cd $R && rm -f $O/${T}_graphab.log && \
+  for i in 1 2 3; do for v in ${GRAPH_AB:-native torch}; do
+    case $v in native) E=CSED_NATIVE_GRAPH=1;; nativeflags) E="CSED_NATIVE_GRAPH=1 CSED_GRAPH_FLAGS=1";; nativeupload) E="CSED_NATIVE_GRAPH=1 CSED_GRAPH_UPLOAD=1";; *) E=CSED_NATIVE_GRAPH=0;; esac
+    echo "$v driver $(env $E timeout -k 10 100 python bench.py --gpus 1 --steps 20 --warmup 5 --no-fp32-record 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["ms_per_step"], d["time_elapsed_s"], d["epoch_s"])')" >> $O/${T}_graphab.log || return 1
+    echo "$v long $(env $E timeout -k 10 100 python bench.py --steps 3000 --warmup 300 --no-epoch --no-fp32-record 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["ms_per_step"])')" >> $O/${T}_graphab.log || return 1
+  done; done
+}
+
 task_quick() {  # the test files this round's changes touch
   cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_modular_graph_gpu.py tests/test_fused_gpu.py tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > $O/${T}_quick.log 2>&1
 }
