@@ -387,6 +387,10 @@ def main(argv=None) -> int:
             None, None, 0, None
         process_elapsed, replicas, fp32_rec = r["process_elapsed_s"], r["replicas"], None
         data_src = e0_rec = ew_rec = None
+        from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc_cpu
+
+        xdiag = _ipc_cpu.gather_diag(ctx, dict(_ipc_cpu.empty_diag(ctx), allreduce=r["allreduce"],
+                                               note="CPU plumbing run: no exchange")) if n > 1 else None
     else:
         from csed_514_project_distributed_training_using_pytorch_amd.engine.fused import FusedLeNetTrainer
         from csed_514_project_distributed_training_using_pytorch_amd.models import Net
@@ -543,6 +547,7 @@ def main(argv=None) -> int:
                         p_el=p_el,
                         epoch_s=epoch_s, val=val, err=err, replicas=same_p and same_m,
                         e0=st0.summary(args.epoch0_stamps), ew=stw.summary(args.epoch0_stamps) if stw else None,
+                        xdiag=eng.exchange_diag(),
                         diag=eng.comm_diag() if err else None)
 
         from csed_514_project_distributed_training_using_pytorch_amd.parallel import ipc as _ipc
@@ -558,6 +563,7 @@ def main(argv=None) -> int:
             # number is a valid training run
             comm_retry = r["eng"].allreduce_kind
             first_fault = {"error_word": r["err"], "replicas_identical": r["replicas"], "first_mismatch": r["diag"]}
+            first_fault_diag = _ipc.gather_diag(ctx, r["xdiag"])
             r["eng"].close()
             del r
             import gc
@@ -570,6 +576,11 @@ def main(argv=None) -> int:
             phases.update({f"retry.{k}": v for k, v in retry_phases.items()})
         eng = r["eng"]
         e0_rec, ew_rec = r["e0"], r["ew"]
+        # every rank's exchange diagnostics (collective): peer access, IPC open, self-test, path
+        # timing, error word, first mismatch -- names the failing stage of an N-GPU bring-up
+        xdiag = _ipc.gather_diag(ctx, r["xdiag"]) if n > 1 else None
+        if first_fault is not None:
+            first_fault["exchange_diag_first_run"] = first_fault_diag
         elapsed, time_elapsed, epoch0_s, epoch_s, val = r["elapsed"], r["t_el"], r["epoch0"], r["epoch_s"], r["val"]
         process_elapsed = r["p_el"]
         comm_err, replicas = r["err"], r["replicas"]
@@ -674,6 +685,8 @@ def main(argv=None) -> int:
             # between HIP events, host ms between enqueues): where a cold epoch loses time
             "epoch0_breakdown": e0_rec,
             "epoch_breakdown": ew_rec,
+            # N > 1: per-rank data-parallel diagnostics (parallel/ipc.py DIAG_KEYS), in rank order
+            "exchange_diag": xdiag,
         }
         if comm_retry:
             rec["config"]["comm_retry"] = f"{comm_retry} path timed out; re-measured on the process-group all-reduce"

@@ -46,6 +46,7 @@ from ..models.net import N_PARAMS, Net
 from ..ops import _native
 from ..parallel import comm
 from ..parallel.comm import DistContext
+from ..parallel import ipc as _ipc
 from ..parallel.ipc import allreduce_mode, open_exchange, open_loopback_exchange, wait_timeout_s
 from ..utils.flat import FlatParams
 
@@ -274,11 +275,18 @@ class FusedLeNetTrainer:
         self.exchange_note: str | None = None  # why the data-parallel step runs as it does (reports)
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
+        self._xdiag: dict = {}  # stage results of the exchange bring-up (exchange_diag)
         self.loopback_world = 0  # (set below; the exchange bring-up's reports read it)
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"
+        if multi:
+            from ..parallel.ipc import ranks_per_gpu
+
+            self._xdiag["ranks_per_gpu"] = ranks_per_gpu(self.ctx)  # (collective: every rank)
         if multi and mode in ("auto", "fused"):
             self._enable_exchange(required=(mode == "fused"))
+        elif multi:
+            self._xdiag["ipc_open"] = f"not tried (CSED_ALLREDUCE={mode})"
         # Loopback exchange (one GPU, no process group): lenet_update runs its full push + poll
         # code for loopback_world - 1 virtual peers that are slots of this rank's own buffer
         # (csrc/comm ipc_open_loopback).  Each peer returns this rank's own gradient, and the
@@ -353,15 +361,30 @@ class FusedLeNetTrainer:
         import time
 
         t0 = time.perf_counter()
-        ex, why = open_exchange(self.ctx, exch_words())
+        xd = self._xdiag
+        xd["peer_access"] = _ipc.peer_access(self.device)
+        ex, why = open_exchange(self.ctx, exch_words(), shared=self._xdiag.get("ranks_per_gpu"))
+        hook = _ipc.test_reject_hook()
+        last = self.ctx.rank == self.ctx.world_size - 1
+        if hook == "open":  # (test hook: the last rank's mapping "fails"; every rank votes)
+            ok_local = not last
+            if not self._vote(ok_local) and ex is not None:
+                ex.close()
+                ex, why = None, "open: test hook CSED_TEST_EXCH_REJECT=open on the last rank"
+        xd["ipc_open"] = "ok" if ex is not None else (why or "failed")
         t1 = time.perf_counter()
         self.bringup_s["ipc_open"] = t1 - t0
         ok = ex is not None
         if ok:
             self.exch = ex
-            ok = self._vote(self._exchange_self_test())
+            local_ok = self._exchange_self_test()
+            if hook == "selftest" and last:
+                local_ok = False
+            xd["self_test"] = bool(local_ok)
+            ok = self._vote(local_ok)
             if not ok:
                 why = "self-test mismatch or timeout on some rank"
+                xd["self_test_all_ranks"] = False
         self.bringup_s["self_test"] = time.perf_counter() - t1
         if not ok:
             if ex is not None:
@@ -377,10 +400,8 @@ class FusedLeNetTrainer:
         self.exchange_note = "fused exchange on (self-test passed)"
         tp = os.environ.get("CSED_TIME_PATHS", "auto").strip().lower()
         if not required and self.ctx.backend == "nccl" and tp != "0":
-            from ..parallel.ipc import ranks_per_gpu
-
-            # (collective: every rank takes the same branch)
-            do_time = tp == "1" or ranks_per_gpu(self.ctx) == 1
+            # (every rank takes the same branch: ranks_per_gpu is the group's value)
+            do_time = tp == "1" or self._xdiag.get("ranks_per_gpu") == 1
         else:
             do_time = False
         if do_time:
@@ -409,6 +430,20 @@ class FusedLeNetTrainer:
                                    else None,
                                    "fallback": "rccl", "kept": "fused" if self.exch is not None else "rccl"}
             self.bringup_s["path_timing"] = time.perf_counter() - t2
+
+    def exchange_diag(self) -> dict:
+        """This rank's data-parallel diagnostics (``parallel/ipc.py`` DIAG_KEYS): the bring-up's
+        stage results plus the exchange's current error word and first recorded mismatch."""
+        d = _ipc.empty_diag(self.ctx)
+        d.update(self._xdiag)
+        d["device_count"] = torch.cuda.device_count()
+        d["path_timing_us"] = self.path_timing_us
+        d["allreduce"] = self.allreduce_kind
+        d["note"] = self.exchange_note
+        if self.exch is not None:
+            d["error_word"] = self.comm_errors()
+            d["first_mismatch"] = self.comm_diag()
+        return d
 
     def _vote(self, ok: bool) -> bool:
         dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")

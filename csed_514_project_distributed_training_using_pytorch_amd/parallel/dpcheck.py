@@ -17,7 +17,9 @@ On GPUs (RCCL process group, one rank per GPU) every rank:
    order-free), to fp32 summation-order tolerance above that (RCCL's ring does not sum
    in rank order).
 
-Rank 0 prints one ``DPCHECK {json}`` line; the exit code is nonzero if a check failed.
+Rank 0 prints one ``DPCHECK {json}`` line (with every rank's ``exchange_diag``: peer access, IPC
+open, self-test, path timing, error word, first mismatch -- parallel/ipc.py DIAG_KEYS); the exit
+code is nonzero if a check failed.
 ``--device cpu`` runs the same launch / rendezvous / replica-check plumbing on gloo with the
 modular (per-op) engine.
 """
@@ -32,6 +34,7 @@ import torch
 import torch.distributed as dist
 
 from .comm import init_distributed, replica_checksum
+from .ipc import empty_diag, gather_diag
 
 
 def _gpu_run(ctx, data, steps: int, mode: str, dtype: torch.dtype) -> dict:
@@ -53,13 +56,15 @@ def _gpu_run(ctx, data, steps: int, mode: str, dtype: torch.dtype) -> dict:
     same_m, _, _ = replica_checksum(ctx, eng.momentum_buf)
     out = {"allreduce": eng.allreduce_kind, "note": eng.exchange_note, "path_timing_us": eng.path_timing_us,
            "error_word": err, "replicas_identical": bool(same_p and same_m),
-           "finite": bool(torch.isfinite(eng.flat.data).all()), "params": eng.flat.data.clone()}
+           "finite": bool(torch.isfinite(eng.flat.data).all()), "params": eng.flat.data.clone(),
+           # every rank's stage results (parallel/ipc.py DIAG_KEYS): names a failing stage / rank
+           "exchange_diag": gather_diag(ctx, eng.exchange_diag())}
     eng.close()
     return out
 
 
 def check(args) -> tuple[bool, dict]:
-    ctx = init_distributed(device=args.device)
+    ctx = init_distributed(device=args.device, backend=None if args.backend == "auto" else args.backend)
     world = ctx.world_size
     rec: dict = {"world": world, "device": args.device, "backend": ctx.backend, "steps": args.steps}
     ok = True
@@ -81,6 +86,7 @@ def check(args) -> tuple[bool, dict]:
         rec.update(fused=fused, rccl=rccl, fused_vs_rccl_rel=rel, fused_equals_rccl_bitwise=bitwise)
         ok &= fused["error_word"] == 0 and fused["replicas_identical"] and fused["finite"]
         ok &= rccl["replicas_identical"] and rccl["finite"] and rccl["allreduce"] == "rccl"
+        # (ranks sharing a GPU: the GPU pairs above are empty and "gpus" counts the distinct GPUs)
         if fused["allreduce"] == "fused-ipc" and world == 2:
             ok &= bitwise
         else:
@@ -102,7 +108,9 @@ def check(args) -> tuple[bool, dict]:
             tr.train_batch(*next(it))
         flat = torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()])
         same, _, _ = replica_checksum(ctx, flat)
-        rec.update(allreduce=f"process group ({ctx.backend})", replicas_identical=bool(same))
+        rec.update(allreduce=f"process group ({ctx.backend})", replicas_identical=bool(same),
+                   exchange_diag=gather_diag(ctx, dict(empty_diag(ctx), allreduce=f"process group ({ctx.backend})",
+                                                       note="CPU plumbing run: no exchange")))
         ok &= bool(same)
     rec["ok"] = bool(ok)
     # every rank's verdict: the job passes only if all do
@@ -118,6 +126,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
+                    help="gloo: ranks may share one GPU (the rehearsal of the one-rank-per-GPU check)")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--tol", type=float, default=1e-4, help="fused vs RCCL relative tolerance (world > 2)")
     ap.add_argument("--require-fused", action="store_true", help="fail unless the fused exchange is kept")

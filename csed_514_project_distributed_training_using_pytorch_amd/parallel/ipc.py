@@ -209,6 +209,46 @@ def ranks_per_gpu(ctx: DistContext) -> int:
     return max(vals.count(v) for v in vals)
 
 
+# Per-rank exchange diagnostics (bench.py JSON ``exchange_diag``, dpcheck's DPCHECK line): enough to
+# name the failing stage of a data-parallel bring-up on a real node -- peer access of this rank's
+# GPU, the IPC buffer's create / map, the exact self-test, the fused-vs-RCCL path timing, and at the
+# end of a run the exchange's error word and first recorded mismatch.  Every rank reports every key
+# (None where a stage did not run), so a report names the stage and the rank.
+DIAG_KEYS = ("rank", "local_rank", "device", "device_count", "ranks_per_gpu", "peer_access", "ipc_open",
+             "self_test", "path_timing_us", "allreduce", "note", "error_word", "first_mismatch")
+
+
+def empty_diag(ctx: DistContext) -> dict:
+    """This rank's diagnostics record with every stage unset."""
+    d = dict.fromkeys(DIAG_KEYS)
+    d.update(rank=ctx.rank, local_rank=int(os.environ.get("LOCAL_RANK", ctx.rank)),
+             device=ctx.device.index if ctx.device.type == "cuda" else str(ctx.device))
+    return d
+
+
+def peer_access(device: torch.device) -> dict:
+    """hipDeviceCanAccessPeer from ``device`` to every other visible GPU: {"i->j": bool}."""
+    if device.type != "cuda":
+        return {}
+    i, n = device.index, torch.cuda.device_count()
+    return {f"{i}->{j}": bool(torch.cuda.can_device_access_peer(i, j)) for j in range(n) if j != i}
+
+
+def gather_diag(ctx: DistContext, local: dict) -> list[dict]:
+    """Every rank's diagnostics, in rank order (collective; the local record alone at world 1)."""
+    if not ctx.is_distributed:
+        return [local]
+    out: list = [None] * ctx.world_size
+    dist.all_gather_object(out, local)
+    return out
+
+
+def test_reject_hook() -> str:
+    """``CSED_TEST_EXCH_REJECT`` (tests): ``open`` -- the last rank reports a failed buffer mapping;
+    ``selftest`` -- its self-test fails.  The engine must fall back to the process group."""
+    return os.environ.get("CSED_TEST_EXCH_REJECT", "").strip().lower()
+
+
 def wait_timeout_s() -> float:
     """Wall-clock bound of every peer wait inside the exchange kernels (``CSED_IPC_TIMEOUT_S``,
     default 2 s): on expiry a kernel raises the comm error word and finishes instead of
@@ -249,13 +289,13 @@ def _open(ctx: DistContext, n: int, blocks: int) -> tuple[IpcAllReduce | None, s
     return (ar if ok else None), (why or ("" if ok else "a peer failed to create / map its buffer"))
 
 
-def open_exchange(ctx: DistContext, words: int) -> tuple[IpcAllReduce | None, str]:
+def open_exchange(ctx: DistContext, words: int, shared: int | None = None) -> tuple[IpcAllReduce | None, str]:
     """An opened IPC exchange buffer of ``words`` 8-byte words per sender for a kernel that
     carries its own LL exchange (lenet_update's fused gradient all-reduce).  The caller
-    self-tests it with that kernel.  Collective."""
+    self-tests it with that kernel.  Collective.  ``shared``: ranks_per_gpu(ctx) if known."""
     if not ctx.is_distributed or ctx.device.type != "cuda":
         return None, "not distributed on a GPU"
-    shared = ranks_per_gpu(ctx)
+    shared = ranks_per_gpu(ctx) if shared is None else int(shared)
     if shared > MAX_RANKS_PER_GPU:
         return None, f"{shared} ranks share one GPU (spin-waiting exchange needs <= {MAX_RANKS_PER_GPU})"
     return _open(ctx, (words + 3) // 4 * 4, blocks=1)

@@ -158,6 +158,14 @@ def test_bench_self_spawns_ranks_cpu():
     assert rec["n_gpus"] == 2 and rec["config"]["process_group"] == {"backend": "gloo", "ranks": 2}
     assert rec["config"]["parallelism"] == "dp2" and rec["steps"] == 3 and rec["value"] > 0
     assert rec["time_elapsed_s"] > 0
+    # every rank's data-parallel diagnostics, every key present (a failing N-GPU bring-up names
+    # its stage: peer access, IPC open, self-test, path timing, error word, first mismatch)
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ipc import DIAG_KEYS
+
+    diag = rec["exchange_diag"]
+    assert [d["rank"] for d in diag] == [0, 1], diag
+    for d in diag:
+        assert set(DIAG_KEYS) <= set(d), d
 
 
 def test_bench_eight_ranks_bringup_phases_cpu():

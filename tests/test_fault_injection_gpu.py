@@ -110,3 +110,32 @@ def test_dist_epoch_rerun_after_injected_fault_matches_clean_run(tmp_path):
     # and the epoch lines: two epochs per rank in each run, the faulted epoch printed once
     for r in (r_fault, r_clean):
         assert r.stdout.count("Epoch=") == 2 * 2, r.stdout  # (two ranks' lines may share a line)
+
+
+@pytest.mark.parametrize("stage", ["open", "selftest"])
+def test_bench_two_ranks_rejected_exchange_still_reports(tmp_path, stage):
+    """bench.py --gpus 2 (two gloo ranks sharing the GPU) with the fused exchange rejected on the
+    last rank (CSED_TEST_EXCH_REJECT: a failed buffer mapping / self-test): every rank falls back to
+    the process group's all-reduce, the line still carries a valid value, and exchange_diag names
+    the failing stage on the failing rank (the first-run diagnostics of a real N-GPU node)."""
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ipc import DIAG_KEYS
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CSED_TEST_EXCH_REJECT=stage, CSED_IPC_TIMEOUT_S="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "20",
+           "--warmup", "2", "--no-epoch", "--no-fp32-record"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] and rec["value"] > 0 and rec["replicas_identical"] is True, rec
+    assert rec["config"]["allreduce"] == "rccl", rec  # (the process-group path: gloo here)
+    diag = rec["exchange_diag"]
+    assert [d["rank"] for d in diag] == [0, 1] and all(set(DIAG_KEYS) <= set(d) for d in diag), diag
+    assert all(d["allreduce"] == "rccl" and d["ranks_per_gpu"] == 2 for d in diag), diag
+    if stage == "open":
+        assert all(d["ipc_open"] != "ok" and d["self_test"] is None for d in diag), diag
+    else:
+        assert all(d["ipc_open"] == "ok" for d in diag), diag
+        assert diag[0]["self_test"] is True and diag[1]["self_test"] is False, diag

@@ -60,6 +60,26 @@ def test_fused_exchange_one_rank_per_gpu():
 
 
 def test_dpcheck_plumbing_gloo_cpu():
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ipc import DIAG_KEYS
+
     rec = _run(2, ["--device", "cpu", "--steps", "3"], timeout=300)
     assert rec["_rc"] == 0 and rec["all_ranks_ok"] and rec["replicas_identical"], rec
     assert rec["backend"] == "gloo" and rec["world"] == 2
+    assert [d["rank"] for d in rec["exchange_diag"]] == [0, 1]
+    assert all(set(DIAG_KEYS) <= set(d) for d in rec["exchange_diag"]), rec["exchange_diag"]
+
+
+@pytest.mark.gpu
+def test_dpcheck_two_ranks_shared_gpu_rehearsal():
+    """The one-rank-per-GPU check's rehearsal on a one-GPU box: two gloo ranks sharing the GPU run
+    dpcheck's fused (auto) and process-group paths from the same state; the DPCHECK line carries
+    every rank's exchange diagnostics (peer access, IPC open, self-test, path timing, error word,
+    first mismatch) and both paths agree bitwise (a + b is order-free)."""
+    from csed_514_project_distributed_training_using_pytorch_amd.parallel.ipc import DIAG_KEYS
+
+    rec = _run(2, ["--backend", "gloo", "--steps", "8"], timeout=600)
+    assert rec["_rc"] == 0 and rec["all_ranks_ok"], rec
+    diag = rec["fused"]["exchange_diag"]
+    assert [d["rank"] for d in diag] == [0, 1] and all(set(DIAG_KEYS) <= set(d) for d in diag), diag
+    assert all(d["ipc_open"] == "ok" and d["self_test"] is True and d["error_word"] == 0 for d in diag), diag
+    assert rec["fused"]["allreduce"] == "fused-ipc" and rec["fused_equals_rccl_bitwise"], rec

@@ -216,6 +216,11 @@ task_graphab() {  # native HipGraph vs torch.cuda.CUDAGraph step graphs, alterna
   done; done
 }
 
+task_diag() {  # the data-parallel diagnostics: rejected-exchange benches, dpcheck rehearsal (2 gloo ranks)
+  cd $R && py 600 python -u -m pytest tests/test_fault_injection_gpu.py tests/test_multigpu_gpu.py -v --timeout 300 --timeout-method thread > $O/${T}_diag_tests.log 2>&1 && \
+  py 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29531 -m csed_514_project_distributed_training_using_pytorch_amd.parallel.dpcheck --backend gloo --steps 8 > $O/${T}_dpcheck2.log 2>&1
+}
+
 task_quick() {  # the test files this round's changes touch
   cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_modular_graph_gpu.py tests/test_fused_gpu.py tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > $O/${T}_quick.log 2>&1
 }
