@@ -352,7 +352,7 @@ def main(argv=None) -> int:
     import torch.distributed as dist
 
     from csed_514_project_distributed_training_using_pytorch_amd.parallel.comm import (
-        all_reduce_max, barrier, init_distributed, replica_checksum)
+        all_reduce_max, barrier, init_distributed, rendezvous, replica_checksum)
     from csed_514_project_distributed_training_using_pytorch_amd.utils import prof
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -371,9 +371,14 @@ def main(argv=None) -> int:
                                         synthetic_mnist(10000, seed=0, train=False)))
         pool.shutdown(wait=False)
     t_mark = time.time()
+    # N > 1: the rendezvous (waiting for every rank to connect: their imports end at different
+    # times) runs here, in the main thread, while this rank's HIP context comes up in its thread;
+    # the process group (RCCL communicator) is then built on the same store
+    store = rendezvous(world_size=world) if world > 1 else None
+    phases["rendezvous"] = time.time() - t_mark
     if ctx_job is not None:
         ctx_job.join()
-    ctx = init_distributed(world_size=world, device=args.device, backend=backend)
+    ctx = init_distributed(world_size=world, device=args.device, backend=backend, store=store)
     phases["process_group"] = time.time() - t_mark
     n = ctx.world_size
     if ctx.is_distributed and dist.get_world_size() != args.gpus:
@@ -419,7 +424,7 @@ def main(argv=None) -> int:
                 barrier(ctx)
                 torch.cuda.synchronize(ctx.device)
 
-        def run_once(loopback_world: int, inject: bool, ph: dict, dt=dt):
+        def run_once(loopback_world: int, inject: bool, ph: dict, dt=dt, reuse=None):
             t_mark = time.time()
             torch.manual_seed(1)
             net = Net()
@@ -427,7 +432,8 @@ def main(argv=None) -> int:
             net = net.to(ctx.device)
             ph["engine.net"] = time.time() - t_mark
             eng = FusedLeNetTrainer(net, train, lr=0.02, momentum=0.5, global_batch=args.global_batch, ctx=ctx,
-                                    compute_dtype=dt, grid=args.grid or None, loopback_world=loopback_world)
+                                    compute_dtype=dt, grid=args.grid or None, loopback_world=loopback_world,
+                                    reuse_exchange=reuse)
             ph["engine"] = time.time() - t_mark
             ph.update({f"engine.{k}": v for k, v in eng.bringup_s.items()})
             if inject and eng.exch is not None and (loopback_world or ctx.rank == ctx.world_size - 1):
@@ -612,12 +618,19 @@ def main(argv=None) -> int:
         # 7. the reference's precision (src/model.py: fp32 defaults) on the same window + warm epoch
         fp32_rec = None
         if args.dtype != "fp32" and not args.no_fp32_record and not args.inject_exchange_fault:
-            eng.close()
+            sync_barrier()
+            donor = eng if eng.exch is not None and not eng.loopback_world else None
+            if donor is None:
+                eng.close()
+            else:
+                donor._graphs.clear()  # (the exchange moves to the fp32 engine: see reuse_exchange)
+                donor._stepper = None
             del r, eng
             import gc
             gc.collect()
             sync_barrier()
-            f = run_once(args.loopback_world, False, {}, dt=torch.float32)
+            f = run_once(args.loopback_world, False, {}, dt=torch.float32, reuse=donor)
+            donor = None
             fe = f["eng"]
             fp32_rec = {"ms_per_step": round(1e3 * f["elapsed"] / args.steps, 5),
                         "value": round(args.steps * args.global_batch / f["elapsed"], 1),

@@ -51,10 +51,54 @@ def _gpu_count() -> int:
         return 0
 
 
+def _wait_listening(addr: str, port: int, timeout_s: float) -> None:
+    import socket
+    import time
+
+    t_end = time.time() + timeout_s
+    while True:
+        try:
+            with socket.create_connection((addr, port), timeout=1.0):
+                return
+        except OSError:
+            if time.time() > t_end:
+                return  # (the rendezvous below reports the failure with torch's own error)
+            time.sleep(0.001)
+
+
+def rendezvous(world_size: int | None = None, rank: int | None = None, timeout_s: float = 600.0):
+    """The job's TCPStore (torch's env:// rendezvous: MASTER_ADDR / MASTER_PORT, torchrun's agent
+    store when it runs under torchrun) and a barrier on it: returns once every rank has connected.
+    Touches no GPU, so a rank can wait here for the others (their imports finish at different
+    times) while its HIP context comes up in another thread; ``init_distributed(store=...)`` then
+    builds the process group on it.  None at world size 1."""
+    world_size = world_size if world_size is not None else env_int("WORLD_SIZE", 1)
+    if world_size <= 1:
+        return None
+    if rank is None:
+        rank = env_int("RANK", None)
+        rank = rank if rank is not None else (env_int("LOCAL_RANK", 0) or 0)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    if rank != 0 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True":
+        # rank 0 hosts the store (no torchrun agent store): wait until it listens, polling every
+        # millisecond -- a TCPStore client that finds no server backs off for up to a second per
+        # retry, which a rank whose imports finished first paid in full (0.65 s of rendezvous
+        # measured with 2 CPU ranks, profiles/r6/rehearsal)
+        _wait_listening(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), timeout_s)
+    store, _, _ = next(dist.rendezvous("env://", rank, world_size, timeout=datetime.timedelta(seconds=timeout_s)))
+    if store.add("csed/rdzv/arrived", 1) == world_size:
+        store.set("csed/rdzv/all", "1")
+    store.wait(["csed/rdzv/all"])
+    return store
+
+
 def init_distributed(rank: int | None = None, world_size: int | None = None, local_rank: int | None = None,
                      backend: str | None = None, master_addr: str | None = None, master_port: int | None = None,
-                     device: str | None = None, timeout_s: float = 600.0) -> DistContext:
-    """Initialise the default process group (if world_size > 1) and pick this rank's device."""
+                     device: str | None = None, timeout_s: float = 600.0, store=None) -> DistContext:
+    """Initialise the default process group (if world_size > 1) and pick this rank's device.
+    ``store``: a store from :func:`rendezvous` (the process group is built on it: no second
+    rendezvous)."""
     world_size = world_size if world_size is not None else env_int("WORLD_SIZE", 1)
     rank = rank if rank is not None else env_int("RANK", None)
     local_rank = local_rank if local_rank is not None else env_int("LOCAL_RANK", None)
@@ -85,6 +129,8 @@ def init_distributed(rank: int | None = None, world_size: int | None = None, loc
             kw = {}
             if be == "nccl":
                 kw["device_id"] = dev
+            if store is not None:
+                kw["store"] = store
             dist.init_process_group(be, rank=rank, world_size=world_size,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistContext(rank, world_size, local_rank, dev, be)

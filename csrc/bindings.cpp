@@ -642,6 +642,17 @@ void lenet_iota_(Tensor& t) {
   CHECK_HIP(csed::launch_lenet_iota(t.data_ptr<int64_t>(), t.numel(), cur_stream(t)));
 }
 
+void lenet_selftest_fill(Tensor& slab, Tensor& vslab, int64_t B, int64_t mfma_dtype, int64_t seed) {
+  dev(slab, "slab"); dev(vslab, "vslab");
+  TORCH_CHECK(slab.scalar_type() == at::kFloat && slab.is_contiguous() && vslab.is_contiguous(), "lenet_selftest_fill");
+  const int64_t rows = mfma_dtype == csed::kF32 ? B : (B + 63) / 64 * 64;
+  TORCH_CHECK(B > 0 && vslab.numel() * vslab.element_size() >= rows * csed::lenet_vec_len() * (mfma_dtype == csed::kF32 ? 4 : 2),
+              "lenet_selftest_fill: vector slab too small");
+  const c10::DeviceGuard gd(slab.device());
+  CHECK_HIP(csed::launch_lenet_selftest_fill(slab.data_ptr<float>(), slab.numel(), vslab.data_ptr(), (int)B,
+                                             lcode(mfma_dtype), (uint32_t)seed, cur_stream(slab)));
+}
+
 void lenet_add_(Tensor& t, int64_t v) {
   dev(t, "t");
   TORCH_CHECK(t.is_contiguous() && t.scalar_type() == at::kLong, "lenet_add_: contiguous int64 tensor");
@@ -996,6 +1007,8 @@ TORCH_LIBRARY(csed, m) {
   m.def("lenet_zero_(Tensor(a!) t) -> ()", &lenet_zero_);
   m.def("lenet_iota_(Tensor(a!) t) -> ()", &lenet_iota_);
   m.def("lenet_add_(Tensor(a!) t, int v) -> ()", &lenet_add_);
+  m.def("lenet_selftest_fill(Tensor(a!) slab, Tensor(b!) vslab, int B, int mfma_dtype, int seed) -> ()",
+        &lenet_selftest_fill);
   m.def("lenet_pack(Tensor params, Tensor(a!) wimg, int mfma_dtype) -> ()");
   m.def("lenet_train(Tensor images, Tensor labels, Tensor perm, Tensor? cursor, int B, int rank, Tensor wimg, "
         "Tensor params, Tensor(a!) slab, Tensor(d!) vslab, Tensor(b!) loss_parts, float grad_scale, float mean, float std, "

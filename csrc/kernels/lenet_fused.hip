@@ -2534,6 +2534,54 @@ __global__ void lenet_add_i64_kernel(int64_t* __restrict__ p, int64_t n, int64_t
   if (i < n) p[i] += v;
 }
 
+// The exchange self-test's operands (engine/fused.py _exchange_self_test): a slab of small integers
+// in [-8, 8] (hash of the element index and the seed) and fc vectors of small integers in [-4, 4]
+// for the batch's samples (zero past B), in the compute dtype's layout (kernels/lenet_layout.h):
+// every sum the update forms is an exact integer in fp32, so the exchanged gradient must equal the
+// process group's sum of the local ones bit for bit.
+__device__ __forceinline__ uint32_t selftest_hash(uint64_t i, uint32_t seed) {
+  uint32_t h = (uint32_t)i * 2654435761u ^ (uint32_t)(i >> 32) * 2246822519u ^ seed * 3266489917u;
+  h ^= h >> 15;
+  h *= 2246822519u;
+  h ^= h >> 13;
+  return h;
+}
+
+template <int DT>
+__global__ void lenet_selftest_fill_kernel(float* __restrict__ slab, int64_t slab_n, void* __restrict__ vslab, int B,
+                                           int rows, uint32_t seed) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = i0; i < slab_n; i += stride) slab[i] = (float)((int)(selftest_hash(i, seed) % 17u) - 8);
+  const int64_t vn = (int64_t)rows * VEC;
+  for (int64_t i = i0; i < vn; i += stride) {
+    const int b = (int)(i / VEC), f = (int)(i - (int64_t)b * VEC);
+    const float v = b < B ? (float)((int)(selftest_hash(i, seed ^ 0x9e3779b9u) % 9u) - 4) : 0.f;
+    if constexpr (DT == kF32) {
+      reinterpret_cast<float*>(vslab)[i] = v;
+    } else if constexpr (DT == kBF16) {
+      reinterpret_cast<unsigned short*>(vslab)[vec16_index(f, b)] = (unsigned short)(__float_as_uint(v) >> 16);
+    } else {
+      const _Float16 h = (_Float16)v;
+      reinterpret_cast<unsigned short*>(vslab)[vec16_index(f, b)] = __builtin_bit_cast(unsigned short, h);
+    }
+  }
+}
+
+hipError_t launch_lenet_selftest_fill(float* slab, int64_t slab_n, void* vslab, int B, int mfma_dtype, uint32_t seed,
+                                      hipStream_t s) {
+  const int rows = mfma_dtype == kF32 ? B : (B + 63) & ~63;
+  const int64_t n = std::max<int64_t>(slab_n, (int64_t)rows * VEC);
+  const int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  if (mfma_dtype == kF32)
+    hipLaunchKernelGGL(lenet_selftest_fill_kernel<kF32>, dim3(blocks), dim3(256), 0, s, slab, slab_n, vslab, B, rows, seed);
+  else if (mfma_dtype == kBF16)
+    hipLaunchKernelGGL(lenet_selftest_fill_kernel<kBF16>, dim3(blocks), dim3(256), 0, s, slab, slab_n, vslab, B, rows, seed);
+  else
+    hipLaunchKernelGGL(lenet_selftest_fill_kernel<kF16>, dim3(blocks), dim3(256), 0, s, slab, slab_n, vslab, B, rows, seed);
+  return hipGetLastError();
+}
+
 hipError_t launch_lenet_zero(void* p, int64_t nbytes, hipStream_t s) {
   if (nbytes <= 0) return hipSuccess;
   const int blocks = (int)std::min<int64_t>(1024, (nbytes / 16 + 255) / 256 + 1);

@@ -293,6 +293,9 @@ hipError_t launch_lenet_pack(const float* params, uint16_t* wimg, int mfma_dtype
 hipError_t launch_lenet_zero(void* p, int64_t nbytes, hipStream_t s);
 hipError_t launch_lenet_iota(int64_t* p, int64_t n, hipStream_t s);
 hipError_t launch_lenet_add_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
+// the exchange self-test's small-integer slab and fc vectors (compute dtype layout)
+hipError_t launch_lenet_selftest_fill(float* slab, int64_t slab_n, void* vslab, int B, int mfma_dtype, uint32_t seed,
+                                      hipStream_t s);
 // Forward-only evaluation: out_parts [min(n,256), 2] per-workgroup (loss sum, correct).
 hipError_t launch_lenet_eval(const uint8_t* images, const int64_t* labels, const int64_t* order,
                              int64_t n, const uint16_t* wimg, const float* params, float mean,

@@ -61,21 +61,28 @@ def test_scaling_report_prediction_from_loopback_log(tmp_path):
 
 
 def test_scaling_report_predicts_time_elapsed():
-    """Predicted time_elapsed: launch phases at N from a CPU record, the N = 1 GPU bring-up, the
-    exchange bring-up of a 2-rank rehearsal (N > 1 only) and epoch 0 at the predicted step."""
+    """Predicted time_elapsed (round-6 model): max(HIP-context wait, N-rank rendezvous) + the RCCL
+    communicator's creation (N > 1), the N = 1 GPU set-up, the exchange bring-up of a 2-rank
+    rehearsal (N > 1) and epoch 0 at the predicted step -- each term from a record."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import scaling_report as sr
 
-    ph1 = {"spawn": 0.0, "import": 1.4, "process_group": 0.0, "data_wait": 0.1, "engine": 0.05, "capture": 0.2,
-           "test_upload": 0.01}
+    ph1 = {"spawn": 0.0, "import_torch": 1.4, "import_pkg": 0.01, "process_group": 0.2, "data_wait": 0.1,
+           "engine": 0.05, "capture": 0.2, "test_upload": 0.01}
     by_n = {1: {"n_gpus": 1, "value": 1.0, "ms_per_step": 0.014, "epoch_s": 0.013, "epoch0_s": 0.05,
                 "bringup_s": ph1}}
-    steps = {(64, 1): 14.0, (8, 8): 13.0}
+    steps = {(64, 1): 14.0, (8, 8): 13.0, (32, 2): 13.5}
     pred = sr.predict(by_n, steps, hop_us=1.0)
-    cpu = {8: {"n_gpus": 8, "bringup_s": {"spawn": 0.3, "import": 3.0, "process_group": 1.0}}}
-    reh = {"n_gpus": 2, "bringup_s": {"engine.ipc_open": 0.02, "engine.self_test": 0.03}}
-    te = sr.predict_time_elapsed(by_n, pred, cpu, reh)
+    cpu = {2: {"n_gpus": 2, "bringup_s": {"rendezvous": 0.1, "process_group": 0.12}},
+           8: {"n_gpus": 8, "bringup_s": {"rendezvous": 0.3, "process_group": 0.35}}}
+    reh = {"n_gpus": 2, "bringup_s": {"engine.ipc_open": 0.02, "engine.self_test": 0.03, "engine.path_timing": 0.01}}
+    rccl = {"init_process_group_s": 0.04, "first_broadcast_s": 0.01}
+    terms = {}
+    te = sr.predict_time_elapsed(by_n, pred, cpu, reh, rccl, terms)
     base = 0.1 + 0.05 + 0.2 + 0.01
-    assert abs(te[1] - (1.4 + base + 0.05)) < 1e-9
-    assert abs(te[8] - (4.3 + base + 0.05 + 0.05 + 938 * 0.0e-6)) < 1e-9  # step_8 = 13 + 1 hop = step_1
+    assert abs(te[1] - (0.2 + base + 0.05)) < 1e-9
+    # N = 2: the rendezvous hides under the context wait; N = 8: it is longer
+    assert abs(te[2] - (0.2 + 0.05 + base + 0.06 + 0.05 + 938 * 0.5e-6)) < 1e-9
+    assert abs(te[8] - (0.3 + 0.05 + base + 0.06 + 0.05)) < 1e-9  # step_8 = 13 + 1 hop = step_1
+    assert set(terms) == {1, 2, 8} and abs(terms[8]["total"] - te[8]) < 1e-12
     assert sr.predict_time_elapsed({}, pred, cpu, reh) == {}

@@ -7,8 +7,9 @@
 # tasks
 #   suite     the whole GPU test suite + smoke()                            (GPUTEST-style record)
 #   bench     the driver's command, default / fp32 / per-rank-8 / large-batch benches (JSON lines)
-#   rehearse  N=1 and a 2-rank gloo rehearsal of the multi-rank bench flow on the one GPU, and
-#             bench.py --device cpu --gpus 2/4/8 (N concurrent imports + rendezvous, bringup_s)
+#   rehearse  N=1 and a 2-rank gloo rehearsal of the multi-rank bench flow on the one GPU (also with
+#             CSED_TIME_PATHS=1), bench.py --device cpu --gpus 2/4/8 under torchrun (N concurrent
+#             imports + rendezvous, bringup_s) and tools/rccl_init_probe.py (one-rank RCCL bring-up)
 #   trace     rocprofv3 kernel traces: default (B=64), per-rank 8, B=1024 / 8192 fp16, fp32 64 / 8
 #   stages    in-kernel stage stamps (train B=64 / 8, tile B=1024, fp32 B=64) + update stamps
 #   exchange  loopback exchange table (tools/exchange_loopback.py) + step breakdown
@@ -62,9 +63,11 @@ task_bench() {
 task_rehearse() {
   cd $R && py 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/${T}_reh_n1.json 2>$O/${T}_reh_n1.err && \
   py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 > $O/${T}_reh_gloo2.json 2>$O/${T}_reh_gloo2.err && \
+  CSED_TIME_PATHS=1 py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-fp32-record > $O/${T}_reh_gloo2_tp.json 2>$O/${T}_reh_gloo2_tp.err && \
   for n in 2 4 8; do
-    py 300 python bench.py --gpus $n --device cpu --steps 2 --warmup 1 > $O/${T}_reh_cpu$n.json 2>$O/${T}_reh_cpu$n.err || return 1
-  done
+    py 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=$n --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --device cpu --steps 2 --warmup 1 > $O/${T}_reh_cpu$n.json 2>$O/${T}_reh_cpu$n.err || return 1
+  done && \
+  py 120 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 --master-port 29611 tools/rccl_init_probe.py > $O/${T}_rccl_init.log 2>&1
 }
 
 task_trace() {

@@ -70,11 +70,11 @@ GLOBAL_BATCH = 64
 # graph-replayed lenet_train + lenet_update step (us) at per-rank batch B with the in-kernel
 # exchange looped back to N virtual ranks, one MI355X (profiles/r4/exchange_loopback_r4f7.log,
 # profiles/dp_exchange_r4.md)
-LOOPBACK_STEP_US = {
-    (8, 1): 12.42, (8, 2): 13.41, (8, 4): 13.84, (8, 8): 14.70,
-    (16, 1): 12.52, (16, 2): 13.61, (16, 4): 14.00, (16, 8): 14.87,
-    (32, 1): 12.71, (32, 2): 13.87, (32, 4): 14.12, (32, 8): 14.94,
-    (64, 1): 13.39, (64, 2): 14.56, (64, 4): 14.94, (64, 8): 15.61,
+LOOPBACK_STEP_US = {  # round 6 (profiles/r6/rehearsal/r6i_loopback.log)
+    (8, 1): 12.34, (8, 2): 13.51, (8, 4): 13.97, (8, 8): 14.59,
+    (16, 1): 12.37, (16, 2): 13.66, (16, 4): 13.96, (16, 8): 14.71,
+    (32, 1): 12.71, (32, 2): 13.88, (32, 4): 14.19, (32, 8): 14.92,
+    (64, 1): 13.43, (64, 2): 14.53, (64, 4): 14.94, (64, 8): 15.71,
 }
 WIRE_BYTES = 21840 * 8  # live exchange words per peer per step (lenet_fused.hip ll_push)
 _LB_LINE = re.compile(r"B=\s*(\d+)\s+N=(\d+).*?step\s+([0-9.]+)\s*us")
@@ -108,28 +108,50 @@ def predict(by_n: dict[int, dict], steps_us: dict, hop_us: float, ns=(1, 2, 4, 8
     return out
 
 
+def load_rccl_init(path) -> dict | None:
+    """The ``RCCL_INIT {json}`` line of tools/rccl_init_probe.py."""
+    for line in Path(path).read_text().splitlines():
+        if line.startswith("RCCL_INIT "):
+            return json.loads(line[len("RCCL_INIT "):])
+    return None
+
+
 def predict_time_elapsed(by_n: dict[int, dict], pred: dict[int, dict], cpu_by_n: dict[int, dict],
-                         rehearsal: dict | None) -> dict[int, float]:
-    """Predicted time_elapsed_s per N (see the module docstring); N needs a CPU record."""
+                         rehearsal: dict | None, rccl: dict | None = None,
+                         terms: dict | None = None) -> dict[int, float]:
+    """Predicted time_elapsed_s per N (the module docstring's formula); every term comes from a
+    record, and ``terms`` (if given) receives them per N for the report."""
     r1 = by_n.get(1) or {}
     ph1 = r1.get("bringup_s") or {}
     if not ph1 or not r1.get("epoch0_s") or 1 not in pred:
         return {}
     base = sum(ph1.get(k, 0.0) for k in ("data_wait", "engine", "capture", "test_upload"))
+    ctx1 = ph1.get("process_group", 0.0)  # N = 1: the wait for this rank's HIP-context thread
     xb = 0.0
     if rehearsal:
         rph = rehearsal.get("bringup_s") or {}
         xb = sum(rph.get(k, 0.0) for k in ("engine.ipc_open", "engine.self_test", "engine.path_timing"))
+    rinit = (rccl.get("init_process_group_s", 0.0) + rccl.get("first_broadcast_s", 0.0)) if rccl else 0.0
     out = {}
     for n, p in pred.items():
-        c = (cpu_by_n.get(n) or {}).get("bringup_s") if n > 1 else ph1
-        if not c:
-            continue
-        # round 5+: t0 after the imports (import_torch / import_pkg are outside the span)
-        keys = ("process_group",) if "import_torch" in c else ("spawn", "import", "process_group")
-        launch = sum(c.get(k, 0.0) for k in keys)
+        if n == 1:
+            launch, rdzv = ctx1, 0.0
+        else:
+            c = (cpu_by_n.get(n) or {}).get("bringup_s")
+            if not c:
+                continue
+            # the rendezvous (N concurrent processes, their import skew) overlaps the HIP context's
+            # creation (bench.py: store barrier in the main thread, context in its own), then the
+            # RCCL communicator is created on the store
+            rdzv = c.get("rendezvous", c.get("process_group", 0.0))
+            launch = max(ctx1, rdzv) + rinit
         ep0 = r1["epoch0_s"] + STEPS_PER_EPOCH * (p["step_us"] - pred[1]["step_us"]) * 1e-6
         out[n] = launch + base + (xb if n > 1 else 0.0) + ep0
+        if terms is not None:
+            terms[n] = {"hip_ctx_wait_1": ctx1, "rendezvous_N": rdzv, "rccl_init": rinit if n > 1 else 0.0,
+                        "setup_1 (data_wait+engine+capture+test_upload)": base,
+                        "exchange_bringup (ipc_open+self_test+path_timing)": xb if n > 1 else 0.0,
+                        "epoch0_N": ep0, "total": out[n]}
     return out
 
 
@@ -269,7 +291,9 @@ def main(argv=None) -> int:
     ap.add_argument("--loopback-log", help="exchange_loopback.py output replacing the built-in step table")
     ap.add_argument("--cpu-bringup", nargs="*", default=[],
                     help="bench.py --device cpu --gpus N JSON lines (spawn / import / rendezvous at N ranks)")
-    ap.add_argument("--rehearsal", help="a 2-rank gloo GPU rehearsal's JSON line (exchange bring-up phases)")
+    ap.add_argument("--rehearsal", help="a 2-rank gloo GPU rehearsal's JSON line (exchange bring-up phases; "
+                                        "run with CSED_TIME_PATHS=1 so the path selection is timed too)")
+    ap.add_argument("--rccl-init", help="tools/rccl_init_probe.py output (the RCCL communicator's creation)")
     a = ap.parse_args(argv)
     by_n = load_records(a.inputs)
     if not by_n:
@@ -281,13 +305,25 @@ def main(argv=None) -> int:
         pred = predict(by_n, load_loopback(a.loopback_log) if a.loopback_log else LOOPBACK_STEP_US, a.hop_us,
                        wire_us=wire_us)
         reh = load_records([a.rehearsal]).get(2) if a.rehearsal else None
+        terms: dict = {}
         for n, t in predict_time_elapsed(by_n, pred, load_records(a.cpu_bringup) if a.cpu_bringup else {},
-                                         reh).items():
+                                         reh, load_rccl_init(a.rccl_init) if a.rccl_init else None,
+                                         terms).items():
             pred[n]["time_elapsed_s"] = t
     rows = table(by_n, pred)
     out = Path(a.out)
     out.parent.mkdir(parents=True, exist_ok=True)
     md = markdown(rows, a.title)
+    if pred and terms:
+        md += "\nPredicted time_elapsed_s, term by term (s):\n\n| N | " + " | ".join(next(iter(terms.values()))) + " |\n"
+        md += "|---:|" + "---:|" * len(next(iter(terms.values()))) + "\n"
+        for n, t in sorted(terms.items()):
+            md += f"| {n} | " + " | ".join(f"{v:.4f}" for v in t.values()) + " |\n"
+        md += ("\nSources: hip_ctx_wait_1, setup_1 and epoch0 from the N = 1 GPU record; rendezvous_N from "
+               "`bench.py --gpus N --device cpu` (N concurrent processes: their import skew); rccl_init from "
+               "tools/rccl_init_probe.py (one rank: the fixed part of the communicator's creation, a lower "
+               "bound at N ranks); exchange_bringup from the 2-rank gloo rehearsal with CSED_TIME_PATHS=1; "
+               "epoch0_N at the predicted step.\n")
     out.with_suffix(".md").write_text(md)
     png = plot(rows, out.with_suffix(".png"), a.title)
     print(md)
