@@ -201,12 +201,7 @@ class FusedLeNetTrainer:
         if self.flat.numel != N_PARAMS:
             raise ValueError("FusedLeNetTrainer needs the reference Net architecture")
         if broadcast_init and self.world > 1:  # the DDP-constructor parameter sync (CS4)
-            if self.ctx.backend == "nccl":
-                dist.broadcast(self.flat.data, src=0)
-            else:  # gloo bootstrap (tests): host copy
-                host = self.flat.data.cpu()
-                dist.broadcast(host, src=0)
-                self.flat.data.copy_(host)
+            comm.ctl_broadcast(self.ctx, self.flat.data, src=0)  # (RCCL, or the host over gloo)
         self.momentum_buf = _native.zeros(self.flat.data.shape, torch.float32, self.flat.data.device)
         wimg_elems, conv_params, vec_len, stage_max = layout()
         # zero-initialised: padding rows / columns of the images must stay zero
@@ -277,6 +272,7 @@ class FusedLeNetTrainer:
         self.exch_timeout_s = wait_timeout_s()
         self.path_timing_us: dict | None = None
         self._xdiag: dict = {}  # stage results of the exchange bring-up (exchange_diag)
+        self._path_pending: str | None = None  # a deferred path timing (select_path)
         self.loopback_world = 0  # (set below; the exchange bring-up's reports read it)
         multi = self.comm and self.world > 1
         mode = allreduce_mode() if multi else "rccl"
@@ -421,33 +417,59 @@ class FusedLeNetTrainer:
             do_time = tp == "1" or (self.ctx.backend == "nccl" and self._xdiag.get("ranks_per_gpu") == 1)
         else:
             do_time = False
-        if do_time:
-            t2 = time.perf_counter()
-            t_fused = self._time_steps()
-            saved, self.exch = self.exch, None
-            # (gloo: the host all-reduce is not capturable -- not timed, the fused path is kept)
-            t_fallback = self._time_steps() if self.ctx.backend == "nccl" else float("inf")
-            t_local = float("inf")
-            if tp == "1":
-                # the same step with no exchange at all (each rank updates on its own gradient;
-                # the state is restored): fused - local = what the exchange costs per step
-                self.comm = False
-                t_local = self._time_steps()
-                self.comm = True
-            # a path whose graph could not be captured times as inf; ties keep the fused path
-            self.exch = saved if t_fused <= t_fallback else None
-            if self.exch is None:
-                self.exchange_note = "fused exchange off: slower than the fallback step"
-                # every rank finished the timing above (device synchronize before the timing
-                # all-reduce), so no peer still pushes into these buffers: the close is safe
-                saved.close()
-            fin = lambda t: round(t, 2) if t != float("inf") else None  # noqa: E731
-            self.path_timing_us = {"fused_step_us": fin(t_fused), "fallback_step_us": fin(t_fallback),
-                                   "local_step_us": fin(t_local),
-                                   "exchange_us": fin(t_fused - t_local) if max(t_fused, t_local) != float("inf")
-                                   else None,
-                                   "fallback": "rccl", "kept": "fused" if self.exch is not None else "rccl"}
-            self.bringup_s["path_timing"] = time.perf_counter() - t2
+        if do_time and self.ctx.control is not None:
+            # lazy RCCL (bench.py at N > 1): the fallback step's all-reduce would create the RCCL
+            # communicator (1-3.6 s) in the middle of the bring-up -- the selection is deferred to
+            # select_path(), which the bench runs after epoch 0 (outside the reference span)
+            self._path_pending = tp
+            self.exchange_note = "fused exchange on (self-test passed; path timing deferred)"
+        elif do_time:
+            self._select_path_now(tp)
+
+    def select_path(self) -> bool:
+        """Run the fused-vs-RCCL step timing deferred by a lazy-RCCL bring-up (collective; a no-op
+        otherwise).  True if the step path changed (the cached graphs are dropped then)."""
+        tp, self._path_pending = self._path_pending, None
+        if tp is None or self.exch is None:
+            return False
+        self._select_path_now(tp)
+        if self.exch is None:
+            self._graphs.clear()
+            self._stepper = None
+            return True
+        return False
+
+    def _select_path_now(self, tp: str) -> None:
+        import time
+
+        t2 = time.perf_counter()
+        t_fused = self._time_steps()
+        saved, self.exch = self.exch, None
+        # (gloo: the host all-reduce is not capturable -- not timed, the fused path is kept)
+        t_fallback = self._time_steps() if self.ctx.backend == "nccl" else float("inf")
+        t_local = float("inf")
+        if tp == "1":
+            # the same step with no exchange at all (each rank updates on its own gradient;
+            # the state is restored): fused - local = what the exchange costs per step
+            self.comm = False
+            t_local = self._time_steps()
+            self.comm = True
+        # a path whose graph could not be captured times as inf; ties keep the fused path
+        self.exch = saved if t_fused <= t_fallback else None
+        if self.exch is None:
+            self.exchange_note = "fused exchange off: slower than the fallback step"
+            # every rank finished the timing above (device synchronize before the timing
+            # all-reduce), so no peer still pushes into these buffers: the close is safe
+            saved.close()
+        else:
+            self.exchange_note = "fused exchange on (self-test passed, timed faster than the fallback)"
+        fin = lambda t: round(t, 2) if t != float("inf") else None  # noqa: E731
+        self.path_timing_us = {"fused_step_us": fin(t_fused), "fallback_step_us": fin(t_fallback),
+                               "local_step_us": fin(t_local),
+                               "exchange_us": fin(t_fused - t_local) if max(t_fused, t_local) != float("inf")
+                               else None,
+                               "fallback": "rccl", "kept": "fused" if self.exch is not None else "rccl"}
+        self.bringup_s["path_timing"] = time.perf_counter() - t2
 
     def exchange_diag(self) -> dict:
         """This rank's data-parallel diagnostics (``parallel/ipc.py`` DIAG_KEYS): the bring-up's
@@ -464,9 +486,8 @@ class FusedLeNetTrainer:
         return d
 
     def _vote(self, ok: bool) -> bool:
-        dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm.ctl_device(self.ctx))
+        comm.ctl_all_reduce(self.ctx, t, dist.ReduceOp.MIN)
         return bool(t.item())
 
     def _exchange_self_test(self, rounds: int = 2) -> bool:
@@ -480,7 +501,7 @@ class FusedLeNetTrainer:
         import numpy as np
 
         ops = torch.ops.csed
-        pg_dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
+        pg_dev = comm.ctl_device(self.ctx)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket, None, None, False, None, 0, None,
                   self.mfma)
@@ -498,7 +519,7 @@ class FusedLeNetTrainer:
             except Exception:
                 ok = False
         ref = local.to(pg_dev, copy=True)
-        dist.all_reduce(ref)
+        comm.ctl_all_reduce(self.ctx, ref)
         ok &= bool(np.array_equal(fused.cpu().numpy(), ref.cpu().numpy()))
         torch.cuda.synchronize(self.device)
         try:
@@ -533,9 +554,8 @@ class FusedLeNetTrainer:
         for t, v in zip(state, saved):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
-        dev = self.device if self.ctx.backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([us], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([us], dtype=torch.float64, device=comm.ctl_device(self.ctx))
+        comm.ctl_all_reduce(self.ctx, t, dist.ReduceOp.MAX)
         return float(t.item())
 
     def close(self) -> None:
@@ -549,10 +569,7 @@ class FusedLeNetTrainer:
             self.exch = None
         if self.exch is not None and dist.is_initialized():
             torch.cuda.synchronize(self.device)
-            if self.ctx.backend == "nccl":
-                dist.barrier(device_ids=[self.device.index])
-            else:
-                dist.barrier()
+            comm.barrier(self.ctx)
         if self.exch is not None:
             self.exch.close()
         self.exch = None

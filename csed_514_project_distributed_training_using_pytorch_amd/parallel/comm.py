@@ -28,6 +28,14 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str | None = None
+    # control plane: a gloo group over every rank for the bring-up's and the bench's small host
+    # collectives (votes, handle / diagnostics gathers, the initial parameter broadcast, timing
+    # maxima, barriers) when the RCCL communicator is created lazily (init_distributed(lazy_rccl=
+    # True)): RCCL's communicator takes 1.0 s (warm) to 3.6 s (fresh box) to create, even for one
+    # rank (tools/rccl_init_probe.py, profiles/r6/rehearsal), and a data-parallel step whose
+    # gradients travel over the in-kernel IPC exchange never needs it -- it is created at its first
+    # collective: the fallback all-reduce or the fused-vs-RCCL path timing
+    control: object = None
 
     @property
     def is_distributed(self) -> bool:
@@ -95,10 +103,13 @@ def rendezvous(world_size: int | None = None, rank: int | None = None, timeout_s
 
 def init_distributed(rank: int | None = None, world_size: int | None = None, local_rank: int | None = None,
                      backend: str | None = None, master_addr: str | None = None, master_port: int | None = None,
-                     device: str | None = None, timeout_s: float = 600.0, store=None) -> DistContext:
+                     device: str | None = None, timeout_s: float = 600.0, store=None,
+                     lazy_rccl: bool = False) -> DistContext:
     """Initialise the default process group (if world_size > 1) and pick this rank's device.
     ``store``: a store from :func:`rendezvous` (the process group is built on it: no second
-    rendezvous)."""
+    rendezvous).  ``lazy_rccl`` (RCCL backend): no eager communicator -- it is created at the
+    first RCCL collective -- and a gloo group over every rank becomes the context's control
+    plane (``DistContext.control``)."""
     world_size = world_size if world_size is not None else env_int("WORLD_SIZE", 1)
     rank = rank if rank is not None else env_int("RANK", None)
     local_rank = local_rank if local_rank is not None else env_int("LOCAL_RANK", None)
@@ -125,15 +136,55 @@ def init_distributed(rank: int | None = None, world_size: int | None = None, loc
             os.environ["MASTER_ADDR"] = master_addr
         if master_port:
             os.environ["MASTER_PORT"] = str(master_port)
+        control = None
         if not dist.is_initialized():
             kw = {}
-            if be == "nccl":
+            if be == "nccl" and not lazy_rccl:
                 kw["device_id"] = dev
             if store is not None:
                 kw["store"] = store
             dist.init_process_group(be, rank=rank, world_size=world_size,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
+            if be == "nccl" and lazy_rccl:
+                control = dist.new_group(backend="gloo")  # (collective: every rank, same order)
+        return DistContext(rank, world_size, local_rank, dev, be, control)
     return DistContext(rank, world_size, local_rank, dev, be)
+
+
+def ctl_device(ctx: DistContext) -> torch.device:
+    """Device of the control plane's tensors: the host when a gloo group carries them."""
+    if ctx.control is not None or ctx.backend != "nccl":
+        return torch.device("cpu")
+    return ctx.device
+
+
+def ctl_all_reduce(ctx: DistContext, t: torch.Tensor, op=None) -> torch.Tensor:
+    """All-reduce of a control-plane tensor (on ``ctl_device``) over every rank, in place."""
+    dist.all_reduce(t, op=op if op is not None else dist.ReduceOp.SUM, group=ctx.control)
+    return t
+
+
+def ctl_all_gather(ctx: DistContext, out: list, t: torch.Tensor) -> list:
+    dist.all_gather(out, t, group=ctx.control)
+    return out
+
+
+def ctl_all_gather_object(ctx: DistContext, obj) -> list:
+    out: list = [None] * ctx.world_size
+    dist.all_gather_object(out, obj, group=ctx.control)
+    return out
+
+
+def ctl_broadcast(ctx: DistContext, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """Broadcast of a device tensor from ``src`` over the control plane (through the host when
+    that is gloo)."""
+    if ctl_device(ctx).type == t.device.type:
+        dist.broadcast(t, src=src, group=ctx.control)
+        return t
+    host = t.cpu()
+    dist.broadcast(host, src=src, group=ctx.control)
+    t.copy_(host)
+    return t
 
 
 def destroy() -> None:
@@ -166,7 +217,9 @@ def quiesce() -> None:
 
 def barrier(ctx: DistContext) -> None:
     if ctx.is_distributed:
-        if ctx.backend == "nccl":
+        if ctx.control is not None:
+            dist.barrier(group=ctx.control)
+        elif ctx.backend == "nccl":
             dist.barrier(device_ids=[ctx.device.index])
         else:
             dist.barrier()
@@ -188,8 +241,8 @@ def all_reduce_max(ctx: DistContext, value: float) -> float:
     """Max of a host scalar over ranks (used to report the slowest rank's time)."""
     if not ctx.is_distributed:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([value], dtype=torch.float64, device=ctl_device(ctx))
+    ctl_all_reduce(ctx, t, dist.ReduceOp.MAX)
     return float(t.item())
 
 
@@ -204,8 +257,8 @@ def replica_checksum(ctx: DistContext, t: torch.Tensor) -> tuple[bool, int, int]
     if not ctx.is_distributed:
         v = int(h.item())
         return True, v, v
-    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    dev = ctl_device(ctx)
     lo, hi = h.to(dev).clone(), h.to(dev).clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    ctl_all_reduce(ctx, lo, dist.ReduceOp.MIN)
+    ctl_all_reduce(ctx, hi, dist.ReduceOp.MAX)
     return bool(lo.item() == hi.item()), int(lo.item()), int(hi.item())

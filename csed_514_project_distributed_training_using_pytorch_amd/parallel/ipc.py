@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _native
-from .comm import DistContext
+from .comm import DistContext, ctl_all_gather, ctl_all_gather_object, ctl_all_reduce, ctl_device
 
 
 # latencies measured by the last auto selection (us per call, max over ranks), for reports
@@ -43,17 +43,15 @@ LAST_NOTE: str | None = None
 
 
 def _gather_handles(ctx: DistContext, h: torch.Tensor) -> torch.Tensor:
-    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
-    mine = h.to(dev)
+    mine = h.to(ctl_device(ctx))
     out = [torch.empty_like(mine) for _ in range(ctx.world_size)]
-    dist.all_gather(out, mine)
+    ctl_all_gather(ctx, out, mine)
     return torch.stack([t.cpu() for t in out]).contiguous()
 
 
 def _all_ok(ctx: DistContext, ok: bool) -> bool:
-    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
-    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=ctl_device(ctx))
+    ctl_all_reduce(ctx, t, dist.ReduceOp.MIN)
     return bool(t.item())
 
 
@@ -159,11 +157,11 @@ class IpcAllReduce:
         dev = ctx.device
         idx = torch.arange(self.n, device=dev, dtype=torch.float32)
         cases = []
-        pg_dev = dev if ctx.backend == "nccl" else torch.device("cpu")
+        pg_dev = ctl_device(ctx)
         for r in range(rounds):
             x = torch.remainder(idx * (ctx.rank + 1) + r, 97.0)  # small integers: sums are exact in fp32
             z = x.to(pg_dev, copy=True)
-            dist.all_reduce(z)
+            ctl_all_reduce(ctx, z)
             z = z.to(dev)
             exact = sum(torch.remainder(idx * (k + 1) + r, 97.0) for k in range(ctx.world_size))
             cases.append((x, z, exact))
@@ -201,10 +199,9 @@ def _device_key(ctx: DistContext) -> int:
 def ranks_per_gpu(ctx: DistContext) -> int:
     """Largest number of ranks of the process group that drive the same physical GPU
     (collective).  One process per GPU gives 1."""
-    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
-    mine = torch.tensor([_device_key(ctx)], dtype=torch.int64, device=dev)
+    mine = torch.tensor([_device_key(ctx)], dtype=torch.int64, device=ctl_device(ctx))
     keys = [torch.empty_like(mine) for _ in range(ctx.world_size)]
-    dist.all_gather(keys, mine)
+    ctl_all_gather(ctx, keys, mine)
     vals = [int(k.item()) for k in keys]
     return max(vals.count(v) for v in vals)
 
@@ -238,9 +235,7 @@ def gather_diag(ctx: DistContext, local: dict) -> list[dict]:
     """Every rank's diagnostics, in rank order (collective; the local record alone at world 1)."""
     if not ctx.is_distributed:
         return [local]
-    out: list = [None] * ctx.world_size
-    dist.all_gather_object(out, local)
-    return out
+    return ctl_all_gather_object(ctx, local)
 
 
 def test_reject_hook() -> str:

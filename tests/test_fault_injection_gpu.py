@@ -139,3 +139,24 @@ def test_bench_two_ranks_rejected_exchange_still_reports(tmp_path, stage):
     else:
         assert all(d["ipc_open"] == "ok" for d in diag), diag
         assert diag[0]["self_test"] is True and diag[1]["self_test"] is False, diag
+
+
+def test_bench_two_ranks_lazy_rccl_shared_gpu(tmp_path):
+    """bench.py --gpus 2 with the default (RCCL) backend on the one GPU: the communicator is created
+    lazily and the bring-up's host collectives run on the gloo control plane, so two ranks sharing a
+    GPU (which RCCL itself refuses) train the fused exchange end to end -- the real N-GPU flow short
+    of xGMI: a valid value, bitwise replicas, no error word, the fp32 sub-record on the reused
+    exchange."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(CSED_IPC_TIMEOUT_S="5")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["config"]["process_group"] == {"backend": "nccl", "ranks": 2}, rec["config"]
+    assert rec["config"]["allreduce"] == "fused-ipc" and rec["value"] > 0, rec
+    assert rec["replicas_identical"] is True and "comm_error" not in rec, rec
+    assert all(d["error_word"] == 0 and d["self_test"] is True for d in rec["exchange_diag"]), rec["exchange_diag"]
+    assert rec["fp32"]["replicas_identical"] and "fused-ipc" in rec["fp32"]["engine"], rec["fp32"]

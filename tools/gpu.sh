@@ -64,6 +64,7 @@ task_rehearse() {
   cd $R && py 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/${T}_reh_n1.json 2>$O/${T}_reh_n1.err && \
   py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 > $O/${T}_reh_gloo2.json 2>$O/${T}_reh_gloo2.err && \
   CSED_TIME_PATHS=1 py 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-fp32-record > $O/${T}_reh_gloo2_tp.json 2>$O/${T}_reh_gloo2_tp.err && \
+  py 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29621 bench.py --gpus 2 --steps 20 --warmup 5 > $O/${T}_reh_nccl2.json 2>$O/${T}_reh_nccl2.err && \
   for n in 2 4 8; do
     py 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=$n --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --device cpu --steps 2 --warmup 1 > $O/${T}_reh_cpu$n.json 2>$O/${T}_reh_cpu$n.err || return 1
   done && \

@@ -28,9 +28,22 @@ def main() -> int:
     store, rank, world = next(dist.rendezvous("env://", int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
                                               timeout=datetime.timedelta(seconds=120)))
     out["rendezvous_s"] = round(time.perf_counter() - t, 4)
+    lazy = "--lazy" in os.sys.argv
     t = time.perf_counter()
-    dist.init_process_group("nccl", store=store, rank=rank, world_size=world, device_id=dev)
+    if lazy:  # no device: the communicator is created at the first collective
+        dist.init_process_group("nccl", store=store, rank=rank, world_size=world)
+    else:
+        dist.init_process_group("nccl", store=store, rank=rank, world_size=world, device_id=dev)
     out["init_process_group_s"] = round(time.perf_counter() - t, 4)
+    out["lazy"] = lazy
+    if lazy:
+        t = time.perf_counter()
+        g = dist.new_group(backend="gloo")
+        out["gloo_subgroup_s"] = round(time.perf_counter() - t, 4)
+        y = torch.ones(4)
+        t = time.perf_counter()
+        dist.all_reduce(y, group=g)
+        out["gloo_first_all_reduce_s"] = round(time.perf_counter() - t, 4)
     x = torch.ones(21840, device=dev)
     for name in ("first_broadcast_s", "first_all_reduce_s", "second_all_reduce_s"):
         torch.cuda.synchronize(dev)
