@@ -44,7 +44,7 @@ import torch.distributed as dist
 from ..data.mnist import MNIST_MEAN, MNIST_STD, MNISTData
 from ..models.net import N_PARAMS, Net
 from ..ops import _native
-from ..parallel import comm
+from ..parallel import comm as _comm
 from ..parallel.comm import DistContext
 from ..parallel import ipc as _ipc
 from ..parallel.ipc import allreduce_mode, open_exchange, open_loopback_exchange, wait_timeout_s
@@ -201,7 +201,7 @@ class FusedLeNetTrainer:
         if self.flat.numel != N_PARAMS:
             raise ValueError("FusedLeNetTrainer needs the reference Net architecture")
         if broadcast_init and self.world > 1:  # the DDP-constructor parameter sync (CS4)
-            comm.ctl_broadcast(self.ctx, self.flat.data, src=0)  # (RCCL, or the host over gloo)
+            _comm.ctl_broadcast(self.ctx, self.flat.data, src=0)  # (RCCL, or the host over gloo)
         self.momentum_buf = _native.zeros(self.flat.data.shape, torch.float32, self.flat.data.device)
         wimg_elems, conv_params, vec_len, stage_max = layout()
         # zero-initialised: padding rows / columns of the images must stay zero
@@ -486,8 +486,8 @@ class FusedLeNetTrainer:
         return d
 
     def _vote(self, ok: bool) -> bool:
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm.ctl_device(self.ctx))
-        comm.ctl_all_reduce(self.ctx, t, dist.ReduceOp.MIN)
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_comm.ctl_device(self.ctx))
+        _comm.ctl_all_reduce(self.ctx, t, dist.ReduceOp.MIN)
         return bool(t.item())
 
     def _exchange_self_test(self, rounds: int = 2) -> bool:
@@ -501,7 +501,7 @@ class FusedLeNetTrainer:
         import numpy as np
 
         ops = torch.ops.csed
-        pg_dev = comm.ctl_device(self.ctx)
+        pg_dev = _comm.ctl_device(self.ctx)
         common = (self.flat.data, self.momentum_buf, self.wimg, self.lr, self.momentum, self.dampening,
                   self.weight_decay, self.nesterov, self.step_count, self.ticket, None, None, False, None, 0, None,
                   self.mfma)
@@ -519,7 +519,7 @@ class FusedLeNetTrainer:
             except Exception:
                 ok = False
         ref = local.to(pg_dev, copy=True)
-        comm.ctl_all_reduce(self.ctx, ref)
+        _comm.ctl_all_reduce(self.ctx, ref)
         ok &= bool(np.array_equal(fused.cpu().numpy(), ref.cpu().numpy()))
         torch.cuda.synchronize(self.device)
         try:
@@ -554,8 +554,8 @@ class FusedLeNetTrainer:
         for t, v in zip(state, saved):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
-        t = torch.tensor([us], dtype=torch.float64, device=comm.ctl_device(self.ctx))
-        comm.ctl_all_reduce(self.ctx, t, dist.ReduceOp.MAX)
+        t = torch.tensor([us], dtype=torch.float64, device=_comm.ctl_device(self.ctx))
+        _comm.ctl_all_reduce(self.ctx, t, dist.ReduceOp.MAX)
         return float(t.item())
 
     def close(self) -> None:
@@ -569,7 +569,7 @@ class FusedLeNetTrainer:
             self.exch = None
         if self.exch is not None and dist.is_initialized():
             torch.cuda.synchronize(self.device)
-            comm.barrier(self.ctx)
+            _comm.barrier(self.ctx)
         if self.exch is not None:
             self.exch.close()
         self.exch = None
@@ -821,7 +821,7 @@ class FusedLeNetTrainer:
             for k, dt in (("snapshot", tb - ta), ("step", tc - tb), ("sync", td - tc), ("restore", te - td)):
                 self._stamp(f"capture.warmup.{k}", dt)
         t1 = time.perf_counter()
-        comm.quiesce()  # (no pending collective for the watchdog to query during the capture)
+        _comm.quiesce()  # (no pending collective for the watchdog to query during the capture)
         # thread_local: only this thread's unsafe calls invalidate the capture.  The process
         # group's watchdog thread keeps querying the events of earlier collectives while a step
         # that contains an RCCL all-reduce is captured; in the default (global) mode that query

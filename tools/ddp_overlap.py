@@ -96,11 +96,16 @@ def run(batch: int, steps: int, warmup: int, trace: bool, only=None, graphs=(Fal
                 step()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if trace:  # phase marker for --phases: the steps window starts after it
+                marker = torch.zeros(1, dtype=torch.long, device=dev)
+                torch.ops.csed.lenet_add_(marker, 0)
             t0 = time.perf_counter()
             e0.record()
             for _ in range(steps):
                 step()
             e1.record()
+            if trace:  # ... and ends before this one
+                torch.ops.csed.lenet_add_(marker, 0)
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / steps
             rows.append({"mode": mode, "graph": graph and tr.use_graph, "batch": batch, "loader": loader, "bucket_mb": cap,
@@ -144,6 +149,41 @@ def parse(path: str) -> dict:
             "streams": sorted({k[2] for k in ks})}
 
 
+MARKER = "lenet_add_i64_kernel"
+
+
+def phases(path: str, steps: int) -> dict:
+    """Per-kernel stats of a --trace run's kernel trace split at the two phase markers (see run):
+    set-up (engine construction, graph capture, warm-up steps) / the timed steps / after, so the
+    step's own kernels are not mixed with set-up copies and fills."""
+    ks = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    ks.sort()
+    marks = [i for i, k in enumerate(ks) if MARKER in k[2]]
+    if len(marks) < 2:
+        return {"error": f"found {len(marks)} phase markers ({MARKER}), need 2"}
+    a, b = marks[-2], marks[-1]
+    out = {}
+    for name, sel in (("setup", ks[:a]), ("steps", ks[a + 1:b]), ("after", ks[b + 1:])):
+        agg: dict = {}
+        for s, e, n in sel:
+            c = agg.setdefault(n[:110], [0, 0])
+            c[0] += 1
+            c[1] += e - s
+        out[name] = {"kernels": len(sel), "busy_us": round(sum(v[1] for v in agg.values()) / 1e3, 2),
+                     "by_kernel": {n: {"calls": v[0], "total_us": round(v[1] / 1e3, 2),
+                                       "per_step_calls": round(v[0] / steps, 2) if name == "steps" else None,
+                                       "avg_us": round(v[1] / v[0] / 1e3, 3)}
+                                   for n, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}}
+    st = ks[a + 1:b]
+    if st:
+        out["steps"]["window_us"] = round((st[-1][1] - st[0][0]) / 1e3, 2)
+        out["steps"]["us_per_step"] = round((st[-1][1] - st[0][0]) / 1e3 / steps, 2)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
@@ -153,11 +193,15 @@ def main() -> None:
     ap.add_argument("--mode", default="overlap", help="--trace: nocomm / overlap / serial")
     ap.add_argument("--bucket-mb", type=float, default=0.01, help="--trace: bucket cap")
     ap.add_argument("--parse", help="run_kernel_trace.csv of a --trace run")
+    ap.add_argument("--phases", help="run_kernel_trace.csv of a --trace run: per-kernel stats of set-up vs steps")
     ap.add_argument("--graph", choices=["both", "eager", "graph"], default="both")
     ap.add_argument("--loader", action="store_true", help="gather a new batch per step (bound DeviceLoader)")
     a = ap.parse_args()
     if a.parse:
         print(json.dumps(parse(a.parse)))
+        return
+    if a.phases:
+        print(json.dumps(phases(a.phases, 20), indent=1))
         return
     only = None
     if a.trace:

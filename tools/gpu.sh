@@ -106,12 +106,15 @@ task_modular() {  # the modular (per-op) engine: fusion / op tests, graph step t
   py 200 python -u tools/ddp_overlap.py --graph graph --steps 500 > $O/${T}_modddp.log 2>&1 && \
   py 200 python -u tools/ddp_overlap.py --graph graph --steps 500 --loader >> $O/${T}_modddp.log 2>&1 && \
   cd /tmp && export TMPDIR=/tmp && \
-  py 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_modkt -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt.log 2>&1
+  py 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_modkt -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt.log 2>&1 && \
+  cd $R && python3 tools/ddp_overlap.py --phases $(ls $O/${T}_modkt/*kernel_trace.csv $O/${T}_modkt/*/*kernel_trace.csv 2>/dev/null | head -1) > $O/${T}_modkt_phases.json 2>&1
 }
 
-task_modpmc() {  # one PMC pass over the modular step's kernels (instruction-fetch vs memory waits)
+task_modpmc() {  # two PMC passes over the modular step's kernels: waits / fetch, then the MFMA share
   cd /tmp && export TMPDIR=/tmp && \
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_IFETCH SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $O/${T}_modpmc -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph eager > $O/${T}_modpmc.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_IFETCH SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $O/${T}_modpmc -o run -- python3 $R/tools/ddp_overlap.py --trace --batch ${MOD_B:-64} --mode nocomm --bucket-mb 25 --graph eager > $O/${T}_modpmc.log 2>&1 && \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU --output-format csv -d $O/${T}_modpmc2 -o run -- python3 $R/tools/ddp_overlap.py --trace --batch ${MOD_B:-64} --mode nocomm --bucket-mb 25 --graph eager > $O/${T}_modpmc2.log 2>&1 && \
+  cd $R && python3 tools/kernel_counters.py --summarize $(ls $O/${T}_modpmc/*counter_collection.csv $O/${T}_modpmc/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $O/${T}_modpmc2/*counter_collection.csv $O/${T}_modpmc2/*/*counter_collection.csv 2>/dev/null | head -1) > $O/${T}_modpmc_summary.log 2>&1
 }
 
 task_abops() {  # per-op launch times of the modular step (tools/op_probe.py) for every ab/*_C.so build

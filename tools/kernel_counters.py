@@ -30,13 +30,32 @@ def run(B: int, n: int):
     torch.cuda.synchronize()
 
 
+def short_name(name: str) -> str:
+    """A kernel's function name without namespaces / template arguments / parameters."""
+    import re
+
+    if name.startswith("_Z"):  # (mangled: <length><identifier> pairs; the kernel is the longest)
+        ids, i = [], 0
+        for m in re.finditer(r"(\d+)", name):
+            n = int(m.group(1))
+            ident = name[m.end():m.end() + n]
+            if len(ident) == n and re.fullmatch(r"[A-Za-z_][A-Za-z0-9_]*", ident):
+                ids.append(ident)
+        kern = [x for x in ids if x.endswith("kernel")]
+        return (kern or ids or [name[:40]])[0] if kern else max(ids, key=len) if ids else name[:40]
+    base = re.sub(r"<.*", "", name.replace("(anonymous namespace)", "").split("(")[0])
+    return base.split("::")[-1].replace("void ", "").strip() or name[:40]
+
+
 def summarize(path: str):
+    """Per-dispatch mean of every counter per kernel (the fused step's kernels by role, every other
+    kernel -- e.g. the modular engine's -- by its short name; the runtime's copy / fill kernels out)."""
     acc = defaultdict(lambda: defaultdict(list))
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name", "")
         short = ("lenet_train" if "lenet_train" in name else "lenet_tile" if "lenet_tile" in name
-                 else "lenet_update" if "lenet_update" in name else None)
-        if short is None:
+                 else "lenet_update" if "lenet_update" in name else short_name(name))
+        if "rocclr" in name or "at::native" in name:
             continue
         acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in acc.items():
