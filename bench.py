@@ -380,14 +380,23 @@ def main(argv=None) -> int:
     # the process group (RCCL communicator) is then built on the same store
     store = rendezvous(world_size=world) if world > 1 else None
     phases["rendezvous"] = time.time() - t_mark
-    if ctx_job is not None:
-        ctx_job.join()
     # RCCL's communicator is created lazily (at its first collective: the fallback all-reduce, or
     # the fused-vs-RCCL path timing after epoch 0) with a gloo control plane for the bring-up's
     # host collectives: creating it takes 1.0-3.6 s even for one rank (tools/rccl_init_probe.py),
-    # and the fused step's gradients travel over the in-kernel IPC exchange
+    # and the fused step's gradients travel over the in-kernel IPC exchange.  Such a process
+    # group touches no GPU: it comes up here too, beside the HIP-context thread
     lazy = args.device == "cuda" and world > 1 and backend in (None, "nccl") and not args.eager_rccl
-    ctx = init_distributed(world_size=world, device=args.device, backend=backend, store=store, lazy_rccl=lazy)
+    ctx = None
+    if lazy:
+        ctx = init_distributed(world_size=world, device=args.device, backend=backend, store=store, lazy_rccl=True,
+                               set_device=False)
+    phases["process_group_init"] = time.time() - t_mark
+    if ctx_job is not None:
+        ctx_job.join()
+    if ctx is None:
+        ctx = init_distributed(world_size=world, device=args.device, backend=backend, store=store)
+    elif ctx.device.type == "cuda":
+        torch.cuda.set_device(ctx.device)
     phases["process_group"] = time.time() - t_mark
     n = ctx.world_size
     if ctx.is_distributed and dist.get_world_size() != args.gpus:

@@ -104,12 +104,14 @@ def rendezvous(world_size: int | None = None, rank: int | None = None, timeout_s
 def init_distributed(rank: int | None = None, world_size: int | None = None, local_rank: int | None = None,
                      backend: str | None = None, master_addr: str | None = None, master_port: int | None = None,
                      device: str | None = None, timeout_s: float = 600.0, store=None,
-                     lazy_rccl: bool = False) -> DistContext:
+                     lazy_rccl: bool = False, set_device: bool = True) -> DistContext:
     """Initialise the default process group (if world_size > 1) and pick this rank's device.
     ``store``: a store from :func:`rendezvous` (the process group is built on it: no second
     rendezvous).  ``lazy_rccl`` (RCCL backend): no eager communicator -- it is created at the
     first RCCL collective -- and a gloo group over every rank becomes the context's control
-    plane (``DistContext.control``)."""
+    plane (``DistContext.control``).  ``set_device=False``: leave torch.cuda.set_device to the
+    caller (a lazy-RCCL process group touches no GPU, so it can come up while another thread
+    creates the HIP context)."""
     world_size = world_size if world_size is not None else env_int("WORLD_SIZE", 1)
     rank = rank if rank is not None else env_int("RANK", None)
     local_rank = local_rank if local_rank is not None else env_int("LOCAL_RANK", None)
@@ -124,7 +126,8 @@ def init_distributed(rank: int | None = None, world_size: int | None = None, loc
         if ngpu == 0:
             raise RuntimeError("device=cuda requested but no GPU is visible")
         dev = torch.device("cuda", local_rank % ngpu)
-        torch.cuda.set_device(dev)
+        if set_device:
+            torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
     be = None

@@ -81,8 +81,9 @@ def test_scaling_report_predicts_time_elapsed():
     te = sr.predict_time_elapsed(by_n, pred, cpu, reh, rccl, terms)
     base = 0.1 + 0.05 + 0.2 + 0.01
     assert abs(te[1] - (0.2 + base + 0.05)) < 1e-9
-    # N = 2: the rendezvous hides under the context wait; N = 8: it is longer
+    # N = 2: rendezvous + process group (0.1 + 0.02) hide under the context wait, then the RCCL
+    # term; N = 8: they are longer (0.3 + 0.05)
     assert abs(te[2] - (0.2 + 0.05 + base + 0.06 + 0.05 + 938 * 0.5e-6)) < 1e-9
-    assert abs(te[8] - (0.3 + 0.05 + base + 0.06 + 0.05)) < 1e-9  # step_8 = 13 + 1 hop = step_1
+    assert abs(te[8] - (0.35 + 0.05 + base + 0.06 + 0.05)) < 1e-9  # step_8 = 13 + 1 hop = step_1
     assert set(terms) == {1, 2, 8} and abs(terms[8]["total"] - te[8]) < 1e-12
     assert sr.predict_time_elapsed({}, pred, cpu, reh) == {}

@@ -144,11 +144,21 @@ def predict_time_elapsed(by_n: dict[int, dict], pred: dict[int, dict], cpu_by_n:
             # creation (bench.py: store barrier in the main thread, context in its own), then the
             # RCCL communicator is created on the store
             rdzv = c.get("rendezvous", c.get("process_group", 0.0))
-            launch = max(ctx1, rdzv) + rinit
+            # then the process group on that store: lazy RCCL + the gloo control group (what the CPU
+            # record's process_group adds to its rendezvous: a gloo group over N ranks); an eager
+            # RCCL communicator (bench.py --eager-rccl) adds --rccl-init on top
+            pg_init = max(0.0, c.get("process_group", 0.0) - c.get("rendezvous", 0.0)) if "rendezvous" in c else 0.0
+            # (rendezvous and the lazy process group both run in the main thread, beside the HIP-
+            # context thread: bench.py bring-up)
+            launch = max(ctx1, rdzv + pg_init) + rinit
         ep0 = r1["epoch0_s"] + STEPS_PER_EPOCH * (p["step_us"] - pred[1]["step_us"]) * 1e-6
         out[n] = launch + base + (xb if n > 1 else 0.0) + ep0
         if terms is not None:
-            terms[n] = {"hip_ctx_wait_1": ctx1, "rendezvous_N": rdzv, "rccl_init": rinit if n > 1 else 0.0,
+            terms[n] = {"hip_ctx_wait_1": ctx1, "rendezvous_N": rdzv,
+                        "pg_init_N": (max(0.0, (cpu_by_n.get(n) or {}).get("bringup_s", {}).get("process_group", 0.0)
+                                          - (cpu_by_n.get(n) or {}).get("bringup_s", {}).get("rendezvous", 0.0))
+                                      if n > 1 else 0.0),
+                        "rccl_init": rinit if n > 1 else 0.0,
                         "setup_1 (data_wait+engine+capture+test_upload)": base,
                         "exchange_bringup (ipc_open+self_test+path_timing)": xb if n > 1 else 0.0,
                         "epoch0_N": ep0, "total": out[n]}
@@ -293,7 +303,9 @@ def main(argv=None) -> int:
                     help="bench.py --device cpu --gpus N JSON lines (spawn / import / rendezvous at N ranks)")
     ap.add_argument("--rehearsal", help="a 2-rank gloo GPU rehearsal's JSON line (exchange bring-up phases; "
                                         "run with CSED_TIME_PATHS=1 so the path selection is timed too)")
-    ap.add_argument("--rccl-init", help="tools/rccl_init_probe.py output (the RCCL communicator's creation)")
+    ap.add_argument("--rccl-init", help="tools/rccl_init_probe.py output: the RCCL communicator's creation, added "
+                                         "for an eager-RCCL bring-up (bench.py --eager-rccl); the default creates "
+                                         "it lazily, after the span")
     a = ap.parse_args(argv)
     by_n = load_records(a.inputs)
     if not by_n:
@@ -320,9 +332,9 @@ def main(argv=None) -> int:
         for n, t in sorted(terms.items()):
             md += f"| {n} | " + " | ".join(f"{v:.4f}" for v in t.values()) + " |\n"
         md += ("\nSources: hip_ctx_wait_1, setup_1 and epoch0 from the N = 1 GPU record; rendezvous_N from "
-               "`bench.py --gpus N --device cpu` (N concurrent processes: their import skew); rccl_init from "
-               "tools/rccl_init_probe.py (one rank: the fixed part of the communicator's creation, a lower "
-               "bound at N ranks); exchange_bringup from the 2-rank gloo rehearsal with CSED_TIME_PATHS=1; "
+               "`bench.py --gpus N --device cpu` under torchrun (N concurrent processes: their import skew) and "
+               "pg_init_N its process-group creation (gloo over N ranks: the control plane); rccl_init (only "
+               "with --rccl-init: an eager RCCL bring-up) from tools/rccl_init_probe.py; exchange_bringup from the 2-rank gloo rehearsal with CSED_TIME_PATHS=1; "
                "epoch0_N at the predicted step.\n")
     out.with_suffix(".md").write_text(md)
     png = plot(rows, out.with_suffix(".png"), a.title)
