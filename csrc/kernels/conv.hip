@@ -39,6 +39,7 @@ struct ConvGeo {
   int TR;                // output rows per block
   int PR, PW;            // patch rows / cols in LDS
   int bands;             // blocks per image
+  int items;             // N * bands (image, band) work items; a launch of fewer blocks walks them
   int Hp, Wp;            // pooled input dims (a.pidx set: the input is given max-pooled)
 };
 
@@ -91,7 +92,7 @@ template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 25
 // NTHR: the block size (512 for a standalone launch: two waves per SIMD interleave the staging's
 // long instruction stream; 256 inside the merged backward kernel)
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& g, const int blk,
-                                              unsigned char* __restrict__ smem) {
+                                              unsigned char* __restrict__ smem, const bool stage_w = true) {
   typedef typename Mfma<T>::frag frag;
   typedef typename Stor<T>::S S;
   const int LDW = g.Kp + 8;                         // 16-B aligned row pad
@@ -202,7 +203,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   // (wave-uniform: a wave that owns no weight column -- conv1's Kp = 32 of 512 threads -- skips the
   // weight batch; the loads were unconditional at clamped addresses, pure VALU / address cost)
   const int wave0 = tid & ~63;
-  if (wfast && (wave0 < g.Kp || (wcols > 1 && wave0 + NTHR < g.Kp))) {
+  // (stage_w false: a later work item of a persistent block -- the weights and the k -> patch
+  // offsets are still in LDS from its first item)
+  if (stage_w && wfast && (wave0 < g.Kp || (wcols > 1 && wave0 + NTHR < g.Kp))) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < wcols && tid + NTHR * i < g.Kp) wcol(tid + NTHR * i, wb[i], wko[i]);
@@ -246,7 +249,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   }
 
   // ---- LDS stores of the first round, then any further rounds
-  if (wfast) {
+  if (!stage_w) {
+  } else if (wfast) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < wcols && tid + NTHR * i < g.Kp) koff[tid + NTHR * i] = wko[i];
@@ -429,12 +433,21 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 // conv1 fwd at B = 64 10.8 -> 9.6 us; large grids: 256, more blocks per CU -- 512 there was slower)
 // RB: patch rows per thread per staging batch -- the host picks 4 when the geometry needs no more
 // (an unrolled batch's unused rows are VALU issue, the stagings' bound), else 8 (more: extra rounds)
+// A block walks work items blockIdx.x, + gridDim.x, ... (conv_launch_grid: at large batch fewer,
+// persistent blocks): the weights and the k -> patch offsets are staged into LDS once, for the
+// first item, and only each item's patch and epilogue operands after that.  (One block per item
+// restaged the same weight tile in every block -- conv2's data gradient at B = 4096: 8192 blocks
+// x 16 KB of weights through the index math, the modular step's longest kernel, profiles/r6.)
 template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8>
 __global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blockIdx.x, smem);
-  else if (g.Cop == 32) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 2>(a, g, blockIdx.x, smem);
-  else conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blockIdx.x, smem);
+  for (int blk = blockIdx.x; blk < g.items; blk += gridDim.x) {
+    const bool first = blk == (int)blockIdx.x;
+    if (!first) __syncthreads();  // (the previous item's MFMA reads of the patch are done)
+    if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blk, smem, first);
+    else if (g.Cop == 32) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 2>(a, g, blk, smem, first);
+    else conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blk, smem, first);
+  }
 }
 
 // ------------------------------------------------------------- wgrad ----
@@ -834,6 +847,10 @@ hipError_t with_in_type(int dt, F&& f) {
 
 }  // namespace
 
+// Blocks of a forward / data-gradient launch: at most 8 per CU (one full wave of the chip for the
+// narrow 256-thread form); more work items are walked by these blocks (conv_fwd_kernel).
+constexpr int kConvPersistBlocks = 8 * 256;
+
 // Geometry + LDS bytes of a forward / data-gradient launch (hipSuccess with grid 0: nothing to do).
 static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid) {
   grid = 0;
@@ -862,8 +879,10 @@ static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid
   g.Cop = rup(g.Co, 16);
   g.PW = g.W + 2 * g.pad;
   if (g.PW > 256) return hipErrorInvalidConfiguration;  // (patch staging: one column per thread)
-  // ~128 output pixels per block, LDS-limited
+  // ~128 output pixels per block, LDS-limited; at large batch (more than ~8 blocks per CU of
+  // images x bands) whole images per work item: a band's patch restages KH - 1 halo rows
   int tr = std::max(1, std::min(g.OH, (128 + g.OW - 1) / g.OW));
+  if ((int64_t)a.N * ((g.OH + tr - 1) / tr) > kConvPersistBlocks) tr = g.OH;
   int bands = (g.OH + tr - 1) / tr;
   tr = (g.OH + bands - 1) / bands;
   if (a.pool_k == 2 && (tr & 1)) tr += 1;
@@ -878,7 +897,8 @@ static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid
   g.PR = tr + g.KH - 1;
   g.bands = (g.OH + tr - 1) / tr;
   lds = lds_bytes(tr);
-  grid = a.N * g.bands;
+  g.items = a.N * g.bands;
+  grid = std::min(g.items, kConvPersistBlocks);  // (persistent blocks past one full wave of the chip)
   return hipSuccess;
 }
 

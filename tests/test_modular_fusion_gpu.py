@@ -466,3 +466,72 @@ def test_shared_weights_with_destinations_match_cpu(defer):
         ops.set_compute_dtype(torch.bfloat16)
         fn.set_defer_wgrad_reduce(True)
         _drop_destinations(flat)
+
+
+@pytest.mark.parametrize("kind", ["fwd_pool", "fwd_plain", "dgrad", "dgrad_pooled"])
+def test_conv_persistent_blocks_match_per_item_launches_bitwise(kind):
+    """Large batches: the conv forward / data-gradient launch runs at most 2048 persistent blocks that
+    walk the (image, band) items with the weights staged once per block (conv.hip conv_fwd_kernel).
+    A batch of 2100 images (items > blocks) must give the same bits as the same images launched in
+    chunks of 500 (one block per item), and match an fp32 reference."""
+    g = torch.Generator(device=DEV).manual_seed(17)
+    N = 2100
+    o = _native.ops()
+    if kind.startswith("fwd"):
+        x = torch.randn(N, 1, 28, 28, device=DEV, generator=g).to(torch.bfloat16)
+        w = torch.randn(10, 1, 5, 5, device=DEV, generator=g) * 0.3
+        b = torch.randn(10, device=DEV, generator=g) * 0.1
+        pool = kind == "fwd_pool"
+
+        def run(xx):
+            if pool:
+                y = torch.empty(xx.shape[0], 10, 12, 12, device=DEV, dtype=torch.bfloat16)
+                idx = torch.empty(y.shape, device=DEV, dtype=torch.uint8)
+                o.conv2d_fwd(xx, w, b, y, 0, idx, None, 2, MF[torch.bfloat16])
+                return y, idx
+            y = torch.empty(xx.shape[0], 10, 24, 24, device=DEV, dtype=torch.bfloat16)
+            o.conv2d_fwd(xx, w, b, y, 0, None, None, 0, MF[torch.bfloat16])
+            return (y,)
+
+        full = run(x)
+        parts = [run(x[i:i + 500]) for i in range(0, N, 500)]
+        for j, t in enumerate(full):
+            assert torch.equal(t, torch.cat([p[j] for p in parts])), j
+        ref = F.conv2d(x.float().cpu(), w.to(torch.bfloat16).float().cpu(), b.cpu())
+        if pool:
+            ref = F.relu(F.max_pool2d(ref, 2))
+        err = (full[0].float().cpu() - ref).abs().max().item()
+        assert err <= 3e-2 * ref.abs().max().item(), err
+    else:
+        w = torch.randn(20, 10, 5, 5, device=DEV, generator=g) * 0.2
+        if kind == "dgrad":
+            dy = torch.randn(N, 20, 8, 8, device=DEV, generator=g).to(torch.bfloat16)
+
+            def run(d):
+                dx = torch.empty(d.shape[0], 10, 12, 12, device=DEV, dtype=torch.bfloat16)
+                o.conv2d_dgrad(d, w, dx, 0, MF[torch.bfloat16])
+                return dx
+
+            full = run(dy)
+            parts = torch.cat([run(dy[i:i + 500]) for i in range(0, N, 500)])
+            assert torch.equal(full, parts)
+            ref = torch.nn.grad.conv2d_input((N, 10, 12, 12), w.to(torch.bfloat16).float().cpu(), dy.float().cpu())
+            err = (full.float().cpu() - ref).abs().max().item()
+            assert err <= 3e-2 * ref.abs().max().item(), err
+        else:  # the pooled backward (conv2d_bwd: dgrad launch past the merged form's grid)
+            x = torch.randn(N, 10, 12, 12, device=DEV, generator=g).to(torch.bfloat16)
+            bb = torch.randn(20, device=DEV, generator=g) * 0.1
+            scale = (torch.rand(N * 20, device=DEV, generator=g) > 0.5).float() * 2.0
+
+            def run(xx, sc):
+                y, idx = _pooled_fwd(xx, w, bb, torch.bfloat16, sc)
+                dyp = torch.ones(y.shape, device=DEV, dtype=torch.bfloat16)
+                ws = torch.empty(wgrad_workspace_elems(xx.shape[0], 10, 5, 5, 20), device=DEV)
+                dw, db = torch.empty_like(w), torch.empty_like(bb)
+                dx = torch.empty_like(xx)
+                o.conv2d_bwd(xx, dyp, w, dw, db, ws, dx, 0, idx, y, sc, MF[torch.bfloat16])
+                return dx
+
+            full = run(x, scale)
+            parts = torch.cat([run(x[i:i + 500], scale[i * 20:(i + 500) * 20]) for i in range(0, N, 500)])
+            assert torch.equal(full, parts)

@@ -107,7 +107,9 @@ task_modular() {  # the modular (per-op) engine: fusion / op tests, graph step t
   py 200 python -u tools/ddp_overlap.py --graph graph --steps 500 --loader >> $O/${T}_modddp.log 2>&1 && \
   cd /tmp && export TMPDIR=/tmp && \
   py 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_modkt -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 64 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt.log 2>&1 && \
-  cd $R && python3 tools/ddp_overlap.py --phases $(ls $O/${T}_modkt/*kernel_trace.csv $O/${T}_modkt/*/*kernel_trace.csv 2>/dev/null | head -1) > $O/${T}_modkt_phases.json 2>&1
+  cd $R && python3 tools/ddp_overlap.py --phases $(ls $O/${T}_modkt/*kernel_trace.csv $O/${T}_modkt/*/*kernel_trace.csv 2>/dev/null | head -1) > $O/${T}_modkt_phases.json 2>&1 && \
+  cd /tmp && py 300 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_modkt4096 -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 4096 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt4096.log 2>&1 && \
+  cd $R && python3 tools/ddp_overlap.py --phases $(ls $O/${T}_modkt4096/*kernel_trace.csv $O/${T}_modkt4096/*/*kernel_trace.csv 2>/dev/null | head -1) > $O/${T}_modkt4096_phases.json 2>&1
 }
 
 task_modpmc() {  # two PMC passes over the modular step's kernels: waits / fetch, then the MFMA share
