@@ -189,6 +189,13 @@ def _watched(t) -> bool:
     return t is not None and bool(getattr(t, "_post_accumulate_grad_hooks", None) or getattr(t, "_backward_hooks", None))
 
 
+def _unpool_min_batch(with_dx: bool) -> int:
+    """Smallest batch whose pooled conv backward materialises dL/dconv first (CSED_UNPOOL_MIN_BATCH
+    / CSED_UNPOOL_MIN_BATCH_WGRAD; the fused expansion stays below: one launch fewer)."""
+    v = os.environ.get("CSED_UNPOOL_MIN_BATCH" if with_dx else "CSED_UNPOOL_MIN_BATCH_WGRAD")
+    return int(v) if v else (1024 if with_dx else 1 << 30)
+
+
 # ----------------------------------------------------------------- conv ----
 class _Conv2d(torch.autograd.Function):
     @staticmethod
@@ -230,6 +237,13 @@ class _Conv2d(torch.autograd.Function):
             if dy.dtype != y.dtype:
                 dy = dy.to(y.dtype)
             pooled = (idx, y, chscale)
+            if x.shape[0] >= _unpool_min_batch(ctx.needs_input_grad[0]):
+                # large batch: dL/dconv materialised once (one elementwise launch) instead of every
+                # weight- / data-gradient block expanding the pooled gradient on load -- 4 loads
+                # (value, argmax, gate, scale) per patch element, in dependent rounds
+                dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)
+                _ops().maxpool_relu_bwd(dy, y, idx, chscale, dconv, 2)
+                dy, pooled = dconv, (None, None, None)
         else:
             x, w = ctx.saved_tensors
             pooled = (None, None, None)

@@ -360,12 +360,55 @@ __global__ void maxpool_relu_bwd_kernel(const TD* __restrict__ dout, const TO* _
   dx[i] = from_f32<TX>(g);
 }
 
+// 2x2 windows with even H, W: one thread per POOLED element writing its window's four dx values
+// (the one-thread-per-input-element form above does three 64-bit divisions per element: 22 us for
+// the modular step's [4096, 20, 8, 8] conv2 gradient, profiles/r6/modular).  A block takes whole
+// (n, c) planes, so the index math is 32-bit divisions by the block-uniform plane size.
+template <typename TD, typename TX>
+__global__ void maxpool2_relu_bwd_kernel(const TD* __restrict__ dout, const TX* __restrict__ out,
+                                         const uint8_t* __restrict__ idx, const float* __restrict__ chscale,
+                                         TX* __restrict__ dx, int planes, int PH, int PW) {
+  const int per = PH * PW;
+  const int ppb = max(1, (int)blockDim.x / per);  // planes per block
+  for (int t = threadIdx.x; t < ppb * per; t += blockDim.x) {
+    const int q = t / per;
+    const int pl = blockIdx.x * ppb + q;
+    if (pl >= planes) break;
+    const int r = t - q * per, ph = r / PW, pw = r - ph * PW;
+    const int64_t o = (int64_t)pl * per + r;
+    const int sel = idx[o];
+    const float g = to_f32(out[o]) > 0.f ? to_f32(dout[o]) * (chscale ? chscale[pl] : 1.f) : 0.f;
+    TX* d = dx + (int64_t)pl * 4 * per + (2 * ph) * (2 * PW) + 2 * pw;
+    d[0] = from_f32<TX>(sel == 0 ? g : 0.f);
+    d[1] = from_f32<TX>(sel == 1 ? g : 0.f);
+    d[2 * PW] = from_f32<TX>(sel == 2 ? g : 0.f);
+    d[2 * PW + 1] = from_f32<TX>(sel == 3 ? g : 0.f);
+  }
+}
+
 hipError_t launch_maxpool_relu_bwd(const void* dout, int dout_dtype, const void* out, int out_dtype,
                                    const uint8_t* idx, const float* chscale, void* dx, int dx_dtype,
                                    int N, int C, int H, int W, int k, hipStream_t s) {
   int64_t total = (int64_t)N * C * H * W;
   if (total == 0) return hipSuccess;
   if (out_dtype != dx_dtype) return hipErrorInvalidValue;
+  if (k == 2 && !(H & 1) && !(W & 1) && (int64_t)N * C < INT32_MAX) {
+    const int planes = N * C, PH = H / 2, PW = W / 2, ppb = std::max(1, 256 / (PH * PW));
+    const dim3 grid(cdiv(planes, ppb));
+    CSED_DISPATCH_FLOAT(dx_dtype, {
+      typedef scalar_t TX;
+      if (dout_dtype == kF32) {
+        hipLaunchKernelGGL((maxpool2_relu_bwd_kernel<float, TX>), grid, dim3(256), 0, s, (const float*)dout,
+                           (const TX*)out, idx, chscale, (TX*)dx, planes, PH, PW);
+      } else if (dout_dtype == dx_dtype) {
+        hipLaunchKernelGGL((maxpool2_relu_bwd_kernel<TX, TX>), grid, dim3(256), 0, s, (const TX*)dout,
+                           (const TX*)out, idx, chscale, (TX*)dx, planes, PH, PW);
+      } else {
+        return hipErrorInvalidValue;
+      }
+    });
+    return hipGetLastError();
+  }
   CSED_DISPATCH_FLOAT(dx_dtype, {
     typedef scalar_t TX;
     if (dout_dtype == kF32) {

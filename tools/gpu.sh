@@ -230,6 +230,15 @@ task_diag() {  # the data-parallel diagnostics: rejected-exchange benches, dpche
   py 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29531 -m csed_514_project_distributed_training_using_pytorch_amd.parallel.dpcheck --backend gloo --steps 8 > $O/${T}_dpcheck2.log 2>&1
 }
 
+task_conv4096() {  # the per-op conv kernels at large batch: fusion tests, B = 4096 step times, phase-split trace
+  cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_kernels_gpu.py -x -v --timeout 200 --timeout-method thread > $O/${T}_convtests.log 2>&1 && \
+  py 300 python -u tools/ddp_overlap.py --batch 4096 --steps 50 --graph graph > $O/${T}_mod4096.log 2>&1 && \
+  CSED_UNPOOL_MIN_BATCH=1000000 py 300 python -u tools/ddp_overlap.py --batch 4096 --steps 50 --graph graph > $O/${T}_mod4096_fusedpool.log 2>&1 && \
+  py 300 python -u tools/conv_stamps.py --batch 4096 > $O/${T}_convstamps4096.log 2>&1 && \
+  cd /tmp && py 300 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_modkt4096 -o run -- python3 $R/tools/ddp_overlap.py --trace --batch 4096 --mode nocomm --bucket-mb 25 --graph graph > $O/${T}_modkt4096.log 2>&1 && \
+  cd $R && python3 tools/ddp_overlap.py --phases $(ls $O/${T}_modkt4096/*kernel_trace.csv $O/${T}_modkt4096/*/*kernel_trace.csv 2>/dev/null | head -1) > $O/${T}_modkt4096_phases.json 2>&1
+}
+
 task_quick() {  # the test files this round's changes touch
   cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_modular_graph_gpu.py tests/test_fused_gpu.py tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > $O/${T}_quick.log 2>&1
 }
