@@ -34,15 +34,16 @@ def short_name(name: str) -> str:
     """A kernel's function name without namespaces / template arguments / parameters."""
     import re
 
-    if name.startswith("_Z"):  # (mangled: <length><identifier> pairs; the kernel is the longest)
-        ids, i = [], 0
-        for m in re.finditer(r"(\d+)", name):
-            n = int(m.group(1))
-            ident = name[m.end():m.end() + n]
-            if len(ident) == n and re.fullmatch(r"[A-Za-z_][A-Za-z0-9_]*", ident):
-                ids.append(ident)
-        kern = [x for x in ids if x.endswith("kernel")]
-        return (kern or ids or [name[:40]])[0] if kern else max(ids, key=len) if ids else name[:40]
+    if name.startswith("_Z"):  # mangled: _ZN <len><id> ... (the last id is the function) or _Z <len><id>
+        i = 3 if name.startswith("_ZN") else 2
+        last = None
+        while i < len(name) and name[i].isdigit():
+            j = i
+            while j < len(name) and name[j].isdigit():
+                j += 1
+            n = int(name[i:j])
+            last, i = name[j:j + n], j + n
+        return last or name[:40]
     base = re.sub(r"<.*", "", name.replace("(anonymous namespace)", "").split("(")[0])
     return base.split("::")[-1].replace("void ", "").strip() or name[:40]
 
