@@ -398,6 +398,11 @@ def main(argv=None) -> int:
     elif ctx.device.type == "cuda":
         torch.cuda.set_device(ctx.device)
     phases["process_group"] = time.time() - t_mark
+    if args.device == "cuda" and os.environ.get("CSED_BENCH_STREAM") == "1":
+        # every launch of this rank on one created stream instead of the null stream (A/B knob)
+        t_mark = time.time()
+        torch.cuda.set_stream(torch.cuda.Stream(ctx.device))
+        phases["work_stream"] = time.time() - t_mark
     n = ctx.world_size
     if ctx.is_distributed and dist.get_world_size() != args.gpus:
         raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
@@ -518,7 +523,13 @@ def main(argv=None) -> int:
             # a path timing deferred by the lazy-RCCL bring-up (fused exchange vs RCCL all-reduce;
             # collective, creates the RCCL communicator): outside the span, before anything timed
             t_mark = time.time()
-            switched = eng.select_path()
+            try:
+                switched = eng.select_path()
+            except Exception as e:  # (e.g. the RCCL communicator could not be created: the fused
+                # exchange, self-tested on every rank, stays; the JSON says why)
+                print(f"[bench] path selection failed ({e!r}); keeping {eng.allreduce_kind}", file=sys.stderr)
+                eng.exchange_note = f"{eng.exchange_note}; path timing failed: {type(e).__name__}: {e}"
+                switched = False
             ph["path_select"] = time.time() - t_mark
             if use_graph:  # the timed window's graphs (outside the span: not epoch-0 work)
                 t_mark = time.time()

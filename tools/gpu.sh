@@ -219,7 +219,8 @@ task_graphab() {  # native HipGraph vs torch.cuda.CUDAGraph step graphs, alterna
                  # GRAPH_AB: native nativeflags nativeupload torch)
   cd $R && rm -f $O/${T}_graphab.log && \
   for i in 1 2 3; do for v in ${GRAPH_AB:-native torch}; do
-    case $v in native) E=CSED_NATIVE_GRAPH=1;; nativeflags) E="CSED_NATIVE_GRAPH=1 CSED_GRAPH_FLAGS=1";; nativeupload) E="CSED_NATIVE_GRAPH=1 CSED_GRAPH_UPLOAD=1";; *) E=CSED_NATIVE_GRAPH=0;; esac
+    case $v in native) E=CSED_NATIVE_GRAPH=1;; nativeflags) E="CSED_NATIVE_GRAPH=1 CSED_GRAPH_FLAGS=1";; nativeupload) E="CSED_NATIVE_GRAPH=1 CSED_GRAPH_UPLOAD=1";;
+      stream) E=CSED_BENCH_STREAM=1;; nativestream) E="CSED_NATIVE_GRAPH=1 CSED_BENCH_STREAM=1";; *) E=CSED_NATIVE_GRAPH=0;; esac
     echo "$v driver $(env $E timeout -k 10 100 python bench.py --gpus 1 --steps 20 --warmup 5 --no-fp32-record 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["ms_per_step"], d["time_elapsed_s"], d["epoch_s"])')" >> $O/${T}_graphab.log || return 1
     echo "$v long $(env $E timeout -k 10 100 python bench.py --steps 3000 --warmup 300 --no-epoch --no-fp32-record 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["ms_per_step"])')" >> $O/${T}_graphab.log || return 1
   done; done
