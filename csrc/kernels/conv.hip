@@ -23,6 +23,8 @@
 // MFMA C layout (row = 4*(lane>>4) + reg) every lane then holds one complete
 // 2x2 window of one channel in its 4 accumulators, so the max-pool, argmax,
 // ReLU and channel scale happen in registers with no shuffles.
+#include <type_traits>
+
 #include "common.h"
 #include "dispatch.h"
 
@@ -42,6 +44,13 @@ struct ConvGeo {
   int items;             // N * bands (image, band) work items; a launch of fewer blocks walks them
   int Hp, Wp;            // pooled input dims (a.pidx set: the input is given max-pooled)
 };
+
+// LDS of a forward / data-gradient block: the weight image [Cop][Kp + 8], the k -> patch offsets
+// [Kp], the patch [Ci][PR][PW] (element size es), then at this 16-byte aligned offset the epilogue
+// operands [2][Cop] floats (conv_geo's lds_bytes)
+__host__ __device__ inline int conv_ep_offset(const ConvGeo& g, int es) {
+  return (g.Cop * (g.Kp + 8) * es + g.Kp * 4 + g.Ci * g.PR * g.PW * es + 15) & ~15;
+}
 
 // a / d for small non-negative ints (0 <= a < 2^20, d >= 1): (a + 0.5) * rcp(d) truncated.  v_rcp_f32
 // is within 1 ulp, so the product's relative error (< 1.5 * 2^-23) stays below the 0.5 / d margin
@@ -99,6 +108,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   S* Ws = (S*)smem;                                 // [Cop][LDW]
   int* koff = (int*)(Ws + g.Cop * LDW);             // [Kp]
   S* patch = (S*)(koff + g.Kp);                     // [Ci][PR][PW]
+  float* EPB = (float*)(smem + conv_ep_offset(g, sizeof(S)));  // [Cop] bias, then [Cop] channel scale
+  float* EPS = EPB + g.Cop;
 
   const int n = blk / g.bands, band = blk % g.bands;
   const int oh0 = band * g.TR;
@@ -132,7 +143,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
   int wb[2] = {-1, -1};
   int wko[2] = {0, 0};
   float wv[WB];
-  float eb[4], es[4];
+  float ebv = 0.f, esv = 1.f;  // epilogue operands of channel tid (staged into EPB / EPS)
 
   // the zero-padded input patch: a thread owns one patch column, rows step by NTHR / PW.
   // Addresses: per-image base pointers (scalar) + 32-bit element offsets advanced incrementally.
@@ -219,34 +230,26 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       wv[j] = ok ? t : 0.f;
     }
   }
-  {  // epilogue operands of this lane's channels (N-tiles 0..3)
+  {  // epilogue operands of channel tid: bias and channel scale, staged into LDS with the patch so
+     // that the M-tile loop below issues no global load.  (A load there -- the operands of channels
+     // past the first 64, read in the epilogue -- made the compiler wait vmcnt(0) in every K-step,
+     // and vmcnt counts stores too: each M-tile waited for the previous tile's output stores to be
+     // acknowledged, 1-3k cycles: conv1 forward at B = 4096 spent 13.9k cycles per image there.)
     const float* bp = a.bias ? a.bias : a.w;        // (a valid address when absent: loads stay
     const float* cp = a.chscale ? a.chscale : a.w;  // unconditional, no branch + wait per element)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      eb[j] = 0.f;
-      es[j] = 1.f;
-      if (j >= NT) continue;  // (uniform: N-tiles past the channels' -- conv1 has 1 of 4)
-      const int oc = j * 16 + (tid & 15);
-      const bool ok = oc < g.Co;
-      const float tb = bp[(unsigned)(ok ? oc : 0)], tc = cp[(unsigned)(ok ? n * g.Co + oc : 0)];
-      eb[j] = ok && a.bias ? tb : 0.f;
-      es[j] = ok && a.chscale ? tc : 1.f;
-    }
+    const bool ok = tid < g.Co;
+    const float tb = bp[(unsigned)(ok ? tid : 0)], tc = cp[(unsigned)(ok ? n * g.Co + tid : 0)];
+    ebv = ok && a.bias ? tb : 0.f;
+    esv = ok && a.chscale ? tc : 1.f;
   }
   const uint64_t drop_off = a.chscale_out ? rng_offset(a.offset, a.offset_dev) : 0;
   __builtin_amdgcn_sched_barrier(0);
   CONV_STAMP(1);
 
   // ---- while the loads fly: the Dropout2d draw (channel_mask_kernel's draw, index n*Co + oc)
-  if (a.chscale_out) {
-    const float keep_sc = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int oc = j * 16 + (tid & 15);
-      es[j] = j < NT && oc < g.Co && dropout_keep(a.seed, drop_off, (uint64_t)n * g.Co + oc, a.drop_p) ? keep_sc : 0.f;
-    }
-  }
+  const float keep_sc = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+  if (a.chscale_out)
+    esv = tid < g.Co && dropout_keep(a.seed, drop_off, (uint64_t)n * g.Co + tid, a.drop_p) ? keep_sc : 0.f;
 
   // ---- LDS stores of the first round, then any further rounds
   if (!stage_w) {
@@ -279,6 +282,21 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     }
   }
   store_rows();
+  if (tid < g.Cop) {
+    EPB[tid] = ebv;
+    EPS[tid] = esv;
+  }
+  if (a.chscale_out && band == 0 && tid < g.Co) a.chscale_out[(int64_t)n * g.Co + tid] = esv;  // once per (n, oc)
+  for (int c = tid + NTHR; c < g.Cop; c += NTHR) {  // (more channels than threads: rare, once per item)
+    const bool ok = c < g.Co;
+    float b = ok && a.bias ? a.bias[c] : 0.f, s = ok && a.chscale ? a.chscale[(int64_t)n * g.Co + c] : 1.f;
+    if (a.chscale_out) {
+      s = ok && dropout_keep(a.seed, drop_off, (uint64_t)n * g.Co + c, a.drop_p) ? keep_sc : 0.f;
+      if (band == 0 && ok) a.chscale_out[(int64_t)n * g.Co + c] = s;
+    }
+    EPB[c] = b;
+    EPS[c] = s;
+  }
   while (prow && rr < nrows) {
     load_rows();
     store_rows();
@@ -289,142 +307,139 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 
   const int lane = tid & 63, wave = tid >> 6;
   const int mtiles = (npix + 15) >> 4;
-  const int pooled = a.pool_k == 2;
-  const int PWb = g.OW >> 1;
-  for (int mt = wave; mt < mtiles; mt += NTHR / 64) {
-    // pixel owned by this lane as an A row
-    const int m = mt * 16 + (lane & 15);
-    int oh, ow;
-    if (pooled) {
-      const int p = m >> 2, q = m & 3, pq = qdiv(p, PWb);
-      oh = 2 * pq + (q >> 1);
-      ow = 2 * (p - pq * PWb) + (q & 1);
-    } else {
-      oh = qdiv(m, g.OW);
-      ow = m - oh * g.OW;
-    }
-    const bool valid = m < npix;
-    const int pb = valid ? oh * g.PW + ow : 0;     // oh is band-relative
-    for (int nc = 0; nc < NT; nc += NTM) {
-      f32x4 acc[NTM];
+  const int PWb = g.OW >> 1, PH = g.OH >> 1;
+  // this image's outputs: a scalar base pointer, then 32-bit element offsets (conv_geo bounds
+  // Co * OH * OW below 2^31); 64-bit index products per store were ~20 VALU instructions each
+  const int64_t obase = (int64_t)n * g.Co * (a.pool_k == 2 ? PH * PWb : g.OH * g.OW);
+  Y* const yimg = static_cast<Y*>(a.y) + obase;
+  uint8_t* const iimg = a.idx + (a.pool_k == 2 ? obase : 0);
+  // The M-tile loop, once per epilogue kind (pooled or plain), so that neither kind's address
+  // arithmetic is computed for the other (hoisted above a runtime branch, both were: the loop was
+  // VALU-bound, ~130 VALU instructions per M-tile against one MFMA for conv1)
+  auto mtile_loop = [&](auto pool_tag) {
+    constexpr bool pooled = decltype(pool_tag)::value;
+    for (int mt = wave; mt < mtiles; mt += NTHR / 64) {
+      // pixel owned by this lane as an A row
+      const int m = mt * 16 + (lane & 15);
+      int oh, ow;
+      if constexpr (pooled) {
+        const int p = m >> 2, q = m & 3, pq = qdiv(p, PWb);
+        oh = 2 * pq + (q >> 1);
+        ow = 2 * (p - pq * PWb) + (q & 1);
+      } else {
+        oh = qdiv(m, g.OW);
+        ow = m - oh * g.OW;
+      }
+      // (a pixel past npix reads the block's first: its accumulator row is garbage and never
+      // stored -- an MFMA row depends on its own A row only -- so no select zeroes it)
+      const int pb = m < npix ? oh * g.PW + ow : 0;     // oh is band-relative
+      for (int nc = 0; nc < NT; nc += NTM) {
+        f32x4 acc[NTM];
 #pragma unroll
-      for (int j = 0; j < NTM; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (WIDE) {
-        // Software-pipelined K loop: K-step s+1's patch gathers and weight fragments are read (LDS)
-        // while step s runs on the MFMAs, and the k -> patch offsets two steps ahead.  Every read is
-        // unconditional at a valid address (a pixel past npix reads the block's first and is zeroed
-        // after; N-tiles past NT read row 0): a predicated LDS read was a branch + wait per element.
-        const int kq8 = 8 * (lane >> 4);
-        int wrow[NTM];
-  #pragma unroll
-        for (int j = 0; j < NTM; ++j) wrow[j] = (nc + j < NT ? (nc + j) * 16 + (lane & 15) : 0) * LDW;
-        typename Stor<T>::V8 raw;
-        frag fb[NTM];
-        int4 o0 = *reinterpret_cast<const int4*>(koff + kq8);
-        int4 o1 = *reinterpret_cast<const int4*>(koff + kq8 + 4);
-        {
-          const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-  #pragma unroll
-          for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
-  #pragma unroll
-          for (int j = 0; j < NTM; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kq8);
-        }
-        {
-          const int kn = min(kq8 + 32, g.Kp - 8);  // (step 1's offsets; clamped: a valid slot)
-          o0 = *reinterpret_cast<const int4*>(koff + kn);
-          o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
-        }
-        for (int k0 = 0; k0 < g.Kp; k0 += 32) {
-          const typename Stor<T>::V8 cur = raw;
-          frag fbc[NTM];
-  #pragma unroll
-          for (int j = 0; j < NTM; ++j) fbc[j] = fb[j];
-          {  // step s+1's reads (clamped past the last step: valid slots, unused)
-            const int kb1 = min(k0 + 32, g.Kp - 32) + kq8;
+        for (int j = 0; j < NTM; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (WIDE) {
+          // Software-pipelined K loop: K-step s+1's patch gathers and weight fragments are read (LDS)
+          // while step s runs on the MFMAs, and the k -> patch offsets two steps ahead.  Every read is
+          // unconditional at a valid address (N-tiles past NT read row 0): a predicated LDS read was
+          // a branch + wait per element.
+          const int kq8 = 8 * (lane >> 4);
+          int wrow[NTM];
+#pragma unroll
+          for (int j = 0; j < NTM; ++j) wrow[j] = (nc + j < NT ? (nc + j) * 16 + (lane & 15) : 0) * LDW;
+          typename Stor<T>::V8 raw;
+          frag fb[NTM];
+          int4 o0 = *reinterpret_cast<const int4*>(koff + kq8);
+          int4 o1 = *reinterpret_cast<const int4*>(koff + kq8 + 4);
+          {
             const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-  #pragma unroll
+#pragma unroll
             for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
-  #pragma unroll
-            for (int j = 0; j < NTM; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kb1);
-            const int kn = min(k0 + 64 + kq8, g.Kp - 8);
+#pragma unroll
+            for (int j = 0; j < NTM; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kq8);
+          }
+          {
+            const int kn = min(kq8 + 32, g.Kp - 8);  // (step 1's offsets; clamped: a valid slot)
             o0 = *reinterpret_cast<const int4*>(koff + kn);
             o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
           }
-          typename Stor<T>::V8 am;
-  #pragma unroll
-          for (int j = 0; j < 8; ++j) am[j] = valid ? cur[j] : (S)0;
-          const frag fa = __builtin_bit_cast(frag, am);
-  #pragma unroll
-          for (int j = 0; j < NTM; ++j)
-            if (nc + j < NT) acc[j] = Mfma<T>::mma(fa, fbc[j], acc[j]);
+          for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+            const typename Stor<T>::V8 cur = raw;
+            frag fbc[NTM];
+#pragma unroll
+            for (int j = 0; j < NTM; ++j) fbc[j] = fb[j];
+            {  // step s+1's reads (clamped past the last step: valid slots, unused)
+              const int kb1 = min(k0 + 32, g.Kp - 32) + kq8;
+              const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+#pragma unroll
+              for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
+#pragma unroll
+              for (int j = 0; j < NTM; ++j) fb[j] = *reinterpret_cast<const frag*>(Ws + wrow[j] + kb1);
+              const int kn = min(k0 + 64 + kq8, g.Kp - 8);
+              o0 = *reinterpret_cast<const int4*>(koff + kn);
+              o1 = *reinterpret_cast<const int4*>(koff + kn + 4);
+            }
+            const frag fa = __builtin_bit_cast(frag, cur);
+#pragma unroll
+            for (int j = 0; j < NTM; ++j)
+              if (nc + j < NT) acc[j] = Mfma<T>::mma(fa, fbc[j], acc[j]);
+          }
+        } else {
+          // narrow form (large grids: fewer registers, more blocks per CU hide the LDS latency):
+          // one K-step's reads, then its MFMAs; reads unconditional at valid addresses as above
+          const int kq8 = 8 * (lane >> 4);
+          for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+            const int kb = k0 + kq8;
+            const int4 o0 = *reinterpret_cast<const int4*>(koff + kb);
+            const int4 o1 = *reinterpret_cast<const int4*>(koff + kb + 4);
+            const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            typename Stor<T>::V8 raw;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
+            const frag fa = __builtin_bit_cast(frag, raw);
+#pragma unroll
+            for (int j = 0; j < NTM; ++j) {
+              if (nc + j < NT) {
+                const frag fb = *reinterpret_cast<const frag*>(Ws + ((nc + j) * 16 + (lane & 15)) * LDW + kb);
+                acc[j] = Mfma<T>::mma(fa, fb, acc[j]);
+              }
+            }
+          }
         }
-      } else {
-        // narrow form (large grids: fewer registers, more blocks per CU hide the LDS latency):
-        // one K-step's reads, then its MFMAs; reads unconditional at valid addresses as above
-        const int kq8 = 8 * (lane >> 4);
-        for (int k0 = 0; k0 < g.Kp; k0 += 32) {
-          const int kb = k0 + kq8;
-          const int4 o0 = *reinterpret_cast<const int4*>(koff + kb);
-          const int4 o1 = *reinterpret_cast<const int4*>(koff + kb + 4);
-          const int oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-          typename Stor<T>::V8 raw;
+        // ---- epilogue (operands from LDS: no global load in this loop)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) raw[j] = patch[pb + oo[j]];
+        for (int j = 0; j < NTM; ++j) {
+          if (nc + j >= NT) continue;
+          const int oc = (nc + j) * 16 + (lane & 15);
+          if (oc >= g.Co) continue;
+          const float b = EPB[oc];
+          if constexpr (pooled) {
+            const int wbase = mt * 16 + 4 * (lane >> 4);  // first pixel of this lane's window
+            if (wbase >= npix) continue;
+            float best = acc[j][0];
+            int bi = 0;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) raw[j] = valid ? raw[j] : (S)0;
-          const frag fa = __builtin_bit_cast(frag, raw);
+            for (int r = 1; r < 4; ++r)
+              if (acc[j][r] > best) { best = acc[j][r]; bi = r; }
+            const int p = wbase >> 2, pq = qdiv(p, PWb);
+            const int o = (oc * PH + (oh0 >> 1) + pq) * PWb + (p - pq * PWb);
+            yimg[o] = (Y)(fmaxf(best + b, 0.f) * EPS[oc]);
+            iimg[o] = (uint8_t)bi;
+          } else {
+            const int ob = oc * g.OH + oh0;
 #pragma unroll
-          for (int j = 0; j < NTM; ++j) {
-            if (nc + j < NT) {
-              const frag fb = *reinterpret_cast<const frag*>(Ws + ((nc + j) * 16 + (lane & 15)) * LDW + kb);
-              acc[j] = Mfma<T>::mma(fa, fb, acc[j]);
+            for (int r = 0; r < 4; ++r) {
+              const int mm = mt * 16 + 4 * (lane >> 4) + r;
+              if (mm >= npix) continue;
+              const int mq = qdiv(mm, g.OW);
+              yimg[(ob + mq) * g.OW + (mm - mq * g.OW)] = (Y)(acc[j][r] + b);
             }
           }
         }
       }
-      // ---- epilogue
-#pragma unroll
-      for (int j = 0; j < NTM; ++j) {
-        if (nc + j >= NT) continue;
-        const int oc = (nc + j) * 16 + (lane & 15);
-        if (oc >= g.Co) continue;
-        const float b = nc == 0 ? eb[j] : (a.bias ? a.bias[oc] : 0.f);
-        if (pooled) {
-          const int wbase = mt * 16 + 4 * (lane >> 4);  // first pixel of this lane's window
-          if (wbase >= npix) continue;
-          float best = acc[j][0];
-          int bi = 0;
-#pragma unroll
-          for (int r = 1; r < 4; ++r)
-            if (acc[j][r] > best) { best = acc[j][r]; bi = r; }
-          const int p = wbase >> 2, pq = qdiv(p, PWb);
-          const int ph = (oh0 >> 1) + pq, pw = p - pq * PWb;
-          const int PH = g.OH >> 1;
-          float sc = es[j];
-          if (nc != 0) {  // (channels past the first 64: operands not preloaded)
-            sc = a.chscale ? a.chscale[(int64_t)n * g.Co + oc] : 1.f;
-            if (a.chscale_out)
-              sc = dropout_keep(a.seed, rng_offset(a.offset, a.offset_dev), (uint64_t)n * g.Co + oc, a.drop_p)
-                       ? (a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f)
-                       : 0.f;
-          }
-          if (a.chscale_out && band == 0 && wbase == 0) a.chscale_out[(int64_t)n * g.Co + oc] = sc;  // once per (n, oc)
-          const float v = fmaxf(best + b, 0.f) * sc;
-          const int64_t o = (((int64_t)n * g.Co + oc) * PH + ph) * PWb + pw;
-          static_cast<Y*>(a.y)[o] = (Y)v;
-          a.idx[o] = (uint8_t)bi;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int mm = mt * 16 + 4 * (lane >> 4) + r;
-            if (mm >= npix) continue;
-            const int mq = qdiv(mm, g.OW), ohh = oh0 + mq, oww = mm - mq * g.OW;
-            static_cast<Y*>(a.y)[(((int64_t)n * g.Co + oc) * g.OH + ohh) * g.OW + oww] = (Y)(acc[j][r] + b);
-          }
-        }
-      }
     }
-  }
+  };
+  if (a.pool_k == 2) mtile_loop(std::true_type{});
+  else mtile_loop(std::false_type{});
   CONV_STAMP(4);
 #undef CONV_STAMP
 }
@@ -438,15 +453,27 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 // first item, and only each item's patch and epilogue operands after that.  (One block per item
 // restaged the same weight tile in every block -- conv2's data gradient at B = 4096: 8192 blocks
 // x 16 KB of weights through the index math, the modular step's longest kernel, profiles/r6.)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8>
+// NTMK (narrow form): the N-tiles per accumulator group, chosen by the host from Cop (1: 16
+// channels, 2: 32, 4: more), so that one body is compiled per kernel; 0: chosen in the kernel (WIDE)
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8, int NTMK = 0>
 __global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  for (int blk = blockIdx.x; blk < g.items; blk += gridDim.x) {
-    const bool first = blk == (int)blockIdx.x;
-    if (!first) __syncthreads();  // (the previous item's MFMA reads of the patch are done)
-    if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blk, smem, first);
+  auto item = [&](int blk, bool first) {
+    if constexpr (NTMK != 0) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, NTMK>(a, g, blk, smem, first);
+    else if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blk, smem, first);
     else if (g.Cop == 32) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 2>(a, g, blk, smem, first);
     else conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blk, smem, first);
+  };
+  if constexpr (WIDE) {
+    // (small grids: one item per block, grid == items (launch_conv2d).  The item loop's live ranges
+    // across items pushed the software-pipelined form past its 256 VGPRs: 500-900 bytes of scratch)
+    item(blockIdx.x, true);
+  } else {
+    for (int blk = blockIdx.x; blk < g.items; blk += gridDim.x) {
+      const bool first = blk == (int)blockIdx.x;
+      if (!first) __syncthreads();  // (the previous item's MFMA reads of the patch are done)
+      item(blk, first);
+    }
   }
 }
 
@@ -847,9 +874,42 @@ hipError_t with_in_type(int dt, F&& f) {
 
 }  // namespace
 
-// Blocks of a forward / data-gradient launch: at most 8 per CU (one full wave of the chip for the
-// narrow 256-thread form); more work items are walked by these blocks (conv_fwd_kernel).
+// Work items above which a forward / data-gradient launch takes whole images per item (conv_geo);
+// the narrow form's blocks are then sized by persist_grid and walk the items (conv_fwd_kernel).
 constexpr int kConvPersistBlocks = 8 * 256;
+
+// CUs of the current device (cached per device)
+static int device_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// Blocks of a narrow (persistent) launch: as many as are resident on the chip at once -- the
+// kernel's occupancy at this block size and LDS -- at most one per item.  (A fixed 8 per CU with 3
+// resident -- 146 registers per lane -- ran as 2.7 rounds of blocks, each walking 2 items.)
+static int persist_grid(const void* kern, int block, size_t lds, int items) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess || per_cu <= 0) {
+    (void)hipGetLastError();
+    per_cu = 1;
+  }
+  return std::min(items, per_cu * device_cus());
+}
+
+// The narrow forward kernel's accumulator-group width for Cop output channels (conv_fwd_kernel NTMK)
+template <typename F>
+static hipError_t narrow_ntm(int Cop, F&& f) {
+  if (Cop == 16) return f(std::integral_constant<int, 1>{});
+  if (Cop == 32) return f(std::integral_constant<int, 2>{});
+  return f(std::integral_constant<int, 4>{});
+}
 
 // Geometry + LDS bytes of a forward / data-gradient launch (hipSuccess with grid 0: nothing to do).
 static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid) {
@@ -887,9 +947,10 @@ static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid
   tr = (g.OH + bands - 1) / bands;
   if (a.pool_k == 2 && (tr & 1)) tr += 1;
   const size_t es = a.mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
-  auto lds_bytes = [&](int trr) {
+  auto lds_bytes = [&](int trr) {  // (conv_ep_offset + the epilogue operands)
     const int pr = trr + g.KH - 1;
-    return (size_t)g.Cop * (g.Kp + 8) * es + (size_t)g.Kp * 4 + (size_t)g.Ci * pr * g.PW * es + 16;
+    const size_t body = (size_t)g.Cop * (g.Kp + 8) * es + (size_t)g.Kp * 4 + (size_t)g.Ci * pr * g.PW * es;
+    return (body + 15) / 16 * 16 + (size_t)g.Cop * 8;
   };
   while (tr > (a.pool_k == 2 ? 2 : 1) && lds_bytes(tr) > 96 * 1024) tr -= (a.pool_k == 2 ? 2 : 1);
   if (lds_bytes(tr) > 160 * 1024) return hipErrorInvalidConfiguration;
@@ -917,14 +978,16 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
         const dim3 block(wide ? 512 : 256);
         auto go = [&](auto kern) {
           if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-          hipLaunchKernelGGL(kern, dim3(grid), block, lds, s, a, g);
+          // (WIDE: grid == items, one item per block; narrow: persistent blocks walking the items)
+          const int gr = wide ? grid : persist_grid((const void*)kern, 256, lds, g.items);
+          hipLaunchKernelGGL(kern, dim3(gr), block, lds, s, a, g);
           return hipGetLastError();
         };
         const bool rb4 = wide && cdiv(g.Ci * g.PR, 512 / g.PW) <= 4;  // (patch rows per thread)
         if (a.pidx) return wide ? (rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, true, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, true, true>))
-                                : go(conv_fwd_kernel<scalar_t, X, Y, true, false>);
+                                : narrow_ntm(g.Cop, [&](auto k) { return go(conv_fwd_kernel<scalar_t, X, Y, true, false, 8, decltype(k)::value>); });
         return wide ? (rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, false, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, false, true>))
-                    : go(conv_fwd_kernel<scalar_t, X, Y, false, false>);
+                    : narrow_ntm(g.Cop, [&](auto k) { return go(conv_fwd_kernel<scalar_t, X, Y, false, false, 8, decltype(k)::value>); });
       });
     });
   });
@@ -1025,7 +1088,8 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
           hipError_t e2 = hipGetLastError();
           if (e2 != hipSuccess || dgrid == 0) return e2;
           if (lds_d > 64 * 1024) hipFuncSetAttribute((const void*)dgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
-          hipLaunchKernelGGL(dgr, dim3(dgrid), dim3(dw ? 512 : 256), lds_d, s, a, g);
+          const int dgr_grid = dw ? dgrid : persist_grid((const void*)dgr, 256, lds_d, g.items);
+          hipLaunchKernelGGL(dgr, dim3(dgr_grid), dim3(dw ? 512 : 256), lds_d, s, a, g);
           return hipGetLastError();
         };
         if (merged)
@@ -1035,14 +1099,14 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
                              conv_fwd_kernel<T, DY, X, false, true>);
         if (b.pidx) {
           if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, true>)
-                            : go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, false>);
+                            : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, false, 8, decltype(k)::value>); });
           return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, true>)
-                    : go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, false>);
+                    : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, false, 8, decltype(k)::value>); });
         }
         if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, true>)
-                          : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, false>);
+                          : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, false, 8, decltype(k)::value>); });
         return dw ? go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, true>)
-                  : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, false>);
+                  : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, false, 8, decltype(k)::value>); });
       });
     });
   };

@@ -240,6 +240,12 @@ task_conv4096() {  # the per-op conv kernels at large batch: fusion tests, B = 4
   cd $R && python3 tools/ddp_overlap.py --phases $(ls $O/${T}_modkt4096/*kernel_trace.csv $O/${T}_modkt4096/*/*kernel_trace.csv 2>/dev/null | head -1) > $O/${T}_modkt4096_phases.json 2>&1
 }
 
+task_modsteps() {  # the modular step at B = 64 and 4096: per-op launch times and graph step times
+  cd $R && py 200 python -u tools/op_probe.py --batch 64 > $O/${T}_op64.log 2>&1 && \
+  py 300 python -u tools/op_probe.py --batch 4096 --reps 20 > $O/${T}_op4096.log 2>&1 && \
+  py 300 python -u tools/ddp_overlap.py --batch 64 --graph graph > $O/${T}_mod64.log 2>&1
+}
+
 task_quick() {  # the test files this round's changes touch
   cd $R && py 600 python -u -m pytest tests/test_modular_fusion_gpu.py tests/test_modular_graph_gpu.py tests/test_fused_gpu.py tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > $O/${T}_quick.log 2>&1
 }
