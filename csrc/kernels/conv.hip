@@ -24,6 +24,9 @@
 // 2x2 window of one channel in its 4 accumulators, so the max-pool, argmax,
 // ReLU and channel scale happen in registers with no shuffles.
 #include <type_traits>
+#ifndef CONV_W
+#define CONV_W 5
+#endif
 
 #include "common.h"
 #include "dispatch.h"
@@ -456,7 +459,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 // NTMK (narrow form): the N-tiles per accumulator group, chosen by the host from Cop (1: 16
 // channels, 2: 32, 4: more), so that one body is compiled per kernel; 0: chosen in the kernel (WIDE)
 template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8, int NTMK = 0>
-__global__ void __launch_bounds__(WIDE ? 512 : 256) conv_fwd_kernel(ConvArgs a, ConvGeo g) {
+__global__ void __launch_bounds__(WIDE ? 512 : 256)
+__attribute__((amdgpu_waves_per_eu(WIDE || PIN || NTMK == 4 ? 1 : CONV_W)))
+conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   auto item = [&](int blk, bool first) {
     if constexpr (NTMK != 0) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, NTMK>(a, g, blk, smem, first);

@@ -91,10 +91,15 @@ __device__ __forceinline__ void load_raw(Raw& raw, const void* X, int dt, int mo
   }
   // scalar path (any layout / dtype, and the ragged edges of the vector modes).  The dtype is
   // dispatched once around the eight loads: a per-load switch kept them from issuing together
+  // Unconditional loads at clamped, valid offsets, selected after: a bounds-checked load was a
+  // branch per element whose join waited vmcnt(0) -- the eight loads (plus the gate's) ran as a
+  // chain of full memory round trips, ~10 us per K-tile at B = 4096 (fc1's data gradient, profiles/r6)
   float f[8];
   auto gather = [&](auto tag) {
     typedef decltype(tag) X_t;
     const X_t* xp = static_cast<const X_t*>(X);
+    X_t v[8];
+    bool ok[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       int gr, gk;
@@ -105,8 +110,11 @@ __device__ __forceinline__ void load_raw(Raw& raw, const void* X, int dt, int mo
         gr = r0 + (t >> 2);
         gk = k0 + (t & 3) * 8 + j;
       }
-      f[j] = (gr < R && gk < K) ? (float)xp[(int64_t)gr * s_r + (int64_t)gk * s_k] : 0.f;
+      ok[j] = gr < R && gk < K;
+      v[j] = xp[ok[j] ? (int64_t)gr * s_r + (int64_t)gk * s_k : 0];
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = ok[j] ? (float)v[j] : 0.f;
   };
   switch (dt) {
     case kF32: gather(float{}); break;
@@ -139,20 +147,23 @@ __device__ __forceinline__ float raw_at(const Raw& raw, bool pk, int j) {
 
 // Convert (+ gate, + ones row) and write the thread's 8 values into the LDS image.
 template <typename T>
+// (the gate by reference + has_g, not a pointer: a pointer to the caller's register array put it in
+// scratch memory -- 48 bytes per lane, a scratch load per gated element)
 __device__ __forceinline__ void store_tile(typename Stor<T>::S* lds, const Raw& raw, int dt, int mode,
-                                           const Raw* graw, int gdt, float gs, int r0, int ones_row, int k0, int K) {
+                                           const Raw& graw, bool has_g, int gdt, float gs, int r0, int ones_row,
+                                           int k0, int K) {
   typedef typename Stor<T>::V8 V8;
   const int t = threadIdx.x;
   const bool pk = packed<T>(dt);
   V8 v;
-  if (pk && !graw && ones_row < 0) {
+  if (pk && !has_g && ones_row < 0) {
     if constexpr (!__is_same(T, float)) v = __builtin_bit_cast(u16x8, raw.r[0]);
   } else {
-    const bool gpk = graw ? packed<T>(gdt) : false;
+    const bool gpk = has_g ? packed<T>(gdt) : false;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float f = raw_at<T>(raw, pk, j);
-      if (graw) f = raw_at<T>(*graw, gpk, j) > 0.f ? f * gs : 0.f;
+      if (has_g) f = raw_at<T>(graw, gpk, j) > 0.f ? f * gs : 0.f;
       if (ones_row >= 0) {
         const int gr = r0 + (mode == kRContig ? (t & 7) * 8 + j : (t >> 2));
         const int gk = k0 + (mode == kRContig ? (t >> 3) : (t & 3) * 8 + j);
@@ -198,9 +209,21 @@ __device__ __forceinline__ void epilogue_b(const GemmArgs& a, int m, int n, floa
   }
 }
 
+__device__ float kGemmZero[1];  // (a valid address for an absent bias: the load stays unconditional)
+
+// Column n's bias (0 without one), as an unconditional load from a valid address: a conditional
+// load's value used after the branch made the compiler wait vmcnt(0) at the use -- executed with or
+// without a bias, and vmcnt counts stores too: every output element waited for the previous
+// element's store (gemm_kernel's epilogue, 16 elements per lane)
+__device__ __forceinline__ float bias_of(const GemmArgs& a, int n) {
+  const bool ok = a.bias && n < a.N;
+  const float t = (a.bias ? a.bias : kGemmZero)[ok ? n : 0];
+  return ok ? t : 0.f;
+}
+
 template <typename T>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, int m, int n, float acc, uint64_t off, float dscale) {
-  epilogue_b<T>(a, m, n, acc, off, dscale, a.bias && n < a.N ? a.bias[n] : 0.f);
+  epilogue_b<T>(a, m, n, acc, off, dscale, bias_of(a, n));
 }
 
 template <typename T>
@@ -224,7 +247,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Raw ra, rb, rg;
+  Raw ra, rb, rg = {};
   if (kt0 < kt1) {
     load_raw<T>(ra, a.A, a.a_dtype, a.a_mode, a.sam, a.sak, m0, a.M, kt0 * BK, a.K);
     if (a.G) load_raw<T>(rg, a.G, a.g_dtype, a.a_mode, a.sam, a.sak, m0, a.M, kt0 * BK, a.K);
@@ -232,8 +255,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   }
   for (int kt = kt0; kt < kt1; ++kt) {
     const int buf = (kt - kt0) & 1, k0 = kt * BK;
-    store_tile<T>(As[buf], ra, a.a_dtype, a.a_mode, a.G ? &rg : nullptr, a.g_dtype, a.gate_scale, m0, -1, k0, a.K);
-    store_tile<T>(Bs[buf], rb, a.b_dtype, a.b_mode, nullptr, 0, 1.f, n0, ones_row, k0, a.K);
+    store_tile<T>(As[buf], ra, a.a_dtype, a.a_mode, rg, a.G != nullptr, a.g_dtype, a.gate_scale, m0, -1, k0, a.K);
+    store_tile<T>(Bs[buf], rb, a.b_dtype, a.b_mode, rb, false, 0, 1.f, n0, ones_row, k0, a.K);
     __syncthreads();
     if (kt + 1 < kt1) {  // next tile's global loads overlap this tile's MFMAs
       load_raw<T>(ra, a.A, a.a_dtype, a.a_mode, a.sam, a.sak, m0, a.M, k0 + BK, a.K);
@@ -256,6 +279,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   const bool split = gridDim.z > 1;
   const uint64_t off = rng_offset(a.offset, a.offset_dev);
   const float dscale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+  // the epilogue's loads (the lane's two columns' bias) before any store: see bias_of
+  float bias_v[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bias_v[j] = bias_of(a, n0 + wn * 32 + j * 16 + (lane & 15));
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -266,7 +293,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
         const int n = n0 + wn * 32 + j * 16 + (lane & 15);
         if (m >= a.M || n >= Np) continue;
         if (split) a.ws[((int64_t)blockIdx.z * a.M + m) * Np + n] = acc[i][j][r];
-        else epilogue<T>(a, m, n, acc[i][j][r], off, dscale);
+        else epilogue_b<T>(a, m, n, acc[i][j][r], off, dscale, bias_v[j]);
       }
 }
 
@@ -864,8 +891,18 @@ __global__ void gemm_splitk_reduce(GemmArgs a, int splits) {
   if (i >= (int64_t)a.M * Np) return;
   const int m = (int)(i / Np), n = (int)(i - (int64_t)m * Np);
   const int64_t stride = (int64_t)a.M * Np;
+  // the partials' loads in batches of 8 (issued together), summed in split order (the fixed order:
+  // bitwise as one add chain).  One dependent load per add was a chain of memory round trips.
   float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += a.ws[z * stride + i];
+  int z = 0;
+  for (; z + 8 <= splits; z += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = a.ws[(z + u) * stride + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; z < splits; ++z) s += a.ws[z * stride + i];
   epilogue<T>(a, m, n, s, rng_offset(a.offset, a.offset_dev), a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f);
 }
 

@@ -196,6 +196,7 @@ def main() -> None:
     ap.add_argument("--phases", help="run_kernel_trace.csv of a --trace run: per-kernel stats of set-up vs steps")
     ap.add_argument("--graph", choices=["both", "eager", "graph"], default="both")
     ap.add_argument("--loader", action="store_true", help="gather a new batch per step (bound DeviceLoader)")
+    ap.add_argument("--only", help="MODE:BUCKET_MB, e.g. single:25 -- time that mode only")
     a = ap.parse_args()
     if a.parse:
         print(json.dumps(parse(a.parse)))
@@ -204,6 +205,9 @@ def main() -> None:
         print(json.dumps(phases(a.phases, 20), indent=1))
         return
     only = None
+    if a.only:
+        m, c = a.only.split(":")
+        only = (m, float(c))
     if a.trace:
         a.steps, a.warmup, only = 20, 5, (a.mode, a.bucket_mb)
     graphs = {"both": (False, True), "eager": (False,), "graph": (True,)}[a.graph]
