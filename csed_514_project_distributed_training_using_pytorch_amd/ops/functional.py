@@ -144,7 +144,10 @@ def release_grad_buffers(params) -> None:
 
 
 def wgrad_workspace_elems(N: int, IC: int, KH: int, KW: int, OC: int) -> int:
-    return max(1, min(N, 256)) * OC * (IC * KH * KW + 1)
+    """Floats of a conv weight-gradient workspace: one [OC, IC*KH*KW + 1] partial slab per block,
+    sized for the most blocks csrc/kernels/conv.hip conv2d_wgrad_blocks makes (256, 512 from
+    N = 2048; the extension checks the size)."""
+    return max(1, min(N, 512 if N >= 2048 else 256)) * OC * (IC * KH * KW + 1)
 
 
 # The deferred weight-gradient slab reduce.  A conv backward normally ends with its own reduce

@@ -555,7 +555,7 @@ void conv2d_bwd(const Tensor& x, const Tensor& dy, const Tensor& w, Tensor& dw, 
   b.mfma_dtype = mcode(mfma_dtype);
   if (dbg.has_value()) {
     dev(*dbg, "dbg");
-    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= (int64_t)std::min(N, 256) * 8,
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->numel() >= (int64_t)csed::conv2d_wgrad_blocks(std::max(N, 1)) * 8,
                 "conv2d_bwd: dbg must be int64 [>= weight-gradient blocks * 8]");
     b.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr<int64_t>());
   }

@@ -502,10 +502,13 @@ struct WgradGeo {
   int npix, npp;   // OH*OW, roundup(npix, 32)
   int per_block;   // images per block
   int nblocks;
+  int dbuf;        // two image buffers in LDS (wgrad_lds): the next image's staging overlaps this one's MFMAs
 };
 
 // X: the input's element type, DY: dy's, PIN: dy given max-pooled (compile-time, see conv_fwd_body)
-template <typename T, typename X, typename DY, bool PIN, bool WIDE, int NTHR = 256>  // WIDE, NTHR: as conv_fwd_body
+// SMALL: at most 2 M-tiles and 2 N-tiles per wave (the host checks wgrad_small): 16 accumulator
+// registers instead of 64 (128) -- the unused ones were allocated all the same
+template <typename T, typename X, typename DY, bool PIN, bool WIDE, int NTHR = 256, bool SMALL = false>
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const WgradGeo& g, const int blk,
                                                 unsigned char* __restrict__ smem) {
   const void* __restrict__ x = wa.x;
@@ -515,11 +518,14 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   typedef typename Mfma<T>::frag frag;
   typedef typename Stor<T>::S S;
   const int LDY = g.npp + 8;
-  S* dys = (S*)smem;                                        // [Cop][LDY]
-  int* koff = (int*)(dys + g.Cop * LDY);                    // [Kc]
+  const int nbuf = g.dbuf ? 2 : 1;
+  S* const dys0 = (S*)smem;                                 // [nbuf][Cop][LDY]
+  int* koff = (int*)(dys0 + nbuf * g.Cop * LDY);            // [Kc]
   int* pbase = koff + g.Kc;                                 // [npp]
-  S* patch = (S*)(pbase + g.npp);                           // [Ci][PR][PW] (+1 slot holding 1.0)
+  S* const patch0 = (S*)(pbase + g.npp);                    // [nbuf][Ci][PR][PW] (+1 slot holding 1.0)
   const int pe = g.Ci * g.PR * g.PW;
+  S* dys = dys0;      // (this image's buffers)
+  S* patch = patch0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // patch rows / pooled dy channels per batch (512 threads: 8, the same loads per block in flight)
   constexpr int RB = (WIDE && NTHR == 256) ? 16 : NTHR == 512 ? 4 : 8;
@@ -546,136 +552,159 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   const int my_nt0 = NT >= NW ? wave : wave / psplit;
   const int my_s = NT >= NW ? 0 : wave % psplit;
   const int nt_step = NT >= NW ? NW : 1 << 30;
-  constexpr int MAXMT = 4, MAXNTW = NTHR == 512 ? 4 : 8;  // (N-tiles per wave: NT <= NW * MAXNTW)
+  constexpr int MAXMT = SMALL ? 2 : 4, MAXNTW = SMALL ? 2 : NTHR == 512 ? 4 : 8;  // (N-tiles per wave: NT <= NW * MAXNTW)
   f32x4 acc[MAXMT][MAXNTW];
 #pragma unroll
   for (int i = 0; i < MAXMT; ++i)
 #pragma unroll
     for (int j = 0; j < MAXNTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int n_begin = blk * g.per_block;
-  const int n_end = min(N, n_begin + g.per_block);
-  for (int n = n_begin; n < n_end; ++n) {
-    __syncthreads();  // previous image's LDS reads are done
-    // ---- this image's staging in ONE memory round trip where it fits: the first 16 patch rows and
-    // the first dy chunk are loaded before any LDS store (two serial rounds were ~2 us each)
-    // the zero-padded input patch: one patch column per thread, rows stepping by NTHR / PW;
-    // addresses as in conv_fwd_body (per-image base pointer, 32-bit offsets advanced incrementally)
-    const int rpi = qdiv(NTHR, g.PW), nrows = g.Ci * g.PR;
-    const int ic_step = qdiv(rpi, g.PR), pr_step = rpi - ic_step * g.PR;
-    int rr = qdiv(tid, g.PW);
-    const int pc = tid - rr * g.PW;
-    const bool prow = rr < rpi;
-    int ic = prow ? qdiv(rr, g.PR) : 0, pr = rr - ic * g.PR;
-    int ih = pr - g.pad;
-    const int iw = pc - g.pad;
-    const bool colv = iw >= 0 && iw < g.W;
-    const int HWi = g.H * g.W;
-    int xo = ic * HWi + ih * g.W + iw;
-    const int xo_step = ic_step * HWi + pr_step * g.W, xo_wrap = HWi - g.PR * g.W;
-    const X* xs = static_cast<const X*>(x) + (int64_t)n * g.Ci * HWi;
-    float xv[RB];
-    int at[RB];
-    auto load_rows = [&]() {
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        const bool in = prow && rr < nrows;
-        at[j] = in ? rr : -1;
-        const bool ok = in && colv && (unsigned)ih < (unsigned)g.H;
-        const X t = xs[(unsigned)(ok ? xo : 0)];
-        xv[j] = ok ? (float)t : 0.f;
-        rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
-        pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
-        ih += pr_step;
-        ic += ic_step;
-        xo += xo_step;
-        const bool wrap = pr >= g.PR;
-        pr -= wrap ? g.PR : 0;
-        ih -= wrap ? g.PR : 0;
-        ic += wrap ? 1 : 0;
-        xo += wrap ? xo_wrap : 0;
-      }
-    };
-    auto store_rows = [&]() {
-#pragma unroll
-      for (int j = 0; j < RB; ++j)
-        if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(xv[j]);
-    };
-
-    // dy: plain (pst threads per pixel row, NTHR / pst channel groups of 8 side by side) or pooled (a
-    // thread owns one pooling window x 16 channels and writes the window's 4 pixels, one nonzero)
-    const int pst = min(g.npp, NTHR), ocg = qdiv(NTHR, pst), og = qdiv(tid, pst), p0 = tid - og * pst;
-    const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
+  // ---- staging of one image: the zero-padded input patch (one patch column per thread, rows
+  // stepping by NTHR / PW; per-image base pointer, 32-bit offsets advanced incrementally, as in
+  // conv_fwd_body) and dy -- plain (pst threads per pixel row, NTHR / pst channel groups of 8 side by
+  // side) or pooled (a thread owns one pooling window x RB channels and writes the window's 4
+  // pixels, one nonzero).  setup(n) points the state at image n; the load / store lambdas advance it.
+  const int rpi = qdiv(NTHR, g.PW), nrows = g.Ci * g.PR;
+  const int ic_step = qdiv(rpi, g.PR), pr_step = rpi - ic_step * g.PR;
+  const int rr0 = qdiv(tid, g.PW);
+  const int pc = tid - rr0 * g.PW;
+  const bool prow = rr0 < rpi;
+  const int iw = pc - g.pad;
+  const bool colv = iw >= 0 && iw < g.W;
+  const int HWi = g.H * g.W;
+  const int xo_step = ic_step * HWi + pr_step * g.W, xo_wrap = HWi - g.PR * g.W;
+  const int pst = min(g.npp, NTHR), ocg = qdiv(NTHR, pst), og = qdiv(tid, pst), p0 = tid - og * pst;
+  const int PWp = g.OW >> 1, npixp = (g.OH >> 1) * PWp;
+  const int wst = max(1, min(npixp, NTHR)), wgr = qdiv(NTHR, wst), gq = qdiv(tid, wst), q0 = tid - gq * wst;
+  int rr = 0, ic = 0, pr = 0, ih = 0, xo = 0;
+  const X* xs = nullptr;
+  const DY* ys = nullptr;
+  const DY* os = nullptr;
+  const uint8_t* is = nullptr;
+  const float* ss = nullptr;
+  float xv[RB];
+  int at[RB];
+  float dv[RB > 8 ? RB : 8], yo[RB], sc[RB];  // (plain dy: chunks of 8 channels whatever RB)
+  uint8_t bi[RB];
+  int d_p = 0, d_oc0 = 0, d_q = 0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
+  bool d_more = false;
+  auto setup = [&](int n) {
+    rr = rr0;
+    ic = prow ? qdiv(rr, g.PR) : 0;
+    pr = rr - ic * g.PR;
+    ih = pr - g.pad;
+    xo = ic * HWi + ih * g.W + iw;
+    xs = static_cast<const X*>(x) + (int64_t)n * g.Ci * HWi;
     const int64_t yimg = (int64_t)n * g.Co * (PIN ? npixp : g.npix);  // (per-image bases, 32-bit offsets)
-    const DY* ys = static_cast<const DY*>(dy) + yimg;
-    const DY* os = static_cast<const DY*>(wa.pout) + (PIN ? yimg : 0);
-    const uint8_t* is = wa.pidx + (PIN ? yimg : 0);
-    const float* ss = wa.pscale ? wa.pscale + (int64_t)n * g.Co : slab;
-    const int wst = max(1, min(npixp, NTHR)), wgr = qdiv(NTHR, wst), gq = qdiv(tid, wst), q0 = tid - gq * wst;
-    float dv[RB > 8 ? RB : 8], yo[RB], sc[RB];  // (plain dy: chunks of 8 channels whatever RB)
-    uint8_t bi[RB];
-    int d_p = p0, d_oc0 = og * 8, d_q = q0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
+    ys = static_cast<const DY*>(dy) + yimg;
+    os = static_cast<const DY*>(wa.pout) + (PIN ? yimg : 0);
+    is = wa.pidx + (PIN ? yimg : 0);
+    ss = wa.pscale ? wa.pscale + (int64_t)n * g.Co : slab;
+    d_p = p0;
+    d_oc0 = PIN ? gq * RB : og * 8;
+    d_q = q0;
+    d_pb = 0;
     // (pooled: channels up to Co only -- dY rows Co..Cop-1 feed only the MFMA rows the slab write
     // drops, and zero-filling them cost conv1 (10 of 16) a second staging round trip)
-    bool d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Co) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
-    auto load_dy = [&]() {  // one chunk's loads
-      if constexpr (!PIN) {
-        const int yo0 = d_oc0 * g.npix + d_p;
+    d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Co) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
+  };
+  auto load_rows = [&]() {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const bool ok = d_oc0 + j < g.Co && d_p < g.npix;
-          const DY t = ys[(unsigned)(ok ? yo0 + j * g.npix : 0)];
-          dv[j] = ok ? (float)t : 0.f;
-        }
-      } else {
-        const int ph = qdiv(d_q, PWp), pw = d_q - ph * PWp;
-        d_pb = 2 * ph * g.OW + 2 * pw;
-        const int po0 = d_oc0 * npixp + d_q;
+    for (int j = 0; j < RB; ++j) {
+      const bool in = prow && rr < nrows;
+      at[j] = in ? rr : -1;
+      const bool ok = in && colv && (unsigned)ih < (unsigned)g.H;
+      const X t = xs[(unsigned)(ok ? xo : 0)];
+      xv[j] = ok ? (float)t : 0.f;
+      rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
+      pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
+      ih += pr_step;
+      ic += ic_step;
+      xo += xo_step;
+      const bool wrap = pr >= g.PR;
+      pr -= wrap ? g.PR : 0;
+      ih -= wrap ? g.PR : 0;
+      ic += wrap ? 1 : 0;
+      xo += wrap ? xo_wrap : 0;
+    }
+  };
+  auto store_rows = [&]() {
 #pragma unroll
-        for (int j = 0; j < RB; ++j) {
-          const bool ok = d_oc0 + j < g.Co;
-          const unsigned po = ok ? po0 + j * npixp : 0;
-          const DY t0 = ys[po], t1 = os[po];
-          const uint8_t t2 = is[po];
-          const float t3 = ss[(unsigned)(ok && wa.pscale ? d_oc0 + j : 0)];
-          dv[j] = ok ? (float)t0 : 0.f;
-          yo[j] = ok ? (float)t1 : 0.f;
-          bi[j] = ok ? t2 : (uint8_t)255;
-          sc[j] = ok ? (wa.pscale ? t3 : 1.f) : 0.f;
-        }
+    for (int j = 0; j < RB; ++j)
+      if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(xv[j]);
+  };
+  auto load_dy = [&]() {  // one chunk's loads
+    if constexpr (!PIN) {
+      const int yo0 = d_oc0 * g.npix + d_p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = d_oc0 + j < g.Co && d_p < g.npix;
+        const DY t = ys[(unsigned)(ok ? yo0 + j * g.npix : 0)];
+        dv[j] = ok ? (float)t : 0.f;
       }
-    };
-    auto store_dy_next = [&]() {  // store the loaded chunk, advance to the next one
-      if constexpr (!PIN) {
+    } else {
+      const int ph = qdiv(d_q, PWp), pw = d_q - ph * PWp;
+      d_pb = 2 * ph * g.OW + 2 * pw;
+      const int po0 = d_oc0 * npixp + d_q;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dys[(d_oc0 + j) * LDY + d_p] = Stor<T>::of(dv[j]);
-        d_oc0 += ocg * 8;
-        if (d_oc0 >= g.Cop) {
-          d_oc0 = og * 8;
-          d_p += pst;
-        }
-        d_more = d_p < g.npp;
-      } else {
-#pragma unroll
-        for (int j = 0; j < RB; ++j) {
-          if (d_oc0 + j >= g.Co) break;
-          S* d = dys + (d_oc0 + j) * LDY + d_pb;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(dv[j], bi[j], yo[j], sc[j], e));
-        }
-        d_oc0 += wgr * RB;
-        if (d_oc0 >= g.Co) {
-          d_oc0 = gq * RB;
-          d_q += wst;
-        }
-        d_more = d_q < npixp;
+      for (int j = 0; j < RB; ++j) {
+        const bool ok = d_oc0 + j < g.Co;
+        const unsigned po = ok ? po0 + j * npixp : 0;
+        const DY t0 = ys[po], t1 = os[po];
+        const uint8_t t2 = is[po];
+        const float t3 = ss[(unsigned)(ok && wa.pscale ? d_oc0 + j : 0)];
+        dv[j] = ok ? (float)t0 : 0.f;
+        yo[j] = ok ? (float)t1 : 0.f;
+        bi[j] = ok ? t2 : (uint8_t)255;
+        sc[j] = ok ? (wa.pscale ? t3 : 1.f) : 0.f;
       }
-    };
-    if (PIN) d_oc0 = gq * RB;
+    }
+  };
+  auto store_dy_next = [&]() {  // store the loaded chunk, advance to the next one
+    if constexpr (!PIN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dys[(d_oc0 + j) * LDY + d_p] = Stor<T>::of(dv[j]);
+      d_oc0 += ocg * 8;
+      if (d_oc0 >= g.Cop) {
+        d_oc0 = og * 8;
+        d_p += pst;
+      }
+      d_more = d_p < g.npp;
+    } else {
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        if (d_oc0 + j >= g.Co) break;
+        S* d = dys + (d_oc0 + j) * LDY + d_pb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(dv[j], bi[j], yo[j], sc[j], e));
+      }
+      d_oc0 += wgr * RB;
+      if (d_oc0 >= g.Co) {
+        d_oc0 = gq * RB;
+        d_q += wst;
+      }
+      d_more = d_q < npixp;
+    }
+  };
 
-    load_rows();              // round 1: patch rows ...
-    if (d_more) load_dy();    // ... and the first dy chunk in flight together
-    __builtin_amdgcn_sched_barrier(0);  // (no use of a loaded value hoisted between the loads)
+  const int n_begin = blk * g.per_block;
+  const int n_end = min(N, n_begin + g.per_block);
+  // The first staging round (patch rows and the first dy chunk, loaded together) of image n + 1 is
+  // issued right after image n's staging, so its loads are in flight during image n's MFMAs; with
+  // two LDS buffers (g.dbuf) it is stored without waiting for them.  (Staging image by image after
+  // the previous one's MFMAs was a memory round trip per image in series: 16 images per block at
+  // B = 4096, ~3 us each, profiles/r6.)
+  if (n_begin < n_end) {
+    setup(n_begin);
+    load_rows();
+    if (d_more) load_dy();
+  }
+  for (int n = n_begin; n < n_end; ++n) {
+    const int buf = (n - n_begin) % nbuf;
+    if (nbuf == 1 && n > n_begin) __syncthreads();  // (one buffer: the previous image's MFMA reads are done)
+    dys = dys0 + buf * g.Cop * LDY;
+    patch = patch0 + buf * (pe + 1);
+    __builtin_amdgcn_sched_barrier(0);  // (no use of a loaded value hoisted above the buffer switch)
     WG_STAMP(1);
     store_rows();
     if (d_more) store_dy_next();
@@ -694,8 +723,15 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         dys[oc * LDY + pp] = Stor<T>::of(0.f);
       }
     }
+    // (two buffers: every wave passed this barrier after its MFMAs on image n - 1's buffer, the one
+    // image n + 1 will write -- one barrier per image)
     __syncthreads();
     WG_STAMP(2);
+    if (n + 1 < n_end) {  // image n + 1's first round, in flight during this image's MFMAs
+      setup(n + 1);
+      load_rows();
+      if (d_more) load_dy();
+    }
     if (my_nt0 >= NT) continue;
     // this lane's B-column patch offsets, one per N-tile (the same for every pixel step: read once
     // per image instead of once per MFMA, a dependent LDS round trip less per pixel step)
@@ -824,14 +860,18 @@ __device__ __forceinline__ void carried_reduce(const RedArgs& r, int rb, unsigne
   wgrad_reduce_body(r.slab, r.nblocks, r.Co, r.K, r.dw, r.db, r.beta, vb, threadIdx.x & 255, part);
 }
 
-template <typename T, typename X, typename DY, bool PIN, bool WIDE>
-__global__ void __launch_bounds__(WIDE ? 512 : 256) conv_wgrad_kernel(WgradArgs wa, WgradGeo g, RedArgs r) {
+#ifndef CSED_WGRAD_WAVES
+#define CSED_WGRAD_WAVES 1
+#endif
+template <typename T, typename X, typename DY, bool PIN, bool WIDE, bool SMALL = false>
+__global__ void __launch_bounds__(WIDE ? 512 : 256) __attribute__((amdgpu_waves_per_eu(SMALL ? CSED_WGRAD_WAVES : 1)))
+conv_wgrad_kernel(WgradArgs wa, WgradGeo g, RedArgs r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x >= g.nblocks) {  // (a carried reduce of another conv)
     carried_reduce<WIDE ? 512 : 256>(r, blockIdx.x - g.nblocks, smem);
     return;
   }
-  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256>(wa, g, blockIdx.x, smem);
+  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256, SMALL>(wa, g, blockIdx.x, smem);
 }
 
 // The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
@@ -999,6 +1039,15 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
   return hipSuccess;
 }
 
+#ifndef CSED_WGRAD_CAP
+#define CSED_WGRAD_CAP 256
+#endif
+// Weight-gradient blocks for a batch of N images (each walks cdiv(N, blocks) of them)
+int conv2d_wgrad_blocks(int N) {
+  const int cap = N >= 2048 ? CSED_WGRAD_CAP : 256;
+  return cdiv(N, cdiv(N, std::max(1, std::min(N, cap))));
+}
+
 static WgradGeo wgrad_geo(int N, int IC, int H, int W, int OC, int KH, int KW, int pad) {
   WgradGeo g;
   g.Ci = IC; g.Co = OC; g.H = H; g.W = W; g.KH = KH; g.KW = KW; g.pad = pad;
@@ -1011,15 +1060,27 @@ static WgradGeo wgrad_geo(int N, int IC, int H, int W, int OC, int KH, int KW, i
   g.PW = W + 2 * pad;
   g.npix = g.OH * g.OW;
   g.npp = rup(std::max(g.npix, 1), 32);
-  g.nblocks = std::max(1, std::min(N, 256));
+  g.nblocks = conv2d_wgrad_blocks(std::max(N, 1));
   g.per_block = (N + g.nblocks - 1) / g.nblocks;
-  g.nblocks = (N + g.per_block - 1) / g.per_block;
+  g.dbuf = 0;
   return g;
 }
 
+// LDS of a weight-gradient block: nbuf x (dy image [Cop][npp + 8] + patch [Ci][PR][PW] + 1) plus the
+// k -> patch offsets [Kc] and pixel bases [npp]
+static size_t wgrad_lds(const WgradGeo& g, size_t es, int nbuf) {
+  return (size_t)nbuf * g.Cop * (g.npp + 8) * es + (size_t)g.Kc * 4 + (size_t)g.npp * 4 +
+         (size_t)nbuf * ((size_t)g.Ci * g.PR * g.PW + 1) * es + 16;
+}
+
+// conv_wgrad_body's SMALL form fits: at most 2 M-tiles, at most 2 N-tiles per wave of a 512-thread block
+static bool wgrad_small(const WgradGeo& g) {
+  const int MT = g.Cop >> 4, NT = g.Kc >> 4, NW = 8;
+  return MT <= 2 && (NT < NW || cdiv(NT, NW) <= 2);
+}
+
 int64_t conv2d_wgrad_workspace(int N, int IC, int KH, int KW, int OC) {
-  const int nb = std::max(1, std::min(N, 256));
-  return (int64_t)nb * OC * (IC * KH * KW + 1);
+  return (int64_t)conv2d_wgrad_blocks(std::max(N, 1)) * OC * (IC * KH * KW + 1);
 }
 
 hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
@@ -1032,8 +1093,9 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
     return hipErrorInvalidConfiguration;  // (32-bit staging offsets, see conv_geo)
   if (b.pidx && (!b.pout || (wg.OH & 1) || (wg.OW & 1))) return hipErrorInvalidValue;
   const size_t es = b.mfma_dtype == kF32 ? 4 : 2;  // LDS operand element size
-  const size_t lds_main = (size_t)wg.Cop * (wg.npp + 8) * es + (size_t)wg.Kc * 4 + (size_t)wg.npp * 4 +
-                          ((size_t)wg.Ci * wg.PR * wg.PW + 1) * es + 16;
+  // two image buffers when a block walks several images and they fit beside a second block's
+  wg.dbuf = wg.per_block > 1 && wgrad_lds(wg, es, 2) <= 64 * 1024;
+  const size_t lds_main = wgrad_lds(wg, es, wg.dbuf ? 2 : 1);
   const size_t lds_red = (size_t)8 * 4 * 16 * 16 * 4;  // (up to 8 waves x MAXMT x 16 x 16 floats)
   size_t lds = std::max(lds_main, lds_red);
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
@@ -1062,8 +1124,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
   RedArgs red{};
   if (b.carry_ws) {
     const int cK = b.carry_IC * b.carry_KH * b.carry_KW;
-    red.slab = b.carry_ws; red.nblocks = std::max(1, std::min(b.carry_N, 256));
-    red.nblocks = cdiv(b.carry_N, cdiv(b.carry_N, red.nblocks));  // (wgrad_geo's block count)
+    red.slab = b.carry_ws; red.nblocks = conv2d_wgrad_blocks(std::max(b.carry_N, 1));  // (wgrad_geo's block count)
     red.Co = b.carry_OC; red.K = cK; red.dw = b.carry_dw; red.db = b.carry_db; red.beta = 0.f;
     red.blocks = cdiv(b.carry_OC * (cK + 1), 64);  // (256-thread groups)
   }
@@ -1079,7 +1140,9 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
         // kernel's register budget (the wgrad body's) would cap the many data-gradient blocks'
         // occupancy, so they run as their own launch (B = 4096: 750 -> see profiles/round5.md)
         const bool merged = dgrid > 0 && wg.nblocks + dgrid <= 2 * 256;
-        const bool ww = wg.nblocks <= 2 * 256, dw = dgrid <= 2 * 256;  // (WIDE per launch)
+        const bool dw = dgrid <= 2 * 256;  // (WIDE data-gradient launch)
+        // (the weight-gradient launch is the 512-thread form: wgrad_geo makes at most 256 blocks)
+        const bool small = wgrad_small(wg);
         auto go = [&](auto bwd, auto wgr, auto dgr) {
           if (merged) {
             if (lds > 64 * 1024) hipFuncSetAttribute((const void*)bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1088,8 +1151,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
             return hipGetLastError();
           }
           if (lds_w > 64 * 1024) hipFuncSetAttribute((const void*)wgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w);
-          hipLaunchKernelGGL(wgr, dim3(wg.nblocks + red_blocks(ww ? 512 : 256)), dim3(ww ? 512 : 256), lds_w, s, wa, wg,
-                             red);
+          hipLaunchKernelGGL(wgr, dim3(wg.nblocks + red_blocks(512)), dim3(512), lds_w, s, wa, wg, red);
           hipError_t e2 = hipGetLastError();
           if (e2 != hipSuccess || dgrid == 0) return e2;
           if (lds_d > 64 * 1024) hipFuncSetAttribute((const void*)dgr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
@@ -1097,21 +1159,18 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
           hipLaunchKernelGGL(dgr, dim3(dgr_grid), dim3(dw ? 512 : 256), lds_d, s, a, g);
           return hipGetLastError();
         };
-        if (merged)
-          return b.pidx ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>,
-                             conv_fwd_kernel<T, DY, X, true, true>)
-                        : go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>,
-                             conv_fwd_kernel<T, DY, X, false, true>);
-        if (b.pidx) {
-          if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, true>)
-                            : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, true>, conv_fwd_kernel<T, DY, X, true, false, 8, decltype(k)::value>); });
-          return dw ? go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, true>)
-                    : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, true>, conv_wgrad_kernel<T, X, DY, true, false>, conv_fwd_kernel<T, DY, X, true, false, 8, decltype(k)::value>); });
-        }
-        if (ww) return dw ? go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, true>)
-                          : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, true>, conv_fwd_kernel<T, DY, X, false, false, 8, decltype(k)::value>); });
-        return dw ? go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, true>)
-                  : narrow_ntm(g.Cop, [&](auto k) { return go(conv_bwd_kernel<T, X, DY, false>, conv_wgrad_kernel<T, X, DY, false, false>, conv_fwd_kernel<T, DY, X, false, false, 8, decltype(k)::value>); });
+        auto pick = [&](auto pin_tag) -> hipError_t {
+          constexpr bool P = decltype(pin_tag)::value;
+          if (merged) return go(conv_bwd_kernel<T, X, DY, P>, conv_wgrad_kernel<T, X, DY, P, true>, conv_fwd_kernel<T, DY, X, P, true>);
+          auto with_w = [&](auto wk) -> hipError_t {
+            if (dw) return go(conv_bwd_kernel<T, X, DY, P>, wk, conv_fwd_kernel<T, DY, X, P, true>);
+            return narrow_ntm(g.Cop, [&](auto k) {
+              return go(conv_bwd_kernel<T, X, DY, P>, wk, conv_fwd_kernel<T, DY, X, P, false, 8, decltype(k)::value>);
+            });
+          };
+          return small ? with_w(conv_wgrad_kernel<T, X, DY, P, true, true>) : with_w(conv_wgrad_kernel<T, X, DY, P, true, false>);
+        };
+        return b.pidx ? pick(std::true_type{}) : pick(std::false_type{});
       });
     });
   };
@@ -1131,7 +1190,7 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
 hipError_t launch_wgrad_reduce(const float* ws, float* dw, float* db, int N, int IC, int KH, int KW, int OC,
                                hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  const int nb = cdiv(N, cdiv(N, std::max(1, std::min(N, 256))));  // (wgrad_geo's block count)
+  const int nb = conv2d_wgrad_blocks(N);  // (wgrad_geo's block count)
   const int K = IC * KH * KW, L = OC * (K + 1);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(L, 64)), dim3(256), 0, s, ws, nb, OC, K, dw, db, 0.f);
   return hipGetLastError();
