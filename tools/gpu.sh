@@ -243,7 +243,9 @@ task_conv4096() {  # the per-op conv kernels at large batch: fusion tests, B = 4
 task_modsteps() {  # the modular step at B = 64 and 4096: per-op launch times and graph step times
   cd $R && py 200 python -u tools/op_probe.py --batch 64 > $O/${T}_op64.log 2>&1 && \
   py 300 python -u tools/op_probe.py --batch 4096 --reps 20 > $O/${T}_op4096.log 2>&1 && \
-  py 300 python -u tools/ddp_overlap.py --batch 64 --graph graph > $O/${T}_mod64.log 2>&1
+  py 300 python -u tools/ddp_overlap.py --batch 64 --graph graph > $O/${T}_mod64.log 2>&1 && \
+  py 300 python -u tools/ddp_overlap.py --batch 4096 --graph graph --only single:25 --loader > $O/${T}_mod4096_loader.log 2>&1 && \
+  py 300 python -u tools/ddp_overlap.py --batch 64 --graph graph --only single:25 --loader > $O/${T}_mod64_loader.log 2>&1
 }
 
 task_quick() {  # the test files this round's changes touch
