@@ -200,6 +200,43 @@ def _unpool_min_batch(with_dx: bool) -> int:
 
 
 # ----------------------------------------------------------------- conv ----
+# The weight-gradient kernel holds at most 64 output channels (4 M-tiles of accumulators per wave,
+# csrc/kernels/conv.hip launch_conv2d_bwd); a wider conv's backward runs per 64-channel slice.
+_WGRAD_MAX_OC = 64
+
+
+def _conv_bwd_oc_chunks(ctx, x, w, dy, pooled):
+    """Backward of a conv with more than 64 output channels: dW / db per 64-channel slice of dy and
+    W, dX as the sum of the slices' data gradients (fp32).  dL/dconv of a pooled forward is
+    materialised first."""
+    if pooled[0] is not None:
+        idx, y, chscale = pooled
+        dconv = torch.empty(ctx.conv_shape, device=dy.device, dtype=y.dtype)
+        _ops().maxpool_relu_bwd(dy, y, idx, chscale, dconv, 2)
+        dy = dconv
+    N, IC = x.shape[:2]
+    OC, _, KH, KW = w.shape
+    dw = _take_grad_buffer(w, w.shape, w.device)[0] if ctx.needs_input_grad[1] else None
+    db = _take_grad_buffer(ctx.bias_param, (OC,), w.device)[0] if ctx.has_bias and ctx.needs_input_grad[2] else None
+    dx32 = torch.zeros(x.shape, device=x.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+    for c0 in range(0, OC, _WGRAD_MAX_OC):
+        c1 = min(OC, c0 + _WGRAD_MAX_OC)
+        dyc, wc = dy[:, c0:c1].contiguous(), w[c0:c1].contiguous()
+        dwc = torch.empty(wc.shape, device=w.device, dtype=torch.float32)
+        dbc = torch.empty(c1 - c0, device=w.device, dtype=torch.float32) if ctx.has_bias else None
+        ws = torch.empty(wgrad_workspace_elems(N, IC, KH, KW, c1 - c0), device=w.device, dtype=torch.float32)
+        dxc = torch.empty(x.shape, device=x.device, dtype=x.dtype) if dx32 is not None else None
+        _ops().conv2d_bwd(x, dyc, wc, dwc, dbc, ws, dxc, ctx.pad, None, None, None, ctx.mf)
+        if dw is not None:
+            dw[c0:c1].copy_(dwc)
+        if db is not None:
+            db[c0:c1].copy_(dbc)
+        if dxc is not None:
+            dx32 += dxc.float()
+    dx = dx32.to(x.dtype) if dx32 is not None else None
+    return dx, dw, db, None, None, None, None
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, pad, pool, chscale, drop):
@@ -251,6 +288,8 @@ class _Conv2d(torch.autograd.Function):
             x, w = ctx.saved_tensors
             pooled = (None, None, None)
         dx = dw = db = None
+        if (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]) and ctx.conv_shape[1] > _WGRAD_MAX_OC:
+            return _conv_bwd_oc_chunks(ctx, x, w, dy, pooled)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # one launch for dW, db and dX (+ the slab reduce); a pooled forward's gradient is
             # expanded inside the kernels' staging (dL/dconv never materialised)

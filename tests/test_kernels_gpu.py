@@ -37,7 +37,8 @@ def close(a, b, rel=2e-2, name=""):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(4, 1, 28, 28, 10, 5, 0), (3, 10, 12, 12, 20, 5, 0), (2, 3, 9, 11, 7, 3, 1),
-                                   (2, 16, 14, 14, 33, 3, 1), (1, 2, 6, 6, 4, 1, 0)])
+                                   (2, 16, 14, 14, 33, 3, 1), (1, 2, 6, 6, 4, 1, 0), (3, 8, 12, 12, 80, 5, 0),
+                                   (700, 10, 12, 12, 20, 5, 0)])
 def test_conv2d_fwd_bwd(dt, shape):
     ops.set_compute_dtype(dt)
     try:
@@ -65,9 +66,13 @@ def test_conv2d_fwd_bwd(dt, shape):
         ops.set_compute_dtype(torch.bfloat16)
 
 
-@pytest.mark.parametrize("shape", [(5, 1, 28, 28, 10), (7, 10, 12, 12, 20), (3, 4, 10, 14, 16)])
+@pytest.mark.parametrize("shape", [(5, 1, 28, 28, 10), (7, 10, 12, 12, 20), (3, 4, 10, 14, 16), (3, 4, 12, 12, 72),
+                                   (1200, 1, 28, 28, 10), (1100, 10, 12, 12, 20)])
 @pytest.mark.parametrize("with_scale", [False, True])
 def test_conv2d_pool_relu(shape, with_scale):
+    """(3, 4, 12, 12, 72): channels past the first 64 in the pooled epilogue; N >= 1024: the narrow
+    persistent forward and data-gradient kernels, the materialised pool backward and the weight
+    gradient's multi-image blocks (image prefetch, two LDS buffers)."""
     N, C, H, W, OC = shape
     torch.manual_seed(1)
     x = q(torch.randn(N, C, H, W))

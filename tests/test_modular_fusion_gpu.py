@@ -88,8 +88,11 @@ def _unpool_ref(dy, idx, y, scale):
     return val.view(N, OC, PH, PW, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(N, OC, 2 * PH, 2 * PW)
 
 
-def test_conv_fwd_in_kernel_dropout2d_matches_channel_mask():
-    N, C, OC = 64, 10, 20
+@pytest.mark.parametrize("N,OC", [(64, 20), (5, 80), (1100, 20)])
+def test_conv_fwd_in_kernel_dropout2d_matches_channel_mask(N, OC):
+    """OC = 80: channels past the first 64 (their bias / scale from the staged epilogue operands);
+    N = 1100: the narrow persistent-block form (work items walked by fewer blocks)."""
+    C = 10
     g = torch.Generator(device=DEV).manual_seed(4)
     x = torch.randn(N, C, 12, 12, device=DEV, generator=g).to(torch.bfloat16)
     w = torch.randn(OC, C, 5, 5, device=DEV, generator=g) * 0.2
