@@ -961,7 +961,9 @@ int gemm_splits(const GemmArgs& a) {
   const int tiles = cdiv(Np, BN) * cdiv(a.M, BM);
   const int ktiles = cdiv(a.K, BK);
   if (tiles >= 256 || ktiles < 8) return 1;
-  int s = std::min(cdiv(512, tiles), ktiles / 4);
+  // (at least 2 K-tiles per split: 4 were a 4-deep chain of load -> LDS -> MFMA rounds per block --
+  // the fc weight gradients at B = 4096, K = 4096: 6 us more per step than 2, profiles/r6 r7f)
+  int s = std::min(cdiv(512, tiles), ktiles / 2);
   return std::max(1, std::min(s, 64));
 }
 
