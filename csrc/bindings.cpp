@@ -1003,6 +1003,7 @@ TORCH_LIBRARY(csed, m) {
       .def("set_update", &LenetStepper::set_update)
       .def("run", &LenetStepper::run);
   m.def("lenet_layout() -> int[]", &lenet_layout);
+  m.def("conv_wgrad_prefetch(int depth=0) -> int", [](int64_t d) { return (int64_t)csed::conv_wgrad_prefetch((int)d); });
   m.def("preload_kernels(int device, int mask=127) -> float", &preload_kernels);
   m.def("lenet_zero_(Tensor(a!) t) -> ()", &lenet_zero_);
   m.def("lenet_iota_(Tensor(a!) t) -> ()", &lenet_iota_);

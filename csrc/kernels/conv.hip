@@ -23,6 +23,8 @@
 // MFMA C layout (row = 4*(lane>>4) + reg) every lane then holds one complete
 // 2x2 window of one channel in its 4 accumulators, so the max-pool, argmax,
 // ReLU and channel scale happen in registers with no shuffles.
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 #ifndef CONV_W
 #define CONV_W 5
@@ -45,6 +47,7 @@ struct ConvGeo {
   int PR, PW;            // patch rows / cols in LDS
   int bands;             // blocks per image
   int items;             // N * bands (image, band) work items; a launch of fewer blocks walks them
+  int nvec;              // vector staging (conv_fwd_body VM): 16-byte vectors per image, else 0
   int Hp, Wp;            // pooled input dims (a.pidx set: the input is given max-pooled)
 };
 
@@ -98,7 +101,8 @@ __device__ __forceinline__ float unpool(float v, uint8_t bi, float yo, float sc,
 // compiler copy every loaded register at the join: a wait on each load before the next issued)
 // NTM: N-tiles per accumulator group (4; 1 when the output channels fit one tile -- conv1, the
 // data gradients -- so no fragment of an absent tile is read from LDS)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256, int RB = 8, int NTM = 4>  // Y: the output's element type
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int NTHR = 256, int RB = 8, int NTM = 4,
+          bool VM = false>  // Y: the output's element type; VM: vector staging (see load_vec)
 // WIDE: 32 weight / 16 patch-row loads per thread in flight (one round trip: small grids); narrow:
 // 8 / 8 (fewer registers, more blocks per CU: large grids, where other blocks hide the latency).
 // NTHR: the block size (512 for a standalone launch: two waves per SIMD interleave the staging's
@@ -210,10 +214,46 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     for (int j = 0; j < RB; ++j)
       if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(PIN ? unpool(pv[j], bi[j], yo[j], sc[j], sel[j]) : pv[j]);
   };
+  // VM (the host's conv_geo checked it: unpooled input, one item per image, rows of whole 16-byte
+  // vectors -- or, unpadded, the image one contiguous run -- at most 2 vectors per thread): the
+  // image is staged by 16-byte loads, one per vector, instead of one load per element through the
+  // row walk above (conv2's data gradient at large batch: 5120 element loads in three dependent
+  // rounds per image -> 160 vector loads in one).  The zero padding is written once per block
+  // (first item): later items write the interior only.
+  constexpr int VE = 16 / (int)sizeof(X);
+  uint4 vv[2];
+  int vdst[2];
+  auto load_vec = [&]() {
+    const int HW = g.H * g.W;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int idx = tid + v * NTHR;
+      const bool ok = idx < g.nvec;
+      vv[v] = reinterpret_cast<const uint4*>(xs)[ok ? idx : 0];
+      const int e0 = idx * VE, c = qdiv(e0, HW), r0 = e0 - c * HW, y = qdiv(r0, g.W), xc = r0 - y * g.W;
+      vdst[v] = !ok ? -1 : g.pad == 0 ? e0 : (c * g.PR + y + g.pad) * g.PW + g.pad + xc;
+    }
+  };
+  auto store_vec = [&]() {
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      if (vdst[v] < 0) continue;
+      const X* e = reinterpret_cast<const X*>(&vv[v]);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) patch[vdst[v] + j] = Stor<T>::of((float)e[j]);
+    }
+  };
+  if constexpr (VM) {
+    if (stage_w && g.pad > 0) {
+      for (int i = tid; i < g.Ci * g.PR * g.PW; i += NTHR) patch[i] = Stor<T>::of(0.f);
+      __syncthreads();
+    }
+  }
   // issue order: the patch rows first, then the weights and epilogue
   // operands in straight-line code, then a scheduling barrier so no conversion / store of a loaded
   // value is hoisted between them (it would wait on its load mid-issue: a second round trip)
-  load_rows();
+  if constexpr (VM) load_vec();
+  else load_rows();
   // (wave-uniform: a wave that owns no weight column -- conv1's Kp = 32 of 512 threads -- skips the
   // weight batch; the loads were unconditional at clamped addresses, pure VALU / address cost)
   const int wave0 = tid & ~63;
@@ -284,7 +324,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
       }
     }
   }
-  store_rows();
+  if constexpr (VM) store_vec();
+  else store_rows();
   if (tid < g.Cop) {
     EPB[tid] = ebv;
     EPS[tid] = esv;
@@ -300,9 +341,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
     EPB[c] = b;
     EPS[c] = s;
   }
-  while (prow && rr < nrows) {
-    load_rows();
-    store_rows();
+  if constexpr (!VM) {
+    while (prow && rr < nrows) {
+      load_rows();
+      store_rows();
+    }
   }
   CONV_STAMP(2);
   __syncthreads();
@@ -458,13 +501,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const ConvGeo& 
 // x 16 KB of weights through the index math, the modular step's longest kernel, profiles/r6.)
 // NTMK (narrow form): the N-tiles per accumulator group, chosen by the host from Cop (1: 16
 // channels, 2: 32, 4: more), so that one body is compiled per kernel; 0: chosen in the kernel (WIDE)
-template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8, int NTMK = 0>
+template <typename T, typename X, typename Y, bool PIN, bool WIDE, int RB = 8, int NTMK = 0, bool VM = false>
 __global__ void __launch_bounds__(WIDE ? 512 : 256)
 __attribute__((amdgpu_waves_per_eu(WIDE || PIN || NTMK == 4 ? 1 : CONV_W)))
 conv_fwd_kernel(ConvArgs a, ConvGeo g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   auto item = [&](int blk, bool first) {
-    if constexpr (NTMK != 0) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, NTMK>(a, g, blk, smem, first);
+    if constexpr (NTMK != 0) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, NTMK, VM>(a, g, blk, smem, first);
     else if (g.Cop == 16) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 1>(a, g, blk, smem, first);
     else if (g.Cop == 32) conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB, 2>(a, g, blk, smem, first);
     else conv_fwd_body<T, X, Y, PIN, WIDE, WIDE ? 512 : 256, RB>(a, g, blk, smem, first);
@@ -508,7 +551,9 @@ struct WgradGeo {
 // X: the input's element type, DY: dy's, PIN: dy given max-pooled (compile-time, see conv_fwd_body)
 // SMALL: at most 2 M-tiles and 2 N-tiles per wave (the host checks wgrad_small): 16 accumulator
 // registers instead of 64 (128) -- the unused ones were allocated all the same
-template <typename T, typename X, typename DY, bool PIN, bool WIDE, int NTHR = 256, bool SMALL = false>
+// PF: images whose staging loads are in flight at once (1: the next image during this one's MFMAs;
+// > 1 needs one-round stagings and two LDS buffers, see the image loop)
+template <typename T, typename X, typename DY, bool PIN, bool WIDE, int NTHR = 256, bool SMALL = false, int PF = 1>
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const WgradGeo& g, const int blk,
                                                 unsigned char* __restrict__ smem) {
   const void* __restrict__ x = wa.x;
@@ -582,13 +627,16 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
   const DY* os = nullptr;
   const uint8_t* is = nullptr;
   const float* ss = nullptr;
-  float xv[RB];
-  int at[RB];
-  float dv[RB > 8 ? RB : 8], yo[RB], sc[RB];  // (plain dy: chunks of 8 channels whatever RB)
-  uint8_t bi[RB];
-  int d_p = 0, d_oc0 = 0, d_q = 0, d_pb = 0;  // the next chunk (plain: pixel, channel; pooled: window, channel)
-  bool d_more = false;
-  auto setup = [&](int n) {
+  // One image's staging registers (a set per image in flight: PF of them)
+  struct Stg {
+    float xv[RB];
+    int at[RB];
+    float dv[RB > 8 ? RB : 8], yo[RB], sc[RB];  // (plain dy: chunks of 8 channels whatever RB)
+    uint8_t bi[RB];
+    int d_p, d_oc0, d_q, d_pb;  // the next chunk (plain: pixel, channel; pooled: window, channel)
+    bool d_more;
+  };
+  auto setup = [&](Stg& st, int n) {
     rr = rr0;
     ic = prow ? qdiv(rr, g.PR) : 0;
     pr = rr - ic * g.PR;
@@ -600,22 +648,22 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
     os = static_cast<const DY*>(wa.pout) + (PIN ? yimg : 0);
     is = wa.pidx + (PIN ? yimg : 0);
     ss = wa.pscale ? wa.pscale + (int64_t)n * g.Co : slab;
-    d_p = p0;
-    d_oc0 = PIN ? gq * RB : og * 8;
-    d_q = q0;
-    d_pb = 0;
+    st.d_p = p0;
+    st.d_oc0 = PIN ? gq * RB : og * 8;
+    st.d_q = q0;
+    st.d_pb = 0;
     // (pooled: channels up to Co only -- dY rows Co..Cop-1 feed only the MFMA rows the slab write
     // drops, and zero-filling them cost conv1 (10 of 16) a second staging round trip)
-    d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Co) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
+    st.d_more = PIN ? (gq < wgr && q0 < npixp && gq * RB < g.Co) : (og < ocg && p0 < g.npp && og * 8 < g.Cop);
   };
-  auto load_rows = [&]() {
+  auto load_rows = [&](Stg& st) {
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
       const bool in = prow && rr < nrows;
-      at[j] = in ? rr : -1;
+      st.at[j] = in ? rr : -1;
       const bool ok = in && colv && (unsigned)ih < (unsigned)g.H;
       const X t = xs[(unsigned)(ok ? xo : 0)];
-      xv[j] = ok ? (float)t : 0.f;
+      st.xv[j] = ok ? (float)t : 0.f;
       rr += rpi;  // (branch-free (ic, pr) advance: a divergent while loop per row was an exec-mask
       pr += pr_step;  // save / restore and a branch per row, and SGPR pairs spilled to VGPR lanes)
       ih += pr_step;
@@ -628,94 +676,72 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       xo += wrap ? xo_wrap : 0;
     }
   };
-  auto store_rows = [&]() {
+  auto store_rows = [&](const Stg& st) {
 #pragma unroll
     for (int j = 0; j < RB; ++j)
-      if (at[j] >= 0) patch[at[j] * g.PW + pc] = Stor<T>::of(xv[j]);
+      if (st.at[j] >= 0) patch[st.at[j] * g.PW + pc] = Stor<T>::of(st.xv[j]);
   };
-  auto load_dy = [&]() {  // one chunk's loads
+  auto load_dy = [&](Stg& st) {  // one chunk's loads
     if constexpr (!PIN) {
-      const int yo0 = d_oc0 * g.npix + d_p;
+      const int yo0 = st.d_oc0 * g.npix + st.d_p;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const bool ok = d_oc0 + j < g.Co && d_p < g.npix;
+        const bool ok = st.d_oc0 + j < g.Co && st.d_p < g.npix;
         const DY t = ys[(unsigned)(ok ? yo0 + j * g.npix : 0)];
-        dv[j] = ok ? (float)t : 0.f;
+        st.dv[j] = ok ? (float)t : 0.f;
       }
     } else {
-      const int ph = qdiv(d_q, PWp), pw = d_q - ph * PWp;
-      d_pb = 2 * ph * g.OW + 2 * pw;
-      const int po0 = d_oc0 * npixp + d_q;
+      const int ph = qdiv(st.d_q, PWp), pw = st.d_q - ph * PWp;
+      st.d_pb = 2 * ph * g.OW + 2 * pw;
+      const int po0 = st.d_oc0 * npixp + st.d_q;
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
-        const bool ok = d_oc0 + j < g.Co;
+        const bool ok = st.d_oc0 + j < g.Co;
         const unsigned po = ok ? po0 + j * npixp : 0;
         const DY t0 = ys[po], t1 = os[po];
         const uint8_t t2 = is[po];
-        const float t3 = ss[(unsigned)(ok && wa.pscale ? d_oc0 + j : 0)];
-        dv[j] = ok ? (float)t0 : 0.f;
-        yo[j] = ok ? (float)t1 : 0.f;
-        bi[j] = ok ? t2 : (uint8_t)255;
-        sc[j] = ok ? (wa.pscale ? t3 : 1.f) : 0.f;
+        const float t3 = ss[(unsigned)(ok && wa.pscale ? st.d_oc0 + j : 0)];
+        st.dv[j] = ok ? (float)t0 : 0.f;
+        st.yo[j] = ok ? (float)t1 : 0.f;
+        st.bi[j] = ok ? t2 : (uint8_t)255;
+        st.sc[j] = ok ? (wa.pscale ? t3 : 1.f) : 0.f;
       }
     }
   };
-  auto store_dy_next = [&]() {  // store the loaded chunk, advance to the next one
+  auto store_dy_next = [&](Stg& st) {  // store the loaded chunk, advance to the next one
     if constexpr (!PIN) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dys[(d_oc0 + j) * LDY + d_p] = Stor<T>::of(dv[j]);
-      d_oc0 += ocg * 8;
-      if (d_oc0 >= g.Cop) {
-        d_oc0 = og * 8;
-        d_p += pst;
+      for (int j = 0; j < 8; ++j) dys[(st.d_oc0 + j) * LDY + st.d_p] = Stor<T>::of(st.dv[j]);
+      st.d_oc0 += ocg * 8;
+      if (st.d_oc0 >= g.Cop) {
+        st.d_oc0 = og * 8;
+        st.d_p += pst;
       }
-      d_more = d_p < g.npp;
+      st.d_more = st.d_p < g.npp;
     } else {
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
-        if (d_oc0 + j >= g.Co) break;
-        S* d = dys + (d_oc0 + j) * LDY + d_pb;
+        if (st.d_oc0 + j >= g.Co) break;
+        S* d = dys + (st.d_oc0 + j) * LDY + st.d_pb;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(dv[j], bi[j], yo[j], sc[j], e));
+        for (int e = 0; e < 4; ++e)
+          d[(e >> 1) * g.OW + (e & 1)] = Stor<T>::of(unpool(st.dv[j], st.bi[j], st.yo[j], st.sc[j], e));
       }
-      d_oc0 += wgr * RB;
-      if (d_oc0 >= g.Co) {
-        d_oc0 = gq * RB;
-        d_q += wst;
+      st.d_oc0 += wgr * RB;
+      if (st.d_oc0 >= g.Co) {
+        st.d_oc0 = gq * RB;
+        st.d_q += wst;
       }
-      d_more = d_q < npixp;
+      st.d_more = st.d_q < npixp;
     }
   };
-
-  const int n_begin = blk * g.per_block;
-  const int n_end = min(N, n_begin + g.per_block);
-  // The first staging round (patch rows and the first dy chunk, loaded together) of image n + 1 is
-  // issued right after image n's staging, so its loads are in flight during image n's MFMAs; with
-  // two LDS buffers (g.dbuf) it is stored without waiting for them.  (Staging image by image after
-  // the previous one's MFMAs was a memory round trip per image in series: 16 images per block at
-  // B = 4096, ~3 us each, profiles/r6.)
-  if (n_begin < n_end) {
-    setup(n_begin);
-    load_rows();
-    if (d_more) load_dy();
-  }
-  for (int n = n_begin; n < n_end; ++n) {
-    const int buf = (n - n_begin) % nbuf;
-    if (nbuf == 1 && n > n_begin) __syncthreads();  // (one buffer: the previous image's MFMA reads are done)
-    dys = dys0 + buf * g.Cop * LDY;
-    patch = patch0 + buf * (pe + 1);
-    __builtin_amdgcn_sched_barrier(0);  // (no use of a loaded value hoisted above the buffer switch)
-    WG_STAMP(1);
-    store_rows();
-    if (d_more) store_dy_next();
-    while (prow && rr < nrows) {
-      load_rows();
-      store_rows();
-    }
-    while (d_more) {
-      load_dy();
-      store_dy_next();
-    }
+  auto issue = [&](Stg& st, int n) {  // image n's (first) staging round: loads only
+    setup(st, n);
+    load_rows(st);
+    if (st.d_more) load_dy(st);
+  };
+  // the constant-one slot and the pooled form's K padding of the current buffers
+  auto finish_staging = [&]() {
     if (tid == 0) patch[pe] = Stor<T>::of(1.f);  // slot pe holds 1.0 -> db column
     if (PIN) {  // (the MFMA K padding past npix: the window writes cover pixels < npix only)
       for (int i = tid; i < g.Cop * (g.npp - g.npix); i += NTHR) {
@@ -723,16 +749,10 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
         dys[oc * LDY + pp] = Stor<T>::of(0.f);
       }
     }
-    // (two buffers: every wave passed this barrier after its MFMAs on image n - 1's buffer, the one
-    // image n + 1 will write -- one barrier per image)
-    __syncthreads();
-    WG_STAMP(2);
-    if (n + 1 < n_end) {  // image n + 1's first round, in flight during this image's MFMAs
-      setup(n + 1);
-      load_rows();
-      if (d_more) load_dy();
-    }
-    if (my_nt0 >= NT) continue;
+  };
+  // this image's MFMAs over the current buffers
+  auto mfma_image = [&]() {
+    if (my_nt0 >= NT) return;
     // this lane's B-column patch offsets, one per N-tile (the same for every pixel step: read once
     // per image instead of once per MFMA, a dependent LDS round trip less per pixel step)
     int kos[MAXNTW];
@@ -741,11 +761,18 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
       const int nt = (jj == 0 || NT >= NW) ? my_nt0 + jj * NW : NT;  // (NT < NW: only jj = 0 is used)
       kos[jj] = nt < NT ? koff[nt * 16 + (lane & 15)] : pe;
     }
+    // the pixel step's patch bases are read one step ahead (clamped past the last step: a valid
+    // slot), so a step's gathers do not wait on a table read issued in front of them
+    int4 nb0 = *reinterpret_cast<const int4*>(pbase + my_s * 32 + 8 * (lane >> 4));
+    int4 nb1 = *reinterpret_cast<const int4*>(pbase + my_s * 32 + 8 * (lane >> 4) + 4);
     for (int ps = my_s; ps * 32 < g.npp; ps += psplit) {
       const int p0 = ps * 32 + 8 * (lane >> 4);
-      const int4 b0 = *reinterpret_cast<const int4*>(pbase + p0);
-      const int4 b1 = *reinterpret_cast<const int4*>(pbase + p0 + 4);
-      const int bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const int bb[8] = {nb0.x, nb0.y, nb0.z, nb0.w, nb1.x, nb1.y, nb1.z, nb1.w};
+      {
+        const int pn = min((ps + psplit) * 32, g.npp - 32) + 8 * (lane >> 4);
+        nb0 = *reinterpret_cast<const int4*>(pbase + pn);
+        nb1 = *reinterpret_cast<const int4*>(pbase + pn + 4);
+      }
       frag fa[MAXMT];
 #pragma unroll
       for (int mt = 0; mt < MAXMT; ++mt)
@@ -763,6 +790,73 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, const Wgrad
 #pragma unroll
         for (int mt = 0; mt < MAXMT; ++mt)
           if (mt < MT) acc[mt][jj] = Mfma<T>::mma(fa[mt], fb, acc[mt][jj]);
+      }
+    }
+  };
+
+  const int n_begin = blk * g.per_block;
+  const int n_end = min(N, n_begin + g.per_block);
+  if constexpr (PF == 1) {
+    // The first staging round (patch rows and the first dy chunk, loaded together) of image n + 1 is
+    // issued right after image n's staging, so its loads are in flight during image n's MFMAs; with
+    // two LDS buffers (g.dbuf) it is stored without waiting for them.  (Staging image by image after
+    // the previous one's MFMAs was a memory round trip per image in series: 16 images per block at
+    // B = 4096, ~3 us each, profiles/r6.)
+    Stg st;
+    if (n_begin < n_end) issue(st, n_begin);
+    for (int n = n_begin; n < n_end; ++n) {
+      const int buf = (n - n_begin) % nbuf;
+      if (nbuf == 1 && n > n_begin) __syncthreads();  // (one buffer: the previous image's MFMA reads are done)
+      dys = dys0 + buf * g.Cop * LDY;
+      patch = patch0 + buf * (pe + 1);
+      __builtin_amdgcn_sched_barrier(0);  // (no use of a loaded value hoisted above the buffer switch)
+      WG_STAMP(1);
+      store_rows(st);
+      if (st.d_more) store_dy_next(st);
+      while (prow && rr < nrows) {
+        load_rows(st);
+        store_rows(st);
+      }
+      while (st.d_more) {
+        load_dy(st);
+        store_dy_next(st);
+      }
+      finish_staging();
+      // (two buffers: every wave passed this barrier after its MFMAs on image n - 1's buffer, the one
+      // image n + 1 will write -- one barrier per image)
+      __syncthreads();
+      WG_STAMP(2);
+      if (n + 1 < n_end) issue(st, n + 1);  // image n + 1's first round, in flight during these MFMAs
+      mfma_image();
+    }
+  } else {
+    // PF > 1 (the host checked that one round stages a whole image -- wgrad_one_round -- and set
+    // g.dbuf): the loads of images n + 1 .. n + PF - 1 are in flight while image n is stored and
+    // multiplied, one register set per image, so an image's loads have PF - 1 images' MFMAs to land
+    // instead of one (at B = 4096 one image's MFMAs are shorter than a loaded memory round trip).
+    // The LDS keeps two buffers: image n is stored after the barrier that every wave passed once
+    // done with image n - 2's MFMAs on the same buffer.  Same images, same order, same sums.
+    Stg st[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (n_begin + u < n_end) issue(st[u], n_begin + u);
+    for (int n0 = n_begin; n0 < n_end; n0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int n = n0 + u;
+        if (n >= n_end) break;
+        const int buf = (n - n_begin) & 1;
+        dys = dys0 + buf * g.Cop * LDY;
+        patch = patch0 + buf * (pe + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        WG_STAMP(1);
+        store_rows(st[u]);
+        if (st[u].d_more) store_dy_next(st[u]);
+        finish_staging();
+        __syncthreads();
+        WG_STAMP(2);
+        if (n + PF < n_end) issue(st[u], n + PF);
+        mfma_image();
       }
     }
   }
@@ -863,7 +957,7 @@ __device__ __forceinline__ void carried_reduce(const RedArgs& r, int rb, unsigne
 #ifndef CSED_WGRAD_WAVES
 #define CSED_WGRAD_WAVES 1
 #endif
-template <typename T, typename X, typename DY, bool PIN, bool WIDE, bool SMALL = false>
+template <typename T, typename X, typename DY, bool PIN, bool WIDE, bool SMALL = false, int PF = 1>
 __global__ void __launch_bounds__(WIDE ? 512 : 256) __attribute__((amdgpu_waves_per_eu(SMALL ? CSED_WGRAD_WAVES : 1)))
 conv_wgrad_kernel(WgradArgs wa, WgradGeo g, RedArgs r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -871,7 +965,7 @@ conv_wgrad_kernel(WgradArgs wa, WgradGeo g, RedArgs r) {
     carried_reduce<WIDE ? 512 : 256>(r, blockIdx.x - g.nblocks, smem);
     return;
   }
-  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256, SMALL>(wa, g, blockIdx.x, smem);
+  conv_wgrad_body<T, X, DY, PIN, WIDE, WIDE ? 512 : 256, SMALL, PF>(wa, g, blockIdx.x, smem);
 }
 
 // The backward of one conv in one launch: blocks [0, wgrad blocks) write the weight-gradient
@@ -1004,7 +1098,18 @@ static hipError_t conv_geo(const ConvArgs& a, ConvGeo& g, size_t& lds, int& grid
   g.bands = (g.OH + tr - 1) / tr;
   lds = lds_bytes(tr);
   g.items = a.N * g.bands;
-  grid = std::min(g.items, kConvPersistBlocks);  // (persistent blocks past one full wave of the chip)
+  grid = std::min(g.items, kConvPersistBlocks);
+  // vector staging (conv_fwd_body VM, narrow launches): one item per image, unpooled input, 16-byte
+  // aligned images whose rows are whole 16-byte vectors (or unpadded: the image one run), <= 2
+  // vectors per thread of a 256-thread block, offsets in qdiv's range
+  g.nvec = 0;
+  {
+    const int esx = a.x_dtype == kF32 ? 4 : 2;
+    const int64_t img = (int64_t)g.Ci * g.H * g.W;
+    if (!a.pidx && g.bands == 1 && (img * esx) % 16 == 0 && reinterpret_cast<uintptr_t>(a.x) % 16 == 0 &&
+        (g.pad == 0 || (g.W * esx) % 16 == 0) && img * esx / 16 <= 2 * 256 && img < (1 << 20))
+      g.nvec = (int)(img * esx / 16);
+  }  // (persistent blocks past one full wave of the chip)
   return hipSuccess;
 }
 
@@ -1031,8 +1136,11 @@ hipError_t launch_conv2d(const ConvArgs& a, hipStream_t s) {
         const bool rb4 = wide && cdiv(g.Ci * g.PR, 512 / g.PW) <= 4;  // (patch rows per thread)
         if (a.pidx) return wide ? (rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, true, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, true, true>))
                                 : narrow_ntm(g.Cop, [&](auto k) { return go(conv_fwd_kernel<scalar_t, X, Y, true, false, 8, decltype(k)::value>); });
-        return wide ? (rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, false, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, false, true>))
-                    : narrow_ntm(g.Cop, [&](auto k) { return go(conv_fwd_kernel<scalar_t, X, Y, false, false, 8, decltype(k)::value>); });
+        if (wide) return rb4 ? go(conv_fwd_kernel<scalar_t, X, Y, false, true, 4>) : go(conv_fwd_kernel<scalar_t, X, Y, false, true>);
+        return narrow_ntm(g.Cop, [&](auto k) {
+          return g.nvec ? go(conv_fwd_kernel<scalar_t, X, Y, false, false, 8, decltype(k)::value, true>)
+                        : go(conv_fwd_kernel<scalar_t, X, Y, false, false, 8, decltype(k)::value>);
+        });
       });
     });
   });
@@ -1077,6 +1185,44 @@ static size_t wgrad_lds(const WgradGeo& g, size_t es, int nbuf) {
 static bool wgrad_small(const WgradGeo& g) {
   const int MT = g.Cop >> 4, NT = g.Kc >> 4, NW = 8;
   return MT <= 2 && (NT < NW || cdiv(NT, NW) <= 2);
+}
+
+// One staging round (conv_wgrad_body's first load_rows / load_dy) covers a whole image at NTHR = 512
+// threads (RB = 4): every patch row, every dy channel and pixel -- the condition for PF > 1
+static bool wgrad_one_round(const WgradGeo& g, bool pin) {
+  constexpr int NTHR = 512, RB = 4;
+  const int rpi = NTHR / g.PW;
+  if (rpi * RB < g.Ci * g.PR) return false;
+  if (pin) {
+    const int npixp = (g.OH >> 1) * (g.OW >> 1);
+    const int wst = std::max(1, std::min(npixp, NTHR));
+    return npixp <= NTHR && (NTHR / wst) * RB >= g.Co;
+  }
+  const int pst = std::min(g.npp, NTHR);
+  return g.npp <= NTHR && (NTHR / pst) * 8 >= g.Cop;
+}
+
+#ifndef CSED_WGRAD_PF
+#define CSED_WGRAD_PF 2
+#endif
+// The staging depth in use: the instantiated one, or 1 (CSED_WGRAD_PF=1 in the environment, read once
+// -- same-build A/B -- or conv_wgrad_prefetch(1): a test comparing both forms in one process)
+static std::atomic<int> g_wgrad_pf{-1};
+static bool wgrad_pf_on() {
+  int v = g_wgrad_pf.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("CSED_WGRAD_PF");
+    int want = e && std::atoi(e) <= 1 ? 1 : CSED_WGRAD_PF;
+    g_wgrad_pf.compare_exchange_strong(v, want);
+    v = g_wgrad_pf.load(std::memory_order_relaxed);
+  }
+  return v > 1;
+}
+
+int conv_wgrad_prefetch(int depth) {
+  (void)wgrad_pf_on();  // (the environment's default first)
+  if (depth > 0) g_wgrad_pf.store(depth > 1 ? CSED_WGRAD_PF : 1, std::memory_order_relaxed);
+  return g_wgrad_pf.load(std::memory_order_relaxed);
 }
 
 int64_t conv2d_wgrad_workspace(int N, int IC, int KH, int KW, int OC) {
@@ -1165,9 +1311,15 @@ hipError_t launch_conv2d_bwd(const ConvBwdArgs& b, hipStream_t s) {
           auto with_w = [&](auto wk) -> hipError_t {
             if (dw) return go(conv_bwd_kernel<T, X, DY, P>, wk, conv_fwd_kernel<T, DY, X, P, true>);
             return narrow_ntm(g.Cop, [&](auto k) {
+              if constexpr (!P)  // (vector staging: the materialised dL/dconv, conv_geo's nvec)
+                if (g.nvec) return go(conv_bwd_kernel<T, X, DY, P>, wk, conv_fwd_kernel<T, DY, X, P, false, 8, decltype(k)::value, true>);
               return go(conv_bwd_kernel<T, X, DY, P>, wk, conv_fwd_kernel<T, DY, X, P, false, 8, decltype(k)::value>);
             });
           };
+          // deeper staging prefetch: a block walking several images, two LDS buffers, one-round stagings
+          const bool pf = wgrad_pf_on() && wg.dbuf && wg.per_block > 2 && wgrad_one_round(wg, P);
+          if (pf) return small ? with_w(conv_wgrad_kernel<T, X, DY, P, true, true, CSED_WGRAD_PF>)
+                               : with_w(conv_wgrad_kernel<T, X, DY, P, true, false, CSED_WGRAD_PF>);
           return small ? with_w(conv_wgrad_kernel<T, X, DY, P, true, true>) : with_w(conv_wgrad_kernel<T, X, DY, P, true, false>);
         };
         return b.pidx ? pick(std::true_type{}) : pick(std::false_type{});

@@ -191,6 +191,8 @@ hipError_t launch_wgrad_reduce(const float* ws, float* dw, float* db, int N, int
 int64_t conv2d_wgrad_workspace(int N, int IC, int KH, int KW, int OC);
 // weight-gradient blocks (partial slabs) for a batch of N images
 int conv2d_wgrad_blocks(int N);
+// weight-gradient staging depth: depth > 0 sets it (1, or the built depth), returns the one in use
+int conv_wgrad_prefetch(int depth);
 hipError_t launch_conv2d_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw,
                                float* db, float* ws, int N, int IC, int H, int W, int OC, int KH,
                                int KW, int pad, int mfma_dtype, float beta, hipStream_t s);

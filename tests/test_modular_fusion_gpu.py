@@ -471,20 +471,24 @@ def test_shared_weights_with_destinations_match_cpu(defer):
         _drop_destinations(flat)
 
 
-@pytest.mark.parametrize("kind", ["fwd_pool", "fwd_plain", "dgrad", "dgrad_pooled"])
+@pytest.mark.parametrize("kind", ["fwd_pool", "fwd_pool_f32in", "fwd_plain", "dgrad", "dgrad_pooled"])
 def test_conv_persistent_blocks_match_per_item_launches_bitwise(kind):
     """Large batches: the conv forward / data-gradient launch runs at most 2048 persistent blocks that
     walk the (image, band) items with the weights staged once per block (conv.hip conv_fwd_kernel).
     A batch of 2100 images (items > blocks) must give the same bits as the same images launched in
-    chunks of 500 (one block per item), and match an fp32 reference."""
+    chunks of 500 (one block per item), and match an fp32 reference.  The persistent form stages an
+    unpooled input by 16-byte vectors (conv_fwd_body VM; the per-item one element by element): the
+    fp32-input forward (the modular conv1) and the padded data gradient cover both of its layouts."""
     g = torch.Generator(device=DEV).manual_seed(17)
     N = 2100
     o = _native.ops()
     if kind.startswith("fwd"):
-        x = torch.randn(N, 1, 28, 28, device=DEV, generator=g).to(torch.bfloat16)
+        x = torch.randn(N, 1, 28, 28, device=DEV, generator=g)
+        if kind != "fwd_pool_f32in":  # (the modular step's conv1 reads the fp32 input)
+            x = x.to(torch.bfloat16)
         w = torch.randn(10, 1, 5, 5, device=DEV, generator=g) * 0.3
         b = torch.randn(10, device=DEV, generator=g) * 0.1
-        pool = kind == "fwd_pool"
+        pool = kind.startswith("fwd_pool")
 
         def run(xx):
             if pool:
@@ -538,3 +542,49 @@ def test_conv_persistent_blocks_match_per_item_launches_bitwise(kind):
             full = run(x, scale)
             parts = torch.cat([run(x[i:i + 500], scale[i * 20:(i + 500) * 20]) for i in range(0, N, 500)])
             assert torch.equal(full, parts)
+
+
+@pytest.mark.parametrize("pooled", [True, False])
+def test_conv_wgrad_staging_depth_bitwise(pooled):
+    """Large batches: a weight-gradient block walks several images with the loads of the next
+    PF - 1 images in flight (conv.hip conv_wgrad_body, PF > 1).  Same images, same order, same
+    sums: the slab must equal the one-image-ahead form (conv_wgrad_prefetch(1)) bit for bit, and match
+    an fp32 reference.  conv1's shape with a pooled dy (the modular step's conv1 backward), conv2's
+    with a plain one (its materialised dL/dconv at large batch)."""
+    g = torch.Generator(device=DEV).manual_seed(23)
+    N = 1300  # 217 weight-gradient blocks x 6 images: per_block > 2
+    o = _native.ops()
+    dt = torch.bfloat16
+    if pooled:
+        x = torch.randn(N, 1, 28, 28, device=DEV, generator=g).to(dt)
+        w = torch.randn(10, 1, 5, 5, device=DEV, generator=g) * 0.3
+        b = torch.randn(10, device=DEV, generator=g) * 0.1
+        scale = (torch.rand(N * 10, device=DEV, generator=g) > 0.5).float() * 2.0
+        y, idx = _pooled_fwd(x, w, b, dt, scale)
+        dy = torch.randn(y.shape, device=DEV, generator=g).to(dt)
+    else:
+        x = torch.randn(N, 10, 12, 12, device=DEV, generator=g).to(dt)
+        w = torch.randn(20, 10, 5, 5, device=DEV, generator=g) * 0.2
+        dy = torch.randn(N, 20, 8, 8, device=DEV, generator=g).to(dt)
+    OC, C = w.shape[:2]
+    ws = torch.empty(wgrad_workspace_elems(N, C, 5, 5, OC), device=DEV)
+    out = {}
+    prev = o.conv_wgrad_prefetch(0)
+    for pf in ("1", "2"):
+        o.conv_wgrad_prefetch(int(pf))
+        dw, db = torch.empty_like(w), torch.empty(OC, device=DEV)
+        if pooled:
+            o.conv2d_bwd(x, dy, w, dw, db, ws, None, 0, idx, y, scale, MF[dt])
+        else:
+            o.conv2d_wgrad(x, dy, dw, db, ws, 0, MF[dt], 0.0)
+        torch.cuda.synchronize()
+        out[pf] = (dw, db)
+    o.conv_wgrad_prefetch(prev)
+    assert prev > 1, "the weight-gradient staging depth is 2 by default"
+    assert torch.equal(out["1"][0], out["2"][0]) and torch.equal(out["1"][1], out["2"][1])
+    dconv = _unpool_ref(dy, idx, y, scale) if pooled else dy.float().cpu()
+    ref_w = torch.nn.grad.conv2d_weight(x.float().cpu(), w.shape, dconv)
+    ref_b = dconv.sum((0, 2, 3))
+    for got, ref in ((out["2"][0], ref_w), (out["2"][1], ref_b)):
+        err = (got.float().cpu() - ref).abs().max().item()
+        assert err <= 3e-2 * max(ref.abs().max().item(), 1e-6), err

@@ -34,6 +34,7 @@
 #   ipcmem    the exchange receive buffer's allocation: uncached (default) vs CSED_IPC_MEM=finegrained
 #             (was gpu_ipcmem.sh)
 #   bringtrace rocprofv3 HIP-API + kernel + memory-copy trace of the bench bring-up, summarised
+#   wgradab   same-build A/B of the conv weight-gradient staging depth at B = 4096 (op times, step)
 #   epoch0    the reference span on a fresh process, stamped: bench.py --epoch0-stamps at N = 1 (bf16,
 #             fp32) + the driver's own command
 TASKS=${1:?task list}
@@ -246,6 +247,15 @@ task_modsteps() {  # the modular step at B = 64 and 4096: per-op launch times an
   py 300 python -u tools/ddp_overlap.py --batch 64 --graph graph > $O/${T}_mod64.log 2>&1 && \
   py 300 python -u tools/ddp_overlap.py --batch 4096 --graph graph --only single:25 --loader > $O/${T}_mod4096_loader.log 2>&1 && \
   py 300 python -u tools/ddp_overlap.py --batch 64 --graph graph --only single:25 --loader > $O/${T}_mod64_loader.log 2>&1
+}
+
+task_wgradab() {  # same-build A/B of the weight-gradient staging depth (CSED_WGRAD_PF=1 vs the built depth)
+  cd $R && rm -f $O/${T}_wgradab.log && \
+  for i in $(seq ${N_AB:-3}); do for v in 1 2; do
+    echo "PF=$v" >> $O/${T}_wgradab.log && \
+    CSED_WGRAD_PF=$v py 300 python -u tools/op_probe.py --batch 4096 --reps 20 2>/dev/null | grep -E "conv[12] bwd" >> $O/${T}_wgradab.log && \
+    CSED_WGRAD_PF=$v py 300 python -u tools/ddp_overlap.py --batch 4096 --graph graph --only single:25 2>/dev/null | tail -2 >> $O/${T}_wgradab.log || return 1
+  done; done
 }
 
 task_quick() {  # the test files this round's changes touch
